@@ -1,0 +1,1188 @@
+/*
+ * lssp_oracle.c -- CPU restatement of the LSSP Krylov hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP
+ * product path in lssp_amd/.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load it.  The product never links it.
+ *
+ * Every function restates the algorithm of the reference (huiscliu/lssp,
+ * mounted read-only at /root/reference) in its own code; the citations give
+ * the reference file:line it follows.  Floating-point operation order is kept
+ * exactly as in the reference, and the file is compiled with
+ * -O2 -ffp-contract=off (no FMA contraction), so results are bit-identical to
+ * a g++ -O2 (x86-64 baseline, no -march) build of the reference.  The
+ * restatement is pinned against the reference itself: oracle/_ref/libref.so is
+ * compiled from the reference sources in place (oracle/Makefile) and
+ * tests/golden/ holds the vectors it produced (tests/golden/make_golden.py).
+ *
+ * Besides the reference's serial dot product (vector.cxx:123-133), the oracle
+ * implements the GPU's canonical tree reduction order (LSSP_AMD reduction
+ * contract) and the P-rank row-block partitioned order,
+ * so that the GPU solvers can be checked bit-for-bit in every mode.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define EXPORT __attribute__((visibility("default")))
+
+/* reference defaults: pc.cxx:6-7 and lssp.cxx:5-14 */
+static const double ZERO_DIAG_VALUE = 1e-3;
+static const double ZERO_DIAG_TOL = 1e-10;
+static const double BREAKDOWN = 1e-40;
+static const int DEF_MAXIT = 1000;
+static const int DEF_RESTART = 50;
+static const double DEF_TOL = 1e-7;
+
+typedef struct {
+    int nrows, ncols, nnz;
+    int *Ap, *Aj;
+    double *Ax;
+} csr_t;
+
+static void csr_free(csr_t *A)
+{
+    free(A->Ap);
+    free(A->Aj);
+    free(A->Ax);
+    memset(A, 0, sizeof(*A));
+}
+
+static csr_t csr_alloc(int nrows, int ncols, int nnz)
+{
+    csr_t A;
+    A.nrows = nrows;
+    A.ncols = ncols;
+    A.nnz = nnz;
+    A.Ap = (int *)malloc(sizeof(int) * (size_t)(nrows + 1));
+    A.Aj = (int *)malloc(sizeof(int) * (size_t)(nnz > 0 ? nnz : 1));
+    A.Ax = (double *)malloc(sizeof(double) * (size_t)(nnz > 0 ? nnz : 1));
+    return A;
+}
+
+static csr_t csr_copy(int n, int ncols, const int *Ap, const int *Aj, const double *Ax)
+{
+    csr_t A = csr_alloc(n, ncols, Ap[n]);
+    memcpy(A.Ap, Ap, sizeof(int) * (size_t)(n + 1));
+    memcpy(A.Aj, Aj, sizeof(int) * (size_t)Ap[n]);
+    memcpy(A.Ax, Ax, sizeof(double) * (size_t)Ap[n]);
+    return A;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Reductions                                                               */
+/* ------------------------------------------------------------------------ */
+
+enum { RED_SERIAL = 0, RED_TREE = 1 };
+
+/* vector.cxx:123-133: sum += x[i]*y[i], from 0, in index order */
+static double dot_serial(const double *x, const double *y, long n)
+{
+    double s = 0;
+    for (long i = 0; i < n; i++) s += x[i] * y[i];
+    return s;
+}
+
+/* One 64-lane wave: xor-butterfly == halving tree, lane 0 result. */
+static double wave64(double *v)
+{
+    for (int off = 32; off >= 1; off >>= 1)
+        for (int l = 0; l < off; l++) v[l] = v[l] + v[l + off];
+    return v[0];
+}
+
+/* Level 1 of the canonical GPU order: one aligned chunk of 256 products,
+ * zero padded, four waves each halving, then (w0+w1)+(w2+w3). */
+static double chunk256(const double *x, const double *y, long base, long n)
+{
+    double w[4];
+    for (int q = 0; q < 4; q++) {
+        double v[64];
+        for (int l = 0; l < 64; l++) {
+            long i = base + 64 * q + l;
+            v[l] = (i < n) ? x[i] * y[i] : 0.0;
+        }
+        w[q] = wave64(v);
+    }
+    return (w[0] + w[1]) + (w[2] + w[3]);
+}
+
+/* Level 2: 1024 lanes, lane t adds S[t], S[t+1024], ... onto 0.0 in order,
+ * then 16 waves halve, then the 16 wave results halve. */
+static double level2(const double *S, long C)
+{
+    double acc[1024];
+    for (int t = 0; t < 1024; t++) {
+        double a = 0.0;
+        for (long k = t; k < C; k += 1024) a += S[k];
+        acc[t] = a;
+    }
+    double u[16];
+    for (int q = 0; q < 16; q++) u[q] = wave64(acc + 64 * q);
+    for (int off = 8; off >= 1; off >>= 1)
+        for (int l = 0; l < off; l++) u[l] = u[l] + u[l + off];
+    return u[0];
+}
+
+static double dot_tree(const double *x, const double *y, long n)
+{
+    long C = (n + 255) / 256;
+    if (C == 0) return level2(NULL, 0);
+    double *S = (double *)malloc(sizeof(double) * (size_t)C);
+    for (long c = 0; c < C; c++) S[c] = chunk256(x, y, 256 * c, n);
+    double r = level2(S, C);
+    free(S);
+    return r;
+}
+
+/* Reduction context: mode + P-rank row-block partition (blk = ceil(n/P)). */
+typedef struct {
+    int mode;
+    int nranks;
+} red_t;
+
+static double dot_red(const red_t *R, const double *x, const double *y, long n)
+{
+    int P = R->nranks > 1 ? R->nranks : 1;
+    long blk = (n + P - 1) / P;
+    double total = 0.0;
+    for (int r = 0; r < P; r++) {
+        long s = (long)r * blk, e = s + blk;
+        if (s > n) s = n;
+        if (e > n) e = n;
+        double part = R->mode == RED_TREE ? dot_tree(x + s, y + s, e - s)
+                                          : dot_serial(x + s, y + s, e - s);
+        total = r == 0 ? part : total + part;
+    }
+    return total;
+}
+
+EXPORT double orc_dot(int mode, int nranks, const double *x, const double *y, long n)
+{
+    red_t R = {mode, nranks};
+    return dot_red(&R, x, y, n);
+}
+
+/* ------------------------------------------------------------------------ */
+/* L1 kernels: SpMV (mvops.cxx), BLAS-1 (vector.cxx), trisolve               */
+/* ------------------------------------------------------------------------ */
+
+static double row_sum(const csr_t *A, const double *x, int i)
+{
+    double sum = 0;
+    for (int jj = A->Ap[i]; jj < A->Ap[i + 1]; jj++) sum += x[A->Aj[jj]] * A->Ax[jj];
+    return sum;
+}
+
+/* mvops.cxx:42-69  z = y*beta + alpha*(A x) */
+static void mv_amxpbyz(double alpha, const csr_t *A, const double *x, double beta,
+                       const double *y, double *z)
+{
+    for (int i = 0; i < A->nrows; i++) z[i] = y[i] * beta + alpha * row_sum(A, x, i);
+}
+
+/* mvops.cxx:118-142  y = A x */
+static void mv_mxy(const csr_t *A, const double *x, double *y)
+{
+    for (int i = 0; i < A->nrows; i++) y[i] = row_sum(A, x, i);
+}
+
+EXPORT void orc_spmv(int op, int n, const int *Ap, const int *Aj, const double *Ax,
+                     double alpha, const double *x, double beta, const double *y, double *z)
+{
+    /* op 0: mxy (mvops.cxx:118), 1: amxy (:81), 2: amxpby in place on z (:5),
+     * 3: amxpbyz (:42). Ap == NULL means the zero matrix, as in the reference. */
+    for (int i = 0; i < n; i++) {
+        double sum = 0;
+        if (Ap != NULL)
+            for (int jj = Ap[i]; jj < Ap[i + 1]; jj++) sum += x[Aj[jj]] * Ax[jj];
+        switch (op) {
+        case 0: z[i] = Ap ? sum : 0; break;
+        case 1: z[i] = Ap ? sum * alpha : 0; break;
+        case 2: z[i] = Ap ? sum * alpha + z[i] * beta : z[i] * beta; break;
+        default: z[i] = Ap ? y[i] * beta + alpha * sum : y[i] * beta; break;
+        }
+    }
+}
+
+/* solver-tri.cxx:4-24: diagonal stored LAST, ascending storage-order sum */
+static void tri_lower(const csr_t *L, double *x, const double *rhs)
+{
+    for (int i = 0; i < L->nrows; i++) {
+        int end = L->Ap[i + 1] - 1;
+        double r = rhs[i];
+        for (int j = L->Ap[i]; j < end; j++) r = r - L->Ax[j] * x[L->Aj[j]];
+        x[i] = r / L->Ax[end];
+    }
+}
+
+/* solver-tri.cxx:26-46: diagonal stored FIRST, descending storage-order sum */
+static void tri_upper(const csr_t *U, double *x, const double *rhs)
+{
+    for (int i = U->nrows - 1; i >= 0; i--) {
+        int d = U->Ap[i];
+        double r = rhs[i];
+        for (int j = U->Ap[i + 1] - 1; j > d; j--) r = r - U->Ax[j] * x[U->Aj[j]];
+        x[i] = r / U->Ax[d];
+    }
+}
+
+EXPORT void orc_ilu_apply(int n, const int *Lp, const int *Lj, const double *Lx,
+                          const int *Up, const int *Uj, const double *Ux,
+                          double *x, const double *rhs)
+{
+    /* solver-tri.cxx:48-60: cache = L^-1 rhs; x = U^-1 cache */
+    csr_t L = {n, n, Lp[n], (int *)Lp, (int *)Lj, (double *)Lx};
+    csr_t U = {n, n, Up[n], (int *)Up, (int *)Uj, (double *)Ux};
+    double *cache = (double *)malloc(sizeof(double) * (size_t)n);
+    tri_lower(&L, cache, rhs);
+    tri_upper(&U, x, cache);
+    free(cache);
+}
+
+EXPORT void orc_trisolve(int upper, int n, const int *Ap, const int *Aj, const double *Ax,
+                         double *x, const double *rhs)
+{
+    csr_t T = {n, n, Ap[n], (int *)Ap, (int *)Aj, (double *)Ax};
+    if (upper) tri_upper(&T, x, rhs);
+    else tri_lower(&T, x, rhs);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Matrix utilities (matrix-utils.cxx)                                      */
+/* ------------------------------------------------------------------------ */
+
+/* matrix-utils.cxx:387-481: only unsorted rows are touched; entries are
+ * bucketed by column (a duplicate column keeps the last value for every
+ * occurrence) and the column list is sorted ascending. */
+static int cmp_int(const void *a, const void *b)
+{
+    int x = *(const int *)a, y = *(const int *)b;
+    return (x > y) - (x < y);
+}
+
+static void sort_columns(csr_t *A)
+{
+    if (A->nrows <= 0 || A->ncols <= 0 || A->nnz <= 0) return;
+    double *val = (double *)malloc(sizeof(double) * (size_t)A->ncols);
+    int *cols = (int *)malloc(sizeof(int) * (size_t)A->ncols);
+    for (int i = 0; i < A->nrows; i++) {
+        int b = A->Ap[i], e = A->Ap[i + 1], need = 0;
+        for (int j = b + 1; j < e; j++)
+            if (A->Aj[j - 1] > A->Aj[j]) { need = 1; break; }
+        if (!need) continue;
+        int m = 0;
+        for (int j = b; j < e; j++) {
+            val[A->Aj[j]] = A->Ax[j];
+            cols[m++] = A->Aj[j];
+        }
+        qsort(cols, (size_t)m, sizeof(int), cmp_int);
+        for (int j = b, t = 0; j < e; j++, t++) {
+            A->Aj[j] = cols[t];
+            A->Ax[j] = val[cols[t]];
+        }
+    }
+    free(val);
+    free(cols);
+}
+
+/* matrix-utils.cxx:483-587: rows without a diagonal get (i, tol) inserted at
+ * its sorted position (appended, then bubbled left). */
+static csr_t adjust_zero_diag(const csr_t *A, double tol)
+{
+    int n = A->nrows, missing = 0;
+    char *has = (char *)calloc((size_t)n, 1);
+    for (int i = 0; i < n; i++)
+        for (int j = A->Ap[i]; j < A->Ap[i + 1]; j++)
+            if (A->Aj[j] == i) has[i] = 1;
+    for (int i = 0; i < n; i++) missing += !has[i];
+    csr_t M = csr_alloc(n, A->ncols, A->nnz + missing);
+    M.Ap[0] = 0;
+    for (int i = 0; i < n; i++) M.Ap[i + 1] = M.Ap[i] + (A->Ap[i + 1] - A->Ap[i]) + !has[i];
+    for (int i = 0; i < n; i++) {
+        int o = M.Ap[i];
+        for (int j = A->Ap[i]; j < A->Ap[i + 1]; j++, o++) {
+            M.Aj[o] = A->Aj[j];
+            M.Ax[o] = A->Ax[j];
+        }
+        if (has[i]) continue;
+        M.Aj[o] = i;
+        M.Ax[o] = tol;
+        for (int j = M.Ap[i + 1] - 2; j >= M.Ap[i]; j--) {
+            if (M.Aj[j] <= M.Aj[j + 1]) break;
+            int tj = M.Aj[j];
+            double tx = M.Ax[j];
+            M.Aj[j] = M.Aj[j + 1];
+            M.Ax[j] = M.Ax[j + 1];
+            M.Aj[j + 1] = tj;
+            M.Ax[j + 1] = tx;
+        }
+    }
+    free(has);
+    return M;
+}
+
+/* matrix-utils.cxx:589-698: keep entries whose column lies in the row's
+ * block; an emptied row becomes (j, 1.0).  blk == n is a plain copy. */
+static csr_t block_diag(const csr_t *A, int blk)
+{
+    int n = A->nrows;
+    if (blk == n) return csr_copy(n, A->ncols, A->Ap, A->Aj, A->Ax);
+    int *cnt = (int *)calloc((size_t)n + 1, sizeof(int));
+    long total = 0;
+    for (int i = 0; i < n; i++) {
+        int s = (i / blk) * blk, e = s + blk < n ? s + blk : n;
+        for (int k = A->Ap[i]; k < A->Ap[i + 1]; k++)
+            if (A->Aj[k] >= s && A->Aj[k] < e) cnt[i]++;
+        if (cnt[i] == 0) cnt[i] = -1;
+        total += cnt[i] > 0 ? cnt[i] : 1;
+    }
+    csr_t M = csr_alloc(n, A->ncols, (int)total);
+    M.Ap[0] = 0;
+    int o = 0;
+    for (int i = 0; i < n; i++) {
+        int s = (i / blk) * blk, e = s + blk < n ? s + blk : n;
+        if (cnt[i] > 0) {
+            for (int k = A->Ap[i]; k < A->Ap[i + 1]; k++)
+                if (A->Aj[k] >= s && A->Aj[k] < e) {
+                    M.Aj[o] = A->Aj[k];
+                    M.Ax[o] = A->Ax[k];
+                    o++;
+                }
+        } else {
+            M.Aj[o] = i;
+            M.Ax[o] = 1;
+            o++;
+        }
+        M.Ap[i + 1] = o;
+    }
+    free(cnt);
+    return M;
+}
+
+/* ------------------------------------------------------------------------ */
+/* ILUK (pc-iluk.cxx)                                                       */
+/* ------------------------------------------------------------------------ */
+
+/* pc-iluk.cxx:22-135 + :186-229 + :231-277: level-of-fill symbolic ILU(k).
+ * Returns the ILU(k) pattern with A's values (0 on fill), rows sorted. */
+static csr_t iluk_symbolic(const csr_t *A, int level)
+{
+    int n = A->nrows;
+    if (level < 0) level = 0;
+    int *lev = (int *)malloc(sizeof(int) * (size_t)n);
+    int *buf = (int *)malloc(sizeof(int) * (size_t)n);
+    int *pos = (int *)malloc(sizeof(int) * (size_t)n);
+    int **Lrow = (int **)calloc((size_t)n, sizeof(int *));
+    int **Urow = (int **)calloc((size_t)n, sizeof(int *));
+    int **Ulev = (int **)calloc((size_t)n, sizeof(int *));
+    int *Ln = (int *)calloc((size_t)n, sizeof(int));
+    int *Un = (int *)calloc((size_t)n, sizeof(int));
+    for (int j = 0; j < n; j++) pos[j] = -1;
+
+    for (int i = 0; i < n; i++) {
+        int nl = 0, nu = i;
+        for (int jj = A->Ap[i]; jj < A->Ap[i + 1]; jj++) {
+            int c = A->Aj[jj];
+            if (c < i) {
+                buf[nl] = c;
+                lev[nl] = 0;
+                pos[c] = nl++;
+            } else if (c > i) {
+                buf[nu] = c;
+                lev[nu] = 0;
+                pos[c] = nu++;
+            }
+        }
+        for (int piv = 0; piv < nl; piv++) {
+            /* bring the smallest remaining lower column to slot piv */
+            int k = buf[piv], kmin = k, at = piv;
+            for (int j = piv + 1; j < nl; j++)
+                if (buf[j] < kmin) {
+                    kmin = buf[j];
+                    at = j;
+                }
+            if (at != piv) {
+                buf[piv] = kmin;
+                buf[at] = k;
+                pos[kmin] = piv;
+                pos[k] = at;
+                int t = lev[piv];
+                lev[piv] = lev[at];
+                lev[at] = t;
+                k = kmin;
+            }
+            for (int j = 0; j < Un[k]; j++) {
+                int c = Urow[k][j];
+                int it = Ulev[k][j] + lev[piv] + 1;
+                if (it > level) continue;
+                int p = pos[c];
+                if (p == -1) {
+                    if (c < i) {
+                        buf[nl] = c;
+                        lev[nl] = it;
+                        pos[c] = nl++;
+                    } else if (c > i) {
+                        buf[nu] = c;
+                        lev[nu] = it;
+                        pos[c] = nu++;
+                    }
+                } else if (lev[p] < it) {
+                    lev[p] = it;
+                }
+            }
+        }
+        for (int j = 0; j < nl; j++) pos[buf[j]] = -1;
+        for (int j = i; j < nu; j++) pos[buf[j]] = -1;
+        Ln[i] = nl;
+        if (nl) {
+            Lrow[i] = (int *)malloc(sizeof(int) * (size_t)nl);
+            memcpy(Lrow[i], buf, sizeof(int) * (size_t)nl);
+        }
+        Un[i] = nu - i;
+        if (Un[i]) {
+            Urow[i] = (int *)malloc(sizeof(int) * (size_t)Un[i]);
+            Ulev[i] = (int *)malloc(sizeof(int) * (size_t)Un[i]);
+            memcpy(Urow[i], buf + i, sizeof(int) * (size_t)Un[i]);
+            memcpy(Ulev[i], lev + i, sizeof(int) * (size_t)Un[i]);
+        }
+    }
+
+    long nnz = 0;
+    for (int i = 0; i < n; i++) nnz += Ln[i] + Un[i] + 1;
+    csr_t M = csr_alloc(n, n, (int)nnz);
+    M.Ap[0] = 0;
+    int o = 0;
+    for (int i = 0; i < n; i++) {
+        for (int j = 0; j < Ln[i]; j++) M.Aj[o++] = Lrow[i][j];
+        M.Aj[o++] = i;
+        for (int j = 0; j < Un[i]; j++) M.Aj[o++] = Urow[i][j];
+        M.Ap[i + 1] = o;
+    }
+    /* pc-iluk.cxx:231-277: values of A where the pattern matches, else 0 */
+    double *wk = (double *)calloc((size_t)n, sizeof(double));
+    for (int i = 0; i < n; i++) {
+        for (int j = A->Ap[i]; j < A->Ap[i + 1]; j++) wk[A->Aj[j]] = A->Ax[j];
+        for (int j = M.Ap[i]; j < M.Ap[i + 1]; j++) M.Ax[j] = wk[M.Aj[j]];
+        for (int j = A->Ap[i]; j < A->Ap[i + 1]; j++) wk[A->Aj[j]] = 0;
+    }
+    free(wk);
+    sort_columns(&M);
+
+    for (int i = 0; i < n; i++) {
+        free(Lrow[i]);
+        free(Urow[i]);
+        free(Ulev[i]);
+    }
+    free(Lrow);
+    free(Urow);
+    free(Ulev);
+    free(Ln);
+    free(Un);
+    free(lev);
+    free(buf);
+    free(pos);
+    return M;
+}
+
+/* pc-iluk.cxx:347-409: in-place IKJ ILU(0) on a sorted local block.
+ * Multipliers use the stored reciprocal pivot (diag[] holds 1/pivot). */
+static void ilu0_factor(int n, const int *Ap, const int *C, double *Ax)
+{
+    double *wk = (double *)calloc((size_t)n, sizeof(double));
+    double *dinv = (double *)malloc(sizeof(double) * (size_t)n);
+    double d0 = Ax[Ap[0]];
+    if (fabs(d0) < ZERO_DIAG_TOL) d0 = d0 > 0 ? ZERO_DIAG_VALUE : -ZERO_DIAG_VALUE;
+    dinv[0] = 1. / d0;
+    for (int i = 1; i < n; i++) {
+        int end = Ap[i + 1], k;
+        for (k = Ap[i]; k < end && C[k] < i; k++) {
+            int r = C[k];
+            for (int q = Ap[r]; q < Ap[r + 1]; q++) wk[C[q]] = Ax[q];
+            double aik = Ax[k] = Ax[k] * dinv[r];
+            for (int j = k + 1; j < end; j++)
+                if (wk[C[j]] != 0.) Ax[j] = Ax[j] - aik * wk[C[j]];
+            for (int q = Ap[r]; q < Ap[r + 1]; q++) wk[C[q]] = 0;
+        }
+        double d = ZERO_DIAG_VALUE;
+        if (k < end && C[k] == i) {
+            if (fabs(Ax[k]) < ZERO_DIAG_TOL) Ax[k] = ZERO_DIAG_VALUE;
+            d = Ax[k];
+        }
+        dinv[i] = 1. / d;
+    }
+    free(wk);
+    free(dinv);
+}
+
+/* pc-iluk.cxx:501-532 / pc-ilut.cxx:378-405: split a factored row-set into
+ * L (strict lower + unit diagonal LAST) and U (pivot FIRST + upper). */
+static void split_lu(const csr_t *F, csr_t *L, csr_t *U)
+{
+    int n = F->nrows;
+    long nl = 0, nu = 0;
+    for (int i = 0; i < n; i++)
+        for (int k = F->Ap[i]; k < F->Ap[i + 1]; k++) {
+            if (F->Aj[k] <= i) nl++;
+            if (F->Aj[k] >= i) nu++;
+        }
+    *L = csr_alloc(n, n, (int)nl);
+    *U = csr_alloc(n, n, (int)nu);
+    int ol = 0, ou = 0;
+    L->Ap[0] = U->Ap[0] = 0;
+    for (int i = 0; i < n; i++) {
+        for (int k = F->Ap[i]; k < F->Ap[i + 1]; k++) {
+            int c = F->Aj[k];
+            if (c < i) {
+                L->Aj[ol] = c;
+                L->Ax[ol++] = F->Ax[k];
+            } else if (c == i) {
+                L->Aj[ol] = c;
+                L->Ax[ol++] = 1;
+                U->Aj[ou] = c;
+                U->Ax[ou++] = F->Ax[k];
+            } else {
+                U->Aj[ou] = c;
+                U->Ax[ou++] = F->Ax[k];
+            }
+        }
+        L->Ap[i + 1] = ol;
+        U->Ap[i + 1] = ou;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* ILUT (pc-ilut.cxx)                                                       */
+/* ------------------------------------------------------------------------ */
+
+/* pc-ilut.cxx:7-49: partial quicksort by |a|; the ncut largest end up first */
+static void qsplit(double *a, int *ind, int n, int ncut)
+{
+    int first = 0, last = n - 1;
+    if (ncut < first || ncut >= last) return;
+    for (;;) {
+        int mid = first;
+        double key = fabs(a[mid]);
+        for (int j = first + 1; j <= last; j++) {
+            if (fabs(a[j]) > key) {
+                mid++;
+                double t = a[mid];
+                a[mid] = a[j];
+                a[j] = t;
+                int ti = ind[mid];
+                ind[mid] = ind[j];
+                ind[j] = ti;
+            }
+        }
+        double t = a[mid];
+        a[mid] = a[first];
+        a[first] = t;
+        int ti = ind[mid];
+        ind[mid] = ind[first];
+        ind[first] = ti;
+        if (mid == ncut) return;
+        if (mid > ncut) last = mid - 1;
+        else first = mid + 1;
+    }
+}
+
+/* pc-ilut.cxx:51-286: row-wise ILUT(tol, p) of one local block. */
+static csr_t ilut_factor(const csr_t *A, double tol, int p)
+{
+    int n = A->nrows;
+    const int *Ap = A->Ap, *C = A->Aj;
+    const double *Ax = A->Ax;
+    long cap = 8L * n + A->nnz + 16;
+    csr_t M = csr_alloc(n, n, 0);
+    M.Aj = (int *)realloc(M.Aj, sizeof(int) * (size_t)cap);
+    M.Ax = (double *)realloc(M.Ax, sizeof(double) * (size_t)cap);
+    double *w = (double *)malloc(sizeof(double) * (size_t)n);
+    double *diag = (double *)malloc(sizeof(double) * (size_t)n);
+    int *jr = (int *)malloc(sizeof(int) * (size_t)n);
+    int *jw = (int *)malloc(sizeof(int) * (size_t)n);
+
+    /* row 0 is copied unchanged (pc-ilut.cxx:89-96) */
+    long off = 0;
+    M.Ap[0] = 0;
+    for (int k = Ap[0]; k < Ap[1]; k++, off++) {
+        M.Ax[off] = Ax[k];
+        M.Aj[off] = C[k];
+    }
+    M.Ap[1] = (int)off;
+    diag[0] = Ax[Ap[0]];
+    if (fabs(diag[0]) < ZERO_DIAG_TOL) diag[0] = diag[0] > 0 ? ZERO_DIAG_VALUE : -ZERO_DIAG_VALUE;
+    for (int i = 0; i < n; i++) jr[i] = -1;
+
+    for (int i = 1; i < n; i++) {
+        int end = Ap[i + 1], nl = 0, nu = 0;
+        double norm = 0.0;
+        for (int k = Ap[i]; k < end; k++) norm += fabs(Ax[k]);
+        norm /= (double)(end - Ap[i]);
+        double rel = tol * norm;
+
+        jw[i] = i;
+        w[i] = 0.0;
+        jr[i] = i;
+        for (int k = Ap[i]; k < end; k++) {
+            int c = C[k];
+            if (c < i) {
+                jr[c] = nl;
+                jw[nl] = c;
+                w[nl] = Ax[k];
+                nl++;
+            } else if (c == i) {
+                w[i] = Ax[k];
+            } else {
+                nu++;
+                jr[c] = i + nu;
+                jw[i + nu] = c;
+                w[i + nu] = Ax[k];
+            }
+        }
+
+        for (int j = 0; j < nl; j++) {
+            int jrow = jw[j], at = j;
+            for (int k = j + 1; k < nl; k++)
+                if (jw[k] < jrow) {
+                    jrow = jw[k];
+                    at = k;
+                }
+            if (at != j) {
+                int c = jw[j];
+                jw[j] = jw[at];
+                jw[at] = c;
+                jr[jrow] = j;
+                jr[c] = at;
+                double t = w[j];
+                w[j] = w[at];
+                w[at] = t;
+            }
+            jr[jrow] = -1;
+            double aik = w[j] = w[j] / diag[jrow];
+            for (int k = M.Ap[jrow]; k < M.Ap[jrow + 1]; k++) {
+                int c = M.Aj[k];
+                if (c <= jrow) continue;
+                int q = jr[c];
+                double mx = -aik * M.Ax[k];
+                if (q == -1 && fabs(mx) < rel) continue;
+                if (c < i) {
+                    if (q == -1) {
+                        jw[nl] = c;
+                        jr[c] = nl;
+                        w[nl] = mx;
+                        nl++;
+                    } else {
+                        w[q] += mx;
+                    }
+                } else {
+                    if (q == -1) {
+                        nu++;
+                        jw[i + nu] = c;
+                        jr[c] = i + nu;
+                        w[i + nu] = mx;
+                    } else {
+                        w[q] += mx;
+                    }
+                }
+            }
+        }
+
+        if (cap - off < (long)n + 2) {
+            cap += 2L * n + 16;
+            M.Aj = (int *)realloc(M.Aj, sizeof(int) * (size_t)cap);
+            M.Ax = (double *)realloc(M.Ax, sizeof(double) * (size_t)cap);
+        }
+
+        diag[i] = w[i];
+        jr[i] = -1;
+        for (int j = 0; j < nl; j++) jr[jw[j]] = -1;
+        for (int j = 0; j < nu; j++) jr[jw[i + j + 1]] = -1;
+        if (fabs(diag[i]) < ZERO_DIAG_TOL) diag[i] = diag[i] > 0 ? ZERO_DIAG_VALUE : -ZERO_DIAG_VALUE;
+
+        int len = nl < p ? nl : p;
+        qsplit(w, jw, nl, len);
+        for (int k = 0; k < len; k++, off++) {
+            M.Ax[off] = w[k];
+            M.Aj[off] = jw[k];
+        }
+        M.Ax[off] = diag[i];
+        M.Aj[off] = i;
+        off++;
+        len = nu < p ? nu : p;
+        qsplit(w + i + 1, jw + i + 1, nu, len);
+        for (int k = 0; k < len; k++, off++) {
+            M.Ax[off] = w[i + 1 + k];
+            M.Aj[off] = jw[i + 1 + k];
+        }
+        M.Ap[i + 1] = (int)off;
+    }
+    M.nnz = (int)off;
+    free(w);
+    free(diag);
+    free(jr);
+    free(jw);
+    return M;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Preconditioner assembly: pc-iluk.cxx:411-581, pc-ilut.cxx:288-456         */
+/* ------------------------------------------------------------------------ */
+
+typedef struct {
+    csr_t L, U;
+} ilu_t;
+
+/* Extract rows [s,e) of F as a local CSR (columns shifted by -s). */
+static csr_t local_block(const csr_t *F, int s, int e)
+{
+    int nb = e - s, base = F->Ap[s];
+    csr_t B = csr_alloc(nb, nb, F->Ap[e] - base);
+    for (int i = 0; i <= nb; i++) B.Ap[i] = F->Ap[s + i] - base;
+    for (int k = 0; k < B.nnz; k++) {
+        B.Aj[k] = F->Aj[base + k] - s;
+        B.Ax[k] = F->Ax[base + k];
+    }
+    return B;
+}
+
+/* kind 0: ILUK(level), kind 1: ILUT(tol, p).  blk = block-Jacobi block size
+ * (the reference API always passes n: pc-iluk.cxx:574, pc-ilut.cxx:449). */
+EXPORT void *orc_ilu_create(int kind, int n, const int *Ap, const int *Aj, const double *Ax,
+                            int level, double tol, int p, int blk)
+{
+    csr_t A = csr_copy(n, n, Ap, Aj, Ax);
+    sort_columns(&A); /* lssp.cxx:173 (solver assemble sorts its copy) */
+    /* pc-ilut.cxx:436-438: p <= 0 becomes ceil(nnz/n) of the solver's matrix */
+    if (kind == 1 && p <= 0) p = (A.nnz + n - 1) / n;
+    csr_t Az = adjust_zero_diag(&A, ZERO_DIAG_TOL);
+    csr_free(&A);
+    if (blk <= 0 || blk > n) blk = n;
+    csr_t M;
+    if (kind == 0 && level > 0) {
+        csr_t S = iluk_symbolic(&Az, level);
+        M = block_diag(&S, blk);
+        csr_free(&S);
+    } else {
+        M = block_diag(&Az, blk);
+    }
+    csr_free(&Az);
+
+    /* factor every block locally, re-globalise the columns */
+    csr_t F = csr_alloc(n, n, 0);
+    long cap = kind == 0 ? M.nnz : (long)M.nnz + 8L * n, o = 0;
+    F.Aj = (int *)realloc(F.Aj, sizeof(int) * (size_t)(cap + 1));
+    F.Ax = (double *)realloc(F.Ax, sizeof(double) * (size_t)(cap + 1));
+    F.Ap[0] = 0;
+    for (int s = 0; s < n; s += blk) {
+        int e = s + blk < n ? s + blk : n;
+        csr_t B = local_block(&M, s, e), T;
+        if (kind == 0) {
+            ilu0_factor(B.nrows, B.Ap, B.Aj, B.Ax);
+            T = B;
+        } else {
+            T = ilut_factor(&B, tol, p);
+            csr_free(&B);
+        }
+        if (o + T.nnz > cap) {
+            cap = o + T.nnz + 2L * n;
+            F.Aj = (int *)realloc(F.Aj, sizeof(int) * (size_t)cap);
+            F.Ax = (double *)realloc(F.Ax, sizeof(double) * (size_t)cap);
+        }
+        for (int i = 0; i < T.nrows; i++) {
+            for (int k = T.Ap[i]; k < T.Ap[i + 1]; k++, o++) {
+                F.Aj[o] = T.Aj[k] + s;
+                F.Ax[o] = T.Ax[k];
+            }
+            F.Ap[s + i + 1] = (int)o;
+        }
+        csr_free(&T);
+    }
+    F.nnz = (int)o;
+    csr_free(&M);
+
+    ilu_t *h = (ilu_t *)malloc(sizeof(ilu_t));
+    split_lu(&F, &h->L, &h->U);
+    csr_free(&F);
+    return h;
+}
+
+EXPORT void orc_ilu_sizes(void *hp, int *nnzL, int *nnzU)
+{
+    ilu_t *h = (ilu_t *)hp;
+    *nnzL = h->L.Ap[h->L.nrows];
+    *nnzU = h->U.Ap[h->U.nrows];
+}
+
+EXPORT void orc_ilu_get(void *hp, int *Lp, int *Lj, double *Lx, int *Up, int *Uj, double *Ux)
+{
+    ilu_t *h = (ilu_t *)hp;
+    int n = h->L.nrows;
+    memcpy(Lp, h->L.Ap, sizeof(int) * (size_t)(n + 1));
+    memcpy(Up, h->U.Ap, sizeof(int) * (size_t)(n + 1));
+    memcpy(Lj, h->L.Aj, sizeof(int) * (size_t)h->L.Ap[n]);
+    memcpy(Lx, h->L.Ax, sizeof(double) * (size_t)h->L.Ap[n]);
+    memcpy(Uj, h->U.Aj, sizeof(int) * (size_t)h->U.Ap[n]);
+    memcpy(Ux, h->U.Ax, sizeof(double) * (size_t)h->U.Ap[n]);
+}
+
+EXPORT void orc_ilu_free(void *hp)
+{
+    ilu_t *h = (ilu_t *)hp;
+    csr_free(&h->L);
+    csr_free(&h->U);
+    free(h);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Krylov drivers                                                           */
+/* ------------------------------------------------------------------------ */
+
+enum { SOLVER_GMRES = 0, SOLVER_BICGSTAB = 4, SOLVER_CG = 7 }; /* type-defs.h:157-178 */
+
+typedef struct {
+    const csr_t *A;
+    const csr_t *L, *U; /* NULL => PC_NON (pc.cxx:67-70) */
+    double *cache;
+    red_t red;
+    double *trace;
+    int cap, len;
+} ctx_t;
+
+static void trace_push(ctx_t *c, double v)
+{
+    if (c->trace && c->len < c->cap) c->trace[c->len] = v;
+    c->len++;
+}
+
+static double tdot(ctx_t *c, const double *x, const double *y)
+{
+    double v = dot_red(&c->red, x, y, c->A->nrows);
+    trace_push(c, v);
+    return v;
+}
+
+static double tnorm(ctx_t *c, const double *x)
+{
+    double v = sqrt(dot_red(&c->red, x, x, c->A->nrows));
+    trace_push(c, v);
+    return v;
+}
+
+static void pc_apply(ctx_t *c, double *x, const double *rhs)
+{
+    int n = c->A->nrows;
+    if (!c->L) {
+        memcpy(x, rhs, sizeof(double) * (size_t)n);
+        return;
+    }
+    tri_lower(c->L, c->cache, rhs);
+    tri_upper(c->U, x, c->cache);
+}
+
+/* solver-bicgstab.cxx:10-175 */
+static int bicgstab(ctx_t *c, double *x, const double *b, double tol_rel, double tol_abs,
+                    double tol_rb, int maxit, double *res_out)
+{
+    const csr_t *A = c->A;
+    int n = A->nrows, it;
+    if (maxit <= 0) maxit = DEF_MAXIT;
+    if (tol_abs < 0) tol_abs = DEF_TOL;
+    if (tol_rel < 0) tol_rel = DEF_TOL;
+    size_t bytes = sizeof(double) * (size_t)n;
+    double *r = malloc(bytes), *rh = malloc(bytes), *p = malloc(bytes), *ph = malloc(bytes);
+    double *s = malloc(bytes), *sh = malloc(bytes), *t = malloc(bytes), *v = malloc(bytes);
+    double rho0 = 0, rho1 = 0, alpha = 0, beta = 0, omega = 0, res, tol, err_rel;
+
+    mv_amxpbyz(-1, A, x, 1, b, r);
+    for (int i = 0; i < n; i++) {
+        rh[i] = r[i];
+        sh[i] = ph[i] = 0.;
+    }
+    double bnorm = tnorm(c, b);
+    tol_rb *= bnorm;
+    res = err_rel = tnorm(c, r);
+    if (res <= tol_abs) {
+        it = 0;
+        goto done;
+    }
+    tol = res * tol_rel;
+    if (tol < tol_abs) tol = tol_abs;
+    if (tol < tol_rb) tol = tol_rb;
+
+    for (it = 0; it < maxit; it++) {
+        rho1 = tdot(c, r, rh);
+        if (rho1 == 0) break;
+        if (it == 0) {
+            for (int i = 0; i < n; i++) p[i] = r[i];
+        } else {
+            beta = (rho1 * alpha) / (rho0 * omega);
+            for (int i = 0; i < n; i++) p[i] = r[i] + beta * (p[i] - omega * v[i]);
+        }
+        rho0 = rho1;
+        pc_apply(c, ph, p);
+        mv_amxpbyz(1, A, ph, 0, p, v);
+        alpha = rho1 / tdot(c, rh, v);
+        for (int i = 0; i < n; i++) s[i] = r[i] - alpha * v[i];
+        if (tnorm(c, s) <= BREAKDOWN) {
+            (void)tnorm(c, s); /* the reference prints it (solver-bicgstab.cxx:118) */
+            for (int i = 0; i < n; i++) x[i] = x[i] + alpha * ph[i];
+            mv_amxpbyz(-1, A, x, 1, b, r);
+            res = tnorm(c, r);
+            break;
+        }
+        pc_apply(c, sh, s);
+        mv_amxpbyz(1, A, sh, 0, p, t);
+        omega = tdot(c, t, s) / tdot(c, t, t);
+        for (int i = 0; i < n; i++) {
+            x[i] = x[i] + alpha * ph[i] + omega * sh[i];
+            r[i] = s[i] - omega * t[i];
+        }
+        res = tnorm(c, r);
+        if (res <= tol) break;
+    }
+    if (it < maxit) it += 1;
+done:
+    *res_out = res;
+    free(r); free(rh); free(p); free(ph); free(s); free(sh); free(t); free(v);
+    return it;
+}
+
+/* solver-cg.cxx:8-136 */
+static int cg(ctx_t *c, double *x, const double *b, double tol_rel, double tol_abs,
+              double tol_rb, int maxit, double *res_out)
+{
+    const csr_t *A = c->A;
+    int n = A->nrows, it;
+    if (maxit <= 0) maxit = DEF_MAXIT;
+    if (tol_abs < 0) tol_abs = DEF_TOL;
+    if (tol_rel < 0) tol_rel = DEF_TOL;
+    size_t bytes = sizeof(double) * (size_t)n;
+    double *z = malloc(bytes), *r = malloc(bytes), *p = malloc(bytes), *q = malloc(bytes);
+    double rho0 = 0, rho1, beta, res, tol;
+
+    double bnorm = tnorm(c, b);
+    tol_rb *= bnorm;
+    mv_amxpbyz(-1, A, x, 1, b, r);
+    res = tnorm(c, r);
+    if (res <= tol_abs) {
+        it = 0;
+        goto done;
+    }
+    tol = tol_rel * res;
+    if (tol < tol_abs) tol = tol_abs;
+    if (tol < tol_rb) tol = tol_rb;
+    for (int i = 0; i < n; i++) z[i] = 0;
+    for (it = 0; it < maxit; it++) {
+        pc_apply(c, z, r);
+        rho1 = tdot(c, z, r);
+        if (it == 0) {
+            for (int i = 0; i < n; i++) p[i] = z[i];
+        } else {
+            beta = rho1 / rho0;
+            for (int i = 0; i < n; i++) p[i] = z[i] + beta * p[i];
+        }
+        mv_mxy(A, p, q);
+        double alpha = tdot(c, q, p);
+        alpha = rho1 / alpha;
+        rho0 = rho1;
+        for (int i = 0; i < n; i++) {
+            x[i] = x[i] + alpha * p[i];
+            r[i] = r[i] - alpha * q[i];
+        }
+        res = tnorm(c, r);
+        if (res <= tol) break;
+    }
+    if (it < maxit) it += 1;
+done:
+    *res_out = res;
+    free(z); free(r); free(p); free(q);
+    return it;
+}
+
+/* solver-gmres.cxx:12-255: left-preconditioned GMRES(m), MGS Arnoldi,
+ * Givens rotations on the host, true residual at every restart. */
+static int gmres(ctx_t *c, double *x, const double *b, double tol_rel, double tol_abs,
+                 double tol_rb, int maxit, int m, double *res_out)
+{
+    const csr_t *A = c->A;
+    int n = A->nrows, inner = 0;
+    if (m < 0) m = DEF_RESTART;
+    if (maxit <= 0) maxit = DEF_MAXIT;
+    if (tol_abs < 0) tol_abs = DEF_TOL;
+    if (tol_rel < 0) tol_rel = DEF_TOL;
+    if (tol_rb < 0) tol_rb = DEF_TOL;
+    size_t bytes = sizeof(double) * (size_t)n;
+    double *wj = malloc(bytes), *rg = malloc(bytes);
+    double **v = malloc(sizeof(double *) * (size_t)m);
+    for (int i = 0; i < m; i++) v[i] = malloc(bytes);
+    double *gg = malloc(sizeof(double) * (size_t)(m + 1)), *ym = malloc(sizeof(double) * (size_t)m);
+    double *H = malloc(sizeof(double) * (size_t)(m + 1) * (size_t)m);
+    double *cs = malloc(sizeof(double) * (size_t)m), *sn = malloc(sizeof(double) * (size_t)m);
+#define HG(r, col) H[(size_t)(r) * (size_t)m + (size_t)(col)]
+    double tol = 0, err_rel = 0, beta, rtol, gstol = 0.;
+
+    double bnorm = tnorm(c, b);
+    tol_rb *= bnorm;
+    mv_amxpbyz(-1, A, x, 1, b, rg);
+    beta = tnorm(c, rg);
+    if (beta <= tol_abs) goto done;
+    err_rel = beta;
+    tol = tol_rel * err_rel;
+    if (tol < tol_abs) tol = tol_abs;
+    if (tol < tol_rb) tol = tol_rb;
+    rtol = tol / beta;
+
+    while (inner < maxit) {
+        int i, kk;
+        double gs_norm = 0.;
+        pc_apply(c, v[0], rg);
+        beta = tnorm(c, v[0]);
+        gg[0] = beta;
+        for (kk = 1; kk <= m; kk++) gg[kk] = 0;
+        if (inner == 0) gstol = rtol * beta * 0.5;
+        for (size_t q = 0; q < (size_t)(m + 1) * (size_t)m; q++) H[q] = 0;
+        for (int q = 0; q < n; q++) v[0][q] /= beta;
+
+        for (i = 0; i < m; i++) {
+            double h;
+            inner++;
+            mv_mxy(A, v[i], rg);
+            pc_apply(c, wj, rg);
+            for (int j = 0; j <= i; j++) {
+                h = tdot(c, wj, v[j]);
+                for (int q = 0; q < n; q++) wj[q] = wj[q] * 1 + v[j][q] * (-h); /* vector.cxx:98-107 */
+                HG(j, i) = h;
+            }
+            h = tnorm(c, wj);
+            HG(i + 1, i) = h;
+            if (fabs(h) <= BREAKDOWN) {
+                i--;
+                break;
+            } else if (i + 1 < m) {
+                double a = 1 / h;
+                for (int q = 0; q < n; q++) v[i + 1][q] = wj[q] * a; /* vector.cxx:86-95 */
+            }
+            for (int j = 0; j < i; j++) {
+                double h1 = cs[j] * HG(j, i) + sn[j] * HG(j + 1, i);
+                double h2 = -sn[j] * HG(j, i) + cs[j] * HG(j + 1, i);
+                HG(j, i) = h1;
+                HG(j + 1, i) = h2;
+            }
+            double gma = sqrt(HG(i, i) * HG(i, i) + HG(i + 1, i) * HG(i + 1, i));
+            if (fabs(gma) == 0.) gma = 1e-20;
+            cs[i] = HG(i, i) / gma;
+            sn[i] = HG(i + 1, i) / gma;
+            gg[i + 1] = -sn[i] * gg[i];
+            gg[i] = cs[i] * gg[i];
+            HG(i, i) = cs[i] * HG(i, i) + sn[i] * HG(i + 1, i);
+            gs_norm = fabs(gg[i + 1]);
+            if (gs_norm <= gstol) break;
+        }
+        /* i == m after a full cycle; otherwise the last processed column */
+        kk = (i == m) ? m : i + 1;
+        for (i = kk - 1; i >= 0; i--) {
+            ym[i] = gg[i] / HG(i, i);
+            for (int j = 0; j < i; j++) gg[j] = gg[j] - ym[i] * HG(j, i);
+        }
+        for (int q = 0; q < n; q++) {
+            double acc = 0;
+            for (i = 0; i < kk; i++) acc += v[i][q] * ym[i];
+            x[q] += acc;
+        }
+        mv_amxpbyz(-1, A, x, 1, b, rg);
+        beta = tnorm(c, rg);
+        if (beta <= tol) break;
+        gstol = rtol * gs_norm / (beta / err_rel) * 0.5;
+    }
+#undef HG
+done:
+    *res_out = beta;
+    free(wj); free(rg);
+    for (int i = 0; i < m; i++) free(v[i]);
+    free(v); free(gg); free(ym); free(H); free(cs); free(sn);
+    return inner;
+}
+
+/* Solve A x = b (x holds x0 on entry).  L/U == NULL => PC_NON.
+ * trace receives every dot/norm the driver computes, in call order (the same
+ * sequence tests/golden records from the reference). */
+EXPORT int orc_solve(int solver, int n, const int *Ap, const int *Aj, const double *Ax,
+                     const int *Lp, const int *Lj, const double *Lx,
+                     const int *Up, const int *Uj, const double *Ux,
+                     double *x, const double *b, double tol_rel, double tol_abs, double tol_rb,
+                     int maxit, int restart, int red_mode, int nranks,
+                     double *trace, int trace_cap, int *trace_len, double *residual)
+{
+    csr_t A = csr_copy(n, n, Ap, Aj, Ax);
+    sort_columns(&A);
+    csr_t L = {n, n, 0, (int *)Lp, (int *)Lj, (double *)Lx};
+    csr_t U = {n, n, 0, (int *)Up, (int *)Uj, (double *)Ux};
+    ctx_t c;
+    memset(&c, 0, sizeof(c));
+    c.A = &A;
+    c.L = Lp ? &L : NULL;
+    c.U = Up ? &U : NULL;
+    c.cache = (double *)malloc(sizeof(double) * (size_t)n);
+    c.red.mode = red_mode;
+    c.red.nranks = nranks;
+    c.trace = trace;
+    c.cap = trace_cap;
+    int it;
+    double res = 0;
+    switch (solver) {
+    case SOLVER_BICGSTAB: it = bicgstab(&c, x, b, tol_rel, tol_abs, tol_rb, maxit, &res); break;
+    case SOLVER_CG: it = cg(&c, x, b, tol_rel, tol_abs, tol_rb, maxit, &res); break;
+    case SOLVER_GMRES: it = gmres(&c, x, b, tol_rel, tol_abs, tol_rb, maxit, restart, &res); break;
+    default: it = -1;
+    }
+    if (trace_len) *trace_len = c.len;
+    if (residual) *residual = res;
+    free(c.cache);
+    csr_free(&A);
+    return it;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Synthetic inputs                                                         */
+/* ------------------------------------------------------------------------ */
+
+/* example/exam.cxx:4-59 (5-pt, 4/-1) and its 7-pt analogue (6/-1), natural
+ * ordering r = (k*N + j)*N + i, columns ascending. */
+EXPORT long orc_poisson_nnz(int dim, int N)
+{
+    long n = N;
+    return dim == 2 ? 5 * n * n - 4 * n : 7 * n * n * n - 6 * n * n;
+}
+
+EXPORT void orc_poisson(int dim, int N, int *Ap, int *Aj, double *Ax)
+{
+    long o = 0, r = 0;
+    Ap[0] = 0;
+    if (dim == 2) {
+        for (int i = 0; i < N; i++)
+            for (int j = 0; j < N; j++, r++) {
+                long idx = (long)N * i + j;
+                if (i > 0) { Aj[o] = (int)(idx - N); Ax[o++] = -1; }
+                if (j > 0) { Aj[o] = (int)(idx - 1); Ax[o++] = -1; }
+                Aj[o] = (int)idx; Ax[o++] = 4;
+                if (j < N - 1) { Aj[o] = (int)(idx + 1); Ax[o++] = -1; }
+                if (i < N - 1) { Aj[o] = (int)(idx + N); Ax[o++] = -1; }
+                Ap[r + 1] = (int)o;
+            }
+        return;
+    }
+    long N2 = (long)N * N;
+    for (int k = 0; k < N; k++)
+        for (int j = 0; j < N; j++)
+            for (int i = 0; i < N; i++, r++) {
+                if (k > 0) { Aj[o] = (int)(r - N2); Ax[o++] = -1; }
+                if (j > 0) { Aj[o] = (int)(r - N); Ax[o++] = -1; }
+                if (i > 0) { Aj[o] = (int)(r - 1); Ax[o++] = -1; }
+                Aj[o] = (int)r; Ax[o++] = 6;
+                if (i < N - 1) { Aj[o] = (int)(r + 1); Ax[o++] = -1; }
+                if (j < N - 1) { Aj[o] = (int)(r + N); Ax[o++] = -1; }
+                if (k < N - 1) { Aj[o] = (int)(r + N2); Ax[o++] = -1; }
+                Ap[r + 1] = (int)o;
+            }
+}
