@@ -230,3 +230,39 @@ def ref_solve(solver, A: CSR, b, pc=PC_NON, level=0, ilut_tol=1e-3, ilut_p=-1, x
                          maxit, restart, _ptr(tr), trace_cap, ctypes.byref(tl), ctypes.byref(res),
                          ctypes.byref(ts), ctypes.byref(tv))
     return SolveResult(it, res.value, x, tr[: min(tl.value, trace_cap)].copy(), ts.value, tv.value)
+
+
+def ref_bj(A: CSR, nblk: int):
+    """Block-Jacobi ILU(0) factors composed from the reference's public API."""
+    R = ref()
+    R.ref_bj_create.restype = _vp
+    R.ref_bj_create.argtypes = [_ci, _vp, _vp, _vp, _ci]
+    R.ref_bj_free.argtypes = [_vp]
+    h = R.ref_bj_create(A.n, _ptr(A.Ap), _ptr(A.Aj), _ptr(A.Ax), nblk)
+    try:
+        return _ilu_fetch(R.ref_ilu_sizes, R.ref_ilu_get, h, A.n)
+    finally:
+        R.ref_bj_free(h)
+
+
+def ref_solve_bj(solver, A: CSR, b, nblk: int, x0=None, rtol=1e-7, atol=1e-7, rbtol=1e-7,
+                 maxit=1000, restart=30, trace_cap=200000) -> SolveResult:
+    """Solve with block-Jacobi ILU(0) plugged in through LSSP_PC_USER."""
+    R = ref()
+    R.ref_bj_create.restype = _vp
+    R.ref_bj_create.argtypes = [_ci, _vp, _vp, _vp, _ci]
+    R.ref_bj_free.argtypes = [_vp]
+    R.ref_solve_bj.restype = _ci
+    R.ref_solve_bj.argtypes = [_vp, _ci, _ci, _vp, _vp, _vp, _vp, _vp, _cd, _cd, _cd, _ci, _ci,
+                               _vp, _ci, _vp, _vp]
+    h = R.ref_bj_create(A.n, _ptr(A.Ap), _ptr(A.Aj), _ptr(A.Ax), nblk)
+    try:
+        x = np.zeros(A.n) if x0 is None else np.array(x0, dtype=np.float64)
+        tr = np.zeros(trace_cap)
+        tl, res = ctypes.c_int(), ctypes.c_double()
+        it = R.ref_solve_bj(h, solver, A.n, _ptr(A.Ap), _ptr(A.Aj), _ptr(A.Ax), _ptr(x),
+                            _ptr(np.ascontiguousarray(b, dtype=np.float64)), rtol, atol, rbtol, maxit,
+                            restart, _ptr(tr), trace_cap, ctypes.byref(tl), ctypes.byref(res))
+        return SolveResult(it, res.value, x, tr[: min(tl.value, trace_cap)].copy())
+    finally:
+        R.ref_bj_free(h)

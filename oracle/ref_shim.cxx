@@ -195,3 +195,124 @@ int ref_solve(int solver, int pc_type, int level, double ilut_tol, int ilut_p, i
 double ref_time(void) { return lssp_get_time(); }
 
 } // extern "C"
+
+// ---------------------------------------------------------------------------
+// Block-Jacobi ILU(0) composed from the public API: each diagonal block is
+// factored by lssp_solver_assemble with ILUK level 0 and the factors are
+// stitched with a column shift.  For level 0 this equals the reference's own
+// blk_size path (pc-iluk.cxx:411-552 with blk_size < n): adjust_zero_diag
+// only inserts in-block diagonals and get_block_diag keeps exactly the block.
+// Solves use it through the reference's PC plug-in (LSSP_PC_USER, pc.cxx:219)
+// with pc.solve = lssp_pc_ilu_solve.
+static lssp_mat_csr g_bjL, g_bjU;
+
+static void bj_assemble(LSSP_PC &pc, LSSP_SOLVER s)
+{
+    (void)s;
+    pc.L = g_bjL;
+    pc.U = g_bjU;
+    pc.cache = lssp_malloc<double>(pc.L.num_rows);
+    pc.solve = lssp_pc_ilu_solve;
+    pc.destroy = NULL;
+}
+
+static void block_csr(int n, const int *Ap, const int *Aj, const double *Ax, int s, int e,
+                      std::vector<int> &bp, std::vector<int> &bj, std::vector<double> &bx)
+{
+    bp.assign(1, 0);
+    bj.clear();
+    bx.clear();
+    for (int i = s; i < e; i++) {
+        for (int k = Ap[i]; k < Ap[i + 1]; k++)
+            if (Aj[k] >= s && Aj[k] < e) {
+                bj.push_back(Aj[k] - s);
+                bx.push_back(Ax[k]);
+            }
+        bp.push_back((int)bj.size());
+    }
+    (void)n;
+}
+
+extern "C" void *ref_bj_create(int n, const int *Ap, const int *Aj, const double *Ax, int nblk)
+{
+    int blk = (n + nblk - 1) / nblk;
+    std::vector<int> Lp(1, 0), Lj, Up(1, 0), Uj;
+    std::vector<double> Lx, Ux;
+    for (int s = 0; s < n; s += blk) {
+        int e = s + blk < n ? s + blk : n;
+        std::vector<int> bp, bj;
+        std::vector<double> bx;
+        block_csr(n, Ap, Aj, Ax, s, e, bp, bj, bx);
+        ref_pc *h = (ref_pc *)ref_ilu_create(0, e - s, bp.data(), bj.data(), bx.data(), 0, 0, 0);
+        const lssp_mat_csr &L = h->pc.L, &U = h->pc.U;
+        for (int i = 0; i < e - s; i++) {
+            for (int k = L.Ap[i]; k < L.Ap[i + 1]; k++) {
+                Lj.push_back(L.Aj[k] + s);
+                Lx.push_back(L.Ax[k]);
+            }
+            for (int k = U.Ap[i]; k < U.Ap[i + 1]; k++) {
+                Uj.push_back(U.Aj[k] + s);
+                Ux.push_back(U.Ax[k]);
+            }
+            Lp.push_back((int)Lj.size());
+            Up.push_back((int)Uj.size());
+        }
+        ref_ilu_free(h);
+    }
+    ref_pc *h = new ref_pc();
+    h->pc.L.num_rows = h->pc.L.num_cols = n;
+    h->pc.U.num_rows = h->pc.U.num_cols = n;
+    h->pc.L.num_nnzs = (int)Lj.size();
+    h->pc.U.num_nnzs = (int)Uj.size();
+    h->pc.L.Ap = lssp_copy_on<int>(Lp.data(), n + 1);
+    h->pc.L.Aj = lssp_copy_on<int>(Lj.data(), (int)Lj.size());
+    h->pc.L.Ax = lssp_copy_on<double>(Lx.data(), (int)Lx.size());
+    h->pc.U.Ap = lssp_copy_on<int>(Up.data(), n + 1);
+    h->pc.U.Aj = lssp_copy_on<int>(Uj.data(), (int)Uj.size());
+    h->pc.U.Ax = lssp_copy_on<double>(Ux.data(), (int)Ux.size());
+    h->pc.cache = lssp_malloc<double>(n);
+    h->pc.solve = lssp_pc_ilu_solve;
+    return h;
+}
+
+extern "C" void ref_bj_free(void *hp)
+{
+    ref_pc *h = (ref_pc *)hp;
+    lssp_mat_destroy(h->pc.L);
+    lssp_mat_destroy(h->pc.U);
+    lssp_free(h->pc.cache);
+    delete h;
+}
+
+// Solve with a block-Jacobi handle from ref_bj_create, via LSSP_PC_USER.
+extern "C" int ref_solve_bj(void *hp, int solver, int n, const int *Ap, const int *Aj,
+                            const double *Ax, double *x, const double *b, double rtol, double atol,
+                            double rbtol, int maxit, int restart, double *trace, int cap,
+                            int *trace_len, double *residual)
+{
+    ref_pc *h = (ref_pc *)hp;
+    LSSP_SOLVER s;
+    LSSP_PC pc;
+    lssp_mat_csr A = view(n, Ap, Aj, Ax);
+    lssp_verbosity = 0;
+    lssp_solver_create(s, (LSSP_SOLVER_TYPE)solver, pc, LSSP_PC_USER);
+    g_bjL = h->pc.L;
+    g_bjU = h->pc.U;
+    pc.assemble = bj_assemble;
+    lssp_solver_set_rtol(s, rtol);
+    lssp_solver_set_atol(s, atol);
+    lssp_solver_set_rbtol(s, rbtol);
+    lssp_solver_set_maxit(s, maxit);
+    if (restart > 0) lssp_solver_set_restart(s, restart);
+    lssp_solver_assemble(s, A, vview(n, x), vview(n, b), pc);
+    g_trace.clear();
+    g_trace_on = true;
+    int it = lssp_solver_solve(s, pc);
+    g_trace_on = false;
+    if (trace_len) *trace_len = (int)g_trace.size();
+    for (int i = 0; i < (int)g_trace.size() && i < cap; i++) trace[i] = g_trace[i];
+    if (residual) *residual = lssp_solver_get_residual(s);
+    lssp_free(pc.cache);
+    lssp_mat_destroy(s.A);
+    return it;
+}
