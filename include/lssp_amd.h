@@ -1,0 +1,170 @@
+/*
+ * lssp_amd.h -- C-ABI of the MI355X-native LSSP Krylov hot path.
+ *
+ * Plain pointers and sizes only (no torch, no C++ types).  Device vectors are
+ * raw `double *` obtained from lssp_amd_vec_alloc; host arrays are the
+ * caller's.  Every entry point returns an int status (LSSP_AMD_OK == 0) and
+ * never exits the process; the reference-compatible C++ layer
+ * (include/lssp/lssp.h) maps a non-zero status to lssp_error(1, ...), which
+ * reproduces the reference's exit-on-fatal (utils.cxx:114-135).
+ *
+ * Each group cites the reference interface it replaces (paths relative to the
+ * huiscliu/lssp tree).  The binding a maintainer would add on the reference
+ * side is shown in INTEGRATION.md.
+ */
+#ifndef LSSP_AMD_H
+#define LSSP_AMD_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status ------------------------------------------------------------ */
+enum {
+    LSSP_AMD_OK = 0,
+    LSSP_AMD_EINVAL = 1,      /* bad argument (the reference asserts / lssp_error) */
+    LSSP_AMD_EHIP = 2,        /* HIP runtime error */
+    LSSP_AMD_ENOMEM = 3,      /* device or host allocation failed (utils.h:41-57) */
+    LSSP_AMD_ETIMEOUT = 4,    /* a sync-free trisolve wait exceeded its bound */
+    LSSP_AMD_ECOMM = 5,       /* RCCL error */
+    LSSP_AMD_EUNSUPPORTED = 6 /* solver/PC combination not on the hot path */
+};
+
+/* reduction order of every dot / norm (vector.cxx:123-139) */
+enum {
+    LSSP_AMD_REDUCE_SERIAL = 0, /* sequential sum from 0, bitwise == the reference */
+    LSSP_AMD_REDUCE_TREE = 1    /* canonical 256-chunk tree, the fast path */
+};
+
+/* LSSP_SOLVER_TYPE values of the reference (type-defs.h:157-178) */
+enum { LSSP_AMD_GMRES = 0, LSSP_AMD_BICGSTAB = 4, LSSP_AMD_CG = 7 };
+/* ILU kinds (LSSP_PC_TYPE, type-defs.h:63-101) */
+enum { LSSP_AMD_ILUK = 1, LSSP_AMD_ILUT = 2 };
+
+typedef struct lssp_amd_ctx lssp_amd_ctx; /* one device + stream + scratch */
+typedef struct lssp_amd_mat lssp_amd_mat; /* device CSR (lssp_mat_csr, type-defs.h:15-24) */
+typedef struct lssp_amd_ilu lssp_amd_ilu; /* device L/U + trisolve schedules (LSSP_PC.L/.U) */
+
+const char *lssp_amd_strerror(int status);
+int lssp_amd_version(void);
+
+/* ---- context: replaces the implicit single host thread ------------------ */
+int lssp_amd_ctx_create(int device, lssp_amd_ctx **ctx);
+int lssp_amd_ctx_destroy(lssp_amd_ctx *ctx);
+int lssp_amd_ctx_set_reduction(lssp_amd_ctx *ctx, int mode);
+int lssp_amd_ctx_sync(lssp_amd_ctx *ctx);
+/* HIP stream the context enqueues on (a hipStream_t), for timing with events */
+void *lssp_amd_ctx_stream(lssp_amd_ctx *ctx);
+
+/* ---- device vectors: lssp_vec_create/destroy/set_value_by_array/get_value
+ *      (vector.cxx:4-70) ----------------------------------------------- */
+int lssp_amd_vec_alloc(lssp_amd_ctx *ctx, long n, double **d);
+int lssp_amd_vec_free(lssp_amd_ctx *ctx, double *d);
+int lssp_amd_vec_upload(lssp_amd_ctx *ctx, double *d, const double *h, long n);
+int lssp_amd_vec_download(lssp_amd_ctx *ctx, double *h, const double *d, long n);
+
+/* ---- CSR matrix: a device copy of an lssp_mat_csr, kept in the given entry
+ *      order (SpMV sums in that order, mvops.cxx:55-58).  The solvers expect
+ *      the assembled matrix, whose columns lssp_solver_assemble sorts
+ *      (lssp.cxx:173): call lssp_amd_csr_sort_columns first, as that does. */
+int lssp_amd_csr_sort_columns(int nrows, int ncols, int *Ap, int *Aj, double *Ax); /* matrix-utils.cxx:387-481 */
+int lssp_amd_mat_upload(lssp_amd_ctx *ctx, int nrows, int ncols, int nnz, const int *Ap,
+                        const int *Aj, const double *Ax, lssp_amd_mat **A);
+int lssp_amd_mat_destroy(lssp_amd_mat *A);
+int lssp_amd_mat_info(const lssp_amd_mat *A, int *nrows, int *ncols, int *nnz);
+
+/* ---- SpMV: mvops.h:9-19 (mvops.cxx:5-150), bitwise per row -------------- */
+/* y = y*beta + alpha*A*x            (lssp_mv_amxpby,  mvops.cxx:33-39)  */
+int lssp_amd_mv_amxpby(lssp_amd_ctx *ctx, double alpha, const lssp_amd_mat *A, const double *x,
+                       double beta, double *y);
+/* z = y*beta + alpha*A*x            (lssp_mv_amxpbyz, mvops.cxx:71-78)  */
+int lssp_amd_mv_amxpbyz(lssp_amd_ctx *ctx, double alpha, const lssp_amd_mat *A, const double *x,
+                        double beta, const double *y, double *z);
+/* y = a*A*x                         (lssp_mv_amxy,    mvops.cxx:109-115) */
+int lssp_amd_mv_amxy(lssp_amd_ctx *ctx, double a, const lssp_amd_mat *A, const double *x, double *y);
+/* y = A*x                           (lssp_mv_mxy,     mvops.cxx:144-150) */
+int lssp_amd_mv_mxy(lssp_amd_ctx *ctx, const lssp_amd_mat *A, const double *x, double *y);
+
+/* ---- BLAS-1: vector.h:8-39 (vector.cxx:31-146) -------------------------- */
+int lssp_amd_vec_set_value(lssp_amd_ctx *ctx, double *x, long n, double val);
+int lssp_amd_vec_copy(lssp_amd_ctx *ctx, double *x, const double *y, long n);
+int lssp_amd_vec_axy(lssp_amd_ctx *ctx, double alpha, const double *x, double *y, long n);
+int lssp_amd_vec_axpby(lssp_amd_ctx *ctx, double alpha, const double *x, double beta, double *y,
+                       long n);
+int lssp_amd_vec_axpbyz(lssp_amd_ctx *ctx, double alpha, const double *x, double beta,
+                        const double *y, double *z, long n);
+int lssp_amd_vec_scale(lssp_amd_ctx *ctx, double *x, long n, double a);
+int lssp_amd_vec_dot(lssp_amd_ctx *ctx, const double *x, const double *y, long n, double *result);
+int lssp_amd_vec_norm(lssp_amd_ctx *ctx, const double *x, long n, double *result);
+
+/* ---- ILU preconditioner ---------------------------------------------------
+ * Setup on the host, exactly the reference algorithm: ILUK
+ * (lssp_pc_iluk_assemble, pc-iluk.cxx:566-581) or ILUT (lssp_pc_ilut_assemble,
+ * pc-ilut.cxx:429-456); blk > 0 and < n selects block-Jacobi blocks of that
+ * size (the blk_size path of pc-iluk.cxx:411-552), used per rank on multi-GPU.
+ * Then the factors are uploaded with their sync-free trisolve schedules.
+ * Apply: x = U^-1 L^-1 rhs on the device (lssp_pc_ilu_solve,
+ * solver-tri.cxx:57-60), bitwise; x may alias rhs. */
+int lssp_amd_ilu_create(lssp_amd_ctx *ctx, int kind, int n, const int *Ap, const int *Aj,
+                        const double *Ax, int level, double tol, int p, int blk,
+                        lssp_amd_ilu **M);
+/* upload caller-made factors (L: unit diagonal LAST per row; U: pivot FIRST) */
+int lssp_amd_ilu_from_factors(lssp_amd_ctx *ctx, int n, const int *Lp, const int *Lj,
+                              const double *Lx, const int *Up, const int *Uj, const double *Ux,
+                              lssp_amd_ilu **M);
+int lssp_amd_ilu_destroy(lssp_amd_ilu *M);
+int lssp_amd_ilu_apply(lssp_amd_ctx *ctx, const lssp_amd_ilu *M, double *x, const double *rhs);
+/* one triangular sweep: which = 0 lower (solver-tri.cxx:4-24), 1 upper (:26-46) */
+int lssp_amd_ilu_trisolve(lssp_amd_ctx *ctx, const lssp_amd_ilu *M, int which, double *x,
+                          const double *rhs);
+int lssp_amd_ilu_info(const lssp_amd_ilu *M, int *n, int *nnzL, int *nnzU, int *levelsL,
+                      int *levelsU, double *setup_seconds);
+int lssp_amd_ilu_get_factors(const lssp_amd_ilu *M, int *Lp, int *Lj, double *Lx, int *Up,
+                             int *Uj, double *Ux);
+
+/* ---- Krylov solve: lssp_solver_solve (lssp.cxx:250-414) for BiCGSTAB
+ *      (solver-bicgstab.cxx:10-175), GMRES(m) (solver-gmres.cxx:12-255) and
+ *      CG (solver-cg.cxx:8-136).  Same recurrences, guards, defaults and
+ *      iteration counting; vectors stay in HBM. ------------------------- */
+typedef struct {
+    int solver;     /* LSSP_AMD_GMRES / _BICGSTAB / _CG */
+    double tol_rel; /* < 0: default 1e-7 (lssp.cxx:11-13) */
+    double tol_abs;
+    double tol_rb;
+    int maxit;      /* <= 0: default 1000 */
+    int restart;    /* GMRES m; < 0: default 50 */
+    int verb;       /* >= 1 prints the reference's per-iteration line */
+} lssp_amd_solve_params;
+
+/* x: device, x0 on entry, solution on exit; b: device.  M == NULL is PC_NON
+ * (pc.cxx:67-70).  trace (host, optional) receives every dot/norm the driver
+ * evaluates, in the reference's call order. */
+int lssp_amd_solve(lssp_amd_ctx *ctx, const lssp_amd_mat *A, const lssp_amd_ilu *M,
+                   const lssp_amd_solve_params *prm, double *x, const double *b, int *nits,
+                   double *residual, double *trace, int trace_cap, int *trace_len);
+
+/* ---- multi-GPU: one process per GPU, row-block partition, RCCL over xGMI --
+ * The reference is serial (README.md:3); this is the SURVEY 8(e) extension.
+ * Rank r owns rows [r*ceil(n/P), min((r+1)*ceil(n/P), n)).  A distributed
+ * matrix holds the rank's rows with columns renumbered [owned | halo]; SpMV
+ * fetches the halo with grouped ncclSend/ncclRecv; dots all-gather the P rank
+ * partials and sum them in rank order (deterministic, identical on every
+ * rank). */
+int lssp_amd_comm_unique_id_size(void);
+int lssp_amd_comm_get_unique_id(void *id_out);
+int lssp_amd_comm_init(lssp_amd_ctx *ctx, int nranks, int rank, const void *id);
+int lssp_amd_comm_barrier(lssp_amd_ctx *ctx);
+/* rows [row0, row0 + nlocal) of a global n x n CSR given by its local rows */
+int lssp_amd_mat_upload_dist(lssp_amd_ctx *ctx, int n_global, int row0, int nlocal,
+                             const int *Ap, const int *Aj, const double *Ax, lssp_amd_mat **A);
+int lssp_amd_mat_local_rows(const lssp_amd_mat *A, int *row0, int *nlocal, int *nhalo);
+
+/* ---- synthetic inputs (example/exam.cxx:4-59 and its 7-pt analogue) ------ */
+long lssp_amd_poisson_nnz(int dim, int N);
+/* rows [row0, row0+nrows) of the 5-pt (dim 2) or 7-pt (dim 3) Laplacian */
+int lssp_amd_poisson_rows(int dim, int N, long row0, long nrows, int *Ap, int *Aj, double *Ax);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

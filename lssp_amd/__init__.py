@@ -1,0 +1,18 @@
+"""lssp_amd -- MI355X-native hot path of LSSP (CSR SpMV, fused BLAS-1, ILU
+trisolves, BiCGSTAB / GMRES / CG) behind the reference's API.
+
+    from lssp_amd import api          # lssp_solver_create / _assemble / _solve ...
+    from lssp_amd.device import ...   # raw C-ABI handles (include/lssp_amd.h)
+
+The compute lives in lssp_amd/lib/liblssp_amd.so (hand-written HIP for
+gfx950).  Importing the package loads it and fails loudly if it is missing.
+"""
+from . import _lib
+
+_lib.load()
+
+from .device import (BICGSTAB, CG, GMRES, ILUK, ILUT, SERIAL, TREE, DILU, DMat,  # noqa: E402,F401
+                     Device, DVec, LsspError, comm_unique_id, poisson, solve, sort_columns)
+
+__all__ = ["Device", "DVec", "DMat", "DILU", "solve", "poisson", "sort_columns", "LsspError",
+           "comm_unique_id", "GMRES", "BICGSTAB", "CG", "ILUK", "ILUT", "SERIAL", "TREE"]

@@ -1,0 +1,556 @@
+// capi.cpp -- extern "C" entry points of include/lssp_amd.h (everything except
+// the Krylov drivers, solvers.cpp, and the RCCL layer, comm.cpp).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+
+#include "internal.h"
+
+using namespace lssp_amd;
+
+namespace lssp_amd {
+
+long num_chunks(long n) { return (n + CHUNK - 1) / CHUNK; }
+
+int ensure_part(lssp_amd_ctx *c, long C)
+{
+    if (C <= c->part_cap) return LSSP_AMD_OK;
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    if (c->d_part) LSSP_HIP(hipFree(c->d_part));
+    long cap = std::max<long>(C, 4096);
+    LSSP_HIP(hipMalloc(&c->d_part, sizeof(double) * MAX_SLOTS * cap));
+    c->part_cap = cap;
+    return LSSP_AMD_OK;
+}
+
+// Complete a reduction whose level-1 partials a fused pass already wrote
+// (tree) -- or, in serial mode, recompute it in the reference's order from the
+// operand pairs -- then combine ranks and run the finalize program.
+int finish_reduce(lssp_amd_ctx *c, long n, int nslot, const double *const *a,
+                  const double *const *b, const Fin &f)
+{
+    if (c->reduce_mode == LSSP_AMD_REDUCE_SERIAL) {
+        LSSP_TRY(launch_reduce_serial(c, n, nslot, a, b, f));
+    } else {
+        LSSP_TRY(launch_reduce_tree(c, n > 0 ? num_chunks(n) : 0, nslot, f));
+    }
+    if (c->nranks > 1) {
+        LSSP_TRY(comm_allgather_sums(c, nslot));
+        LSSP_TRY(launch_sum_ranks(c, nslot, f));
+    }
+    return LSSP_AMD_OK;
+}
+
+int reduce_dots(lssp_amd_ctx *c, long n, int nslot, const double *const *a, const double *const *b,
+                const Fin &f)
+{
+    if (c->reduce_mode == LSSP_AMD_REDUCE_TREE && n > 0) {
+        Ew e;
+        e.kind = 7;  // EW_DOT
+        e.n = n;
+        e.nred = nslot;
+        e.r0a = a[0];
+        e.r0b = b[0];
+        if (nslot > 1) {
+            e.r1a = a[1];
+            e.r1b = b[1];
+        }
+        LSSP_TRY(launch_ew(c, e));
+    }
+    return finish_reduce(c, n, nslot, a, b, f);
+}
+
+}  // namespace lssp_amd
+
+extern "C" {
+
+const char *lssp_amd_strerror(int s)
+{
+    switch (s) {
+    case LSSP_AMD_OK: return "ok";
+    case LSSP_AMD_EINVAL: return "invalid argument";
+    case LSSP_AMD_EHIP: return "HIP runtime error";
+    case LSSP_AMD_ENOMEM: return "out of memory";
+    case LSSP_AMD_ETIMEOUT: return "trisolve dependency wait timed out";
+    case LSSP_AMD_ECOMM: return "RCCL error";
+    case LSSP_AMD_EUNSUPPORTED: return "unsupported solver / preconditioner";
+    default: return "unknown status";
+    }
+}
+
+int lssp_amd_version(void) { return 10000; }
+
+int lssp_amd_ctx_create(int device, lssp_amd_ctx **out)
+{
+    if (!out) return LSSP_AMD_EINVAL;
+    lssp_amd_ctx *c = new lssp_amd_ctx();
+    c->device = device;
+    LSSP_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    LSSP_HIP(hipGetDeviceProperties(&prop, device));
+    c->num_cus = prop.multiProcessorCount;
+    LSSP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    LSSP_HIP(hipMalloc(&c->d_sums, sizeof(double) * MAX_SLOTS));
+    LSSP_HIP(hipMalloc(&c->d_scal, sizeof(double) * NSCAL));
+    LSSP_HIP(hipMemset(c->d_scal, 0, sizeof(double) * NSCAL));
+    LSSP_HIP(hipHostMalloc(&c->h_scal, sizeof(double) * NSCAL, hipHostMallocDefault));
+    LSSP_HIP(hipMalloc(&c->d_err, sizeof(int)));
+    LSSP_HIP(hipMemset(c->d_err, 0, sizeof(int)));
+    const char *m = getenv("LSSP_AMD_REDUCE");
+    if (m && !strcmp(m, "serial")) c->reduce_mode = LSSP_AMD_REDUCE_SERIAL;
+    const char *tb = getenv("LSSP_AMD_TRI_BLOCKS_PER_CU");
+    if (tb) c->tri_blocks_per_cu = std::max(1, atoi(tb));
+    *out = c;
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_ctx_destroy(lssp_amd_ctx *c)
+{
+    if (!c) return LSSP_AMD_OK;
+    (void)hipStreamSynchronize(c->stream);
+    comm_destroy(c);
+    if (c->d_part) (void)hipFree(c->d_part);
+    if (c->d_trace) (void)hipFree(c->d_trace);
+    (void)hipFree(c->d_sums);
+    (void)hipFree(c->d_scal);
+    (void)hipHostFree(c->h_scal);
+    (void)hipFree(c->d_err);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_ctx_set_reduction(lssp_amd_ctx *c, int mode)
+{
+    if (!c || (mode != LSSP_AMD_REDUCE_SERIAL && mode != LSSP_AMD_REDUCE_TREE)) return LSSP_AMD_EINVAL;
+    c->reduce_mode = mode;
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_ctx_sync(lssp_amd_ctx *c)
+{
+    if (!c) return LSSP_AMD_EINVAL;
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    return LSSP_AMD_OK;
+}
+
+void *lssp_amd_ctx_stream(lssp_amd_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+// ---- vectors ---------------------------------------------------------------
+int lssp_amd_vec_alloc(lssp_amd_ctx *c, long n, double **d)
+{
+    if (!c || !d || n < 0) return LSSP_AMD_EINVAL;
+    if (hipMalloc(d, sizeof(double) * std::max<long>(n, 1)) != hipSuccess) return LSSP_AMD_ENOMEM;
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_vec_free(lssp_amd_ctx *c, double *d)
+{
+    if (!c) return LSSP_AMD_EINVAL;
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    if (d) LSSP_HIP(hipFree(d));
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_vec_upload(lssp_amd_ctx *c, double *d, const double *h, long n)
+{
+    if (!c || (n > 0 && (!d || !h))) return LSSP_AMD_EINVAL;
+    if (n == 0) return LSSP_AMD_OK;
+    LSSP_HIP(hipMemcpyAsync(d, h, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_vec_download(lssp_amd_ctx *c, double *h, const double *d, long n)
+{
+    if (!c || (n > 0 && (!d || !h))) return LSSP_AMD_EINVAL;
+    if (n == 0) return LSSP_AMD_OK;
+    LSSP_HIP(hipMemcpyAsync(h, d, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    return LSSP_AMD_OK;
+}
+
+// ---- matrices --------------------------------------------------------------
+static int check_csr(int nrows, int ncols, int nnz, const int *Ap, const int *Aj)
+{
+    if (nrows < 0 || ncols <= 0 || nnz < 0 || !Ap) return LSSP_AMD_EINVAL;
+    if (Ap[0] != 0 || Ap[nrows] != nnz) return LSSP_AMD_EINVAL;
+    for (int i = 0; i < nrows; i++)
+        if (Ap[i + 1] < Ap[i]) return LSSP_AMD_EINVAL;
+    for (int k = 0; k < nnz; k++)
+        if (Aj[k] < 0 || Aj[k] >= ncols) return LSSP_AMD_EINVAL;
+    return LSSP_AMD_OK;
+}
+
+static int upload_csr(lssp_amd_mat *M, const int *Ap, const int *Aj, const double *Ax)
+{
+    LSSP_HIP(hipMalloc(&M->Ap, sizeof(int) * (M->nrows + 1)));
+    LSSP_HIP(hipMalloc(&M->Aj, sizeof(int) * std::max(M->nnz, 1)));
+    LSSP_HIP(hipMalloc(&M->Ax, sizeof(double) * std::max(M->nnz, 1)));
+    LSSP_HIP(hipMemcpy(M->Ap, Ap, sizeof(int) * (M->nrows + 1), hipMemcpyHostToDevice));
+    if (M->nnz) {
+        LSSP_HIP(hipMemcpy(M->Aj, Aj, sizeof(int) * M->nnz, hipMemcpyHostToDevice));
+        LSSP_HIP(hipMemcpy(M->Ax, Ax, sizeof(double) * M->nnz, hipMemcpyHostToDevice));
+    }
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_mat_upload(lssp_amd_ctx *c, int nrows, int ncols, int nnz, const int *Ap, const int *Aj,
+                        const double *Ax, lssp_amd_mat **out)
+{
+    if (!c || !out) return LSSP_AMD_EINVAL;
+    LSSP_TRY(check_csr(nrows, ncols, nnz, Ap, Aj));
+    LSSP_HIP(hipSetDevice(c->device));
+    lssp_amd_mat *M = new lssp_amd_mat();
+    M->ctx = c;
+    M->nrows = nrows;
+    M->ncols = ncols;
+    M->nnz = nnz;
+    M->n_global = nrows;
+    int st = upload_csr(M, Ap, Aj, Ax);
+    if (st != LSSP_AMD_OK) {
+        lssp_amd_mat_destroy(M);
+        return st;
+    }
+    *out = M;
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_mat_destroy(lssp_amd_mat *M)
+{
+    if (!M) return LSSP_AMD_OK;
+    if (M->ctx) (void)hipStreamSynchronize(M->ctx->stream);
+    if (M->Ap) (void)hipFree(M->Ap);
+    if (M->Aj) (void)hipFree(M->Aj);
+    if (M->Ax) (void)hipFree(M->Ax);
+    if (M->d_send_idx) (void)hipFree(M->d_send_idx);
+    if (M->d_send_buf) (void)hipFree(M->d_send_buf);
+    delete M;
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_mat_info(const lssp_amd_mat *A, int *nrows, int *ncols, int *nnz)
+{
+    if (!A) return LSSP_AMD_EINVAL;
+    if (nrows) *nrows = A->nrows;
+    if (ncols) *ncols = A->ncols;
+    if (nnz) *nnz = A->nnz;
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_mat_local_rows(const lssp_amd_mat *A, int *row0, int *nlocal, int *nhalo)
+{
+    if (!A) return LSSP_AMD_EINVAL;
+    if (row0) *row0 = A->row0;
+    if (nlocal) *nlocal = A->nrows;
+    if (nhalo) *nhalo = A->nhalo;
+    return LSSP_AMD_OK;
+}
+
+// ---- SpMV (mvops.cxx) ----------------------------------------------------------
+// x must hold nrows + nhalo entries on a distributed matrix; its halo part is
+// refreshed here (halo_exchange is a no-op on one rank).
+int lssp_amd_mv_amxpby(lssp_amd_ctx *c, double alpha, const lssp_amd_mat *A, const double *x,
+                       double beta, double *y)
+{
+    if (!c || !A || !x || !y) return LSSP_AMD_EINVAL;
+    LSSP_TRY(halo_exchange(A, const_cast<double *>(x)));
+    return launch_spmv(c, A, EPI_AXPBY, alpha, x, beta, y, y, 0, nullptr, nullptr);
+}
+
+int lssp_amd_mv_amxpbyz(lssp_amd_ctx *c, double alpha, const lssp_amd_mat *A, const double *x,
+                        double beta, const double *y, double *z)
+{
+    if (!c || !A || !x || !y || !z) return LSSP_AMD_EINVAL;
+    LSSP_TRY(halo_exchange(A, const_cast<double *>(x)));
+    if (beta == 0.0 && alpha > 0.0)  // y*0 + alpha*sum == alpha*sum for finite y
+        return launch_spmv(c, A, EPI_AMX, alpha, x, beta, nullptr, z, 0, nullptr, nullptr);
+    return launch_spmv(c, A, EPI_AXPBY, alpha, x, beta, y, z, 0, nullptr, nullptr);
+}
+
+int lssp_amd_mv_amxy(lssp_amd_ctx *c, double a, const lssp_amd_mat *A, const double *x, double *y)
+{
+    if (!c || !A || !x || !y) return LSSP_AMD_EINVAL;
+    LSSP_TRY(halo_exchange(A, const_cast<double *>(x)));
+    return launch_spmv(c, A, EPI_AMXY, a, x, 0, nullptr, y, 0, nullptr, nullptr);
+}
+
+int lssp_amd_mv_mxy(lssp_amd_ctx *c, const lssp_amd_mat *A, const double *x, double *y)
+{
+    if (!c || !A || !x || !y) return LSSP_AMD_EINVAL;
+    LSSP_TRY(halo_exchange(A, const_cast<double *>(x)));
+    return launch_spmv(c, A, EPI_MXY, 1.0, x, 0, nullptr, y, 0, nullptr, nullptr);
+}
+
+// ---- BLAS-1 (vector.cxx) -----------------------------------------------------------
+static int ew_simple(lssp_amd_ctx *c, int kind, long n, double a, double b, const double *x,
+                     const double *y, double *out)
+{
+    if (!c || n < 0 || (n > 0 && !out)) return LSSP_AMD_EINVAL;
+    Ew e;
+    e.kind = kind;
+    e.n = n;
+    e.a = a;
+    e.b = b;
+    e.x = x;
+    e.y = y;
+    e.out0 = out;
+    return launch_ew(c, e);
+}
+
+int lssp_amd_vec_set_value(lssp_amd_ctx *c, double *x, long n, double v)
+{
+    return ew_simple(c, 0, n, v, 0, nullptr, nullptr, x);
+}
+int lssp_amd_vec_copy(lssp_amd_ctx *c, double *x, const double *y, long n)
+{
+    if (!y && n > 0) return LSSP_AMD_EINVAL;
+    return ew_simple(c, 1, n, 0, 0, y, nullptr, x);
+}
+int lssp_amd_vec_axy(lssp_amd_ctx *c, double alpha, const double *x, double *y, long n)
+{
+    if (!x && n > 0) return LSSP_AMD_EINVAL;
+    return ew_simple(c, 2, n, alpha, 0, x, nullptr, y);
+}
+int lssp_amd_vec_axpby(lssp_amd_ctx *c, double alpha, const double *x, double beta, double *y, long n)
+{
+    if (!x && n > 0) return LSSP_AMD_EINVAL;
+    return ew_simple(c, 3, n, alpha, beta, x, nullptr, y);
+}
+int lssp_amd_vec_axpbyz(lssp_amd_ctx *c, double alpha, const double *x, double beta, const double *y,
+                        double *z, long n)
+{
+    if ((!x || !y) && n > 0) return LSSP_AMD_EINVAL;
+    return ew_simple(c, 4, n, alpha, beta, x, y, z);
+}
+int lssp_amd_vec_scale(lssp_amd_ctx *c, double *x, long n, double a)
+{
+    return ew_simple(c, 5, n, a, 0, nullptr, nullptr, x);
+}
+
+int lssp_amd_vec_dot(lssp_amd_ctx *c, const double *x, const double *y, long n, double *result)
+{
+    if (!c || !result || (n > 0 && (!x || !y))) return LSSP_AMD_EINVAL;
+    const double *a[1] = {x}, *b[1] = {y};
+    Fin f;
+    f.op = FIN_STORE;
+    f.dst[0] = S_TMP;
+    LSSP_TRY(reduce_dots(c, n, 1, a, b, f));
+    LSSP_HIP(hipMemcpyAsync(c->h_scal, c->d_scal + S_TMP, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    *result = c->h_scal[0];
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_vec_norm(lssp_amd_ctx *c, const double *x, long n, double *result)
+{
+    if (!c || !result || (n > 0 && !x)) return LSSP_AMD_EINVAL;
+    const double *a[1] = {x}, *b[1] = {x};
+    Fin f;
+    f.op = FIN_NORM;
+    f.dst[0] = S_TMP;
+    LSSP_TRY(reduce_dots(c, n, 1, a, b, f));
+    LSSP_HIP(hipMemcpyAsync(c->h_scal, c->d_scal + S_TMP, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    *result = c->h_scal[0];
+    return LSSP_AMD_OK;
+}
+
+// ---- ILU -------------------------------------------------------------------------
+static int ilu_upload(lssp_amd_ctx *c, lssp_amd_ilu *M)
+{
+    LSSP_TRY(build_trisched(c, M->n, M->Lp, M->Lj, M->Lx, false, M->lower));
+    LSSP_TRY(build_trisched(c, M->n, M->Up, M->Uj, M->Ux, true, M->upper));
+    LSSP_HIP(hipMalloc(&M->d_cache, sizeof(double) * std::max(M->n, 1)));
+    LSSP_TRY(launch_fill(c, M->d_cache, M->n, TRI_SENTINEL));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_ilu_create(lssp_amd_ctx *c, int kind, int n, const int *Ap, const int *Aj,
+                        const double *Ax, int level, double tol, int p, int blk, lssp_amd_ilu **out)
+{
+    if (!c || !out || n <= 0 || (kind != LSSP_AMD_ILUK && kind != LSSP_AMD_ILUT)) return LSSP_AMD_EINVAL;
+    LSSP_TRY(check_csr(n, n, Ap[n], Ap, Aj));
+    if (Ap[n] < 1) return LSSP_AMD_EINVAL;
+    LSSP_HIP(hipSetDevice(c->device));
+    auto t0 = std::chrono::steady_clock::now();
+    HostCSR A;
+    A.n = n;
+    A.ncols = n;
+    A.Ap.assign(Ap, Ap + n + 1);
+    A.Aj.assign(Aj, Aj + Ap[n]);
+    A.Ax.assign(Ax, Ax + Ap[n]);
+    sort_columns(A);  // lssp.cxx:173
+    if (kind == LSSP_AMD_ILUK && level < 0) level = 1;  // pc-iluk.cxx:583-592
+    HostCSR L, U;
+    ilu_factor(kind, A, level, tol < 0 ? 1e-3 : tol, p, blk, L, U);
+    lssp_amd_ilu *M = new lssp_amd_ilu();
+    M->ctx = c;
+    M->n = n;
+    M->Lp = std::move(L.Ap);
+    M->Lj = std::move(L.Aj);
+    M->Lx = std::move(L.Ax);
+    M->Up = std::move(U.Ap);
+    M->Uj = std::move(U.Aj);
+    M->Ux = std::move(U.Ax);
+    int st = ilu_upload(c, M);
+    if (st != LSSP_AMD_OK) {
+        lssp_amd_ilu_destroy(M);
+        return st;
+    }
+    M->setup_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    *out = M;
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_ilu_from_factors(lssp_amd_ctx *c, int n, const int *Lp, const int *Lj, const double *Lx,
+                              const int *Up, const int *Uj, const double *Ux, lssp_amd_ilu **out)
+{
+    if (!c || !out || n <= 0) return LSSP_AMD_EINVAL;
+    LSSP_TRY(check_csr(n, n, Lp[n], Lp, Lj));
+    LSSP_TRY(check_csr(n, n, Up[n], Up, Uj));
+    LSSP_HIP(hipSetDevice(c->device));
+    auto t0 = std::chrono::steady_clock::now();
+    lssp_amd_ilu *M = new lssp_amd_ilu();
+    M->ctx = c;
+    M->n = n;
+    M->Lp.assign(Lp, Lp + n + 1);
+    M->Lj.assign(Lj, Lj + Lp[n]);
+    M->Lx.assign(Lx, Lx + Lp[n]);
+    M->Up.assign(Up, Up + n + 1);
+    M->Uj.assign(Uj, Uj + Up[n]);
+    M->Ux.assign(Ux, Ux + Up[n]);
+    int st = ilu_upload(c, M);
+    if (st != LSSP_AMD_OK) {
+        lssp_amd_ilu_destroy(M);
+        return st;
+    }
+    M->setup_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    *out = M;
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_ilu_destroy(lssp_amd_ilu *M)
+{
+    if (!M) return LSSP_AMD_OK;
+    if (M->ctx) (void)hipStreamSynchronize(M->ctx->stream);
+    free_trisched(M->lower);
+    free_trisched(M->upper);
+    if (M->d_cache) (void)hipFree(M->d_cache);
+    delete M;
+    return LSSP_AMD_OK;
+}
+
+static int check_err(lssp_amd_ctx *c)
+{
+    int e = 0;
+    LSSP_HIP(hipMemcpyAsync(&e, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    if (e) {
+        LSSP_HIP(hipMemset(c->d_err, 0, sizeof(int)));
+        return LSSP_AMD_ETIMEOUT;
+    }
+    return LSSP_AMD_OK;
+}
+
+// solver-tri.cxx:48-60: cache = L^-1 rhs ; x = U^-1 cache.  The L sweep also
+// arms x (sentinel) for the U sweep, the U sweep re-arms the cache.
+int lssp_amd_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const double *rhs)
+{
+    if (!c || !M || !x || !rhs) return LSSP_AMD_EINVAL;
+    LSSP_TRY(launch_trisolve(c, M->lower, rhs, M->d_cache, x));
+    LSSP_TRY(launch_trisolve(c, M->upper, M->d_cache, x, M->d_cache));
+    return check_err(c);
+}
+
+int lssp_amd_ilu_trisolve(lssp_amd_ctx *c, const lssp_amd_ilu *M, int which, double *x, const double *rhs)
+{
+    if (!c || !M || !x || !rhs || x == rhs) return LSSP_AMD_EINVAL;
+    LSSP_TRY(launch_fill(c, x, M->n, TRI_SENTINEL));
+    LSSP_TRY(launch_trisolve(c, which ? M->upper : M->lower, rhs, x, nullptr));
+    return check_err(c);
+}
+
+int lssp_amd_ilu_info(const lssp_amd_ilu *M, int *n, int *nnzL, int *nnzU, int *levelsL, int *levelsU,
+                      double *setup_seconds)
+{
+    if (!M) return LSSP_AMD_EINVAL;
+    if (n) *n = M->n;
+    if (nnzL) *nnzL = (int)M->Lj.size();
+    if (nnzU) *nnzU = (int)M->Uj.size();
+    if (levelsL) *levelsL = M->lower.nlevels;
+    if (levelsU) *levelsU = M->upper.nlevels;
+    if (setup_seconds) *setup_seconds = M->setup_seconds;
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_ilu_get_factors(const lssp_amd_ilu *M, int *Lp, int *Lj, double *Lx, int *Up, int *Uj,
+                             double *Ux)
+{
+    if (!M) return LSSP_AMD_EINVAL;
+    if (Lp) memcpy(Lp, M->Lp.data(), sizeof(int) * M->Lp.size());
+    if (Lj) memcpy(Lj, M->Lj.data(), sizeof(int) * M->Lj.size());
+    if (Lx) memcpy(Lx, M->Lx.data(), sizeof(double) * M->Lx.size());
+    if (Up) memcpy(Up, M->Up.data(), sizeof(int) * M->Up.size());
+    if (Uj) memcpy(Uj, M->Uj.data(), sizeof(int) * M->Uj.size());
+    if (Ux) memcpy(Ux, M->Ux.data(), sizeof(double) * M->Ux.size());
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_csr_sort_columns(int nrows, int ncols, int *Ap, int *Aj, double *Ax)
+{
+    if (nrows < 0 || ncols <= 0 || !Ap || !Aj || !Ax) return LSSP_AMD_EINVAL;
+    HostCSR H;
+    H.n = nrows;
+    H.ncols = ncols;
+    H.Ap.assign(Ap, Ap + nrows + 1);
+    H.Aj.assign(Aj, Aj + Ap[nrows]);
+    H.Ax.assign(Ax, Ax + Ap[nrows]);
+    sort_columns(H);
+    memcpy(Aj, H.Aj.data(), sizeof(int) * H.Aj.size());
+    memcpy(Ax, H.Ax.data(), sizeof(double) * H.Ax.size());
+    return LSSP_AMD_OK;
+}
+
+// ---- synthetic inputs: example/exam.cxx:4-59 (5-pt) and the 7-pt analogue ----------
+long lssp_amd_poisson_nnz(int dim, int N)
+{
+    long n = N;
+    return dim == 2 ? 5 * n * n - 4 * n : 7 * n * n * n - 6 * n * n;
+}
+
+int lssp_amd_poisson_rows(int dim, int N, long row0, long nrows, int *Ap, int *Aj, double *Ax)
+{
+    if ((dim != 2 && dim != 3) || N <= 0 || !Ap || !Aj || !Ax) return LSSP_AMD_EINVAL;
+    const long N2 = (long)N * N, n = dim == 2 ? N2 : N2 * N;
+    if (row0 < 0 || nrows < 0 || row0 + nrows > n) return LSSP_AMD_EINVAL;
+    long o = 0;
+    Ap[0] = 0;
+    for (long q = 0; q < nrows; q++) {
+        const long r = row0 + q;
+        if (dim == 2) {
+            const long i = r / N, j = r % N;
+            if (i > 0) { Aj[o] = (int)(r - N); Ax[o++] = -1; }
+            if (j > 0) { Aj[o] = (int)(r - 1); Ax[o++] = -1; }
+            Aj[o] = (int)r; Ax[o++] = 4;
+            if (j < N - 1) { Aj[o] = (int)(r + 1); Ax[o++] = -1; }
+            if (i < N - 1) { Aj[o] = (int)(r + N); Ax[o++] = -1; }
+        } else {
+            const long k = r / N2, j = (r / N) % N, i = r % N;
+            if (k > 0) { Aj[o] = (int)(r - N2); Ax[o++] = -1; }
+            if (j > 0) { Aj[o] = (int)(r - N); Ax[o++] = -1; }
+            if (i > 0) { Aj[o] = (int)(r - 1); Ax[o++] = -1; }
+            Aj[o] = (int)r; Ax[o++] = 6;
+            if (i < N - 1) { Aj[o] = (int)(r + 1); Ax[o++] = -1; }
+            if (j < N - 1) { Aj[o] = (int)(r + N); Ax[o++] = -1; }
+            if (k < N - 1) { Aj[o] = (int)(r + N2); Ax[o++] = -1; }
+        }
+        Ap[q + 1] = (int)o;
+    }
+    return LSSP_AMD_OK;
+}
+
+}  // extern "C"

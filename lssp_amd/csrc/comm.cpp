@@ -1,0 +1,231 @@
+// comm.cpp -- multi-GPU layer: one process per GPU, RCCL over xGMI.
+//
+// The reference is serial (README.md:3); this is the SURVEY 8(e) extension of
+// the hot path.  Rows are partitioned in contiguous blocks of ceil(n/P) (the
+// same blocks the reference's block-Jacobi path uses, pc-iluk.cxx:467-472).
+//   * SpMV: each rank holds its rows with columns renumbered [owned | halo];
+//     before a product the halo entries are fetched with ONE grouped
+//     ncclSend/ncclRecv round to exactly the peers that own them (for the
+//     7-pt stencil: one N^2 plane from each z-neighbour).
+//   * Dots: each rank reduces its slice in the canonical tree order, the P
+//     rank sums are all-gathered (ncclAllGather, P*4 doubles) and every rank
+//     adds them in rank order -- deterministic and identical on all ranks.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+
+#include "internal.h"
+
+namespace lssp_amd {
+
+#define LSSP_NCCL(call)                                                                            \
+    do {                                                                                           \
+        ncclResult_t r_ = (call);                                                                  \
+        if (r_ != ncclSuccess) {                                                                   \
+            fprintf(stderr, "lssp_amd: RCCL error %s at %s:%d\n", ncclGetErrorString(r_), __FILE__, \
+                    __LINE__);                                                                     \
+            return LSSP_AMD_ECOMM;                                                                 \
+        }                                                                                          \
+    } while (0)
+
+int comm_allgather_sums(lssp_amd_ctx *c, int nslot)
+{
+    (void)nslot;
+    LSSP_NCCL(ncclAllGather(c->d_sums, c->d_gather, MAX_SLOTS, ncclDouble, (ncclComm_t)c->comm, c->stream));
+    return LSSP_AMD_OK;
+}
+
+int halo_exchange(const lssp_amd_mat *A, double *x)
+{
+    if (!A || A->ctx == nullptr || A->ctx->nranks <= 1) return LSSP_AMD_OK;
+    if (A->send_peer.empty() && A->recv_peer.empty()) return LSSP_AMD_OK;
+    lssp_amd_ctx *c = A->ctx;
+    LSSP_TRY(launch_pack(c, A->d_send_idx, x, A->d_send_buf, A->nsend));
+    LSSP_NCCL(ncclGroupStart());
+    for (size_t q = 0; q < A->send_peer.size(); q++)
+        LSSP_NCCL(ncclSend(A->d_send_buf + A->send_off[q], A->send_cnt[q], ncclDouble, A->send_peer[q],
+                           (ncclComm_t)c->comm, c->stream));
+    for (size_t q = 0; q < A->recv_peer.size(); q++)
+        LSSP_NCCL(ncclRecv(x + A->nrows + A->recv_off[q], A->recv_cnt[q], ncclDouble, A->recv_peer[q],
+                           (ncclComm_t)c->comm, c->stream));
+    LSSP_NCCL(ncclGroupEnd());
+    return LSSP_AMD_OK;
+}
+
+int comm_destroy(lssp_amd_ctx *c)
+{
+    if (c->comm) {
+        ncclCommDestroy((ncclComm_t)c->comm);
+        c->comm = nullptr;
+    }
+    if (c->d_gather) {
+        (void)hipFree(c->d_gather);
+        c->d_gather = nullptr;
+    }
+    c->nranks = 1;
+    c->rank = 0;
+    return LSSP_AMD_OK;
+}
+
+}  // namespace lssp_amd
+
+using namespace lssp_amd;
+
+extern "C" {
+
+int lssp_amd_comm_unique_id_size(void) { return (int)sizeof(ncclUniqueId); }
+
+int lssp_amd_comm_get_unique_id(void *out)
+{
+    if (!out) return LSSP_AMD_EINVAL;
+    ncclUniqueId id;
+    LSSP_NCCL(ncclGetUniqueId(&id));
+    memcpy(out, &id, sizeof(id));
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_comm_init(lssp_amd_ctx *c, int nranks, int rank, const void *idp)
+{
+    if (!c || !idp || nranks < 1 || rank < 0 || rank >= nranks) return LSSP_AMD_EINVAL;
+    LSSP_HIP(hipSetDevice(c->device));
+    comm_destroy(c);
+    if (nranks == 1) return LSSP_AMD_OK;
+    ncclUniqueId id;
+    memcpy(&id, idp, sizeof(id));
+    ncclComm_t comm;
+    LSSP_NCCL(ncclCommInitRank(&comm, nranks, id, rank));
+    c->comm = comm;
+    c->nranks = nranks;
+    c->rank = rank;
+    LSSP_HIP(hipMalloc(&c->d_gather, sizeof(double) * MAX_SLOTS * nranks));
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_comm_barrier(lssp_amd_ctx *c)
+{
+    if (!c) return LSSP_AMD_EINVAL;
+    if (c->nranks > 1) {
+        LSSP_NCCL(ncclAllReduce(c->d_sums, c->d_sums, 0, ncclDouble, ncclSum, (ncclComm_t)c->comm, c->stream));
+        double *tmp;
+        LSSP_HIP(hipMalloc(&tmp, sizeof(double)));
+        LSSP_NCCL(ncclAllReduce(tmp, tmp, 1, ncclDouble, ncclSum, (ncclComm_t)c->comm, c->stream));
+        LSSP_HIP(hipStreamSynchronize(c->stream));
+        LSSP_HIP(hipFree(tmp));
+    }
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    return LSSP_AMD_OK;
+}
+
+// Local rows [row0, row0+nlocal) of the global matrix, global column indices.
+int lssp_amd_mat_upload_dist(lssp_amd_ctx *c, int n_global, int row0, int nlocal, const int *Ap,
+                             const int *Aj, const double *Ax, lssp_amd_mat **out)
+{
+    if (!c || !out || !Ap || n_global <= 0 || nlocal < 0) return LSSP_AMD_EINVAL;
+    const int P = c->nranks;
+    const int blk = (n_global + P - 1) / P;
+    const int my0 = std::min(c->rank * blk, n_global);
+    const int myn = std::min(blk, n_global - my0);
+    if (row0 != my0 || nlocal != myn) return LSSP_AMD_EINVAL;  // canonical partition only
+    const int nnz = Ap[nlocal];
+    if (Ap[0] != 0) return LSSP_AMD_EINVAL;
+    // halo columns, grouped by owner then ascending
+    std::map<int, int> halo;  // global col -> slot
+    for (int k = 0; k < nnz; k++) {
+        const int g = Aj[k];
+        if (g < 0 || g >= n_global) return LSSP_AMD_EINVAL;
+        if (g < row0 || g >= row0 + nlocal) halo[g] = 0;
+    }
+    std::vector<int> hcols;
+    hcols.reserve(halo.size());
+    for (auto &kv : halo) hcols.push_back(kv.first);  // std::map is ordered: owners ascending too
+    for (size_t q = 0; q < hcols.size(); q++) halo[hcols[q]] = (int)q;
+    std::vector<int> lj(nnz);
+    for (int k = 0; k < nnz; k++) {
+        const int g = Aj[k];
+        lj[k] = (g >= row0 && g < row0 + nlocal) ? g - row0 : nlocal + halo[g];
+    }
+    lssp_amd_mat *M = new lssp_amd_mat();
+    M->ctx = c;
+    M->nrows = nlocal;
+    M->nhalo = (int)hcols.size();
+    M->ncols = nlocal + M->nhalo;
+    M->nnz = nnz;
+    M->n_global = n_global;
+    M->row0 = row0;
+    // receive plan (per owner)
+    std::vector<int> need(P, 0);
+    for (int g : hcols) need[g / blk]++;
+    int off = 0;
+    for (int q = 0; q < P; q++) {
+        if (need[q]) {
+            M->recv_peer.push_back(q);
+            M->recv_off.push_back(off);
+            M->recv_cnt.push_back(need[q]);
+        }
+        off += need[q];
+    }
+    // tell every owner which of its columns we need: counts then index lists
+    int *d_cnt_mine, *d_cnt_all;
+    LSSP_HIP(hipMalloc(&d_cnt_mine, sizeof(int) * P));
+    LSSP_HIP(hipMalloc(&d_cnt_all, sizeof(int) * P * P));
+    LSSP_HIP(hipMemcpy(d_cnt_mine, need.data(), sizeof(int) * P, hipMemcpyHostToDevice));
+    LSSP_NCCL(ncclAllGather(d_cnt_mine, d_cnt_all, P, ncclInt32, (ncclComm_t)c->comm, c->stream));
+    std::vector<int> all(P * P);
+    LSSP_HIP(hipMemcpyAsync(all.data(), d_cnt_all, sizeof(int) * P * P, hipMemcpyDeviceToHost, c->stream));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    int nsend = 0;
+    for (int q = 0; q < P; q++) {
+        const int cnt = all[q * P + c->rank];  // what rank q needs from me
+        if (cnt) {
+            M->send_peer.push_back(q);
+            M->send_off.push_back(nsend);
+            M->send_cnt.push_back(cnt);
+            nsend += cnt;
+        }
+    }
+    M->nsend = nsend;
+    int *d_hcols = nullptr, *d_sendg = nullptr;
+    LSSP_HIP(hipMalloc(&d_hcols, sizeof(int) * std::max<size_t>(hcols.size(), 1)));
+    LSSP_HIP(hipMalloc(&d_sendg, sizeof(int) * std::max(nsend, 1)));
+    if (!hcols.empty())
+        LSSP_HIP(hipMemcpy(d_hcols, hcols.data(), sizeof(int) * hcols.size(), hipMemcpyHostToDevice));
+    LSSP_NCCL(ncclGroupStart());
+    for (size_t q = 0; q < M->recv_peer.size(); q++)
+        LSSP_NCCL(ncclSend(d_hcols + M->recv_off[q], M->recv_cnt[q], ncclInt32, M->recv_peer[q],
+                           (ncclComm_t)c->comm, c->stream));
+    for (size_t q = 0; q < M->send_peer.size(); q++)
+        LSSP_NCCL(ncclRecv(d_sendg + M->send_off[q], M->send_cnt[q], ncclInt32, M->send_peer[q],
+                           (ncclComm_t)c->comm, c->stream));
+    LSSP_NCCL(ncclGroupEnd());
+    std::vector<int> sendg(nsend);
+    if (nsend)
+        LSSP_HIP(hipMemcpyAsync(sendg.data(), d_sendg, sizeof(int) * nsend, hipMemcpyDeviceToHost, c->stream));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    for (int &g : sendg) {
+        if (g < row0 || g >= row0 + nlocal) return LSSP_AMD_EINVAL;
+        g -= row0;
+    }
+    LSSP_HIP(hipMalloc(&M->d_send_idx, sizeof(int) * std::max(nsend, 1)));
+    LSSP_HIP(hipMalloc(&M->d_send_buf, sizeof(double) * std::max(nsend, 1)));
+    if (nsend)
+        LSSP_HIP(hipMemcpy(M->d_send_idx, sendg.data(), sizeof(int) * nsend, hipMemcpyHostToDevice));
+    (void)hipFree(d_cnt_mine);
+    (void)hipFree(d_cnt_all);
+    (void)hipFree(d_hcols);
+    (void)hipFree(d_sendg);
+    LSSP_HIP(hipMalloc(&M->Ap, sizeof(int) * (nlocal + 1)));
+    LSSP_HIP(hipMalloc(&M->Aj, sizeof(int) * std::max(nnz, 1)));
+    LSSP_HIP(hipMalloc(&M->Ax, sizeof(double) * std::max(nnz, 1)));
+    LSSP_HIP(hipMemcpy(M->Ap, Ap, sizeof(int) * (nlocal + 1), hipMemcpyHostToDevice));
+    if (nnz) {
+        LSSP_HIP(hipMemcpy(M->Aj, lj.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
+        LSSP_HIP(hipMemcpy(M->Ax, Ax, sizeof(double) * nnz, hipMemcpyHostToDevice));
+    }
+    *out = M;
+    return LSSP_AMD_OK;
+}
+
+}  // extern "C"

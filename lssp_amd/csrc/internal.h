@@ -1,0 +1,195 @@
+// internal.h -- shared state of the lssp_amd library (not part of the C-ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/lssp_amd.h"
+
+namespace lssp_amd {
+
+// ---- canonical reduction layout ------------------------------
+constexpr int CHUNK = 256;       // level 1: one aligned chunk of 256 elements per partial
+constexpr int L2_LANES = 1024;   // level 2: one workgroup, lane t sums partials t, t+1024, ...
+constexpr int MAX_SLOTS = 4;     // partial sums one pass can produce
+constexpr int NSCAL = 4096;      // device scalar slots per context
+
+// sync-free trisolve: the value-as-flag "not yet computed" pattern (a NaN payload
+// no arithmetic produces)
+constexpr uint64_t TRI_SENTINEL = 0xFFF7DEADBEEFCAFEull;
+
+// scalar slots of the Krylov drivers (device memory, ctx->d_scal)
+enum Scal {
+    S_RHO0 = 0, S_RHO1, S_ALPHA, S_BETA, S_OMEGA, S_RES, S_SNORM, S_BREAK, S_BNORM, S_TMP,
+    S_SUM0 = 16,   // raw reduced sums of the last reduction
+    S_H = 32,      // GMRES Hessenberg column (up to NSCAL - 32 entries)
+};
+
+// finalize programs run by one lane after a reduction (same code for every
+// reduction mode, so the scalar recurrences are bit-identical across modes)
+enum FinOp {
+    FIN_STORE = 0,       // scal[dst[k]] = sum[k]
+    FIN_NORM,            // scal[dst[0]] = sqrt(sum[0])
+    FIN_BICG_RHO,        // rho1 = s0; beta = (rho1*alpha)/(rho0*omega); rho0 = rho1
+    FIN_BICG_ALPHA,      // alpha = rho1 / s0
+    FIN_BICG_S,          // snorm = sqrt(s0); break = snorm <= 1e-40
+    FIN_BICG_OMEGA,      // omega = s0 / s1
+    FIN_BICG_RES_RHO,    // res = sqrt(s0); then FIN_BICG_RHO on s1
+    FIN_CG_RHO,          // rho1 = s0; beta = rho1 / rho0
+    FIN_CG_ALPHA,        // alpha = rho1 / s0; rho0 = rho1
+    FIN_CG_RES,          // res = sqrt(s0)
+    FIN_CG_RES_RHO,      // res = sqrt(s0); rho1 = s0; beta = rho1/rho0  (PC_NON: z == r)
+};
+
+struct Fin {
+    int op = FIN_STORE;
+    int nsum = 1;
+    int dst[MAX_SLOTS] = {S_SUM0, S_SUM0 + 1, S_SUM0 + 2, S_SUM0 + 3};
+    int tpos[2] = {-1, -1};  // trace positions of the (up to two) traced values
+};
+
+}  // namespace lssp_amd
+
+struct lssp_amd_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int reduce_mode = LSSP_AMD_REDUCE_TREE;
+    int num_cus = 256;
+    // reduction scratch
+    double *d_part = nullptr;  // [MAX_SLOTS][part_cap] level-1 partials
+    long part_cap = 0;
+    double *d_sums = nullptr;  // [MAX_SLOTS] rank-local sums
+    double *d_scal = nullptr;  // [NSCAL] scalar slots
+    double *h_scal = nullptr;  // pinned mirror
+    double *d_trace = nullptr; // device trace buffer
+    long trace_cap = 0;
+    int *d_err = nullptr;      // error word (trisolve timeouts)
+    // multi-GPU (RCCL)
+    int nranks = 1, rank = 0;
+    void *comm = nullptr;      // ncclComm_t
+    double *d_gather = nullptr;  // [nranks][MAX_SLOTS]
+    int tri_blocks_per_cu = 4;
+};
+
+struct lssp_amd_mat {
+    lssp_amd_ctx *ctx = nullptr;
+    int nrows = 0, ncols = 0, nnz = 0;  // local rows; ncols = local column space (owned + halo)
+    int *Ap = nullptr, *Aj = nullptr;
+    double *Ax = nullptr;
+    // distributed layout
+    int n_global = 0, row0 = 0, nhalo = 0;
+    // halo exchange plan: for each peer, indices (local) to send and the count to receive
+    std::vector<int> send_peer, send_off, send_cnt;  // host plan
+    std::vector<int> recv_peer, recv_off, recv_cnt;  // recv_off relative to the halo region
+    int *d_send_idx = nullptr;
+    double *d_send_buf = nullptr;
+    int nsend = 0;
+};
+
+namespace lssp_amd {
+
+struct TriSched {
+    int n = 0, nnz = 0, nlevels = 0, unit = 0;
+    int *perm = nullptr;   // position -> row, rows ordered by level
+    int *rp = nullptr;     // [n+1] entry ranges in schedule order
+    int *cols = nullptr;   // strict entries, in the reference's summation order
+    double *vals = nullptr;
+    double *diag = nullptr;  // per position (nullptr when unit)
+};
+
+}  // namespace lssp_amd
+
+struct lssp_amd_ilu {
+    lssp_amd_ctx *ctx = nullptr;
+    int n = 0;
+    std::vector<int> Lp, Lj, Up, Uj;  // host copies (for get_factors / tests)
+    std::vector<double> Lx, Ux;
+    lssp_amd::TriSched lower, upper;
+    double *d_cache = nullptr;  // L sweep output, kept all-sentinel between applies
+    double setup_seconds = 0;
+};
+
+namespace lssp_amd {
+
+// ---- error handling --------------------------------------------------------
+#define LSSP_HIP(call)                                                                    \
+    do {                                                                                  \
+        hipError_t e_ = (call);                                                           \
+        if (e_ != hipSuccess) {                                                           \
+            fprintf(stderr, "lssp_amd: HIP error %s at %s:%d\n", hipGetErrorString(e_), \
+                    __FILE__, __LINE__);                                                  \
+            return LSSP_AMD_EHIP;                                                         \
+        }                                                                                 \
+    } while (0)
+
+#define LSSP_TRY(call)               \
+    do {                             \
+        int s_ = (call);             \
+        if (s_ != LSSP_AMD_OK) return s_; \
+    } while (0)
+
+// ---- kernel launchers (kernels.hip) ------------------------------------------
+enum Epi { EPI_MXY = 0, EPI_AMXY, EPI_AXPBY, EPI_AMX };  // see spmv kernel
+int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, const double *x,
+                double beta, const double *y, double *z, int nred, const double *w0,
+                const double *w1);
+// elementwise + optional partials; kinds in kernels.hip (EwKind)
+struct Ew {
+    int kind = 0;
+    long n = 0;
+    double a = 0, b = 0;
+    const double *x = nullptr, *y = nullptr, *u = nullptr, *v = nullptr;
+    double *out0 = nullptr, *out1 = nullptr;
+    const double *scal = nullptr;   // device scalars
+    int nred = 0;
+    const double *r0a = nullptr, *r0b = nullptr, *r1a = nullptr, *r1b = nullptr;
+    const double *vbase = nullptr;  // GMRES basis [k][n]
+    int k = 0;
+    int sidx = 0;                   // scalar index for device-scalar kinds
+};
+int launch_ew(lssp_amd_ctx *c, const Ew &e);
+// finish a reduction whose level-1 partials (tree) or operands (serial) are set:
+// tree: level-2 over nslot partial rows of C entries; then the finalize program
+int launch_reduce_tree(lssp_amd_ctx *c, long C, int nslot, const Fin &f);
+// serial: sums of products a_k[i]*b_k[i] in index order (== vector.cxx:123-133)
+int launch_reduce_serial(lssp_amd_ctx *c, long n, int nslot, const double *const *a,
+                         const double *const *b, const Fin &f);
+int launch_finalize(lssp_amd_ctx *c, const double *sums, int nslot, const Fin &f);
+int launch_fill(lssp_amd_ctx *c, double *x, long n, uint64_t bits);
+int launch_trisolve(lssp_amd_ctx *c, const TriSched &t, const double *rhs, double *x,
+                    double *reset);
+int launch_pack(lssp_amd_ctx *c, const int *idx, const double *x, double *buf, int n);
+int launch_sum_ranks(lssp_amd_ctx *c, int nslot, const Fin &f);
+
+long num_chunks(long n);
+int ensure_part(lssp_amd_ctx *c, long C);
+
+// ---- host pieces ---------------------------------------------------------------
+// ILU setup (ilu_setup.cpp), exact restatement of pc-iluk.cxx / pc-ilut.cxx
+struct HostCSR {
+    int n = 0, ncols = 0;
+    std::vector<int> Ap, Aj;
+    std::vector<double> Ax;
+};
+void sort_columns(HostCSR &A);
+void ilu_factor(int kind, const HostCSR &A, int level, double tol, int p, int blk, HostCSR &L,
+                HostCSR &U);
+int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std::vector<int> &Tj,
+                   const std::vector<double> &Tx, bool upper, TriSched &t);
+void free_trisched(TriSched &t);
+
+// reductions with the context's mode; result left in d_sums / scal per Fin
+int finish_reduce(lssp_amd_ctx *c, long n, int nslot, const double *const *a,
+                  const double *const *b, const Fin &f);
+int reduce_dots(lssp_amd_ctx *c, long n, int nslot, const double *const *a,
+                const double *const *b, const Fin &f);
+// multi-rank: all-gather rank sums and sum in rank order, then the finalize
+int comm_allgather_sums(lssp_amd_ctx *c, int nslot);
+int halo_exchange(const lssp_amd_mat *A, double *x);
+int comm_destroy(lssp_amd_ctx *c);
+
+}  // namespace lssp_amd

@@ -1,0 +1,589 @@
+// kernels.hip -- gfx950 kernels of the LSSP Krylov hot path.
+//
+// Compiled with -ffp-contract=off: every a*b+c below is a v_mul_f64 followed
+// by a v_add_f64, exactly like the x86-64 -O2 build of the reference, so the
+// per-element arithmetic is bit-identical to mvops.cxx / vector.cxx /
+// solver-tri.cxx and to the solver drivers' inline loops.
+//
+// Reductions follow ONE canonical order, shared by every pass
+// that produces a dot product, including the SpMV epilogues:
+//   level 1: aligned chunks of 256 elements, element 64q+l of a chunk on lane
+//            l of wave q; each wave halves (xor butterfly == halving tree,
+//            lane 0 result), then (w0 + w1) + (w2 + w3);
+//   level 2: one 1024-lane workgroup; lane t adds partials t, t+1024, ... onto
+//            0.0 in order; 16 waves halve; the 16 wave sums halve.
+// oracle/lssp_oracle.c (dot_tree) restates this order on the CPU.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "internal.h"
+
+namespace lssp_amd {
+
+// ---------------------------------------------------------------------------
+// reduction helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
+    return v;  // lane 0 holds the halving-tree result
+}
+
+// level-1 combine of one 256-element chunk held one element per thread of a
+// 256-thread block; the block-combined value is written by thread 0.
+template <int NRED>
+__device__ __forceinline__ void chunk_reduce(double (&v)[NRED > 0 ? NRED : 1], double *part, long pcap,
+                                             long chunk, double (*lds)[4])
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int r = 0; r < NRED; r++) {
+        double s = wave_sum(v[r]);
+        if (lane == 0) lds[r][wave] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int r = 0; r < NRED; r++)
+            part[r * pcap + chunk] = (lds[r][0] + lds[r][1]) + (lds[r][2] + lds[r][3]);
+    }
+    __syncthreads();
+}
+
+__device__ void finalize(const Fin &f, const double *s, double *scal, double *trace)
+{
+    double t0 = s[0], t1 = f.nsum > 1 ? s[1] : 0.0;
+    for (int k = 0; k < f.nsum; k++) scal[S_SUM0 + k] = s[k];
+    switch (f.op) {
+    case FIN_STORE:
+        for (int k = 0; k < f.nsum; k++) scal[f.dst[k]] = s[k];
+        break;
+    case FIN_NORM:
+        t0 = sqrt(s[0]);
+        scal[f.dst[0]] = t0;
+        break;
+    case FIN_BICG_RHO: {  // solver-bicgstab.cxx:87, :99, :105
+        double rho1 = s[0];
+        scal[S_RHO1] = rho1;
+        scal[S_BETA] = (rho1 * scal[S_ALPHA]) / (scal[S_RHO0] * scal[S_OMEGA]);
+        scal[S_RHO0] = rho1;
+        break;
+    }
+    case FIN_BICG_ALPHA:  // :112
+        scal[S_ALPHA] = scal[S_RHO1] / s[0];
+        break;
+    case FIN_BICG_S: {  // :117
+        t0 = sqrt(s[0]);
+        scal[S_SNORM] = t0;
+        scal[S_BREAK] = t0 <= 1e-40 ? 1.0 : 0.0;
+        break;
+    }
+    case FIN_BICG_OMEGA:  // :135
+        scal[S_OMEGA] = s[0] / s[1];
+        break;
+    case FIN_BICG_RES_RHO: {  // :141 then the next iteration's :87
+        t0 = sqrt(s[0]);
+        scal[S_RES] = t0;
+        double rho1 = s[1];
+        t1 = rho1;
+        scal[S_RHO1] = rho1;
+        scal[S_BETA] = (rho1 * scal[S_ALPHA]) / (scal[S_RHO0] * scal[S_OMEGA]);
+        scal[S_RHO0] = rho1;
+        break;
+    }
+    case FIN_CG_RHO:  // solver-cg.cxx:80, :88
+        scal[S_RHO1] = s[0];
+        scal[S_BETA] = s[0] / scal[S_RHO0];
+        break;
+    case FIN_CG_ALPHA:  // :96-99
+        scal[S_ALPHA] = scal[S_RHO1] / s[0];
+        scal[S_RHO0] = scal[S_RHO1];
+        break;
+    case FIN_CG_RES:  // :106
+        t0 = sqrt(s[0]);
+        scal[S_RES] = t0;
+        break;
+    case FIN_CG_RES_RHO: {  // :106, then the next :80 with z == r (PC_NON)
+        t0 = sqrt(s[0]);
+        scal[S_RES] = t0;
+        t1 = s[0];
+        scal[S_RHO1] = s[0];
+        scal[S_BETA] = s[0] / scal[S_RHO0];
+        break;
+    }
+    }
+    if (trace) {
+        if (f.tpos[0] >= 0) trace[f.tpos[0]] = t0;
+        if (f.tpos[1] >= 0) trace[f.tpos[1]] = t1;
+    }
+}
+
+// level 2 (tree) + finalize
+__global__ __launch_bounds__(1024) void k_reduce2(const double *__restrict__ part, long pcap, long C,
+                                                  int nslot, double *sums, double *scal, double *trace,
+                                                  Fin f, int do_fin)
+{
+    __shared__ double wsum[MAX_SLOTS][16];
+    const int t = threadIdx.x;
+    for (int s = 0; s < nslot; s++) {
+        const double *p = part + s * pcap;
+        double a = 0.0;
+#pragma unroll 8
+        for (long k = t; k < C; k += L2_LANES) a += p[k];
+        a = wave_sum(a);
+        if ((t & 63) == 0) wsum[s][t >> 6] = a;
+    }
+    __syncthreads();
+    if (t == 0) {
+        double r[MAX_SLOTS] = {0, 0, 0, 0};
+        for (int s = 0; s < nslot; s++) {
+            double u[16];
+            for (int q = 0; q < 16; q++) u[q] = wsum[s][q];
+            for (int off = 8; off >= 1; off >>= 1)
+                for (int l = 0; l < off; l++) u[l] = u[l] + u[l + off];
+            r[s] = u[0];
+            sums[s] = r[s];
+        }
+        if (do_fin) finalize(f, r, scal, trace);
+    }
+}
+
+// serial order: one lane, sum += a[i]*b[i] from 0 (vector.cxx:123-133)
+struct SerialArgs {
+    const double *a[MAX_SLOTS];
+    const double *b[MAX_SLOTS];
+};
+
+__global__ void k_dot_serial(SerialArgs g, long n, int nslot, double *sums, double *scal,
+                             double *trace, Fin f, int do_fin)
+{
+    double r[MAX_SLOTS] = {0, 0, 0, 0};
+    for (int s = 0; s < nslot; s++) {
+        const double *x = g.a[s], *y = g.b[s];
+        double acc = 0;
+        long i = 0;
+        for (; i + 8 <= n; i += 8) {
+            double p[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) p[u] = x[i + u] * y[i + u];
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc += p[u];
+        }
+        for (; i < n; i++) acc += x[i] * y[i];
+        r[s] = acc;
+        sums[s] = acc;
+    }
+    if (do_fin) finalize(f, r, scal, trace);
+}
+
+__global__ void k_finalize(const double *sums, double *scal, double *trace, Fin f)
+{
+    double r[MAX_SLOTS];
+    for (int s = 0; s < MAX_SLOTS; s++) r[s] = s < f.nsum ? sums[s] : 0.0;
+    finalize(f, r, scal, trace);
+}
+
+// multi-rank: gathered [P][MAX_SLOTS] rank sums, summed in rank order
+__global__ void k_sum_ranks(const double *gath, int P, int nslot, double *sums, double *scal,
+                            double *trace, Fin f)
+{
+    double r[MAX_SLOTS] = {0, 0, 0, 0};
+    for (int s = 0; s < nslot; s++) {
+        double t = gath[s];
+        for (int q = 1; q < P; q++) t = t + gath[q * MAX_SLOTS + s];
+        r[s] = t;
+        sums[s] = t;
+    }
+    finalize(f, r, scal, trace);
+}
+
+// ---------------------------------------------------------------------------
+// SpMV: one 256-row block == one reduction chunk; every row summed by ONE
+// lane in CSR order from 0.0 (mvops.cxx:49-62).  The block's Aj/Ax range is
+// staged through LDS with coalesced loads when it fits, otherwise the lanes
+// read their rows straight from HBM (same arithmetic).
+// ---------------------------------------------------------------------------
+constexpr int SPMV_CAP = 2048;
+
+struct SpmvArgs {
+    int nrows;
+    const int *Ap, *Aj;
+    const double *Ax, *x, *y;
+    double *z;
+    double alpha, beta;
+    const double *w0, *w1;  // fused dot operands: red0 = z*w0, red1 = z*(w1 ? w1 : z)
+    double *part;
+    long pcap;
+};
+
+template <int EPI, int NRED>
+__global__ __launch_bounds__(256) void k_spmv(SpmvArgs a)
+{
+    __shared__ int sj[SPMV_CAP];
+    __shared__ double sx[SPMV_CAP];
+    __shared__ double lds[MAX_SLOTS][4];
+    const long blk = blockIdx.x;
+    const int r0 = (int)(blk * 256);
+    const int tid = threadIdx.x;
+    const int r = r0 + tid;
+    const int rend = min(r0 + 256, a.nrows);
+    const int base = a.Ap[r0];
+    const int cnt = a.Ap[rend] - base;
+    double sum = 0;
+    if (cnt <= SPMV_CAP) {
+        for (int k = tid; k < cnt; k += 256) {
+            sj[k] = __builtin_nontemporal_load(a.Aj + base + k);
+            sx[k] = __builtin_nontemporal_load(a.Ax + base + k);
+        }
+        __syncthreads();
+        if (r < a.nrows) {
+            const int b = a.Ap[r] - base, e = a.Ap[r + 1] - base;
+            for (int k = b; k < e; k++) sum += a.x[sj[k]] * sx[k];
+        }
+    } else if (r < a.nrows) {
+        const int b = a.Ap[r], e = a.Ap[r + 1];
+        for (int k = b; k < e; k++) sum += a.x[a.Aj[k]] * a.Ax[k];
+    }
+    double zv = 0;
+    if (r < a.nrows) {
+        if (EPI == EPI_MXY) zv = sum;                          // mvops.cxx:134
+        else if (EPI == EPI_AMXY) zv = sum * a.alpha;          // :99
+        else if (EPI == EPI_AXPBY) zv = a.y[r] * a.beta + a.alpha * sum;  // :23, :61
+        else zv = a.alpha * sum;  // :61 with beta == 0 and alpha > 0
+        a.z[r] = zv;
+    }
+    if (NRED > 0) {
+        double v[NRED > 0 ? NRED : 1];
+        if (r < a.nrows) {
+            v[0] = zv * a.w0[r];
+            if (NRED > 1) v[NRED > 1 ? 1 : 0] = zv * (a.w1 ? a.w1[r] : zv);
+        } else {
+#pragma unroll
+            for (int q = 0; q < NRED; q++) v[q] = 0.0;
+        }
+        chunk_reduce<NRED>(v, a.part, a.pcap, blk, lds);
+    }
+}
+
+template <int EPI>
+static void spmv_dispatch(const SpmvArgs &a, int nred, long nblocks, hipStream_t s)
+{
+    if (nred == 0) k_spmv<EPI, 0><<<nblocks, 256, 0, s>>>(a);
+    else if (nred == 1) k_spmv<EPI, 1><<<nblocks, 256, 0, s>>>(a);
+    else k_spmv<EPI, 2><<<nblocks, 256, 0, s>>>(a);
+}
+
+int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, const double *x,
+                double beta, const double *y, double *z, int nred, const double *w0,
+                const double *w1)
+{
+    if (A->nrows == 0) return LSSP_AMD_OK;
+    long nb = num_chunks(A->nrows);
+    LSSP_TRY(ensure_part(c, nb));
+    SpmvArgs a{A->nrows, A->Ap, A->Aj, A->Ax, x, y, z, alpha, beta, w0, w1, c->d_part, c->part_cap};
+    switch (epi) {
+    case EPI_MXY: spmv_dispatch<EPI_MXY>(a, nred, nb, c->stream); break;
+    case EPI_AMXY: spmv_dispatch<EPI_AMXY>(a, nred, nb, c->stream); break;
+    case EPI_AXPBY: spmv_dispatch<EPI_AXPBY>(a, nred, nb, c->stream); break;
+    default: spmv_dispatch<EPI_AMX>(a, nred, nb, c->stream); break;
+    }
+    LSSP_HIP(hipGetLastError());
+    return LSSP_AMD_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Elementwise passes (vector.cxx and the drivers' inline loops), one element
+// per lane in the canonical chunk layout so any of them can carry partial
+// sums.  Operand order inside each expression is the reference's.
+// ---------------------------------------------------------------------------
+enum EwKind {
+    EW_FILL = 0,   // out0 = a                         (vector.cxx:31-38)
+    EW_COPY,       // out0 = x                         (:73-83)
+    EW_AXY,        // out0 = x * a                     (:86-95)
+    EW_AXPBY,      // out0 = out0 * b + x * a          (:98-107)
+    EW_AXPBYZ,     // out0 = y * b + x * a             (:110-120)
+    EW_SCALE,      // out0 = out0 * a                  (:141-146)
+    EW_DIVS,       // out0 = out0 / scal[sidx]         (solver-gmres.cxx:129-131)
+    EW_DOT,        // partials only
+    EW_BICG_P,     // out0 = x + beta*(out0 - omega*y) (solver-bicgstab.cxx:99-102), x=r, y=v
+    EW_BICG_S,     // out0 = x - alpha*y               (:113-115), x=r, y=v
+    EW_BICG_XR,    // out0(x) = out0 + alpha*x + omega*y ; out1(r) = u - omega*v   (:136-139)
+                   // (break flag set: out0 = out0 + alpha*x only, :120-122)
+    EW_CG_P,       // out0 = x + beta*out0             (solver-cg.cxx:90-92)
+    EW_CG_XR,      // out0(x) = out0 + alpha*x ; out1(r) = out1 - alpha*y   (:101-104)
+    EW_GM_MGS,     // out0 = out0 * 1 + x * (-scal[sidx])  (solver-gmres.cxx:144)
+    EW_GM_X,       // out0[q] += sum_{i<k} vbase[i][q] * scal[S_H..]  (:196-204); ym passed in u
+};
+
+struct EwArgs {
+    int kind;
+    long n;
+    double a, b;
+    const double *x, *y, *u, *v;
+    double *out0, *out1;
+    const double *scal;
+    const double *r0a, *r0b, *r1a, *r1b;
+    const double *vbase;
+    int k, sidx;
+    double *part;
+    long pcap;
+    long nchunks;
+};
+
+template <int NRED>
+__global__ __launch_bounds__(256) void k_ew(EwArgs g)
+{
+    __shared__ double lds[MAX_SLOTS][4];
+    for (long c = blockIdx.x; c < g.nchunks; c += gridDim.x) {
+        const long i = c * 256 + threadIdx.x;
+        const bool in = i < g.n;
+        if (in) {
+            switch (g.kind) {
+            case EW_FILL: g.out0[i] = g.a; break;
+            case EW_COPY: g.out0[i] = g.x[i]; break;
+            case EW_AXY: g.out0[i] = g.x[i] * g.a; break;
+            case EW_AXPBY: g.out0[i] = g.out0[i] * g.b + g.x[i] * g.a; break;
+            case EW_AXPBYZ: g.out0[i] = g.y[i] * g.b + g.x[i] * g.a; break;
+            case EW_SCALE: g.out0[i] = g.out0[i] * g.a; break;
+            case EW_DIVS: g.out0[i] = g.out0[i] / g.scal[g.sidx]; break;
+            case EW_DOT: break;
+            case EW_BICG_P: {
+                const double beta = g.scal[S_BETA], omega = g.scal[S_OMEGA];
+                g.out0[i] = g.x[i] + beta * (g.out0[i] - omega * g.y[i]);
+                break;
+            }
+            case EW_BICG_S: g.out0[i] = g.x[i] - g.scal[S_ALPHA] * g.y[i]; break;
+            case EW_BICG_XR: {
+                const double alpha = g.scal[S_ALPHA];
+                if (g.scal[S_BREAK] != 0.0) {
+                    g.out0[i] = g.out0[i] + alpha * g.x[i];
+                } else {
+                    const double omega = g.scal[S_OMEGA];
+                    g.out0[i] = g.out0[i] + alpha * g.x[i] + omega * g.y[i];
+                    g.out1[i] = g.u[i] - omega * g.v[i];
+                }
+                break;
+            }
+            case EW_CG_P: g.out0[i] = g.x[i] + g.scal[S_BETA] * g.out0[i]; break;
+            case EW_CG_XR: {
+                const double alpha = g.scal[S_ALPHA];
+                g.out0[i] = g.out0[i] + alpha * g.x[i];
+                g.out1[i] = g.out1[i] - alpha * g.y[i];
+                break;
+            }
+            case EW_GM_MGS: g.out0[i] = g.out0[i] * 1 + g.x[i] * (-g.scal[g.sidx]); break;
+            case EW_GM_X: {  // b carries the basis stride (vectors hold owned + halo entries)
+                const long ld = (long)g.b;
+                double acc = 0;
+                for (int q = 0; q < g.k; q++) acc += g.vbase[(long)q * ld + i] * g.u[q];
+                g.out0[i] += acc;
+                break;
+            }
+            }
+        }
+        if (NRED > 0) {
+            double v[NRED > 0 ? NRED : 1];
+            v[0] = in ? g.r0a[i] * g.r0b[i] : 0.0;
+            if (NRED > 1) v[NRED > 1 ? 1 : 0] = in ? g.r1a[i] * g.r1b[i] : 0.0;
+            chunk_reduce<NRED>(v, g.part, g.pcap, c, lds);
+        }
+    }
+}
+
+int launch_ew(lssp_amd_ctx *c, const Ew &e)
+{
+    if (e.n <= 0) return LSSP_AMD_OK;
+    long C = num_chunks(e.n);
+    LSSP_TRY(ensure_part(c, C));
+    EwArgs g{e.kind, e.n, e.a, e.b, e.x, e.y, e.u, e.v, e.out0, e.out1, e.scal,
+             e.r0a, e.r0b, e.r1a, e.r1b, e.vbase, e.k, e.sidx, c->d_part, c->part_cap, C};
+    // one chunk per block up to a cap; the cap keeps >= 8 blocks per CU resident
+    long grid = C < 8L * c->num_cus * 4 ? C : 8L * c->num_cus * 4;
+    if (e.nred == 0) k_ew<0><<<grid, 256, 0, c->stream>>>(g);
+    else if (e.nred == 1) k_ew<1><<<grid, 256, 0, c->stream>>>(g);
+    else k_ew<2><<<grid, 256, 0, c->stream>>>(g);
+    LSSP_HIP(hipGetLastError());
+    return LSSP_AMD_OK;
+}
+
+int launch_reduce_tree(lssp_amd_ctx *c, long C, int nslot, const Fin &f)
+{
+    int do_fin = c->nranks > 1 ? 0 : 1;
+    k_reduce2<<<1, L2_LANES, 0, c->stream>>>(c->d_part, c->part_cap, C, nslot, c->d_sums, c->d_scal,
+                                              c->d_trace, f, do_fin);
+    LSSP_HIP(hipGetLastError());
+    return LSSP_AMD_OK;
+}
+
+int launch_reduce_serial(lssp_amd_ctx *c, long n, int nslot, const double *const *a,
+                         const double *const *b, const Fin &f)
+{
+    SerialArgs g{};
+    for (int s = 0; s < nslot; s++) {
+        g.a[s] = a[s];
+        g.b[s] = b[s];
+    }
+    int do_fin = c->nranks > 1 ? 0 : 1;
+    k_dot_serial<<<1, 1, 0, c->stream>>>(g, n, nslot, c->d_sums, c->d_scal, c->d_trace, f, do_fin);
+    LSSP_HIP(hipGetLastError());
+    return LSSP_AMD_OK;
+}
+
+int launch_finalize(lssp_amd_ctx *c, const double *sums, int nslot, const Fin &f)
+{
+    (void)nslot;
+    k_finalize<<<1, 1, 0, c->stream>>>(sums, c->d_scal, c->d_trace, f);
+    LSSP_HIP(hipGetLastError());
+    return LSSP_AMD_OK;
+}
+
+int launch_sum_ranks(lssp_amd_ctx *c, int nslot, const Fin &f)
+{
+    k_sum_ranks<<<1, 1, 0, c->stream>>>(c->d_gather, c->nranks, nslot, c->d_sums, c->d_scal,
+                                         c->d_trace, f);
+    LSSP_HIP(hipGetLastError());
+    return LSSP_AMD_OK;
+}
+
+__global__ void k_fill_bits(uint64_t *x, long n, uint64_t bits)
+{
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        x[i] = bits;
+}
+
+int launch_fill(lssp_amd_ctx *c, double *x, long n, uint64_t bits)
+{
+    if (n <= 0) return LSSP_AMD_OK;
+    long grid = (n + 255) / 256;
+    if (grid > 8L * c->num_cus * 4) grid = 8L * c->num_cus * 4;
+    k_fill_bits<<<grid, 256, 0, c->stream>>>(reinterpret_cast<uint64_t *>(x), n, bits);
+    LSSP_HIP(hipGetLastError());
+    return LSSP_AMD_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Sync-free level-ordered triangular sweep (solver-tri.cxx:4-46).
+//
+// Rows are visited in level order (host analysis, ilu_setup.cpp); 64
+// consecutive scheduled rows form a chunk and wave w of the persistent grid
+// takes chunks w, w+W, w+2W, ... in order.  x starts as TRI_SENTINEL
+// everywhere; a row's value is published by ONE 8-byte agent-scope store and
+// read by agent-scope (sc1, L1-bypassing) loads -- the data is the flag
+// (MI355X_MICROARCH: R2 granule).  Each lane consumes its row's entries in the
+// reference's order as they become available, so the arithmetic is exactly
+// result = result - val*x[col] ... ; x = result / diag.  The smallest
+// unfinished chunk can always progress (its dependencies lie in earlier chunks
+// or earlier in the same chunk, and its wave is resident), so the sweep
+// cannot deadlock; every wait is still bounded (4 s of s_memrealtime) and a
+// timeout raises ctx->d_err instead of hanging the GPU.
+// ---------------------------------------------------------------------------
+struct TriArgs {
+    int n;
+    long nchunks;
+    const int *perm, *rp, *cols;
+    const double *vals, *diag;
+    int unit;
+    const double *rhs;
+    double *x;
+    double *reset;  // if set: reset[row] = TRI_SENTINEL once rhs[row] has been read
+    int *err;
+};
+
+__device__ __forceinline__ uint64_t ld_agent(const double *p)
+{
+    return __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void st_agent(double *p, double v)
+{
+    __hip_atomic_store(reinterpret_cast<uint64_t *>(p), (uint64_t)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void k_trisolve(TriArgs a)
+{
+    const int lane = threadIdx.x & 63;
+    const long wave = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const long nwaves = (long)gridDim.x * (blockDim.x >> 6);
+    for (long c = wave; c < a.nchunks; c += nwaves) {
+        const long p = c * 64 + lane;
+        bool active = p < a.n;
+        int row = 0, k = 0, end = 0;
+        double acc = 0;
+        if (active) {
+            row = a.perm[p];
+            k = a.rp[p];
+            end = a.rp[p + 1];
+            acc = a.rhs[row];
+            if (a.reset) a.reset[row] = __longlong_as_double((long long)TRI_SENTINEL);
+        }
+        uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        int nap = 0;
+        for (;;) {
+            if (active) {
+                while (k < end) {
+                    const int m = end - k < 4 ? end - k : 4;
+                    uint64_t bits[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (u < m) bits[u] = ld_agent(a.x + a.cols[k + u]);
+                    int u = 0;
+                    for (; u < m; u++) {
+                        if (bits[u] == TRI_SENTINEL) break;
+                        acc = acc - a.vals[k] * __longlong_as_double((long long)bits[u]);
+                        k++;
+                    }
+                    if (u < m) break;
+                }
+                if (k == end) {
+                    const double xi = a.unit ? acc : acc / a.diag[p];
+                    st_agent(a.x + row, xi);
+                    active = false;
+                }
+            }
+            if (!__any(active)) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s at 100 MHz
+                if (active) {
+                    atomicOr(a.err, 1);
+                    st_agent(a.x + row, __longlong_as_double(0x7FF8000000000000ll));
+                }
+                break;
+            }
+            if (nap < 8) nap++;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
+int launch_trisolve(lssp_amd_ctx *c, const TriSched &t, const double *rhs, double *x, double *reset)
+{
+    if (t.n == 0) return LSSP_AMD_OK;
+    long nchunks = (t.n + 63) / 64;
+    long grid = (long)c->num_cus * c->tri_blocks_per_cu;
+    long need = (nchunks + 3) / 4;
+    if (grid > need) grid = need;
+    TriArgs a{t.n, nchunks, t.perm, t.rp, t.cols, t.vals, t.diag, t.unit, rhs, x, reset, c->d_err};
+    k_trisolve<<<grid, 256, 0, c->stream>>>(a);
+    LSSP_HIP(hipGetLastError());
+    return LSSP_AMD_OK;
+}
+
+// halo: gather owned entries to send
+__global__ void k_pack(const int *idx, const double *x, double *buf, int n)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) buf[i] = x[idx[i]];
+}
+
+int launch_pack(lssp_amd_ctx *c, const int *idx, const double *x, double *buf, int n)
+{
+    if (n <= 0) return LSSP_AMD_OK;
+    k_pack<<<(n + 255) / 256, 256, 0, c->stream>>>(idx, x, buf, n);
+    LSSP_HIP(hipGetLastError());
+    return LSSP_AMD_OK;
+}
+
+}  // namespace lssp_amd

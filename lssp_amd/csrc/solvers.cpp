@@ -1,0 +1,577 @@
+// solvers.cpp -- BiCGSTAB, GMRES(m) and CG on device-resident vectors.
+//
+// Each driver replays the reference's scalar recurrences, guards, defaults and
+// iteration counting step for step (solver-bicgstab.cxx:10-175,
+// solver-gmres.cxx:12-255, solver-cg.cxx:8-136).  The inline host loops of the
+// reference become fused elementwise passes (kernels.hip, EwKind); every dot
+// or norm becomes a reduction whose finalize program updates the scalar
+// recurrence on the device, so an iteration runs without host round trips
+// and the host synchronises once per iteration (once per Arnoldi step in
+// GMRES) to test convergence, exactly where the reference branches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "internal.h"
+
+namespace lssp_amd {
+
+namespace {
+
+constexpr double BREAKDOWN = 1e-40;  // lssp.cxx:14
+constexpr int DEF_MAXIT = 1000;      // lssp.cxx:9
+constexpr int DEF_RESTART = 50;      // lssp.cxx:5
+constexpr double DEF_TOL = 1e-7;     // lssp.cxx:11-13
+
+enum EwK {  // mirror of kernels.hip EwKind
+    K_FILL = 0, K_COPY, K_AXY, K_AXPBY, K_AXPBYZ, K_SCALE, K_DIVS, K_DOT,
+    K_BICG_P, K_BICG_S, K_BICG_XR, K_CG_P, K_CG_XR, K_GM_MGS, K_GM_X
+};
+
+struct Run {
+    lssp_amd_ctx *c;
+    const lssp_amd_mat *A;
+    const lssp_amd_ilu *M;
+    long n = 0, nx = 0;
+    bool tree = true;
+    bool want_trace = false;
+    long tcap = 0;
+    long tl = 0;  // logical trace length
+    std::vector<std::pair<long, double>> patches;
+    std::vector<double *> bufs;
+    int rank = 0;
+
+    ~Run()
+    {
+        (void)hipStreamSynchronize(c->stream);
+        for (double *p : bufs) (void)hipFree(p);
+    }
+    double *vec(long len = -1)
+    {
+        double *p = nullptr;
+        if (hipMalloc(&p, sizeof(double) * std::max<long>(len < 0 ? nx : len, 1)) != hipSuccess) return nullptr;
+        bufs.push_back(p);
+        return p;
+    }
+    int T()
+    {
+        long p = tl++;
+        return (want_trace && p < tcap) ? (int)p : -1;
+    }
+    Fin fin(int op, int nsum, int t0 = -1, int t1 = -1, int dst0 = S_SUM0)
+    {
+        Fin f;
+        f.op = op;
+        f.nsum = nsum;
+        f.dst[0] = dst0;
+        f.tpos[0] = t0;
+        f.tpos[1] = t1;
+        return f;
+    }
+    int pc(double *x, const double *rhs)
+    {
+        if (!M) {
+            Ew e;
+            e.kind = K_COPY;
+            e.n = n;
+            e.x = rhs;
+            e.out0 = x;
+            return launch_ew(c, e);
+        }
+        LSSP_TRY(launch_trisolve(c, M->lower, rhs, M->d_cache, x));
+        return launch_trisolve(c, M->upper, M->d_cache, x, M->d_cache);
+    }
+    int sync(int first, int count)
+    {
+        LSSP_HIP(hipMemcpyAsync(c->h_scal + first, c->d_scal + first, sizeof(double) * count,
+                                hipMemcpyDeviceToHost, c->stream));
+        int e = 0;
+        LSSP_HIP(hipMemcpyAsync(&e, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        LSSP_HIP(hipStreamSynchronize(c->stream));
+        if (e) {
+            LSSP_HIP(hipMemset(c->d_err, 0, sizeof(int)));
+            return LSSP_AMD_ETIMEOUT;
+        }
+        return LSSP_AMD_OK;
+    }
+    double h(int i) const { return c->h_scal[i]; }
+    int spmv(int epi, double alpha, double *x, double beta, const double *y, double *z, int nred = 0,
+             const double *w0 = nullptr, const double *w1 = nullptr)
+    {
+        LSSP_TRY(halo_exchange(A, x));
+        return launch_spmv(c, A, epi, alpha, x, beta, y, z, tree ? nred : 0, w0, w1);
+    }
+    int ew(Ew e)
+    {
+        e.n = n;
+        e.scal = c->d_scal;
+        if (!tree) e.nred = 0;
+        return launch_ew(c, e);
+    }
+    int fin1(const double *a, const double *b, const Fin &f)
+    {
+        const double *A_[1] = {a}, *B_[1] = {b};
+        return finish_reduce(c, n, 1, A_, B_, f);
+    }
+    int fin2(const double *a0, const double *b0, const double *a1, const double *b1, const Fin &f)
+    {
+        const double *A_[2] = {a0, a1}, *B_[2] = {b0, b1};
+        return finish_reduce(c, n, 2, A_, B_, f);
+    }
+    int dot1(const double *a, const double *b, const Fin &f)
+    {
+        const double *A_[1] = {a}, *B_[1] = {b};
+        return reduce_dots(c, n, 1, A_, B_, f);
+    }
+};
+
+void defaults(const lssp_amd_solve_params &P, double &tol_rel, double &tol_abs, int &maxit)
+{
+    tol_rel = P.tol_rel < 0 ? DEF_TOL : P.tol_rel;
+    tol_abs = P.tol_abs < 0 ? DEF_TOL : P.tol_abs;
+    maxit = P.maxit <= 0 ? DEF_MAXIT : P.maxit;
+}
+
+// ---------------------------------------------------------------------------
+// BiCGSTAB, right preconditioned (solver-bicgstab.cxx:10-175)
+// ---------------------------------------------------------------------------
+int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits,
+             double *res_out)
+{
+    double tol_rel, tol_abs, tol_rb = P.tol_rb, tol;
+    int maxit, it;
+    defaults(P, tol_rel, tol_abs, maxit);
+    if (P.verb >= 2 && R.rank == 0) {
+        printf("bicgstab: maximal iteration: %d\n", maxit);
+        printf("bicgstab: tolerance abs: %g\n", tol_abs);
+        printf("bicgstab: tolerance rel: %g\n", tol_rel);
+        printf("bicgstab: tolerance rbn: %g\n", tol_rb);
+    }
+    double *r = R.vec(), *rh = R.vec(), *p = R.vec(), *ph = R.vec();
+    double *s = R.vec(), *sh = R.vec(), *t = R.vec(), *v = R.vec();
+    if (!r || !rh || !p || !ph || !s || !sh || !t || !v) return LSSP_AMD_ENOMEM;
+
+    LSSP_TRY(R.spmv(EPI_AXPBY, -1, x, 1, b, r));  // :67
+    {
+        Ew e;
+        e.kind = K_COPY;
+        e.x = r;
+        e.out0 = rh;
+        LSSP_TRY(R.ew(e));  // :68-71 (the sh/ph zero fill is dead work)
+    }
+    LSSP_TRY(R.dot1(b, b, R.fin(FIN_NORM, 1, R.T(), -1, S_BNORM)));  // :73
+    LSSP_TRY(R.dot1(r, r, R.fin(FIN_NORM, 1, R.T(), -1, S_RES)));    // :76
+    LSSP_TRY(R.sync(0, 16));
+    const double b_norm = R.h(S_BNORM);
+    tol_rb *= b_norm;
+    double res = R.h(S_RES);
+    const double err_rel = res;
+    if (res <= tol_abs) {
+        *nits = 0;
+        *res_out = res;
+        return LSSP_AMD_OK;
+    }
+    tol = res * tol_rel;
+    if (tol < tol_abs) tol = tol_abs;
+    if (tol < tol_rb) tol = tol_rb;
+
+    LSSP_TRY(R.dot1(r, rh, R.fin(FIN_BICG_RHO, 1, R.T())));  // :87 (first iteration)
+    LSSP_TRY(R.sync(0, 16));
+    double rho1 = R.h(S_RHO1);
+    bool pending_rho = false;  // a fused next-iteration rho1 sits in the trace
+
+    for (it = 0; it < maxit; it++) {
+        pending_rho = false;
+        if (rho1 == 0) {  // :89-92
+            if (R.rank == 0) printf("bicgstab: method failed.!\n");
+            break;
+        }
+        Ew e;
+        if (it == 0) {
+            e.kind = K_COPY;  // :96
+            e.x = r;
+            e.out0 = p;
+        } else {
+            e.kind = K_BICG_P;  // :99-102
+            e.x = r;
+            e.y = v;
+            e.out0 = p;
+        }
+        LSSP_TRY(R.ew(e));
+        LSSP_TRY(R.pc(ph, p));                                   // :107-108
+        LSSP_TRY(R.spmv(EPI_AMX, 1, ph, 0, p, v, 1, rh));         // :110
+        LSSP_TRY(R.fin1(rh, v, R.fin(FIN_BICG_ALPHA, 1, R.T())));  // :112
+        e = Ew();
+        e.kind = K_BICG_S;  // :113-115
+        e.x = r;
+        e.y = v;
+        e.out0 = s;
+        e.nred = 1;
+        e.r0a = s;
+        e.r0b = s;
+        LSSP_TRY(R.ew(e));
+        const long pos_s = R.tl;
+        LSSP_TRY(R.fin1(s, s, R.fin(FIN_BICG_S, 1, R.T())));  // :117
+        LSSP_TRY(R.pc(sh, s));                                 // :130-131
+        LSSP_TRY(R.spmv(EPI_AMX, 1, sh, 0, p, t, 2, s, nullptr));  // :133
+        {
+            int t0 = R.T(), t1 = R.T();
+            LSSP_TRY(R.fin2(t, s, t, t, R.fin(FIN_BICG_OMEGA, 2, t0, t1)));  // :135
+        }
+        e = Ew();
+        e.kind = K_BICG_XR;  // :136-139
+        e.out0 = x;
+        e.x = ph;
+        e.y = sh;
+        e.out1 = r;
+        e.u = s;
+        e.v = t;
+        e.nred = 2;
+        e.r0a = r;
+        e.r0b = r;
+        e.r1a = r;
+        e.r1b = rh;
+        LSSP_TRY(R.ew(e));
+        {
+            int t0 = R.T(), t1 = R.T();
+            LSSP_TRY(R.fin2(r, r, r, rh, R.fin(FIN_BICG_RES_RHO, 2, t0, t1)));  // :141, next :87
+        }
+        LSSP_TRY(R.sync(0, 16));
+        if (R.h(S_BREAK) != 0.0) {  // :117-128 -- x += alpha*ph already done on the device
+            if (R.rank == 0) printf("bicgstab: ||s|| is too small: %f, terminated.\n", R.h(S_SNORM));
+            R.tl = pos_s + 1;
+            long q = R.tl++;
+            R.patches.push_back({q, R.h(S_SNORM)});  // the reference evaluates the norm again (:118)
+            LSSP_TRY(R.spmv(EPI_AXPBY, -1, x, 1, b, r));  // :124
+            LSSP_TRY(R.dot1(r, r, R.fin(FIN_NORM, 1, R.T(), -1, S_RES)));
+            LSSP_TRY(R.sync(0, 16));
+            res = R.h(S_RES);
+            break;
+        }
+        pending_rho = true;
+        res = R.h(S_RES);
+        if (P.verb >= 1 && R.rank == 0)
+            printf("bicgstab: itr: %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", it, res,
+                   (err_rel == 0 ? 0 : res / err_rel), (b_norm == 0 ? 0 : res / b_norm));
+        if (res <= tol) break;  // :149
+        rho1 = R.h(S_RHO1);
+    }
+    if (pending_rho) R.tl--;  // the fused next-iteration rho1 is not part of the reference's run
+    if (it < maxit) it += 1;  // :152
+    if (P.verb >= 2 && R.rank == 0) printf("bicgstab: total iteration: %d\n", it);
+    *nits = it;
+    *res_out = res;
+    return LSSP_AMD_OK;
+}
+
+// ---------------------------------------------------------------------------
+// CG (solver-cg.cxx:8-136)
+// ---------------------------------------------------------------------------
+int cg(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
+{
+    double tol_rel, tol_abs, tol_rb = P.tol_rb, tol;
+    int maxit, it;
+    defaults(P, tol_rel, tol_abs, maxit);
+    if (P.verb >= 2 && R.rank == 0) {
+        printf("cg: maximal iteration: %d\n", maxit);
+        printf("cg: tolerance abs: %g\n", tol_abs);
+        printf("cg: tolerance rel: %g\n", tol_rel);
+        printf("cg: tolerance rbn: %g\n", tol_rb);
+    }
+    double *r = R.vec(), *p = R.vec(), *q = R.vec();
+    double *z = R.M ? R.vec() : r;  // PC_NON copies r into z (pc.cxx:67-70): alias instead
+    if (!r || !p || !q || !z) return LSSP_AMD_ENOMEM;
+
+    LSSP_TRY(R.dot1(b, b, R.fin(FIN_NORM, 1, R.T(), -1, S_BNORM)));  // :231
+    LSSP_TRY(R.spmv(EPI_AXPBY, -1, x, 1, b, r));                      // :234
+    LSSP_TRY(R.dot1(r, r, R.fin(FIN_NORM, 1, R.T(), -1, S_RES)));    // :235
+    LSSP_TRY(R.sync(0, 16));
+    const double b_norm = R.h(S_BNORM);
+    tol_rb *= b_norm;
+    double res = R.h(S_RES);
+    if (res <= tol_abs) {
+        *nits = 0;
+        *res_out = res;
+        return LSSP_AMD_OK;
+    }
+    const double err_rel = res;
+    tol = tol_rel * err_rel;
+    if (tol < tol_abs) tol = tol_abs;
+    if (tol < tol_rb) tol = tol_rb;
+    bool pending_rho = false;
+
+    for (it = 0; it < maxit; it++) {
+        pending_rho = false;
+        if (R.M) {
+            LSSP_TRY(R.pc(z, r));                                   // :79
+            LSSP_TRY(R.dot1(z, r, R.fin(FIN_CG_RHO, 1, R.T())));   // :80
+        } else if (it == 0) {
+            LSSP_TRY(R.dot1(r, r, R.fin(FIN_CG_RHO, 1, R.T())));
+        }
+        Ew e;
+        if (it == 0) {
+            e.kind = K_COPY;  // :83-86
+            e.x = z;
+            e.out0 = p;
+        } else {
+            e.kind = K_CG_P;  // :88-92
+            e.x = z;
+            e.out0 = p;
+        }
+        LSSP_TRY(R.ew(e));
+        LSSP_TRY(R.spmv(EPI_MXY, 1, p, 0, nullptr, q, 1, p));        // :95
+        LSSP_TRY(R.fin1(q, p, R.fin(FIN_CG_ALPHA, 1, R.T())));      // :96-99
+        e = Ew();
+        e.kind = K_CG_XR;  // :101-104
+        e.out0 = x;
+        e.x = p;
+        e.out1 = r;
+        e.y = q;
+        e.nred = 1;
+        e.r0a = r;
+        e.r0b = r;
+        LSSP_TRY(R.ew(e));
+        if (R.M) {
+            LSSP_TRY(R.fin1(r, r, R.fin(FIN_CG_RES, 1, R.T())));  // :106
+        } else {
+            int t0 = R.T(), t1 = R.T();
+            LSSP_TRY(R.fin1(r, r, R.fin(FIN_CG_RES_RHO, 1, t0, t1)));  // :106, next :80 (z == r)
+            pending_rho = true;
+        }
+        LSSP_TRY(R.sync(0, 16));
+        res = R.h(S_RES);
+        if (P.verb >= 1 && R.rank == 0)
+            printf("cg: itr: %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", it, res,
+                   (err_rel == 0 ? 0 : res / err_rel), (b_norm == 0 ? 0 : res / b_norm));
+        if (res <= tol) break;  // :109
+    }
+    if (pending_rho) R.tl--;
+    if (it < maxit) it += 1;
+    if (P.verb >= 2 && R.rank == 0) printf("cg: total iteration: %d\n", it);
+    *nits = it;
+    *res_out = res;
+    return LSSP_AMD_OK;
+}
+
+// ---------------------------------------------------------------------------
+// GMRES(m), left preconditioned, MGS Arnoldi, Givens on the host
+// (solver-gmres.cxx:12-255)
+// ---------------------------------------------------------------------------
+int gmres(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
+{
+    lssp_amd_ctx *c = R.c;
+    double tol_rel, tol_abs, tol_rb = P.tol_rb;
+    int maxit;
+    defaults(P, tol_rel, tol_abs, maxit);
+    int m = P.restart < 0 ? DEF_RESTART : P.restart;
+    if (tol_rb < 0) tol_rb = DEF_TOL;
+    if (m <= 0) return LSSP_AMD_EINVAL;
+    if (S_H + 2 * m + 2 > NSCAL) return LSSP_AMD_EUNSUPPORTED;  // Hessenberg column + ym staging
+    if (P.verb >= 2 && R.rank == 0) {
+        printf("gmres: restart parameter m: %d\n", m);
+        printf("gmres: maximal iteration: %d\n", maxit);
+        printf("gmres: tolerance abs: %g\n", tol_abs);
+        printf("gmres: tolerance rel: %g\n", tol_rel);
+        printf("gmres: tolerance rbn: %g\n", tol_rb);
+    }
+    double *wj = R.vec(), *rg = R.vec();
+    double *V = R.vec(R.nx * (long)m);
+    double *d_ym = R.vec(m);
+    if (!wj || !rg || !V || !d_ym) return LSSP_AMD_ENOMEM;
+    auto Vi = [&](int i) { return V + (long)i * R.nx; };
+    std::vector<double> H((size_t)(m + 1) * m), gg(m + 1), cs(m), sn(m), ym(m);
+    auto HG = [&](int row, int col) -> double & { return H[(size_t)row * m + col]; };
+
+    LSSP_TRY(R.dot1(b, b, R.fin(FIN_NORM, 1, R.T(), -1, S_BNORM)));  // :85
+    LSSP_TRY(R.spmv(EPI_AXPBY, -1, x, 1, b, rg));                     // :88
+    LSSP_TRY(R.dot1(rg, rg, R.fin(FIN_NORM, 1, R.T(), -1, S_RES)));  // :89
+    LSSP_TRY(R.sync(0, 16));
+    const double b_norm = R.h(S_BNORM);
+    tol_rb *= b_norm;
+    double beta = R.h(S_RES);
+    int inner = 0;
+    if (beta <= tol_abs) {
+        *nits = 0;
+        *res_out = beta;
+        return LSSP_AMD_OK;
+    }
+    const double err_rel = beta;
+    double tol = tol_rel * err_rel;
+    if (tol < tol_abs) tol = tol_abs;
+    if (tol < tol_rb) tol = tol_rb;
+    const double rtol = tol / beta;
+    double gstol = 0.;
+
+    while (inner < maxit) {
+        int i, kk;
+        double gs_norm = 0.;
+        const bool first_cycle = inner == 0;
+        LSSP_TRY(R.pc(Vi(0), rg));                                             // :112-113
+        LSSP_TRY(R.dot1(Vi(0), Vi(0), R.fin(FIN_NORM, 1, R.T(), -1, S_TMP)));  // :115
+        {
+            Ew e;
+            e.kind = K_DIVS;  // :129-131
+            e.out0 = Vi(0);
+            e.sidx = S_TMP;
+            LSSP_TRY(R.ew(e));
+        }
+        std::fill(gg.begin(), gg.end(), 0.0);
+        std::fill(H.begin(), H.end(), 0.0);
+        bool have_beta = false;
+        for (i = 0; i < m; i++) {
+            inner++;
+            LSSP_TRY(R.spmv(EPI_MXY, 1, Vi(i), 0, nullptr, rg));  // :138
+            LSSP_TRY(R.pc(wj, rg));                                // :139-140
+            LSSP_TRY(R.dot1(wj, Vi(0), R.fin(FIN_STORE, 1, R.T(), -1, S_H)));  // :143, j = 0
+            for (int j = 0; j <= i; j++) {  // :142-147, axpy fused with the next dot / the norm
+                Ew e;
+                e.kind = K_GM_MGS;
+                e.out0 = wj;
+                e.x = Vi(j);
+                e.sidx = S_H + j;
+                e.nred = 1;
+                e.r0a = wj;
+                e.r0b = j < i ? Vi(j + 1) : wj;
+                LSSP_TRY(R.ew(e));
+                if (j < i)
+                    LSSP_TRY(R.fin1(wj, Vi(j + 1), R.fin(FIN_STORE, 1, R.T(), -1, S_H + j + 1)));
+                else
+                    LSSP_TRY(R.fin1(wj, wj, R.fin(FIN_NORM, 1, R.T(), -1, S_H + i + 1)));  // :149
+            }
+            LSSP_TRY(R.sync(0, S_H + i + 2));
+            if (!have_beta) {
+                beta = R.h(S_TMP);
+                gg[0] = beta;  // :116
+                if (first_cycle) gstol = rtol * beta * 0.5;  // :121-123
+                have_beta = true;
+            }
+            for (int j = 0; j <= i; j++) HG(j, i) = R.h(S_H + j);
+            const double hij = R.h(S_H + i + 1);
+            HG(i + 1, i) = hij;
+            if (std::fabs(hij) <= BREAKDOWN) {  // :152-155
+                i--;
+                break;
+            } else if (i + 1 < m) {
+                Ew e;
+                e.kind = K_AXY;  // :157
+                e.a = 1 / hij;
+                e.x = wj;
+                e.out0 = Vi(i + 1);
+                LSSP_TRY(R.ew(e));
+            }
+            for (int j = 0; j < i; j++) {  // :160-166
+                const double h1 = cs[j] * HG(j, i) + sn[j] * HG(j + 1, i);
+                const double h2 = -sn[j] * HG(j, i) + cs[j] * HG(j + 1, i);
+                HG(j, i) = h1;
+                HG(j + 1, i) = h2;
+            }
+            double gma = std::sqrt(HG(i, i) * HG(i, i) + HG(i + 1, i) * HG(i + 1, i));  // :168
+            if (std::fabs(gma) == 0.) gma = 1e-20;
+            cs[i] = HG(i, i) / gma;
+            sn[i] = HG(i + 1, i) / gma;
+            gg[i + 1] = -sn[i] * gg[i];
+            gg[i] = cs[i] * gg[i];
+            HG(i, i) = cs[i] * HG(i, i) + sn[i] * HG(i + 1, i);
+            gs_norm = std::fabs(gg[i + 1]);
+            if (gs_norm <= gstol) break;  // :179-181
+        }
+        if (!have_beta) {  // (i == 0 breakdown without a sync is impossible; kept for safety)
+            LSSP_TRY(R.sync(0, 16));
+            beta = R.h(S_TMP);
+            gg[0] = beta;
+            if (first_cycle) gstol = rtol * beta * 0.5;
+        }
+        kk = i == m ? m : i + 1;  // :185
+        for (i = kk - 1; i >= 0; i--) {  // :186-194
+            ym[i] = gg[i] / HG(i, i);
+            for (int j = 0; j < i; j++) gg[j] = gg[j] - ym[i] * HG(j, i);
+        }
+        if (kk > 0) {
+            memcpy(c->h_scal + NSCAL - m, ym.data(), sizeof(double) * kk);
+            LSSP_HIP(hipMemcpyAsync(d_ym, c->h_scal + NSCAL - m, sizeof(double) * kk,
+                                    hipMemcpyHostToDevice, c->stream));
+        }
+        {
+            Ew e;
+            e.kind = K_GM_X;  // :196-204
+            e.out0 = x;
+            e.vbase = V;
+            e.k = kk;
+            e.u = d_ym;
+            e.b = (double)R.nx;  // basis stride
+            LSSP_TRY(R.ew(e));
+        }
+        LSSP_TRY(R.spmv(EPI_AXPBY, -1, x, 1, b, rg));                     // :206
+        LSSP_TRY(R.dot1(rg, rg, R.fin(FIN_NORM, 1, R.T(), -1, S_RES)));  // :207
+        LSSP_TRY(R.sync(0, 16));
+        beta = R.h(S_RES);
+        if (P.verb >= 1 && R.rank == 0)
+            printf("gmres: itr: %4d / %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", inner, inner, beta,
+                   (err_rel == 0 ? 0 : beta / err_rel), (b_norm == 0 ? 0 : beta / b_norm));
+        if (beta <= tol) break;                                  // :215-217
+        gstol = rtol * gs_norm / (beta / err_rel) * 0.5;          // :220
+    }
+    if (P.verb >= 2 && R.rank == 0) printf("gmres: total iteration: %d\n", inner);
+    *nits = inner;
+    *res_out = beta;
+    return LSSP_AMD_OK;
+}
+
+}  // namespace
+}  // namespace lssp_amd
+
+using namespace lssp_amd;
+
+extern "C" int lssp_amd_solve(lssp_amd_ctx *c, const lssp_amd_mat *A, const lssp_amd_ilu *M,
+                              const lssp_amd_solve_params *prm, double *x, const double *b, int *nits,
+                              double *residual, double *trace, int trace_cap, int *trace_len)
+{
+    if (!c || !A || !prm || !x || !b) return LSSP_AMD_EINVAL;
+    if (A->nrows != A->ncols - A->nhalo) return LSSP_AMD_EINVAL;  // square (lssp.cxx:152)
+    if (M && M->n != A->nrows) return LSSP_AMD_EINVAL;
+    LSSP_HIP(hipSetDevice(c->device));
+    Run R;
+    R.c = c;
+    R.A = A;
+    R.M = M;
+    R.n = A->nrows;
+    R.nx = (long)A->nrows + A->nhalo;
+    R.tree = c->reduce_mode == LSSP_AMD_REDUCE_TREE;
+    R.want_trace = trace && trace_cap > 0;
+    R.tcap = R.want_trace ? trace_cap : 0;
+    R.rank = c->rank;
+    if (R.want_trace && c->trace_cap < trace_cap) {
+        LSSP_HIP(hipStreamSynchronize(c->stream));
+        if (c->d_trace) LSSP_HIP(hipFree(c->d_trace));
+        LSSP_HIP(hipMalloc(&c->d_trace, sizeof(double) * trace_cap));
+        c->trace_cap = trace_cap;
+    }
+    double *saved_trace = c->d_trace;
+    if (!R.want_trace) c->d_trace = nullptr;
+    LSSP_HIP(hipMemsetAsync(c->d_scal, 0, sizeof(double) * NSCAL, c->stream));
+    int it = 0, st;
+    double res = 0;
+    switch (prm->solver) {
+    case LSSP_AMD_BICGSTAB: st = bicgstab(R, *prm, x, b, &it, &res); break;
+    case LSSP_AMD_CG: st = cg(R, *prm, x, b, &it, &res); break;
+    case LSSP_AMD_GMRES: st = gmres(R, *prm, x, b, &it, &res); break;
+    default: st = LSSP_AMD_EUNSUPPORTED;
+    }
+    c->d_trace = saved_trace;
+    if (st != LSSP_AMD_OK) return st;
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    if (nits) *nits = it;
+    if (residual) *residual = res;
+    if (R.want_trace) {
+        long len = std::min<long>(R.tl, trace_cap);
+        if (len > 0)
+            LSSP_HIP(hipMemcpy(trace, c->d_trace, sizeof(double) * len, hipMemcpyDeviceToHost));
+        for (auto &pq : R.patches)
+            if (pq.first < trace_cap) trace[pq.first] = pq.second;
+    }
+    if (trace_len) *trace_len = (int)R.tl;
+    return LSSP_AMD_OK;
+}

@@ -63,9 +63,13 @@ def rand_csr(n: int, per_row: int, seed: int, unsorted=True, missing_diag_every=
 
 
 def digest(*arrays) -> str:
+    """sha256 over dtype + bytes; every NaN is canonicalised first (x86 and
+    gfx950 produce default NaNs of opposite sign, both are "NaN" results)"""
     h = hashlib.sha256()
     for a in arrays:
         a = np.ascontiguousarray(a)
+        if a.dtype.kind == "f" and np.isnan(a).any():
+            a = np.where(np.isnan(a), np.float64(np.nan), a)
         h.update(str(a.dtype).encode())
         h.update(a.tobytes())
     return h.hexdigest()

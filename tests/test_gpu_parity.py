@@ -1,0 +1,188 @@
+"""HIP path vs the reference (tests/golden/) and vs the CPU oracle.
+
+All comparisons are bitwise except where a test says otherwise:
+  * SpMV, BLAS-1 and ILU setup/apply against the reference's own outputs;
+  * solvers in SERIAL reduction mode against the reference's full scalar trace
+    (every dot and norm), iteration count, residual and solution;
+  * solvers in TREE mode (the fast path) against the oracle restating the same
+    canonical reduction order.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from golden_util import build_matrix, case_id, cases, fx, matches, vec
+from inputs import uniform
+
+pytestmark = pytest.mark.gpu
+
+SPMV = cases("spmv")
+ILU = cases("ilu")
+SOLVE = cases("solve")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import lssp_amd
+    d = lssp_amd.Device(0)
+    yield d
+    d.close()
+
+
+def _ilu_kw(pc, n):
+    if pc["kind"] == "iluk":
+        return dict(kind=1, level=pc["level"])
+    if pc["kind"] == "ilut":
+        return dict(kind=2, tol=pc["tol"], p=pc["p"])
+    return dict(kind=1, level=0, blk=(n + pc["nblk"] - 1) // pc["nblk"])
+
+
+@pytest.mark.parametrize("c", SPMV, ids=[case_id(c) for c in SPMV])
+def test_spmv_bitwise_vs_reference(dev, c):
+    import lssp_amd
+    A = build_matrix(c["mat"])
+    M = lssp_amd.DMat(dev, A.Ap, A.Aj, A.Ax)
+    x = dev.vec(A.n, uniform(c["xseed"], A.n))
+    y = dev.vec(A.n, uniform(c["yseed"], A.n))
+    z = dev.vec(A.n, uniform(c["yseed"], A.n))
+    a, b = fx(c["alpha"]), fx(c["beta"])
+    op = c["op"]
+    if op == 0:
+        M.mv_mxy(x, z)
+    elif op == 1:
+        M.mv_amxy(a, x, z)
+    elif op == 2:
+        M.mv_amxpby(a, x, b, z)
+    else:
+        M.mv_amxpbyz(a, x, b, y, z)
+    assert matches(c["out"], z.download())
+
+
+@pytest.mark.parametrize("c", ILU, ids=[case_id(c) for c in ILU])
+def test_ilu_setup_and_apply_bitwise_vs_reference(dev, c):
+    import lssp_amd
+    A = build_matrix(c["mat"])
+    M = lssp_amd.DILU.create(dev, A.Ap, A.Aj, A.Ax, **_ilu_kw(c["pc"], A.n))
+    (Lp, Lj, Lx), (Up, Uj, Ux) = M.factors()
+    assert matches(c["L"], Lp, Lj, Lx)
+    assert matches(c["U"], Up, Uj, Ux)
+    rhs = uniform(c["rhs_seed"], A.n)
+    x = dev.vec(A.n)
+    r = dev.vec(A.n, rhs)
+    M.apply(x, r)
+    assert matches(c["apply"], x.download())
+    M.apply(r, r)  # x may alias rhs (solver-tri.cxx:48-55 goes through pc->cache)
+    assert matches(c["apply"], r.download())
+
+
+def _solve_inputs(dev, c):
+    import lssp_amd
+    A = build_matrix(c["mat"])
+    Ap, Aj, Ax = lssp_amd.sort_columns(A.Ap, A.Aj, A.Ax)  # lssp.cxx:173
+    D = lssp_amd.DMat(dev, Ap, Aj, Ax)
+    M = None
+    if c["pc"]["kind"] != "none":
+        M = lssp_amd.DILU.create(dev, A.Ap, A.Aj, A.Ax, **_ilu_kw(c["pc"], A.n))
+    b = dev.vec(A.n, vec(c["b"], A.n))
+    x = dev.vec(A.n, np.zeros(A.n) if c["x0"] is None else vec(c["x0"], A.n))
+    return A, D, M, x, b
+
+
+@pytest.mark.parametrize("c", SOLVE, ids=[case_id(c) for c in SOLVE])
+def test_solver_serial_mode_trace_bitwise_vs_reference(dev, c):
+    """SERIAL reduction mode reproduces the reference run bit for bit."""
+    import lssp_amd
+    dev.set_reduction(lssp_amd.SERIAL)
+    try:
+        A, D, M, x, b = _solve_inputs(dev, c)
+        r = lssp_amd.solve(dev, D, M, x, b, solver=c["solver"], tol_rel=fx(c["rtol"]), tol_abs=fx(c["atol"]),
+                           tol_rb=fx(c["rbtol"]), maxit=c["maxit"], restart=c["restart"], trace_cap=100000)
+    finally:
+        dev.set_reduction(lssp_amd.TREE)
+    assert r.nits == c["nits"]
+    assert r.residual == fx(c["residual"])
+    assert matches(c["trace"], r.trace)
+    assert matches(c["x"], x.download())
+
+
+TREE_CASES = [c for c in SOLVE if c["mat"].get("N", 0) <= 64 or c["mat"]["type"] == "rand"]
+
+
+@pytest.mark.parametrize("c", TREE_CASES, ids=[case_id(c) for c in TREE_CASES])
+def test_solver_tree_mode_bitwise_vs_oracle(dev, c):
+    """The fast path: canonical tree reductions, bitwise equal to the oracle's
+    restatement of the same order; iteration count within 1 of the reference."""
+    import lssp_amd
+    A, D, M, x, b = _solve_inputs(dev, c)
+    r = lssp_amd.solve(dev, D, M, x, b, solver=c["solver"], tol_rel=fx(c["rtol"]), tol_abs=fx(c["atol"]),
+                       tol_rb=fx(c["rbtol"]), maxit=c["maxit"], restart=c["restart"], trace_cap=100000)
+    L = U = None
+    if M is not None:
+        (Lp, Lj, Lx), (Up, Uj, Ux) = M.factors()
+        L, U = O.CSR(A.n, Lp, Lj, Lx), O.CSR(A.n, Up, Uj, Ux)
+    x0 = None if c["x0"] is None else vec(c["x0"], A.n)
+    o = O.solve(c["solver"], A, vec(c["b"], A.n), x0=x0, L=L, U=U, rtol=fx(c["rtol"]), atol=fx(c["atol"]),
+                rbtol=fx(c["rbtol"]), maxit=c["maxit"], restart=c["restart"], mode=O.TREE)
+    assert r.nits == o.nits
+    assert r.residual == o.residual
+    assert np.array_equal(r.trace, o.trace)
+    assert np.array_equal(x.download(), o.x)
+    assert abs(r.nits - c["nits"]) <= max(1, c["nits"] // 20)
+
+
+@pytest.mark.parametrize("n", [1, 255, 256, 257, 4099, 100000, 1 << 20])
+def test_dot_norm_tree_and_serial(dev, n):
+    import lssp_amd
+    xh, yh = uniform(5, n), uniform(6, n)
+    x, y = dev.vec(n, xh), dev.vec(n, yh)
+    import ctypes
+    out = ctypes.c_double()
+    for mode in (lssp_amd.TREE, lssp_amd.SERIAL):
+        dev.set_reduction(mode)
+        assert dev.L.lssp_amd_vec_dot(dev.h, x.ptr, y.ptr, n, ctypes.byref(out)) == 0
+        assert out.value == O.dot(xh, yh, mode)
+        assert dev.L.lssp_amd_vec_norm(dev.h, x.ptr, n, ctypes.byref(out)) == 0
+        assert out.value == np.sqrt(O.dot(xh, xh, mode))
+    dev.set_reduction(lssp_amd.TREE)
+
+
+def test_blas1_bitwise(dev):
+    n = 100003
+    xh, yh, zh = uniform(1, n), uniform(2, n), uniform(3, n)
+    a, b = -0.375, 1.625
+    L = dev.L
+    x, y, z = dev.vec(n, xh), dev.vec(n, yh), dev.vec(n, zh)
+    assert L.lssp_amd_vec_axpby(dev.h, a, x.ptr, b, y.ptr, n) == 0
+    assert np.array_equal(y.download(), yh * b + xh * a)          # vector.cxx:98-107
+    assert L.lssp_amd_vec_axpbyz(dev.h, a, x.ptr, b, z.ptr, y.ptr, n) == 0
+    assert np.array_equal(y.download(), zh * b + xh * a)          # :110-120
+    assert L.lssp_amd_vec_axy(dev.h, a, x.ptr, y.ptr, n) == 0
+    assert np.array_equal(y.download(), xh * a)                   # :86-95
+    assert L.lssp_amd_vec_scale(dev.h, x.ptr, n, b) == 0
+    assert np.array_equal(x.download(), xh * b)                   # :141-146
+    assert L.lssp_amd_vec_copy(dev.h, y.ptr, z.ptr, n) == 0
+    assert np.array_equal(y.download(), zh)
+    assert L.lssp_amd_vec_set_value(dev.h, y.ptr, n, 2.5) == 0
+    assert np.all(y.download() == 2.5)
+
+
+@pytest.mark.parametrize("N,kind,kw", [(48, 1, dict(level=0)), (40, 1, dict(level=1)),
+                                        (32, 2, dict(tol=1e-4, p=20))])
+def test_trisolve_sweeps_and_levels_vs_oracle(dev, N, kind, kw):
+    import lssp_amd
+    A = O.poisson(3, N)
+    M = lssp_amd.DILU.create(dev, A.Ap, A.Aj, A.Ax, kind=kind, **kw)
+    if kind == 1 and kw["level"] == 0:
+        assert M.levelsL == 3 * N - 2 and M.levelsU == 3 * N - 2
+    (Lp, Lj, Lx), (Up, Uj, Ux) = M.factors()
+    rhs = uniform(99, A.n)
+    r = dev.vec(A.n, rhs)
+    x = dev.vec(A.n)
+    for which, (P, J, X) in [(0, (Lp, Lj, Lx)), (1, (Up, Uj, Ux))]:
+        M.trisolve(which, x, r)
+        ref = np.zeros(A.n)
+        O.lib().orc_trisolve(which, A.n, O._ptr(P), O._ptr(J), O._ptr(X), O._ptr(ref), O._ptr(rhs))
+        assert np.array_equal(x.download(), ref)
+    for _ in range(3):  # repeated applies: the sentinel re-arming must hold
+        M.apply(x, r)
+        assert np.array_equal(x.download(), O.ilu_apply(O.CSR(A.n, Lp, Lj, Lx), O.CSR(A.n, Up, Uj, Ux), rhs))
