@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Benchmark of the LSSP Krylov hot path on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--grid 216]
+
+Workload: 7-point Poisson on a 216^3 grid (n = 10,077,696 rows, 70,263,936
+nnz -- the "n=10M" of BASELINE.json), fp64, b = 1, x0 = 0, BiCGSTAB with an
+ILUK(0) preconditioner (solver-bicgstab.cxx, pc-iluk.cxx).  One STEP is one
+BiCGSTAB iteration: 2 SpMV, 2 ILU applies (4 triangular sweeps), 4 dots and
+2 norms.  The solve runs with zero tolerances, so it performs exactly the
+requested number of iterations.  value = iterations per second of the whole
+job.  With N > 1 (torchrun, one process per GPU) the same global matrix is
+row-partitioned into N z-slabs (strong scaling); halos move with RCCL
+send/recv and dots with an RCCL all-gather; the preconditioner becomes
+block-Jacobi ILU(0) per slab (the reference's blk_size path).
+
+The roofline object describes the metric's SpMV kernel, y = A x
+(lssp_mv_mxy), timed live with HIP events on the library's stream.
+cpu_baseline is the REFERENCE itself (oracle/_ref/libref.so, compiled from
+/root/reference, g++ -O2, 1 core) on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def spmv_bytes(nnz: int, n: int) -> int:
+    """algorithmic bytes of y = A x: Ax 8 + Aj 4 per nnz, Ap 4 + x 8 + y 8 per row"""
+    return 12 * nnz + 20 * n + 4
+
+
+def build_local(N: int, rank: int, P: int):
+    import lssp_amd
+    n = N ** 3
+    blk = (n + P - 1) // P
+    row0 = min(rank * blk, n)
+    nl = min(blk, n - row0)
+    Ap, Aj, Ax = lssp_amd.poisson(3, N, row0, nl)
+    return n, row0, nl, Ap, Aj, Ax
+
+
+def local_block(Ap, Aj, Ax, row0, nl):
+    """the rank's diagonal block (block-Jacobi, pc-iluk.cxx:441-447)"""
+    keep = (Aj >= row0) & (Aj < row0 + nl)
+    rows = np.repeat(np.arange(nl), np.diff(Ap))
+    cnt = np.bincount(rows[keep], minlength=nl)
+    bp = np.zeros(nl + 1, np.int32)
+    np.cumsum(cnt, out=bp[1:])
+    return bp, (Aj[keep] - row0).astype(np.int32), Ax[keep]
+
+
+def cpu_baseline(N: int, iters: int):
+    """The reference on a bounded sample: SpMV reps + BiCGSTAB+ILU(0) iterations."""
+    import oracle as O
+    if not O.ref_available():
+        return None
+    A = O.poisson(3, N)
+    x = np.random.default_rng(0).uniform(-1, 1, A.n)
+    z = np.zeros(A.n)
+    R = O.ref()
+    O.ref_spmv(0, A, x, z=z)
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        O.ref_spmv(0, A, x, z=z)
+    t_spmv = (time.perf_counter() - t0) / reps
+    b = np.ones(A.n)
+    r = O.ref_solve(O.BICGSTAB, A, b, pc=O.PC_ILUK, level=0, rtol=0.0, atol=0.0, rbtol=0.0, maxit=iters,
+                    trace_cap=16)
+    del R
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next(line.split(":", 1)[1].strip() for line in f if line.startswith("model name"))
+    except Exception:
+        pass
+    return {"value": round(r.nits / r.t_solve, 4), "unit": "iters/s", "cores": 1, "kind": "reference",
+            "sample": f"reference lssp_solver_solve BiCGSTAB+ILUK(0) on the same 7-pt {N}^3 system, "
+                      f"{r.nits} iterations in {r.t_solve:.2f} s (ILU setup {r.t_setup:.2f} s, not counted); "
+                      f"lssp_mv_mxy {t_spmv * 1e3:.1f} ms = {spmv_bytes(A.nnz, A.n) / t_spmv / 1e9:.2f} GB/s",
+            "spmv_gbps": round(spmv_bytes(A.nnz, A.n) / t_spmv / 1e9, 3),
+            "cpu_model": cpu, "host_cpus": os.cpu_count()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--grid", type=int, default=216)
+    ap.add_argument("--spmv-reps", type=int, default=50)
+    ap.add_argument("--cpu-iters", type=int, default=8)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")  # control plane only; the data path is RCCL in the library
+    torch.cuda.set_device(local_rank)
+
+    import lssp_amd
+    dev = lssp_amd.Device(local_rank)
+    if world > 1:
+        uid = [lssp_amd.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        dev.comm_init(world, rank, uid[0])
+
+    N = args.grid
+    t_setup0 = time.perf_counter()
+    n, row0, nl, Ap, Aj, Ax = build_local(N, rank, world)
+    if world > 1:
+        A = lssp_amd.DMat(dev, Ap, Aj, Ax, dist=(n, row0))
+        bp, bj, bx = local_block(Ap, Aj, Ax, row0, nl)
+        M = lssp_amd.DILU.create(dev, bp, bj, bx, kind=lssp_amd.ILUK, level=0)
+    else:
+        A = lssp_amd.DMat(dev, Ap, Aj, Ax)
+        M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=0)
+    nnz_local = int(Ap[-1])
+    x = dev.vec(A.nx, np.zeros(A.nx))
+    b = dev.vec(A.nx, np.ones(A.nx))
+    y = dev.vec(A.nx)
+    t_setup = time.perf_counter() - t_setup0
+
+    # ---- SpMV roofline leg: y = A x, HIP events on the library's stream ----
+    xs = dev.vec(A.nx, np.random.default_rng(rank).uniform(-1, 1, A.nx))
+    stream = torch.cuda.ExternalStream(dev.stream)
+    for _ in range(5):
+        A.mv_mxy(xs, y)
+    dev.sync()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.spmv_reps):
+        A.mv_mxy(xs, y)
+    e1.record(stream)
+    e1.synchronize()
+    spmv_ms = e0.elapsed_time(e1) / args.spmv_reps
+    spmv_gbs = spmv_bytes(nnz_local, nl) / (spmv_ms * 1e-3) / 1e9
+
+    # ---- BiCGSTAB steps ----
+    def run(iters):
+        return lssp_amd.solve(dev, A, M, x, b, solver=lssp_amd.BICGSTAB, tol_rel=0.0, tol_abs=0.0, tol_rb=0.0,
+                              maxit=iters)
+
+    if args.warmup > 0:
+        run(args.warmup)
+    if world > 1:
+        dist.barrier()
+    dev.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = run(args.steps)
+    dev.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        g = torch.tensor([spmv_gbs], dtype=torch.float64)
+        dist.all_reduce(g, op=dist.ReduceOp.SUM)
+        spmv_gbs_total = float(g.item())
+    else:
+        spmv_gbs_total = spmv_gbs
+    assert res.nits == args.steps, f"expected {args.steps} iterations, got {res.nits}"
+
+    if rank == 0:
+        it_s = args.steps / elapsed
+        out = {
+            "metric": "fp64 CSR SpMV GB/s (% HBM peak) + BiCGSTAB iters/s, 7-pt Poisson n=10M",
+            "value": round(it_s, 3),
+            "unit": "iters/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": f"7-pt Poisson {N}^3 (n={n}, nnz={int(7 * N ** 3 - 6 * N ** 2)}), "
+                                   f"BiCGSTAB + ILUK(0){' block-Jacobi per rank' if world > 1 else ''}, "
+                                   "b=1, x0=0, fp64 CSR int32",
+                       "rows": n, "partition": f"{world} z-slab row blocks", "reduction": "tree"},
+            "spmv": {"gbps": round(spmv_gbs_total, 1), "frac_hbm_peak": round(spmv_gbs / HBM_PEAK_GBS, 4),
+                     "ms_per_call": round(spmv_ms, 5)},
+            "roofline": {"bound": "hbm", "achieved": round(spmv_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(spmv_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "k_spmv<EPI_MXY,0> (y = A x)",
+                         "bytes_per_launch": spmv_bytes(nnz_local, nl)},
+            "ilu": {"levels_L": M.levelsL, "levels_U": M.levelsU, "setup_s": round(M.setup_seconds, 3)},
+            "setup_s": round(t_setup, 2),
+        }
+        if not args.no_cpu and world == 1:
+            out["cpu_baseline"] = cpu_baseline(N, args.cpu_iters)
+        print(json.dumps(out), flush=True)
+    dev.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -102,6 +102,8 @@ int lssp_amd_ctx_create(int device, lssp_amd_ctx **out)
     if (m && !strcmp(m, "serial")) c->reduce_mode = LSSP_AMD_REDUCE_SERIAL;
     const char *tb = getenv("LSSP_AMD_TRI_BLOCKS_PER_CU");
     if (tb) c->tri_blocks_per_cu = std::max(1, atoi(tb));
+    const char *tm = getenv("LSSP_AMD_TRI_MODE");
+    if (tm) c->tri_mode = atoi(tm);
     *out = c;
     return LSSP_AMD_OK;
 }
@@ -111,6 +113,7 @@ int lssp_amd_ctx_destroy(lssp_amd_ctx *c)
     if (!c) return LSSP_AMD_OK;
     (void)hipStreamSynchronize(c->stream);
     comm_destroy(c);
+    for (auto &w : c->pool) (void)hipFree(w.p);
     if (c->d_part) (void)hipFree(c->d_part);
     if (c->d_trace) (void)hipFree(c->d_trace);
     (void)hipFree(c->d_sums);

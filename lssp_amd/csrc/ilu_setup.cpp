@@ -494,6 +494,9 @@ int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std
     std::vector<int> start(nlev + 1, 0), perm(n);
     for (int i = 0; i < n; i++) start[lev[i] + 1]++;
     for (int l = 0; l < nlev; l++) start[l + 1] += start[l];
+    t.level_ptr = start;
+    t.max_level_rows = 0;
+    for (int l = 0; l < nlev; l++) t.max_level_rows = std::max(t.max_level_rows, start[l + 1] - start[l]);
     if (!upper) {
         for (int i = 0; i < n; i++) perm[start[lev[i]]++] = i;
     } else {

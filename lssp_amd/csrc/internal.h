@@ -72,7 +72,15 @@ struct lssp_amd_ctx {
     int nranks = 1, rank = 0;
     void *comm = nullptr;      // ncclComm_t
     double *d_gather = nullptr;  // [nranks][MAX_SLOTS]
-    int tri_blocks_per_cu = 4;
+    int tri_blocks_per_cu = 1;
+    int tri_mode = 2;  // 0 sync-free + back-off, 1 one launch per level, 2 sync-free no back-off
+    // Krylov work vectors, kept across solves (no hipMalloc on the solve path)
+    struct WsBuf {
+        double *p;
+        long n;
+        bool used;
+    };
+    std::vector<WsBuf> pool;
 };
 
 struct lssp_amd_mat {
@@ -99,6 +107,8 @@ struct TriSched {
     int *cols = nullptr;   // strict entries, in the reference's summation order
     double *vals = nullptr;
     double *diag = nullptr;  // per position (nullptr when unit)
+    std::vector<int> level_ptr;  // host: schedule positions of each level
+    int max_level_rows = 0;
 };
 
 }  // namespace lssp_amd

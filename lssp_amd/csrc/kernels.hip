@@ -503,6 +503,11 @@ __device__ __forceinline__ void st_agent(double *p, double v)
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Sync-free sweep.  First pass over a row's entries loads them in batches of
+// four; once a dependency is found missing, the lane re-polls only that one
+// entry (one load per lane per poll) with an exponential back-off, so waves
+// far ahead of the wavefront do not flood the memory system with polls.
+template <int BACKOFF>
 __global__ __launch_bounds__(256) void k_trisolve(TriArgs a)
 {
     const int lane = threadIdx.x & 63;
@@ -520,12 +525,13 @@ __global__ __launch_bounds__(256) void k_trisolve(TriArgs a)
             acc = a.rhs[row];
             if (a.reset) a.reset[row] = __longlong_as_double((long long)TRI_SENTINEL);
         }
-        uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        int nap = 0;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        int nap = 1;
+        int mcap = 4;
         for (;;) {
             if (active) {
                 while (k < end) {
-                    const int m = end - k < 4 ? end - k : 4;
+                    const int m = end - k < mcap ? end - k : mcap;
                     uint64_t bits[4];
 #pragma unroll
                     for (int u = 0; u < 4; u++)
@@ -536,7 +542,11 @@ __global__ __launch_bounds__(256) void k_trisolve(TriArgs a)
                         acc = acc - a.vals[k] * __longlong_as_double((long long)bits[u]);
                         k++;
                     }
-                    if (u < m) break;
+                    if (u < m) {
+                        mcap = 1;  // re-poll just the first missing dependency
+                        break;
+                    }
+                    mcap = 4;
                 }
                 if (k == end) {
                     const double xi = a.unit ? acc : acc / a.diag[p];
@@ -552,21 +562,42 @@ __global__ __launch_bounds__(256) void k_trisolve(TriArgs a)
                 }
                 break;
             }
-            if (nap < 8) nap++;
-            __builtin_amdgcn_s_sleep(1);
+            for (int q = 0; q < nap; q++) __builtin_amdgcn_s_sleep(2);
+            if (BACKOFF && nap < 32) nap <<= 1;
         }
     }
+}
+
+// Level-synchronous alternative: one launch per level, every dependency lies in
+// an earlier launch, so plain loads suffice and nothing waits.
+__global__ __launch_bounds__(256) void k_trisolve_level(TriArgs a, int lo, int hi)
+{
+    const int p = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= hi) return;
+    const int row = a.perm[p];
+    double acc = a.rhs[row];
+    if (a.reset) a.reset[row] = __longlong_as_double((long long)TRI_SENTINEL);
+    for (int k = a.rp[p]; k < a.rp[p + 1]; k++) acc = acc - a.vals[k] * a.x[a.cols[k]];
+    a.x[row] = a.unit ? acc : acc / a.diag[p];
 }
 
 int launch_trisolve(lssp_amd_ctx *c, const TriSched &t, const double *rhs, double *x, double *reset)
 {
     if (t.n == 0) return LSSP_AMD_OK;
     long nchunks = (t.n + 63) / 64;
-    long grid = (long)c->num_cus * c->tri_blocks_per_cu;
-    long need = (nchunks + 3) / 4;
-    if (grid > need) grid = need;
     TriArgs a{t.n, nchunks, t.perm, t.rp, t.cols, t.vals, t.diag, t.unit, rhs, x, reset, c->d_err};
-    k_trisolve<<<grid, 256, 0, c->stream>>>(a);
+    if (c->tri_mode == 1) {
+        for (int l = 0; l < t.nlevels; l++) {
+            const int lo = t.level_ptr[l], hi = t.level_ptr[l + 1];
+            k_trisolve_level<<<(hi - lo + 255) / 256, 256, 0, c->stream>>>(a, lo, hi);
+        }
+    } else {
+        long grid = (long)c->num_cus * c->tri_blocks_per_cu;
+        long need = (nchunks + 3) / 4;
+        if (grid > need) grid = need;
+        if (c->tri_mode == 2) k_trisolve<0><<<grid, 256, 0, c->stream>>>(a);
+        else k_trisolve<1><<<grid, 256, 0, c->stream>>>(a);
+    }
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;
 }

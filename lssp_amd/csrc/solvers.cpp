@@ -47,12 +47,24 @@ struct Run {
     ~Run()
     {
         (void)hipStreamSynchronize(c->stream);
-        for (double *p : bufs) (void)hipFree(p);
+        for (double *p : bufs)
+            for (auto &w : c->pool)
+                if (w.p == p) w.used = false;
     }
+    // work vectors come from the context's pool: allocated once, reused by
+    // every later solve of the same size
     double *vec(long len = -1)
     {
+        const long want = std::max<long>(len < 0 ? nx : len, 1);
+        for (auto &w : c->pool)
+            if (!w.used && w.n == want) {
+                w.used = true;
+                bufs.push_back(w.p);
+                return w.p;
+            }
         double *p = nullptr;
-        if (hipMalloc(&p, sizeof(double) * std::max<long>(len < 0 ? nx : len, 1)) != hipSuccess) return nullptr;
+        if (hipMalloc(&p, sizeof(double) * want) != hipSuccess) return nullptr;
+        c->pool.push_back({p, want, true});
         bufs.push_back(p);
         return p;
     }
