@@ -489,6 +489,7 @@ int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std
     int nlev = 0;
     for (int i = 0; i < n; i++) nlev = std::max(nlev, lev[i] + 1);
     t.nlevels = n ? nlev : 0;
+    LSSP_TRY(build_bp_schedule(c, n, Tp, Tj, Tx, upper, lev, t));
     // counting sort by level; rows of a level stay in row order (lower) or in
     // descending row order (upper, mirroring the backward sweep)
     std::vector<int> start(nlev + 1, 0), perm(n);
@@ -551,6 +552,11 @@ void free_trisched(TriSched &t)
     if (t.cols) (void)hipFree(t.cols);
     if (t.vals) (void)hipFree(t.vals);
     if (t.diag) (void)hipFree(t.diag);
+    for (void *p : {(void *)t.bp_perm, (void *)t.bp_rp, (void *)t.bp_cols, (void *)t.bp_vals, (void *)t.bp_diag,
+                    (void *)t.bp_step_pos, (void *)t.bp_step_need, (void *)t.bp_step_done,
+                    (void *)t.bp_step_flag, (void *)t.bp_blk_step, (void *)t.bp_prog, (void *)t.bp_claim,
+                    (void *)t.pk_blk, (void *)t.pk_off, t.pk_data, (void *)t.pk_claim})
+        if (p) (void)hipFree(p);
     t = TriSched();
 }
 

@@ -73,7 +73,9 @@ struct lssp_amd_ctx {
     void *comm = nullptr;      // ncclComm_t
     double *d_gather = nullptr;  // [nranks][MAX_SLOTS]
     int tri_blocks_per_cu = 1;
-    int tri_mode = 2;  // 0 sync-free + back-off, 1 one launch per level, 2 sync-free no back-off
+    // 0 sync-free + back-off, 1 one launch per level, 2 sync-free no back-off,
+    // 3 block pipeline with progress words, 4 packet-streamed block pipeline
+    int tri_mode = 4;
     // Krylov work vectors, kept across solves (no hipMalloc on the solve path)
     struct WsBuf {
         double *p;
@@ -109,7 +111,28 @@ struct TriSched {
     double *diag = nullptr;  // per position (nullptr when unit)
     std::vector<int> level_ptr;  // host: schedule positions of each level
     int max_level_rows = 0;
+    // block-pipelined schedule (tri_mode 3): contiguous row blocks of B >=
+    // bandwidth rows in sweep order, each processed level by level by one
+    // workgroup; see kernels.hip k_tri_bp
+    int bp_B = 0, bp_nb = 0, bp_nsteps = 0;
+    int *bp_perm = nullptr, *bp_rp = nullptr, *bp_cols = nullptr;  // cols < 0: LDS ring slot
+    double *bp_vals = nullptr, *bp_diag = nullptr;
+    int *bp_step_pos = nullptr, *bp_step_need = nullptr, *bp_step_done = nullptr;
+    int *bp_step_flag = nullptr, *bp_blk_step = nullptr;
+    unsigned long long *bp_prog = nullptr, *bp_claim = nullptr;
+    mutable unsigned long long bp_base = 0;  // claim-ticket base of the next launch
+    mutable unsigned bp_epoch = 0;           // progress-word epoch of the last launch
+    // packet-streamed block pipeline (tri_mode 4): each block's steps cut into
+    // packets of <= PK_ROWS rows / PK_BYTES bytes, laid out contiguously
+    int pk_n = 0;
+    int *pk_blk = nullptr;        // [nb+1] first packet of each block
+    int *pk_off = nullptr;        // [npk+1] packet offsets in 16-byte units
+    void *pk_data = nullptr;
+    mutable unsigned long long pk_base = 0;
+    unsigned long long *pk_claim = nullptr;
 };
+constexpr int PK_ROWS = 256;
+constexpr int PK_BYTES = 12288;
 
 }  // namespace lssp_amd
 
@@ -172,6 +195,14 @@ int launch_finalize(lssp_amd_ctx *c, const double *sums, int nslot, const Fin &f
 int launch_fill(lssp_amd_ctx *c, double *x, long n, uint64_t bits);
 int launch_trisolve(lssp_amd_ctx *c, const TriSched &t, const double *rhs, double *x,
                     double *reset);
+constexpr int BP_RING = 4096;  // LDS ring of recently computed values (32 KB)
+int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std::vector<int> &Tj,
+                      const std::vector<double> &Tx, bool upper, const std::vector<int> &lev,
+                      TriSched &t);
+int build_packets(int n, const std::vector<int> &perm, const std::vector<int> &rp,
+                  const std::vector<int> &cols, const std::vector<double> &vals,
+                  const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
+                  const std::vector<int> &blk_step, int nb, long B, TriSched &t);
 int launch_pack(lssp_amd_ctx *c, const int *idx, const double *x, double *buf, int n);
 int launch_sum_ranks(lssp_amd_ctx *c, int nslot, const Fin &f);
 

@@ -581,11 +581,240 @@ __global__ __launch_bounds__(256) void k_trisolve_level(TriArgs a, int lo, int h
     a.x[row] = a.unit ? acc : acc / a.diag[p];
 }
 
+// Block-pipelined sweep (tri_mode 3, schedule from tri_bp.cpp).  Workgroups
+// claim blocks in sweep order from a ticket counter (so a block only ever
+// waits on a block claimed earlier by a running workgroup: no residency
+// assumption, no deadlock), walk the block's steps (levels) in order, read
+// same-block values of the last BP_RING positions from LDS and everything else
+// with agent-scope loads, and publish "all my rows up to level L are done" in a
+// 64-bit progress word {epoch, L+1} after draining their stores (every wave
+// s_waitcnt vmcnt(0), barrier, one sc1 store: MI355X_MICROARCH hand-off row 1).
+struct BPArgs {
+    int B, nb;
+    const int *blk_step, *step_pos, *step_need, *step_done, *step_flag;
+    const int *perm, *rp, *cols;
+    const double *vals, *diag;
+    int unit;
+    const double *rhs;
+    double *x;
+    double *reset;
+    unsigned long long *prog, *claim;
+    unsigned long long base;
+    unsigned epoch;
+    int *err;
+};
+
+__global__ __launch_bounds__(256) void k_tri_bp(BPArgs a)
+{
+    __shared__ double ring[BP_RING];
+    __shared__ int s_blk;
+    const int tid = threadIdx.x;
+    const unsigned long long tag = (unsigned long long)a.epoch << 32;
+    for (;;) {
+        __syncthreads();  // ring and s_blk are free again
+        if (tid == 0) s_blk = (int)(atomicAdd(a.claim, 1ull) - a.base);
+        __syncthreads();
+        const int b = s_blk;
+        if (b >= a.nb) break;
+        const long base = (long)b * a.B;
+        unsigned long long seen = 0;
+        bool dead = false;
+        for (int s = a.blk_step[b]; s < a.blk_step[b + 1]; s++) {
+            const int need = a.step_need[s];
+            if (need >= 0 && tid == 0 && !dead) {
+                const unsigned long long want = tag | (unsigned)(need + 1);
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                while (seen < want) {
+                    seen = __hip_atomic_load(a.prog + (b - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (seen >= want) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s
+                        atomicOr(a.err, 2);
+                        dead = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            __syncthreads();
+            const int p0 = a.step_pos[s], p1 = a.step_pos[s + 1];
+            for (int p = p0 + tid; p < p1; p += 256) {
+                const int row = a.perm[p];
+                double acc = a.rhs[row];
+                if (a.reset) a.reset[row] = __longlong_as_double((long long)TRI_SENTINEL);
+                for (int k = a.rp[p]; k < a.rp[p + 1]; k++) {
+                    const int code = a.cols[k];
+                    const double xv = code < 0 ? ring[-1 - code] : __longlong_as_double((long long)ld_agent(a.x + code));
+                    acc = acc - a.vals[k] * xv;
+                }
+                const double xi = a.unit ? acc : acc / a.diag[p];
+                ring[(p - base) % BP_RING] = xi;
+                st_agent(a.x + row, xi);
+            }
+            if (a.step_flag[s] & 1) {  // drain this block's stores, then publish
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (tid == 0)
+                    __hip_atomic_store(a.prog + b, tag | (unsigned)(a.step_done[s] + 1), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+}
+
+// Packet-streamed block pipeline (tri_mode 4, packets from tri_bp.cpp).
+// Blocks are claimed in sweep order as in k_tri_bp.  Inside a block the
+// workgroup streams its packets (one level's rows each) through a 3-slot LDS
+// ring: while it computes packet q it loads packet q+2 with 16-byte loads and
+// gathers the right-hand side of packet q+1, so only the x dependencies are
+// on the critical path.  Same-block values of the last BP_RING positions come
+// from the LDS value ring; all other x values are read with agent-scope loads
+// and, because x is armed with TRI_SENTINEL before the sweep, a value that is
+// not yet visible is simply re-read (value-as-flag): no store drains, no
+// progress words.  A block only ever waits on the block before it, which was
+// claimed earlier by a running workgroup, so the sweep always drains.
+struct PkArgs {
+    int nb;
+    const int *blk, *off;
+    const int4 *data;
+    int unit;
+    const double *rhs;
+    double *x;
+    double *reset;
+    unsigned long long *claim;
+    unsigned long long base;
+    int *err;
+};
+
+__device__ __forceinline__ double ld_ready(const double *p, int *err)
+{
+    uint64_t bits = ld_agent(p);
+    if (bits == TRI_SENTINEL) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        do {
+            __builtin_amdgcn_s_sleep(1);
+            bits = ld_agent(p);
+            if (bits != TRI_SENTINEL) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s
+                atomicOr(err, 4);
+                return __longlong_as_double(0x7FF8000000000000ll);
+            }
+        } while (true);
+    }
+    return __longlong_as_double((long long)bits);
+}
+
+constexpr int PK_VEC = PK_BYTES / 16;         // int4 per packet slot
+constexpr int PK_LD = (PK_VEC + 255) / 256;   // int4 loads per thread to stage one packet
+
+__global__ __launch_bounds__(256) void k_tri_pk(PkArgs a)
+{
+    __shared__ double ring[BP_RING];
+    __shared__ int4 pbuf[3][PK_VEC];
+    __shared__ double rbuf[3][PK_ROWS];
+    __shared__ int s_blk;
+    const int tid = threadIdx.x;
+    for (;;) {
+        __syncthreads();
+        if (tid == 0) s_blk = (int)(atomicAdd(a.claim, 1ull) - a.base);
+        __syncthreads();
+        const int b = s_blk;
+        if (b >= a.nb) break;
+        const int q0 = a.blk[b], q1 = a.blk[b + 1];
+        // prologue: packets q0, q0+1 into slots 0, 1; rhs of q0 into rbuf[0]
+        for (int j = 0; j < 2 && q0 + j < q1; j++) {
+            const int o = a.off[q0 + j], len = a.off[q0 + j + 1] - o;
+            for (int i = tid; i < len; i += 256) pbuf[j][i] = a.data[o + i];
+        }
+        __syncthreads();
+        {
+            const int *w = reinterpret_cast<const int *>(pbuf[0]);
+            if (tid < w[0]) rbuf[0][tid] = a.rhs[w[4 + tid]];
+        }
+        __syncthreads();
+        for (int q = q0; q < q1; q++) {
+            const int cur = (q - q0) % 3, nxt = (cur + 1) % 3, nn = (cur + 2) % 3;
+            // (1) stage packet q+2
+            int4 st[PK_LD];
+            int o2 = 0, len2 = 0;
+            if (q + 2 < q1) {
+                o2 = a.off[q + 2];
+                len2 = a.off[q + 3] - o2;
+#pragma unroll
+                for (int u = 0; u < PK_LD; u++) {
+                    const int i = tid + 256 * u;
+                    if (i < len2) st[u] = a.data[o2 + i];
+                }
+            }
+            // (2) gather the right-hand side of packet q+1
+            double rh = 0;
+            bool have_rh = false;
+            if (q + 1 < q1) {
+                const int *w = reinterpret_cast<const int *>(pbuf[nxt]);
+                if (tid < w[0]) {
+                    rh = a.rhs[w[4 + tid]];
+                    have_rh = true;
+                }
+            }
+            // (3) packet q
+            {
+                const int *w = reinterpret_cast<const int *>(pbuf[cur]);
+                const int nr = w[0], ne = w[1], pos0 = w[2];
+                if (tid < nr) {
+                    const int *rows = w + 4, *rp = w + 4 + nr, *codes = w + 5 + 2 * nr;
+                    const int vo = (5 + 2 * nr + ne + 1) & ~1;
+                    const double *vals = reinterpret_cast<const double *>(w + vo);
+                    const int row = rows[tid];
+                    double acc = rbuf[cur][tid];
+                    if (a.reset) a.reset[row] = __longlong_as_double((long long)TRI_SENTINEL);
+                    for (int k = rp[tid]; k < rp[tid + 1]; k++) {
+                        const int code = codes[k];
+                        const double xv = code < 0 ? ring[-1 - code] : ld_ready(a.x + code, a.err);
+                        acc = acc - vals[k] * xv;
+                    }
+                    const double xi = a.unit ? acc : acc / reinterpret_cast<const double *>(w + vo + 2 * ne)[tid];
+                    ring[(pos0 + tid) % BP_RING] = xi;
+                    st_agent(a.x + row, xi);
+                }
+            }
+            // (4) land the staged data
+            if (q + 2 < q1) {
+#pragma unroll
+                for (int u = 0; u < PK_LD; u++) {
+                    const int i = tid + 256 * u;
+                    if (i < len2) pbuf[nn][i] = st[u];
+                }
+            }
+            if (have_rh) rbuf[nxt][tid] = rh;
+            __syncthreads();
+        }
+    }
+}
+
 int launch_trisolve(lssp_amd_ctx *c, const TriSched &t, const double *rhs, double *x, double *reset)
 {
     if (t.n == 0) return LSSP_AMD_OK;
     long nchunks = (t.n + 63) / 64;
     TriArgs a{t.n, nchunks, t.perm, t.rp, t.cols, t.vals, t.diag, t.unit, rhs, x, reset, c->d_err};
+    if (c->tri_mode == 4 && t.pk_n >= 0) {
+        const int grid = std::min(t.bp_nb, c->num_cus);
+        PkArgs g{t.bp_nb, t.pk_blk, t.pk_off, reinterpret_cast<const int4 *>(t.pk_data), t.unit, rhs, x, reset,
+                 t.pk_claim, t.pk_base, c->d_err};
+        k_tri_pk<<<grid, 256, 0, c->stream>>>(g);
+        t.pk_base += (unsigned long long)t.bp_nb + grid;
+        LSSP_HIP(hipGetLastError());
+        return LSSP_AMD_OK;
+    }
+    if (c->tri_mode == 3) {
+        const int grid = std::min(t.bp_nb, c->num_cus);
+        t.bp_epoch++;
+        BPArgs g{t.bp_B, t.bp_nb, t.bp_blk_step, t.bp_step_pos, t.bp_step_need, t.bp_step_done,
+                 t.bp_step_flag, t.bp_perm, t.bp_rp, t.bp_cols, t.bp_vals, t.bp_diag, t.unit, rhs, x,
+                 nullptr /* no sentinel protocol here */, t.bp_prog, t.bp_claim, t.bp_base, t.bp_epoch, c->d_err};
+        k_tri_bp<<<grid, 256, 0, c->stream>>>(g);
+        t.bp_base += (unsigned long long)t.bp_nb + grid;
+        LSSP_HIP(hipGetLastError());
+        return LSSP_AMD_OK;
+    }
     if (c->tri_mode == 1) {
         for (int l = 0; l < t.nlevels; l++) {
             const int lo = t.level_ptr[l], hi = t.level_ptr[l + 1];
