@@ -104,6 +104,8 @@ int lssp_amd_ctx_create(int device, lssp_amd_ctx **out)
     if (tb) c->tri_blocks_per_cu = std::max(1, atoi(tb));
     const char *tm = getenv("LSSP_AMD_TRI_MODE");
     if (tm) c->tri_mode = atoi(tm);
+    const char *td = getenv("LSSP_AMD_TRI_DIAG");
+    if (td) c->tri_diag = atoi(td);
     *out = c;
     return LSSP_AMD_OK;
 }
@@ -190,8 +192,10 @@ static int check_csr(int nrows, int ncols, int nnz, const int *Ap, const int *Aj
 static int upload_csr(lssp_amd_mat *M, const int *Ap, const int *Aj, const double *Ax)
 {
     LSSP_HIP(hipMalloc(&M->Ap, sizeof(int) * (M->nrows + 1)));
-    LSSP_HIP(hipMalloc(&M->Aj, sizeof(int) * std::max(M->nnz, 1)));
-    LSSP_HIP(hipMalloc(&M->Ax, sizeof(double) * std::max(M->nnz, 1)));
+    // +4 entries: the 16-byte staging loads of k_spmv2 may touch up to one
+    // vector past the last entry
+    LSSP_HIP(hipMalloc(&M->Aj, sizeof(int) * (M->nnz + 4)));
+    LSSP_HIP(hipMalloc(&M->Ax, sizeof(double) * (M->nnz + 4)));
     LSSP_HIP(hipMemcpy(M->Ap, Ap, sizeof(int) * (M->nrows + 1), hipMemcpyHostToDevice));
     if (M->nnz) {
         LSSP_HIP(hipMemcpy(M->Aj, Aj, sizeof(int) * M->nnz, hipMemcpyHostToDevice));

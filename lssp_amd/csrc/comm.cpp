@@ -217,8 +217,8 @@ int lssp_amd_mat_upload_dist(lssp_amd_ctx *c, int n_global, int row0, int nlocal
     (void)hipFree(d_hcols);
     (void)hipFree(d_sendg);
     LSSP_HIP(hipMalloc(&M->Ap, sizeof(int) * (nlocal + 1)));
-    LSSP_HIP(hipMalloc(&M->Aj, sizeof(int) * std::max(nnz, 1)));
-    LSSP_HIP(hipMalloc(&M->Ax, sizeof(double) * std::max(nnz, 1)));
+    LSSP_HIP(hipMalloc(&M->Aj, sizeof(int) * (nnz + 4)));  // +4: see upload_csr (capi.cpp)
+    LSSP_HIP(hipMalloc(&M->Ax, sizeof(double) * (nnz + 4)));
     LSSP_HIP(hipMemcpy(M->Ap, Ap, sizeof(int) * (nlocal + 1), hipMemcpyHostToDevice));
     if (nnz) {
         LSSP_HIP(hipMemcpy(M->Aj, lj.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));

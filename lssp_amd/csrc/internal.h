@@ -76,6 +76,7 @@ struct lssp_amd_ctx {
     // 0 sync-free + back-off, 1 one launch per level, 2 sync-free no back-off,
     // 3 block pipeline with progress words, 4 packet-streamed block pipeline
     int tri_mode = 4;
+    int tri_diag = 0;  // LSSP_AMD_TRI_DIAG timing experiments (wrong results when != 0)
     // Krylov work vectors, kept across solves (no hipMalloc on the solve path)
     struct WsBuf {
         double *p;

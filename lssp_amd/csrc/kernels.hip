@@ -267,12 +267,108 @@ __global__ __launch_bounds__(256) void k_spmv(SpmvArgs a)
     }
 }
 
+// Variant 2: the block's Ax / Aj ranges are staged with 16-byte loads (the
+// range is widened to 16-byte boundaries; the extra head/tail entries are
+// dropped when landing in LDS), all loads of a thread are issued before any
+// LDS store, and with XCD != 0 the 256-row blocks are dealt so that each of
+// the 8 XCDs owns one contiguous eighth of the rows (dispatch round-robins
+// blocks over XCDs: block b runs on XCD b % 8), keeping the x gathers of
+// neighbouring blocks in one L2.  Same per-row arithmetic as k_spmv.
+constexpr int SPMV2_CAP = 2048;
+template <int EPI, int NRED, int XCD>
+__global__ __launch_bounds__(256) void k_spmv2(SpmvArgs a, long nblk)
+{
+    __shared__ __attribute__((aligned(16))) double sx[SPMV2_CAP + 2];
+    __shared__ __attribute__((aligned(16))) int sj[SPMV2_CAP + 4];
+    __shared__ double lds[MAX_SLOTS][4];
+    long blk = blockIdx.x;
+    if (XCD) {
+        const long per = gridDim.x / 8;
+        blk = (blockIdx.x % 8) * per + blockIdx.x / 8;
+        if (blk >= nblk) return;
+    }
+    const int r0 = (int)(blk * 256);
+    const int tid = threadIdx.x;
+    const int r = r0 + tid;
+    const int rend = min(r0 + 256, a.nrows);
+    const int base = a.Ap[r0];
+    const int cnt = a.Ap[rend] - base;
+    double sum = 0;
+    if (cnt <= SPMV2_CAP) {
+        const int xb = base & ~1, xn = (base + cnt - xb + 1) >> 1;  // double2 count
+        const int jb = base & ~3, jn = (base + cnt - jb + 3) >> 2;  // int4 count
+        typedef double dbl2_t __attribute__((ext_vector_type(2)));
+        typedef int int4_t __attribute__((ext_vector_type(4)));
+        const dbl2_t *X2 = reinterpret_cast<const dbl2_t *>(a.Ax + xb);
+        const int4_t *J4 = reinterpret_cast<const int4_t *>(a.Aj + jb);
+        dbl2_t vx[(SPMV2_CAP / 2 + 1 + 255) / 256];
+        int4_t vj[(SPMV2_CAP / 4 + 1 + 255) / 256];
+#pragma unroll
+        for (int u = 0; u < (int)(sizeof(vx) / sizeof(vx[0])); u++)
+            if (tid + 256 * u < xn) vx[u] = __builtin_nontemporal_load(X2 + tid + 256 * u);
+#pragma unroll
+        for (int u = 0; u < (int)(sizeof(vj) / sizeof(vj[0])); u++)
+            if (tid + 256 * u < jn) vj[u] = __builtin_nontemporal_load(J4 + tid + 256 * u);
+        const int ox = base - xb, oj = base - jb;  // LDS entry e lives at e + o
+#pragma unroll
+        for (int u = 0; u < (int)(sizeof(vx) / sizeof(vx[0])); u++)
+            if (tid + 256 * u < xn) reinterpret_cast<dbl2_t *>(sx)[tid + 256 * u] = vx[u];
+#pragma unroll
+        for (int u = 0; u < (int)(sizeof(vj) / sizeof(vj[0])); u++)
+            if (tid + 256 * u < jn) reinterpret_cast<int4_t *>(sj)[tid + 256 * u] = vj[u];
+        __syncthreads();
+        if (r < a.nrows) {
+            const int b = a.Ap[r] - base, e = a.Ap[r + 1] - base;
+            for (int k = b; k < e; k++) sum += a.x[sj[k + oj]] * sx[k + ox];
+        }
+    } else if (r < a.nrows) {
+        const int b = a.Ap[r], e = a.Ap[r + 1];
+        for (int k = b; k < e; k++) sum += a.x[a.Aj[k]] * a.Ax[k];
+    }
+    double zv = 0;
+    if (r < a.nrows) {
+        if (EPI == EPI_MXY) zv = sum;
+        else if (EPI == EPI_AMXY) zv = sum * a.alpha;
+        else if (EPI == EPI_AXPBY) zv = a.y[r] * a.beta + a.alpha * sum;
+        else zv = a.alpha * sum;
+        a.z[r] = zv;
+    }
+    if (NRED > 0) {
+        double v[NRED > 0 ? NRED : 1];
+        if (r < a.nrows) {
+            v[0] = zv * a.w0[r];
+            if (NRED > 1) v[NRED > 1 ? 1 : 0] = zv * (a.w1 ? a.w1[r] : zv);
+        } else {
+#pragma unroll
+            for (int q = 0; q < NRED; q++) v[q] = 0.0;
+        }
+        chunk_reduce<NRED>(v, a.part, a.pcap, blk, lds);
+    }
+}
+
+static int g_spmv_variant = -1;  // LSSP_AMD_SPMV: 0 k_spmv, 1 k_spmv2, 2 k_spmv2 + XCD order
+
 template <int EPI>
 static void spmv_dispatch(const SpmvArgs &a, int nred, long nblocks, hipStream_t s)
 {
-    if (nred == 0) k_spmv<EPI, 0><<<nblocks, 256, 0, s>>>(a);
-    else if (nred == 1) k_spmv<EPI, 1><<<nblocks, 256, 0, s>>>(a);
-    else k_spmv<EPI, 2><<<nblocks, 256, 0, s>>>(a);
+    if (g_spmv_variant < 0) {
+        const char *e = getenv("LSSP_AMD_SPMV");
+        g_spmv_variant = e ? atoi(e) : 0;
+    }
+    if (g_spmv_variant == 0) {
+        if (nred == 0) k_spmv<EPI, 0><<<nblocks, 256, 0, s>>>(a);
+        else if (nred == 1) k_spmv<EPI, 1><<<nblocks, 256, 0, s>>>(a);
+        else k_spmv<EPI, 2><<<nblocks, 256, 0, s>>>(a);
+    } else if (g_spmv_variant == 1) {
+        if (nred == 0) k_spmv2<EPI, 0, 0><<<nblocks, 256, 0, s>>>(a, nblocks);
+        else if (nred == 1) k_spmv2<EPI, 1, 0><<<nblocks, 256, 0, s>>>(a, nblocks);
+        else k_spmv2<EPI, 2, 0><<<nblocks, 256, 0, s>>>(a, nblocks);
+    } else {
+        const long g = (nblocks + 7) / 8 * 8;
+        if (nred == 0) k_spmv2<EPI, 0, 1><<<g, 256, 0, s>>>(a, nblocks);
+        else if (nred == 1) k_spmv2<EPI, 1, 1><<<g, 256, 0, s>>>(a, nblocks);
+        else k_spmv2<EPI, 2, 1><<<g, 256, 0, s>>>(a, nblocks);
+    }
 }
 
 int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, const double *x,
@@ -683,7 +779,18 @@ struct PkArgs {
     unsigned long long *claim;
     unsigned long long base;
     int *err;
+    int diag;  // diagnostics only (LSSP_AMD_TRI_DIAG): 1 = no waiting, 2 = no cross-block loads
 };
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a
+// workgroup-scope fence + s_barrier, which on gfx950 also waits vmcnt(0): every
+// in-flight global load AND every x store would be waited for at each step.
+// Here only LDS traffic must be complete; global loads are waited for where
+// their registers are used, the sc1 x stores are never waited for.
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
 __device__ __forceinline__ double ld_ready(const double *p, int *err)
 {
@@ -768,7 +875,11 @@ __global__ __launch_bounds__(256) void k_tri_pk(PkArgs a)
                     if (a.reset) a.reset[row] = __longlong_as_double((long long)TRI_SENTINEL);
                     for (int k = rp[tid]; k < rp[tid + 1]; k++) {
                         const int code = codes[k];
-                        const double xv = code < 0 ? ring[-1 - code] : ld_ready(a.x + code, a.err);
+                        double xv;
+                        if (code < 0) xv = ring[-1 - code];
+                        else if (a.diag == 0) xv = ld_ready(a.x + code, a.err);
+                        else if (a.diag == 1) xv = __longlong_as_double((long long)ld_agent(a.x + code));
+                        else xv = 0.0;
                         acc = acc - vals[k] * xv;
                     }
                     const double xi = a.unit ? acc : acc / reinterpret_cast<const double *>(w + vo + 2 * ne)[tid];
@@ -785,8 +896,177 @@ __global__ __launch_bounds__(256) void k_tri_pk(PkArgs a)
                 }
             }
             if (have_rh) rbuf[nxt][tid] = rh;
-            __syncthreads();
+            lds_barrier();
         }
+    }
+}
+
+// tri_mode 5: k_tri_pk with a deeper software pipeline.  Iteration i computes
+// packet i of the block; at that time packets i..i+2 sit in LDS, the loads of
+// packet i+3 (issued one iteration earlier) land in LDS at the end of the
+// iteration and the loads of packet i+4 are issued; the right-hand side and the
+// first PF_E cross-block / far values of packet i+2 are gathered into
+// registers and land in LDS one iteration later, two iterations before they
+// are used.  Every global load therefore has one to two iterations to arrive
+// instead of being waited for inside the iteration that issued it.
+constexpr int PF_E = 2;
+
+struct PkRegs {
+    int4 pk[PK_LD];
+    int len;
+    double rh;
+    double ev[PF_E];
+    int ek[PF_E];
+};
+
+__device__ __forceinline__ void pk_issue(const PkArgs &a, int p, int q1, PkRegs &R)
+{
+    R.len = 0;
+    if (p < q1) {
+        const int o = a.off[p];
+        R.len = a.off[p + 1] - o;
+#pragma unroll
+        for (int u = 0; u < PK_LD; u++) {
+            const int i = threadIdx.x + 256 * u;
+            if (i < R.len) R.pk[u] = a.data[o + i];
+        }
+    }
+}
+
+__device__ __forceinline__ void pk_land(int4 *slot, const PkRegs &R)
+{
+#pragma unroll
+    for (int u = 0; u < PK_LD; u++) {
+        const int i = threadIdx.x + 256 * u;
+        if (i < R.len) slot[i] = R.pk[u];
+    }
+}
+
+// gather rhs and the first PF_E HBM-resident x values of this thread's row of
+// the packet in `slot` (already in LDS)
+__device__ __forceinline__ void pk_gather(const PkArgs &a, const int4 *slot, bool valid, PkRegs &R)
+{
+    R.ek[0] = R.ek[1] = -1;
+    if (!valid) return;
+    const int *w = reinterpret_cast<const int *>(slot);
+    const int nr = w[0];
+    const int tid = threadIdx.x;
+    if (tid >= nr) return;
+    R.rh = a.rhs[w[4 + tid]];
+    const int *rp = w + 4 + nr, *codes = w + 5 + 2 * nr;
+    int m = 0;
+    for (int k = rp[tid]; k < rp[tid + 1] && m < PF_E; k++) {
+        const int code = codes[k];
+        if (code >= 0) {
+            R.ek[m] = k;
+            R.ev[m] = __longlong_as_double((long long)ld_agent(a.x + code));
+            m++;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_tri_pk2(PkArgs a)
+{
+    __shared__ double ring[BP_RING];
+    __shared__ int4 pbuf[4][PK_VEC];
+    __shared__ double rbuf[4][PK_ROWS];
+    __shared__ double ebuf[4][PF_E][PK_ROWS];
+    __shared__ int kbuf[4][PF_E][PK_ROWS];
+    __shared__ int s_blk;
+    const int tid = threadIdx.x;
+    for (;;) {
+        __syncthreads();
+        if (tid == 0) s_blk = (int)(atomicAdd(a.claim, 1ull) - a.base);
+        __syncthreads();
+        const int b = s_blk;
+        if (b >= a.nb) break;
+        const int q0 = a.blk[b], q1 = a.blk[b + 1];
+        PkRegs RA, RB;
+        // prologue: packets 0..2 into slots 0..2
+        for (int j = 0; j < 3 && q0 + j < q1; j++) {
+            pk_issue(a, q0 + j, q1, RA);
+            pk_land(pbuf[j], RA);
+        }
+        __syncthreads();
+        pk_gather(a, pbuf[0], q0 < q1, RA);  // packet 0: straight to LDS
+        if (q0 < q1 && tid < PK_ROWS) {
+            rbuf[0][tid] = RA.rh;
+            for (int e = 0; e < PF_E; e++) {
+                ebuf[0][e][tid] = RA.ev[e];
+                kbuf[0][e][tid] = RA.ek[e];
+            }
+        }
+        pk_gather(a, pbuf[1], q0 + 1 < q1, RB);  // packet 1: lands at iteration 0
+        pk_issue(a, q0 + 3, q1, RA);             // packet 3: lands at iteration 0
+        __syncthreads();
+
+        auto iteration = [&](int i, PkRegs &cur, PkRegs &nxt) {
+            // cur: loads of packet i+3 + gathers of packet i+1 (issued last iteration)
+            // nxt: receives loads of packet i+4 and gathers of packet i+2
+            const int p = q0 + i;
+            PkRegs G;  // gathers of packet i+2 (registers)
+            pk_gather(a, pbuf[(i + 2) & 3], p + 2 < q1, G);
+            {
+                const int *w = reinterpret_cast<const int *>(pbuf[i & 3]);
+                const int nr = w[0], ne = w[1], pos0 = w[2];
+                if (tid < nr) {
+                    const int *rows = w + 4, *rp = w + 4 + nr, *codes = w + 5 + 2 * nr;
+                    const int vo = (5 + 2 * nr + ne + 1) & ~1;
+                    const double *vals = reinterpret_cast<const double *>(w + vo);
+                    const int row = rows[tid];
+                    double acc = rbuf[i & 3][tid];
+                    if (a.reset) a.reset[row] = __longlong_as_double((long long)TRI_SENTINEL);
+                    const int k0 = kbuf[i & 3][0][tid], k1 = kbuf[i & 3][1][tid];
+                    for (int k = rp[tid]; k < rp[tid + 1]; k++) {
+                        const int code = codes[k];
+                        double xv;
+                        if (code < 0) {
+                            xv = ring[-1 - code];
+                        } else {
+                            double pv = 0;
+                            bool have = false;
+                            if (k == k0) { pv = ebuf[i & 3][0][tid]; have = true; }
+                            else if (k == k1) { pv = ebuf[i & 3][1][tid]; have = true; }
+                            if (have && __double_as_longlong(pv) != (long long)TRI_SENTINEL) xv = pv;
+                            else xv = ld_ready(a.x + code, a.err);
+                        }
+                        acc = acc - vals[k] * xv;
+                    }
+                    const double xi = a.unit ? acc : acc / reinterpret_cast<const double *>(w + vo + 2 * ne)[tid];
+                    ring[(pos0 + tid) % BP_RING] = xi;
+                    st_agent(a.x + row, xi);
+                }
+            }
+            // land packet i+3 and the gathers of packet i+1; issue packet i+4
+            pk_land(pbuf[(i + 3) & 3], cur);
+            if (p + 1 < q1 && tid < PK_ROWS) {
+                rbuf[(i + 1) & 3][tid] = cur.rh;
+                ebuf[(i + 1) & 3][0][tid] = cur.ev[0];
+                ebuf[(i + 1) & 3][1][tid] = cur.ev[1];
+                kbuf[(i + 1) & 3][0][tid] = cur.ek[0];
+                kbuf[(i + 1) & 3][1][tid] = cur.ek[1];
+            }
+            pk_issue(a, p + 4, q1, nxt);
+            nxt.rh = G.rh;
+            for (int e = 0; e < PF_E; e++) {
+                nxt.ev[e] = G.ev[e];
+                nxt.ek[e] = G.ek[e];
+            }
+            lds_barrier();
+        };
+        // RB holds gathers of packet 1; RA holds loads of packet 3 -- merge into one "cur"
+        RA.rh = RB.rh;
+        for (int e = 0; e < PF_E; e++) {
+            RA.ev[e] = RB.ev[e];
+            RA.ek[e] = RB.ek[e];
+        }
+        const int np = q1 - q0;
+        int i = 0;
+        for (; i + 1 < np; i += 2) {
+            iteration(i, RA, RB);
+            iteration(i + 1, RB, RA);
+        }
+        if (i < np) iteration(i, RA, RB);
     }
 }
 
@@ -795,10 +1075,19 @@ int launch_trisolve(lssp_amd_ctx *c, const TriSched &t, const double *rhs, doubl
     if (t.n == 0) return LSSP_AMD_OK;
     long nchunks = (t.n + 63) / 64;
     TriArgs a{t.n, nchunks, t.perm, t.rp, t.cols, t.vals, t.diag, t.unit, rhs, x, reset, c->d_err};
+    if (c->tri_mode == 5 && t.pk_n >= 0) {
+        const int grid = std::min(t.bp_nb, c->num_cus);
+        PkArgs g{t.bp_nb, t.pk_blk, t.pk_off, reinterpret_cast<const int4 *>(t.pk_data), t.unit, rhs, x, reset,
+                 t.pk_claim, t.pk_base, c->d_err, c->tri_diag};
+        k_tri_pk2<<<grid, 256, 0, c->stream>>>(g);
+        t.pk_base += (unsigned long long)t.bp_nb + grid;
+        LSSP_HIP(hipGetLastError());
+        return LSSP_AMD_OK;
+    }
     if (c->tri_mode == 4 && t.pk_n >= 0) {
         const int grid = std::min(t.bp_nb, c->num_cus);
         PkArgs g{t.bp_nb, t.pk_blk, t.pk_off, reinterpret_cast<const int4 *>(t.pk_data), t.unit, rhs, x, reset,
-                 t.pk_claim, t.pk_base, c->d_err};
+                 t.pk_claim, t.pk_base, c->d_err, c->tri_diag};
         k_tri_pk<<<grid, 256, 0, c->stream>>>(g);
         t.pk_base += (unsigned long long)t.bp_nb + grid;
         LSSP_HIP(hipGetLastError());

@@ -1,0 +1,42 @@
+"""SpMV micro-benchmark (tuning aid): y = A x on the 7-pt grid, HIP events on the
+library stream; variant chosen by LSSP_AMD_SPMV (read once per process)."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--grid", type=int, default=216)
+    ap.add_argument("--reps", type=int, default=50)
+    args = ap.parse_args()
+    import torch
+    import lssp_amd
+    Ap, Aj, Ax = lssp_amd.poisson(3, args.grid)
+    n = Ap.size - 1
+    dev = lssp_amd.Device(0)
+    A = lssp_amd.DMat(dev, Ap, Aj, Ax)
+    x = dev.vec(n, np.random.default_rng(1).uniform(-1, 1, n))
+    y = dev.vec(n)
+    for _ in range(5):
+        A.mv_mxy(x, y)
+    s = torch.cuda.ExternalStream(dev.stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(args.reps):
+        A.mv_mxy(x, y)
+    e1.record(s)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / args.reps
+    b = 12 * int(Ap[-1]) + 20 * n + 4
+    print(json.dumps({"variant": os.environ.get("LSSP_AMD_SPMV", "0"), "grid": args.grid, "ms": round(ms, 5),
+                      "GBps": round(b / ms / 1e6, 1), "sum": float(y.download().sum())}))
+
+
+if __name__ == "__main__":
+    main()
