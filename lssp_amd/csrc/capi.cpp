@@ -106,6 +106,8 @@ int lssp_amd_ctx_create(int device, lssp_amd_ctx **out)
     if (tm) c->tri_mode = atoi(tm);
     const char *td = getenv("LSSP_AMD_TRI_DIAG");
     if (td) c->tri_diag = atoi(td);
+    const char *tdp = getenv("LSSP_AMD_TRI_DEPTH");
+    if (tdp) c->tri_depth = std::min(3, std::max(1, atoi(tdp)));
     *out = c;
     return LSSP_AMD_OK;
 }
@@ -369,7 +371,9 @@ int lssp_amd_vec_norm(lssp_amd_ctx *c, const double *x, long n, double *result)
 static int ilu_upload(lssp_amd_ctx *c, lssp_amd_ilu *M)
 {
     LSSP_TRY(build_trisched(c, M->n, M->Lp, M->Lj, M->Lx, false, M->lower));
-    LSSP_TRY(build_trisched(c, M->n, M->Up, M->Uj, M->Ux, true, M->upper));
+    LSSP_TRY(build_trisched(c, M->n, M->Up, M->Uj, M->Ux, true, M->upper, &M->lower));
+    M->lower.h_pos.clear();
+    M->lower.h_pos.shrink_to_fit();
     LSSP_HIP(hipMalloc(&M->d_cache, sizeof(double) * std::max(M->n, 1)));
     LSSP_TRY(launch_fill(c, M->d_cache, M->n, TRI_SENTINEL));
     LSSP_HIP(hipStreamSynchronize(c->stream));
@@ -447,6 +451,9 @@ int lssp_amd_ilu_destroy(lssp_amd_ilu *M)
     free_trisched(M->lower);
     free_trisched(M->upper);
     if (M->d_cache) (void)hipFree(M->d_cache);
+    for (double *p : M->d_sh)
+        if (p) (void)hipFree(p);
+    if (M->d_rperm) (void)hipFree(M->d_rperm);
     delete M;
     return LSSP_AMD_OK;
 }
@@ -468,8 +475,7 @@ static int check_err(lssp_amd_ctx *c)
 int lssp_amd_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const double *rhs)
 {
     if (!c || !M || !x || !rhs) return LSSP_AMD_EINVAL;
-    LSSP_TRY(launch_trisolve(c, M->lower, rhs, M->d_cache, x));
-    LSSP_TRY(launch_trisolve(c, M->upper, M->d_cache, x, M->d_cache));
+    LSSP_TRY(launch_ilu_apply(c, M, x, rhs));
     return check_err(c);
 }
 

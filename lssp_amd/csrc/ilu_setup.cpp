@@ -451,7 +451,7 @@ void ilu_factor(int kind, const HostCSR &A0, int level, double tol, int p, int b
 //          storage order (solver-tri.cxx:35-41) -- stored reversed here so the
 //          kernel always walks forward.
 int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std::vector<int> &Tj,
-                   const std::vector<double> &Tx, bool upper, TriSched &t)
+                   const std::vector<double> &Tx, bool upper, TriSched &t, const TriSched *prod)
 {
     t.n = n;
     std::vector<int> lev(n, 0);
@@ -489,7 +489,7 @@ int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std
     int nlev = 0;
     for (int i = 0; i < n; i++) nlev = std::max(nlev, lev[i] + 1);
     t.nlevels = n ? nlev : 0;
-    LSSP_TRY(build_bp_schedule(c, n, Tp, Tj, Tx, upper, lev, t));
+    LSSP_TRY(build_bp_schedule(c, n, Tp, Tj, Tx, upper, lev, t, prod));
     // counting sort by level; rows of a level stay in row order (lower) or in
     // descending row order (upper, mirroring the backward sweep)
     std::vector<int> start(nlev + 1, 0), perm(n);
@@ -555,7 +555,12 @@ void free_trisched(TriSched &t)
     for (void *p : {(void *)t.bp_perm, (void *)t.bp_rp, (void *)t.bp_cols, (void *)t.bp_vals, (void *)t.bp_diag,
                     (void *)t.bp_step_pos, (void *)t.bp_step_need, (void *)t.bp_step_done,
                     (void *)t.bp_step_flag, (void *)t.bp_blk_step, (void *)t.bp_prog, (void *)t.bp_claim,
-                    (void *)t.pk_blk, (void *)t.pk_off, t.pk_data, (void *)t.pk_claim})
+                    (void *)t.pk_blk, (void *)t.pk_off, t.pk_data, (void *)t.pk_claim,
+                    (void *)t.pk3_blk, (void *)t.pk3_off, t.pk3_data, (void *)t.pk3_claim,
+                    (void *)t.pk4_blk, (void *)t.pk4_off, t.pk4_data, (void *)t.pk4_claim,
+                    (void *)t.pk5_blk, (void *)t.pk5_desc, (void *)t.pk5_idx, (void *)t.pk5_rec,
+                    (void *)t.pk5_claim, (void *)t.pk6_blk, (void *)t.pk6_desc, (void *)t.pk6_idx,
+                    (void *)t.pk6_rec, (void *)t.pk6_claim})
         if (p) (void)hipFree(p);
     t = TriSched();
 }

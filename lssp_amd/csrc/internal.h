@@ -77,6 +77,7 @@ struct lssp_amd_ctx {
     // 3 block pipeline with progress words, 4 packet-streamed block pipeline
     int tri_mode = 4;
     int tri_diag = 0;  // LSSP_AMD_TRI_DIAG timing experiments (wrong results when != 0)
+    int tri_depth = 2; // LSSP_AMD_TRI_DEPTH: tri_mode 6 prefetch depth S (2, 3), tri_mode 7 x lead KE (1, 2)
     // Krylov work vectors, kept across solves (no hipMalloc on the solve path)
     struct WsBuf {
         double *p;
@@ -104,7 +105,7 @@ struct lssp_amd_mat {
 namespace lssp_amd {
 
 struct TriSched {
-    int n = 0, nnz = 0, nlevels = 0, unit = 0;
+    int n = 0, nnz = 0, nlevels = 0, unit = 0, upper = 0;
     int *perm = nullptr;   // position -> row, rows ordered by level
     int *rp = nullptr;     // [n+1] entry ranges in schedule order
     int *cols = nullptr;   // strict entries, in the reference's summation order
@@ -131,9 +132,39 @@ struct TriSched {
     void *pk_data = nullptr;
     mutable unsigned long long pk_base = 0;
     unsigned long long *pk_claim = nullptr;
+    // packets v3 (tri_mode 6: loader waves gather HBM operands ahead, tri_bp.cpp)
+    int pk3_n = 0;
+    int *pk3_blk = nullptr, *pk3_off = nullptr;
+    void *pk3_data = nullptr;
+    mutable unsigned long long pk3_base = 0;
+    unsigned long long *pk3_claim = nullptr;
+    // packets v4 (tri_mode 7: column-major fixed-width rows, register-prefetched)
+    int pk4_n = 0;
+    int *pk4_blk = nullptr, *pk4_off = nullptr;
+    void *pk4_data = nullptr;
+    mutable unsigned long long pk4_base = 0;
+    unsigned long long *pk4_claim = nullptr;
+    // packets v5 (tri_mode 8: register records straight from HBM, LDS only for values)
+    int pk5_n = 0, pk5_ep = 4;
+    int *pk5_blk = nullptr, *pk5_desc = nullptr, *pk5_idx = nullptr;
+    uint32_t *pk5_rec = nullptr;
+    mutable unsigned long long pk5_base = 0;
+    unsigned long long *pk5_claim = nullptr;
+    // packets v6 (tri_mode 9: schedule-ordered shadow vectors between sweeps)
+    int pk6_n = 0, pk6_ep = 4;
+    int *pk6_blk = nullptr, *pk6_desc = nullptr, *pk6_idx = nullptr;
+    uint32_t *pk6_rec = nullptr;
+    mutable unsigned long long pk6_base = 0;
+    unsigned long long *pk6_claim = nullptr;
+    std::vector<int> h_pos;  // L factor: row -> schedule position (for the U factor's build)
 };
 constexpr int PK_ROWS = 256;
 constexpr int PK_BYTES = 12288;
+constexpr int PK3_ROWS = 256;    // rows per packet = compute lanes = loader lanes
+constexpr int PK3_EXT = 2;       // HBM x operands per packet row (on average)
+constexpr int PK3_BYTES = 12288;
+constexpr int PK3_CAP = 4096;    // packets per block (offsets staged in LDS)
+constexpr int PK4_PAD = -1 - 4096;  // v4 padding code: the value-ring slot past the end (holds +0.0)
 
 }  // namespace lssp_amd
 
@@ -144,6 +175,11 @@ struct lssp_amd_ilu {
     std::vector<double> Lx, Ux;
     lssp_amd::TriSched lower, upper;
     double *d_cache = nullptr;  // L sweep output, kept all-sentinel between applies
+    // tri_mode 9: schedule-ordered shadows {L out, L out', U out, U out'} and the
+    // apply counter selecting the buffer pair (kernels.hip launch_ilu_apply)
+    mutable double *d_sh[4] = {nullptr, nullptr, nullptr, nullptr};
+    mutable double *d_rperm = nullptr;  // the apply's rhs in L order
+    mutable unsigned epoch = 0;
     double setup_seconds = 0;
 };
 
@@ -199,11 +235,29 @@ int launch_trisolve(lssp_amd_ctx *c, const TriSched &t, const double *rhs, doubl
 constexpr int BP_RING = 4096;  // LDS ring of recently computed values (32 KB)
 int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std::vector<int> &Tj,
                       const std::vector<double> &Tx, bool upper, const std::vector<int> &lev,
-                      TriSched &t);
+                      TriSched &t, const TriSched *prod = nullptr);
 int build_packets(int n, const std::vector<int> &perm, const std::vector<int> &rp,
                   const std::vector<int> &cols, const std::vector<double> &vals,
                   const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
                   const std::vector<int> &blk_step, int nb, long B, TriSched &t);
+int build_packets3(int n, const std::vector<int> &perm, const std::vector<int> &rp,
+                   const std::vector<int> &cols, const std::vector<double> &vals,
+                   const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
+                   const std::vector<int> &blk_step, int nb, long B, TriSched &t);
+int build_packets4(int n, const std::vector<int> &perm, const std::vector<int> &rp,
+                   const std::vector<int> &cols, const std::vector<double> &vals,
+                   const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
+                   const std::vector<int> &blk_step, int nb, long B, TriSched &t);
+int build_packets5(int n, const std::vector<int> &perm, const std::vector<int> &rp,
+                   const std::vector<int> &cols, const std::vector<double> &vals,
+                   const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
+                   const std::vector<int> &blk_step, int nb, long B, TriSched &t);
+int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &pos, const std::vector<int> &rp,
+                   const std::vector<int> &cols, const std::vector<double> &vals,
+                   const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
+                   const std::vector<int> &blk_step, int nb, long B, const std::vector<int> &rhs_index,
+                   TriSched &t);
+int launch_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const double *rhs);
 int launch_pack(lssp_amd_ctx *c, const int *idx, const double *x, double *buf, int n);
 int launch_sum_ranks(lssp_amd_ctx *c, int nslot, const Fin &f);
 
@@ -221,7 +275,7 @@ void sort_columns(HostCSR &A);
 void ilu_factor(int kind, const HostCSR &A, int level, double tol, int p, int blk, HostCSR &L,
                 HostCSR &U);
 int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std::vector<int> &Tj,
-                   const std::vector<double> &Tx, bool upper, TriSched &t);
+                   const std::vector<double> &Tx, bool upper, TriSched &t, const TriSched *prod = nullptr);
 void free_trisched(TriSched &t);
 
 // reductions with the context's mode; result left in d_sums / scal per Fin

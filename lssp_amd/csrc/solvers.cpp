@@ -93,8 +93,7 @@ struct Run {
             e.out0 = x;
             return launch_ew(c, e);
         }
-        LSSP_TRY(launch_trisolve(c, M->lower, rhs, M->d_cache, x));
-        return launch_trisolve(c, M->upper, M->d_cache, x, M->d_cache);
+        return launch_ilu_apply(c, M, x, rhs);
     }
     int sync(int first, int count)
     {

@@ -33,9 +33,11 @@ def main():
     out = []
     M = None
     for cfg in args.configs.split(","):
-        mode, bpc = cfg.split(":")
+        f = cfg.split(":")
+        mode, bpc = f[0], f[1]
         os.environ["LSSP_AMD_TRI_MODE"] = mode
         os.environ["LSSP_AMD_TRI_BLOCKS_PER_CU"] = bpc
+        os.environ["LSSP_AMD_TRI_DEPTH"] = f[2] if len(f) > 2 else "2"
         dev = lssp_amd.Device(0)
         kind = lssp_amd.ILUK if args.kind == "iluk" else lssp_amd.ILUT
         if M is None:
@@ -58,7 +60,7 @@ def main():
         e1.synchronize()
         ms = e0.elapsed_time(e1) / args.reps
         ok = bool(np.array_equal(x.download(), ref))
-        out.append({"mode": int(mode), "blocks_per_cu": int(bpc), "apply_ms": round(ms, 4),
+        out.append({"mode": int(mode), "blocks_per_cu": int(bpc), "depth": int(os.environ["LSSP_AMD_TRI_DEPTH"]), "apply_ms": round(ms, 4),
                     "us_per_level": round(ms * 1e3 / (levels[0] + levels[1]), 3), "stable": ok})
         print(json.dumps(out[-1]), flush=True)
         dev.close()
