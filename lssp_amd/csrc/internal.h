@@ -74,8 +74,10 @@ struct lssp_amd_ctx {
     double *d_gather = nullptr;  // [nranks][MAX_SLOTS]
     int tri_blocks_per_cu = 1;
     // 0 sync-free + back-off, 1 one launch per level, 2 sync-free no back-off,
-    // 3 block pipeline with progress words, 4 packet-streamed block pipeline
-    int tri_mode = 4;
+    // 3 block pipeline with progress words, 4 packet-streamed block pipeline,
+    // 5-8 packet-pipeline experiments, 9 role-split packet sweeps through
+    // schedule-ordered shadows (default; kernels.hip k_tri_pk6)
+    int tri_mode = 9;
     int tri_diag = 0;  // LSSP_AMD_TRI_DIAG timing experiments (wrong results when != 0)
     int tri_depth = 2; // LSSP_AMD_TRI_DEPTH: tri_mode 6 prefetch depth S (2, 3), tri_mode 7 x lead KE (1, 2)
     // Krylov work vectors, kept across solves (no hipMalloc on the solve path)
@@ -151,7 +153,7 @@ struct TriSched {
     mutable unsigned long long pk5_base = 0;
     unsigned long long *pk5_claim = nullptr;
     // packets v6 (tri_mode 9: schedule-ordered shadow vectors between sweeps)
-    int pk6_n = 0, pk6_ep = 4;
+    int pk6_n = 0, pk6_ep = 4, pk6_rows = 256;
     int *pk6_blk = nullptr, *pk6_desc = nullptr, *pk6_idx = nullptr;
     uint32_t *pk6_rec = nullptr;
     mutable unsigned long long pk6_base = 0;

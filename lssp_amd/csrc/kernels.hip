@@ -1947,22 +1947,23 @@ struct Pk6Rec {
 
 __device__ __forceinline__ int code16(int w, int hi) { return hi ? (w >> 16) : (int)(short)(w & 0xffff); }
 
-template <int EP, int KE, bool NAT>
-__global__ __launch_bounds__(2 * PK3_ROWS + 64) void k_tri_pk6(Pk6Args a)
+template <int EP, int KE, bool NAT, int NR>
+__global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args a)
 {
     constexpr int IA = KE + 2;
     constexpr int D = KE + 2;
     constexpr int Q = D + 1;
     __shared__ double ring[BP_RING + 1];
-    __shared__ double rbuf[2][PK3_ROWS];
-    __shared__ double xbuf[2][PK3_ROWS * PK3_EXT];
-    __shared__ int rowbuf[2][PK3_ROWS];
+    __shared__ double rbuf[2][NR];
+    __shared__ double xbuf[2][NR * PK3_EXT];
+    __shared__ int rowbuf[2][NR];
     __shared__ int4 sdesc[PK3_CAP];
     __shared__ int s_blk;
     __shared__ unsigned s_polls;
     const int tid = threadIdx.x;
-    const int role = __builtin_amdgcn_readfirstlane(tid) / PK3_ROWS;  // 0 compute, 1 loader, 2 store
-    const int t = tid & (PK3_ROWS - 1);
+    const int role = __builtin_amdgcn_readfirstlane(tid) / NR;  // 0 compute, 1 loader, 2 store
+    static_assert(!NAT || NR == 256, "the store wave needs a 256-row packet");
+    const int t = tid & (NR - 1);
     if (tid == 0) ring[BP_RING] = 0.0;
     int prev = -1;
     for (;;) {
@@ -1996,33 +1997,33 @@ __global__ __launch_bounds__(2 * PK3_ROWS + 64) void k_tri_pk6(Pk6Args a)
                              __builtin_amdgcn_readfirstlane(d.z), __builtin_amdgcn_readfirstlane(d.w));
         };
 
+        // descriptor of a packet, clamped: out-of-range packets get nr = nx = 0
+        // and read valid dummy records (no branches around the loads)
+        auto descc = [&](int p) {
+            int4 d = desc(min(max(p, 0), max(np - 1, 0)));
+            if (p < 0 || p >= np) d.z = 0;
+            return d;
+        };
         if (role == 0) {
             uint64_t c0 = 0, c1 = 0, acc_c = 0, acc_b = 0;
-            // descriptor of a packet, clamped: out-of-range packets get nr = 0
-            // and read valid dummy records (no branches around the loads)
-            auto descc = [&](int p) {
-                int4 d = desc(min(max(p, 0), max(np - 1, 0)));
-                if (p < 0 || p >= np) d.z = 0;
-                return d;
-            };
-            auto issue = [&](const int4 d, Pk6Rec<EP> &R) {
-                const int nr = d.z & 0x1ff;
+            auto issue = [&](const int4 d, Pk6Rec<EP> &Rr) {
+                const int nr = d.z & 0x3ff;
                 const int n1 = nr > 0 ? nr : 1, tt = min(t, n1 - 1);
                 const uint32_t *base = a.rec + 4L * d.x;
                 const int wc = ((EP / 2) * n1 + 3) & ~3, wd = (2 * n1 + 3) & ~3;
-                R.c = reinterpret_cast<const decltype(R.c) *>(base)[tt];
+                Rr.c = reinterpret_cast<const decltype(Rr.c) *>(base)[tt];
                 typedef double v2d __attribute__((ext_vector_type(2)));
                 const v2d *vb = reinterpret_cast<const v2d *>(base + wc);
 #pragma unroll
                 for (int q = 0; q < EP / 2; q++) {
                     const v2d v = vb[q * n1 + tt];
-                    R.v[2 * q] = v.x;
-                    R.v[2 * q + 1] = v.y;
+                    Rr.v[2 * q] = v.x;
+                    Rr.v[2 * q + 1] = v.y;
                 }
-                R.dg = reinterpret_cast<const double *>(vb + (EP / 2) * n1)[tt];
-                if (NAT) R.row = reinterpret_cast<const int *>(base + wc + 2 * EP * n1 + wd)[tt];
-                R.nr = nr;
-                R.pos0 = d.w;
+                Rr.dg = reinterpret_cast<const double *>(vb + (EP / 2) * n1)[tt];
+                if (NAT) Rr.row = reinterpret_cast<const int *>(base + wc + 2 * EP * n1 + wd)[tt];
+                Rr.nr = nr;
+                Rr.pos0 = d.w;
             };
             int4 dn = descc(-1);  // descriptor of packet j+D, read one step ahead
             auto step = [&](int j, Pk6Rec<EP> &Rc, Pk6Rec<EP> &Rn) {
@@ -2064,7 +2065,7 @@ __global__ __launch_bounds__(2 * PK3_ROWS + 64) void k_tri_pk6(Pk6Args a)
             Pk6Rec<EP> R0, R1, R2, R3, R4;
             R0.nr = R1.nr = R2.nr = R3.nr = R4.nr = 0;
             dn = descc(-D + D);  // packet 0 is issued at step -D
-            for (int j0 = -D; j0 < T - D; j0 += Q) {  // packet p in R[(p+1) % Q], j0 == 1 (mod Q)
+            for (int j0 = -D; j0 < T - D; j0 += Q) {  // packet p in NR[(p+1) % Q], j0 == 1 (mod Q)
                 if constexpr (Q == 4) {
                     step(j0, R2, R1);
                     step(j0 + 1, R3, R2);
@@ -2083,26 +2084,20 @@ __global__ __launch_bounds__(2 * PK3_ROWS + 64) void k_tri_pk6(Pk6Args a)
             if (!(a.diag & 1)) {
                 const long s0 = bbase, s1 = min(s0 + a.B, (long)a.n);
                 uint64_t *rs = reinterpret_cast<uint64_t *>(a.sh_next);
-                for (long i = s0 + t; i < s1; i += PK3_ROWS) rs[i] = TRI_SENTINEL;
+                for (long i = s0 + t; i < s1; i += NR) rs[i] = TRI_SENTINEL;
             }
             if (a.trace && tid == 0) {
                 a.trace[8 * b + 4] = acc_c;
                 a.trace[8 * b + 5] = acc_b;
             }
         } else if (role == 1) {
-            uint64_t acc_w = 0, acc_lb = 0;
-            auto issue_idx = [&](int p, Pk5Ld &L) {
-                int io = 0, nr = 0, nx = 0;
-                if (p >= 0 && p < np) {
-                    const int4 d = desc(p);
-                    io = d.y;
-                    nr = d.z & 0x1ff;
-                    nx = (d.z >> 9) & 0x3ff;
-                }
-                const int *base = a.idx + io;
+            uint64_t acc_w = 0, acc_lb = 0, acc_is = 0, acc_ld = 0, m0 = 0;
+            auto issue_idx = [&](const int4 d, Pk5Ld &L) {
+                const int nr = d.z & 0x3ff, nx = (d.z >> 10) & 0x7ff;
+                const int *base = a.idx + d.y;
                 L.row = base[max(min(t, nr - 1), 0)];
 #pragma unroll
-                for (int e = 0; e < PK3_EXT; e++) L.xi[e] = base[nr + max(min(t + PK3_ROWS * e, nx - 1), 0)];
+                for (int e = 0; e < PK3_EXT; e++) L.xi[e] = base[nr + max(min(t + NR * e, nx - 1), 0)];
                 L.nr = nr;
                 L.nx = nx;
             };
@@ -2111,34 +2106,46 @@ __global__ __launch_bounds__(2 * PK3_ROWS + 64) void k_tri_pk6(Pk6Args a)
 #pragma unroll
                 for (int e = 0; e < PK3_EXT; e++) L.ev[e] = ld_agent(a.sh + ((a.diag & 8) ? 0 : L.xi[e]));
             };
+            int4 dl = descc(-D + IA);  // descriptor of packet j+IA, read one step ahead
             auto step = [&](int j, Pk5Ld &Li, Pk5Ld &Lg, Pk5Ld &Ll) {
                 if (a.diag & 16) {  // timing experiment: loader idle
                     lds_barrier();
                     return;
                 }
-                issue_idx(j + IA, Li);
+                if (a.trace) m0 = __builtin_amdgcn_s_memtime();
+                issue_idx(dl, Li);
                 gather(Lg);
+                dl = descc(j + IA + 1);
                 uint64_t l0 = 0;
-                if (a.trace) l0 = __builtin_amdgcn_s_memtime();
+                if (a.trace) {
+                    l0 = __builtin_amdgcn_s_memtime();
+                    acc_is += l0 - m0;
+                }
                 asm volatile("" ::"v"(Ll.rh), "v"(Ll.ev[0]), "v"(Ll.ev[1]));
-                if (a.trace) acc_w += __builtin_amdgcn_s_memtime() - l0;
-                if (j + 1 >= 0 && j + 1 < np) {  // land packet j+1
-                    if (t < Ll.nr) rbuf[(j + 1) & 1][t] = Ll.rh;
+                uint64_t l2 = 0;
+                if (a.trace) {
+                    l2 = __builtin_amdgcn_s_memtime();
+                    acc_w += l2 - l0;
+                }
+                // land packet j+1 (nr = nx = 0 outside the block's packets)
+                if (t < Ll.nr) rbuf[(j + 1) & 1][t] = Ll.rh;
 #pragma unroll
-                    for (int e = 0; e < PK3_EXT; e++) {
-                        const int k = t + PK3_ROWS * e;
-                        if (k < Ll.nx) {
-                            uint64_t bits = Ll.ev[e];
-                            if (bits == TRI_SENTINEL && !(a.diag & 8)) {
-                                bits = poll_ready(a.sh + Ll.xi[e], a.err);
-                                if (a.trace) atomicAdd(&s_polls, 1u);
-                            }
-                            xbuf[(j + 1) & 1][k] = __longlong_as_double((long long)bits);
+                for (int e = 0; e < PK3_EXT; e++) {
+                    const int k = t + NR * e;
+                    if (k < Ll.nx) {
+                        uint64_t bits = Ll.ev[e];
+                        if (bits == TRI_SENTINEL && !(a.diag & 8)) {
+                            bits = poll_ready(a.sh + Ll.xi[e], a.err);
+                            if (a.trace) atomicAdd(&s_polls, 1u);
                         }
+                        xbuf[(j + 1) & 1][k] = __longlong_as_double((long long)bits);
                     }
                 }
                 uint64_t l1 = 0;
-                if (a.trace) l1 = __builtin_amdgcn_s_memtime();
+                if (a.trace) {
+                    l1 = __builtin_amdgcn_s_memtime();
+                    acc_ld += l1 - l2;
+                }
                 lds_barrier();
                 if (a.trace) acc_lb += __builtin_amdgcn_s_memtime() - l1;
             };
@@ -2163,9 +2170,10 @@ __global__ __launch_bounds__(2 * PK3_ROWS + 64) void k_tri_pk6(Pk6Args a)
                 }
             }
             (void)L4;
-            if (a.trace && tid == PK3_ROWS) {
-                a.trace[8 * b + 6] = acc_w;
-                a.trace[8 * b + 7] = acc_lb;
+            if (a.trace && tid == NR) {  // compute's barrier share is dropped here
+                a.trace[8 * b + 5] = acc_w;
+                a.trace[8 * b + 6] = acc_is;
+                a.trace[8 * b + 7] = acc_ld;
             }
         } else {
             // store wave: at step j write packet j-1's values in natural order
@@ -2174,7 +2182,7 @@ __global__ __launch_bounds__(2 * PK3_ROWS + 64) void k_tri_pk6(Pk6Args a)
             auto store = [&](int p) {
                 if (NAT && p >= 0 && p < np) {
                     const int4 d = desc(p);
-                    const int nr = d.z & 0x1ff;
+                    const int nr = d.z & 0x3ff;
                     for (int k = lane; k < nr; k += 64)
                         a.nat[rowbuf[p & 1][k]] = ring[(d.w + k - bbase) % BP_RING];
                 }
@@ -2332,14 +2340,33 @@ static int launch_pk6(lssp_amd_ctx *c, const TriSched &t, const double *rhs, dou
     }
     Pk6Args g{t.bp_nb, t.pk6_blk, reinterpret_cast<const int4 *>(t.pk6_desc), t.pk6_rec, t.pk6_idx, rhs, sh,
               sh_next, nat, t.n, t.bp_B, t.pk6_claim, t.pk6_base, c->d_err, c->tri_diag, d_trace};
-    const int threads = 2 * PK3_ROWS + (NAT ? 64 : 0);
     const bool ke2 = c->tri_depth == 2;
-    if (t.pk6_ep == 4) {
-        if (ke2) k_tri_pk6<4, 2, NAT><<<grid, threads, 0, c->stream>>>(g);
-        else k_tri_pk6<4, 1, NAT><<<grid, threads, 0, c->stream>>>(g);
+    if constexpr (NAT) {
+        const int threads = 2 * 256 + 64;
+        if (t.pk6_rows != 256) return LSSP_AMD_EUNSUPPORTED;
+        if (t.pk6_ep == 4) {
+            if (ke2) k_tri_pk6<4, 2, true, 256><<<grid, threads, 0, c->stream>>>(g);
+            else k_tri_pk6<4, 1, true, 256><<<grid, threads, 0, c->stream>>>(g);
+        } else {
+            if (ke2) k_tri_pk6<8, 2, true, 256><<<grid, threads, 0, c->stream>>>(g);
+            else k_tri_pk6<8, 1, true, 256><<<grid, threads, 0, c->stream>>>(g);
+        }
+    } else if (t.pk6_rows == 512) {
+        if (t.pk6_ep == 4) {
+            if (ke2) k_tri_pk6<4, 2, false, 512><<<grid, 1024, 0, c->stream>>>(g);
+            else k_tri_pk6<4, 1, false, 512><<<grid, 1024, 0, c->stream>>>(g);
+        } else {
+            if (ke2) k_tri_pk6<8, 2, false, 512><<<grid, 1024, 0, c->stream>>>(g);
+            else k_tri_pk6<8, 1, false, 512><<<grid, 1024, 0, c->stream>>>(g);
+        }
     } else {
-        if (ke2) k_tri_pk6<8, 2, NAT><<<grid, threads, 0, c->stream>>>(g);
-        else k_tri_pk6<8, 1, NAT><<<grid, threads, 0, c->stream>>>(g);
+        if (t.pk6_ep == 4) {
+            if (ke2) k_tri_pk6<4, 2, false, 256><<<grid, 512, 0, c->stream>>>(g);
+            else k_tri_pk6<4, 1, false, 256><<<grid, 512, 0, c->stream>>>(g);
+        } else {
+            if (ke2) k_tri_pk6<8, 2, false, 256><<<grid, 512, 0, c->stream>>>(g);
+            else k_tri_pk6<8, 1, false, 256><<<grid, 512, 0, c->stream>>>(g);
+        }
     }
     t.pk6_base += (unsigned long long)t.bp_nb + grid;
     LSSP_HIP(hipGetLastError());

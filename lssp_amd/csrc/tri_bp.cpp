@@ -544,7 +544,7 @@ int build_packets5(int n, const std::vector<int> &perm, const std::vector<int> &
 // of row perm[p]), so the cross-block operands of a packet and its output are
 // contiguous runs instead of one cache line per row.  Per packet:
 //   desc  int4 {record offset (16 B units), index offset (4 B units),
-//               nr | nx << 9 | emax << 19, schedule position of the first row}
+//               nr | nx << 10 | emax << 21, schedule position of the first row}
 //   records (compute lanes), arrays over the packet's rows, 16-byte aligned:
 //     C  codes as int16 pairs: uint2 {c0|c1<<16, c2|c3<<16} (EP 4) or uint4 (EP 8)
 //        -- -1-slot (value ring), PK4_PAD, or an xidx index
@@ -559,6 +559,8 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
                    const std::vector<int> &blk_step, int nb, long B, const std::vector<int> &rhs_index,
                    TriSched &t)
 {
+    const char *er = getenv("LSSP_AMD_TRI_PK_ROWS");
+    const int ROWS = er && atoi(er) == 512 ? 512 : 256;  // rows per packet = compute lanes
     int maxlen = 0;
     for (int p = 0; p < n; p++) maxlen = std::max(maxlen, rp[p + 1] - rp[p]);
     if (maxlen > 8) return LSSP_AMD_EUNSUPPORTED;
@@ -577,12 +579,12 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
             while (p < step_pos[s + 1]) {
                 int nr = 0, emax = 0;
                 xl.clear();
-                while (p + nr < step_pos[s + 1] && nr < PK3_ROWS) {
+                while (p + nr < step_pos[s + 1] && nr < ROWS) {
                     const int r = p + nr;
                     int newx = 0;
                     for (int k = rp[r]; k < rp[r + 1]; k++)
                         if (cols[k] >= 0 && stamp[cols[k]] != pid) newx++;
-                    if ((long)xl.size() + newx > (long)PK3_ROWS * PK3_EXT) break;
+                    if ((long)xl.size() + newx > (long)ROWS * PK3_EXT) break;
                     for (int k = rp[r]; k < rp[r + 1]; k++) {
                         const int g = cols[k];
                         if (g >= 0 && stamp[g] != pid) {
@@ -599,7 +601,7 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
                 if (ro > INT_MAX || io > INT_MAX) return LSSP_AMD_EUNSUPPORTED;
                 desc.push_back((int)ro);
                 desc.push_back((int)io);
-                desc.push_back(nr | (nx << 9) | (emax << 19));
+                desc.push_back(nr | (nx << 10) | (emax << 21));
                 desc.push_back(p);
                 // C: (EP/2) words per row, V: 2*EP, D: 2, ROW: 1 -- each array padded to 4 words
                 auto pad4 = [](long w) { return (w + 3) & ~3L; };
@@ -635,6 +637,7 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
     idx.push_back(0);
     t.pk6_n = blk[nb];
     t.pk6_ep = EP;
+    t.pk6_rows = ROWS;
     auto up = [](auto *&d, const auto &h) -> int {
         using T = typename std::remove_reference<decltype(h)>::type::value_type;
         LSSP_HIP(hipMalloc(&d, sizeof(T) * std::max<size_t>(h.size(), 1)));

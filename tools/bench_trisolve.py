@@ -38,6 +38,8 @@ def main():
         os.environ["LSSP_AMD_TRI_MODE"] = mode
         os.environ["LSSP_AMD_TRI_BLOCKS_PER_CU"] = bpc
         os.environ["LSSP_AMD_TRI_DEPTH"] = f[2] if len(f) > 2 else "2"
+        os.environ["LSSP_AMD_TRI_PK_ROWS"] = f[3] if len(f) > 3 else "256"
+        os.environ["LSSP_AMD_TRI_BP_MULT"] = f[4] if len(f) > 4 else "1"
         dev = lssp_amd.Device(0)
         kind = lssp_amd.ILUK if args.kind == "iluk" else lssp_amd.ILUT
         if M is None:
@@ -60,7 +62,8 @@ def main():
         e1.synchronize()
         ms = e0.elapsed_time(e1) / args.reps
         ok = bool(np.array_equal(x.download(), ref))
-        out.append({"mode": int(mode), "blocks_per_cu": int(bpc), "depth": int(os.environ["LSSP_AMD_TRI_DEPTH"]), "apply_ms": round(ms, 4),
+        out.append({"mode": int(mode), "blocks_per_cu": int(bpc), "depth": int(os.environ["LSSP_AMD_TRI_DEPTH"]),
+                    "rows": int(os.environ["LSSP_AMD_TRI_PK_ROWS"]), "mult": int(os.environ["LSSP_AMD_TRI_BP_MULT"]), "apply_ms": round(ms, 4),
                     "us_per_level": round(ms * 1e3 / (levels[0] + levels[1]), 3), "stable": ok})
         print(json.dumps(out[-1]), flush=True)
         dev.close()

@@ -123,6 +123,47 @@ __global__ __launch_bounds__(512) void k_step(const double *rec, double *out, in
     if (t == 0) cyc[0] = t1 - t0;
 }
 
+
+// ping-pong with explicit cache policies: MODE 0 sc1 store / sc1 load,
+// MODE 1 plain store / sc0 load (L2-coherent, same XCD only), MODE 2 sc1 store / sc0 load
+template <int MODE>
+__device__ __forceinline__ void pp_store(unsigned long long *p, unsigned long long v)
+{
+    if (MODE == 1) asm volatile("global_store_dwordx2 %0, %1, off" :: "v"(p), "v"(v) : "memory");
+    else asm volatile("global_store_dwordx2 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
+}
+template <int MODE>
+__device__ __forceinline__ unsigned long long pp_load(const unsigned long long *p)
+{
+    unsigned long long v;
+    if (MODE == 0) asm volatile("global_load_dwordx2 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    else asm volatile("global_load_dwordx2 %0, %1, off sc0\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+template <int MODE>
+__global__ void k_pp2(unsigned long long *v, unsigned long long *w, int iters, int partner, unsigned long long *out)
+{
+    if (threadIdx.x != 0) return;
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (blockIdx.x == 0) {
+        uint64_t t0 = __builtin_amdgcn_s_memtime();
+        for (int i = 0; i < iters; i++) {
+            pp_store<MODE>(v + i, (unsigned long long)(i + 1));
+            for (long g = 0; g < (1L << 14) && pp_load<MODE>(w + i) != (unsigned long long)(i + 1); g++) {}
+        }
+        uint64_t t1 = __builtin_amdgcn_s_memtime();
+        out[0] = t1 - t0;
+        out[2] = xcc;
+    } else if ((int)blockIdx.x == partner) {
+        for (int i = 0; i < iters; i++) {
+            for (long g = 0; g < (1L << 14) && pp_load<MODE>(v + i) != (unsigned long long)(i + 1); g++) {}
+            pp_store<MODE>(w + i, (unsigned long long)(i + 1));
+        }
+        out[3] = xcc;
+    }
+}
+
 int main()
 {
     unsigned long long *d_out;
@@ -147,9 +188,12 @@ int main()
         CK(hipMemcpy(d, nx.data(), N * sizeof(long), hipMemcpyHostToDevice));
         const int ci = 2000;
         k_chase<0><<<1, 1>>>(d, ci, d_out);
+        CK(hipMemcpy(h, d_out, 16, hipMemcpyDeviceToHost));
+        double cold = (double)h[0] / ci;
         k_chase<0><<<1, 1>>>(d, ci, d_out);
         CK(hipMemcpy(h, d_out, 16, hipMemcpyDeviceToHost));
         double plain = (double)h[0] / ci;
+        printf("{\"chase_bytes\": %ld, \"cold_cycles\": %.1f}\n", N * 8, cold);
         k_chase<1><<<1, 1>>>(d, ci, d_out);
         CK(hipMemcpy(h, d_out, 16, hipMemcpyDeviceToHost));
         printf("{\"chase_bytes\": %ld, \"plain_cycles\": %.1f, \"sc1_cycles\": %.1f}\n", N * 8, plain,
@@ -157,7 +201,7 @@ int main()
         CK(hipFree(d));
     }
     unsigned long long *v, *w;
-    const int pi = 2000;
+    const int pi = 200;
     CK(hipMalloc(&v, pi * 8));
     CK(hipMalloc(&w, pi * 8));
     for (int partner : {1, 2, 8, 16, 100}) {
@@ -189,6 +233,21 @@ int main()
             }
         }
     }
+    for (int mode = 0; mode < 3; mode++)
+        for (int partner : {8, 1}) {
+            if (mode == 1 && partner == 1) continue;  // plain stores are not visible across XCDs
+            CK(hipMemset(v, 0, pi * 8));
+            CK(hipMemset(w, 0, pi * 8));
+            CK(hipMemset(d_out, 0, 64));
+            if (mode == 0) k_pp2<0><<<256, 64>>>(v, w, pi, partner, d_out);
+            if (mode == 1) k_pp2<1><<<256, 64>>>(v, w, pi, partner, d_out);
+            if (mode == 2) k_pp2<2><<<256, 64>>>(v, w, pi, partner, d_out);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(h, d_out, 32, hipMemcpyDeviceToHost));
+            printf("{\"pp2_round_trip_cycles\": %.1f, \"mode\": %d, \"partner\": %d, \"xcc\": [%llu, %llu]}\n",
+                   (double)h[0] / pi, mode, partner, h[2], h[3]);
+            fflush(stdout);
+        }
     // s_memtime frequency: compare with wall clock
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
