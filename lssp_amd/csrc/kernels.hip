@@ -2091,20 +2091,37 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                 a.trace[8 * b + 5] = acc_b;
             }
         } else if (role == 1) {
+            // The loader's loads are issued from inline asm with explicit
+            // vmcnt waits: its register sets rotate across the loop back-edge,
+            // where the compiler's own wait counting turns conservative and
+            // waited for the previous step's gathers before issuing new ones.
+            // Per step, in issue order: 3 index loads (packet j+IA), then 3
+            // gathers (packet j+KE) -- so before the gathers, the indices they
+            // use (issued at step j-2) have exactly 12 younger loads, and the
+            // gathers landed at the end of step j (packet j+1, issued at step
+            // j+1-KE) have 6 (KE 2) or 0 (KE 1) younger loads.
+            static_assert(PK3_EXT == 2 && IA - KE == 2, "wait counts below assume this layout");
             uint64_t acc_w = 0, acc_lb = 0, acc_is = 0, acc_ld = 0, m0 = 0;
             auto issue_idx = [&](const int4 d, Pk5Ld &L) {
                 const int nr = d.z & 0x3ff, nx = (d.z >> 10) & 0x7ff;
                 const int *base = a.idx + d.y;
-                L.row = base[max(min(t, nr - 1), 0)];
-#pragma unroll
-                for (int e = 0; e < PK3_EXT; e++) L.xi[e] = base[nr + max(min(t + NR * e, nx - 1), 0)];
+                const int *p0 = base + max(min(t, nr - 1), 0);
+                const int *p1 = base + nr + max(min(t, nx - 1), 0);
+                const int *p2 = base + nr + max(min(t + NR, nx - 1), 0);
+                asm volatile("global_load_dword %0, %1, off" : "=v"(L.row) : "v"(p0) : "memory");
+                asm volatile("global_load_dword %0, %1, off" : "=v"(L.xi[0]) : "v"(p1) : "memory");
+                asm volatile("global_load_dword %0, %1, off" : "=v"(L.xi[1]) : "v"(p2) : "memory");
                 L.nr = nr;
                 L.nx = nx;
             };
             auto gather = [&](Pk5Ld &L) {
-                L.rh = a.rhs[(a.diag & 4) ? t : L.row];
-#pragma unroll
-                for (int e = 0; e < PK3_EXT; e++) L.ev[e] = ld_agent(a.sh + ((a.diag & 8) ? 0 : L.xi[e]));
+                asm volatile("s_waitcnt vmcnt(12)" : "+v"(L.row), "+v"(L.xi[0]), "+v"(L.xi[1]) :: "memory");
+                const double *pr = a.rhs + ((a.diag & 4) ? t : L.row);
+                const double *px0 = a.sh + ((a.diag & 8) ? 0 : L.xi[0]);
+                const double *px1 = a.sh + ((a.diag & 8) ? 0 : L.xi[1]);
+                asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(L.rh) : "v"(pr) : "memory");
+                asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(L.ev[0]) : "v"(px0) : "memory");
+                asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(L.ev[1]) : "v"(px1) : "memory");
             };
             int4 dl = descc(-D + IA);  // descriptor of packet j+IA, read one step ahead
             auto step = [&](int j, Pk5Ld &Li, Pk5Ld &Lg, Pk5Ld &Ll) {
@@ -2121,7 +2138,10 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                     l0 = __builtin_amdgcn_s_memtime();
                     acc_is += l0 - m0;
                 }
-                asm volatile("" ::"v"(Ll.rh), "v"(Ll.ev[0]), "v"(Ll.ev[1]));
+                if constexpr (KE == 2)
+                    asm volatile("s_waitcnt vmcnt(6)" : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]) :: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(0)" : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]) :: "memory");
                 uint64_t l2 = 0;
                 if (a.trace) {
                     l2 = __builtin_amdgcn_s_memtime();
@@ -2155,6 +2175,7 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
             L0.row = L1.row = L2.row = L3.row = L4.row = 0;
 #pragma unroll
             for (int e = 0; e < PK3_EXT; e++) L0.xi[e] = L1.xi[e] = L2.xi[e] = L3.xi[e] = L4.xi[e] = 0;
+            L0.rh = L1.rh = L2.rh = L3.rh = L4.rh = 0;
             for (int j0 = -D; j0 < T - D; j0 += Q) {  // as in k_tri_pk5
                 if constexpr (Q == 4) {
                     step(j0, L1, L3, L3);
@@ -2169,7 +2190,9 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                     step(j0 + 4, L0, L3, L2);
                 }
             }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             (void)L4;
+            (void)acc_lb;
             if (a.trace && tid == NR) {  // compute's barrier share is dropped here
                 a.trace[8 * b + 5] = acc_w;
                 a.trace[8 * b + 6] = acc_is;
@@ -2340,33 +2363,16 @@ static int launch_pk6(lssp_amd_ctx *c, const TriSched &t, const double *rhs, dou
     }
     Pk6Args g{t.bp_nb, t.pk6_blk, reinterpret_cast<const int4 *>(t.pk6_desc), t.pk6_rec, t.pk6_idx, rhs, sh,
               sh_next, nat, t.n, t.bp_B, t.pk6_claim, t.pk6_base, c->d_err, c->tri_diag, d_trace};
-    const bool ke2 = c->tri_depth == 2;
+    // Instantiated: 256-row packets, x operands gathered 2 steps ahead (KE 2),
+    // EP 4 or 8 -- the variants whose inline-asm loader tools/check_vmcnt.py
+    // (tests/test_isa_vmcnt.py) verifies hazard-free
+    if (t.pk6_rows != 256) return LSSP_AMD_EUNSUPPORTED;
     if constexpr (NAT) {
-        const int threads = 2 * 256 + 64;
-        if (t.pk6_rows != 256) return LSSP_AMD_EUNSUPPORTED;
-        if (t.pk6_ep == 4) {
-            if (ke2) k_tri_pk6<4, 2, true, 256><<<grid, threads, 0, c->stream>>>(g);
-            else k_tri_pk6<4, 1, true, 256><<<grid, threads, 0, c->stream>>>(g);
-        } else {
-            if (ke2) k_tri_pk6<8, 2, true, 256><<<grid, threads, 0, c->stream>>>(g);
-            else k_tri_pk6<8, 1, true, 256><<<grid, threads, 0, c->stream>>>(g);
-        }
-    } else if (t.pk6_rows == 512) {
-        if (t.pk6_ep == 4) {
-            if (ke2) k_tri_pk6<4, 2, false, 512><<<grid, 1024, 0, c->stream>>>(g);
-            else k_tri_pk6<4, 1, false, 512><<<grid, 1024, 0, c->stream>>>(g);
-        } else {
-            if (ke2) k_tri_pk6<8, 2, false, 512><<<grid, 1024, 0, c->stream>>>(g);
-            else k_tri_pk6<8, 1, false, 512><<<grid, 1024, 0, c->stream>>>(g);
-        }
+        if (t.pk6_ep != 4) return LSSP_AMD_EUNSUPPORTED;
+        k_tri_pk6<4, 2, true, 256><<<grid, 2 * 256 + 64, 0, c->stream>>>(g);
     } else {
-        if (t.pk6_ep == 4) {
-            if (ke2) k_tri_pk6<4, 2, false, 256><<<grid, 512, 0, c->stream>>>(g);
-            else k_tri_pk6<4, 1, false, 256><<<grid, 512, 0, c->stream>>>(g);
-        } else {
-            if (ke2) k_tri_pk6<8, 2, false, 256><<<grid, 512, 0, c->stream>>>(g);
-            else k_tri_pk6<8, 1, false, 256><<<grid, 512, 0, c->stream>>>(g);
-        }
+        if (t.pk6_ep == 4) k_tri_pk6<4, 2, false, 256><<<grid, 512, 0, c->stream>>>(g);
+        else k_tri_pk6<8, 2, false, 256><<<grid, 512, 0, c->stream>>>(g);
     }
     t.pk6_base += (unsigned long long)t.bp_nb + grid;
     LSSP_HIP(hipGetLastError());
@@ -2374,14 +2380,22 @@ static int launch_pk6(lssp_amd_ctx *c, const TriSched &t, const double *rhs, dou
     return LSSP_AMD_OK;
 }
 
-// permutations between natural order and a sweep's schedule order (positions)
-__global__ void k_perm_gather(double *dst, const double *src, const int *perm, int n)
+// permutations between natural order and a sweep's schedule order (positions).
+// XCD-aware: workgroup w runs on XCD w % 8 (round-robin dispatch) and walks
+// the XCD's contiguous eighth of the positions, so the natural-order lines a
+// position range touches (the same few z-planes for a stencil) are reused
+// inside one XCD's L2 instead of being fetched once per XCD.
+template <bool GATHER>
+__global__ __launch_bounds__(256) void k_perm(double *dst, const double *src, const int *perm, int n)
 {
-    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) dst[p] = src[perm[p]];
-}
-__global__ void k_perm_scatter(double *dst, const double *src, const int *perm, int n)
-{
-    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) dst[perm[p]] = src[p];
+    const int nx = 8, per = gridDim.x / nx;
+    const int xcd = blockIdx.x % nx, k = blockIdx.x / nx;
+    const long chunk = ((long)n + nx - 1) / nx;
+    const long lo = xcd * chunk, hi = min((long)n, lo + chunk);
+    for (long p = lo + (long)k * 256 + threadIdx.x; p < hi; p += (long)per * 256) {
+        if (GATHER) dst[p] = src[perm[p]];
+        else dst[perm[p]] = src[p];
+    }
 }
 
 // tri_mode 9 apply.  The scattered halves of the work -- reading the rhs in L
@@ -2402,14 +2416,14 @@ int launch_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const do
         }
         const int e = M->epoch & 1;
         M->epoch++;
-        const int pg = std::min((n + 255) / 256, 8 * c->num_cus);
-        k_perm_gather<<<pg, 256, 0, c->stream>>>(M->d_rperm, rhs, M->lower.bp_perm, n);
+        const int pg = 8 * std::max(1, std::min((n + 2047) / 2048, c->num_cus));  // multiple of 8
+        k_perm<true><<<pg, 256, 0, c->stream>>>(M->d_rperm, rhs, M->lower.bp_perm, n);
         LSSP_HIP(hipGetLastError());
         LSSP_TRY(launch_pk6<false>(c, M->lower, M->d_rperm, M->d_sh[e], M->d_sh[e ^ 1], nullptr));
         static const bool nat = getenv("LSSP_AMD_TRI_NAT") && atoi(getenv("LSSP_AMD_TRI_NAT"));
         if (nat) return launch_pk6<true>(c, M->upper, M->d_sh[e], M->d_sh[2 + e], M->d_sh[2 + (e ^ 1)], x);
         LSSP_TRY(launch_pk6<false>(c, M->upper, M->d_sh[e], M->d_sh[2 + e], M->d_sh[2 + (e ^ 1)], nullptr));
-        k_perm_scatter<<<pg, 256, 0, c->stream>>>(x, M->d_sh[2 + e], M->upper.bp_perm, n);
+        k_perm<false><<<pg, 256, 0, c->stream>>>(x, M->d_sh[2 + e], M->upper.bp_perm, n);
         LSSP_HIP(hipGetLastError());
         return LSSP_AMD_OK;
     }

@@ -559,8 +559,7 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
                    const std::vector<int> &blk_step, int nb, long B, const std::vector<int> &rhs_index,
                    TriSched &t)
 {
-    const char *er = getenv("LSSP_AMD_TRI_PK_ROWS");
-    const int ROWS = er && atoi(er) == 512 ? 512 : 256;  // rows per packet = compute lanes
+    const int ROWS = 256;  // rows per packet = compute lanes (512 measured slower)
     int maxlen = 0;
     for (int p = 0; p < n; p++) maxlen = std::max(maxlen, rp[p + 1] - rp[p]);
     if (maxlen > 8) return LSSP_AMD_EUNSUPPORTED;
