@@ -14,8 +14,13 @@ row-partitioned into N z-slabs (strong scaling); halos move with RCCL
 send/recv and dots with an RCCL all-gather; the preconditioner becomes
 block-Jacobi ILU(0) per slab (the reference's blk_size path).
 
-The roofline object describes the metric's SpMV kernel, y = A x
-(lssp_mv_mxy), timed live with HIP events on the library's stream.
+The roofline object describes the dominant operator, the ILU(0) apply
+(pc.solve: a permutation kernel, the two pipelined triangular sweeps
+k_tri_pk6, a permutation kernel -- rocprof attributes ~60% of a step to the
+sweeps); roofline_spmv describes the metric's SpMV kernel, y = A x
+(lssp_mv_mxy).  Both are timed live with HIP events on the library's stream.
+traffic: HBM bytes per launch from rocprofv3 PMC counters (FETCH_SIZE x 2 on
+gfx950, + WRITE_SIZE), read from profiles/pmc_traffic.json when present.
 cpu_baseline is the REFERENCE itself (oracle/_ref/libref.so, compiled from
 /root/reference, g++ -O2, 1 core) on a bounded sample of the same workload.
 """
@@ -38,6 +43,22 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def spmv_bytes(nnz: int, n: int) -> int:
     """algorithmic bytes of y = A x: Ax 8 + Aj 4 per nnz, Ap 4 + x 8 + y 8 per row"""
     return 12 * nnz + 20 * n + 4
+
+
+def ilu_apply_bytes(nnzL: int, nnzU: int, n: int) -> int:
+    """algorithmic bytes of one ILU apply: both factors in CSR (8 + 4 per entry,
+    4 per row pointer), rhs read, the L sweep's output written and read back by
+    the U sweep, x written"""
+    return 12 * (nnzL + nnzU) + 8 * (n + 1) + 8 * n * 4
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch measured with rocprofv3 --pmc (tools/pmc_traffic.py)"""
+    try:
+        with open(os.path.join(HERE, "profiles", "pmc_traffic.json")) as f:
+            return json.load(f).get(kernel)
+    except (OSError, ValueError):
+        return None
 
 
 def build_local(N: int, rank: int, P: int):
@@ -100,6 +121,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--grid", type=int, default=216)
     ap.add_argument("--spmv-reps", type=int, default=50)
+    ap.add_argument("--apply-reps", type=int, default=10)
     ap.add_argument("--cpu-iters", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -151,6 +173,19 @@ def main():
     spmv_ms = e0.elapsed_time(e1) / args.spmv_reps
     spmv_gbs = spmv_bytes(nnz_local, nl) / (spmv_ms * 1e-3) / 1e9
 
+    # ---- ILU apply roofline leg (the dominant operator) ----
+    zs = dev.vec(A.nx)
+    for _ in range(3):
+        M.apply(zs, xs)
+    e0.record(stream)
+    for _ in range(args.apply_reps):
+        M.apply(zs, xs)
+    e1.record(stream)
+    e1.synchronize()
+    apply_ms = e0.elapsed_time(e1) / args.apply_reps
+    apply_b = ilu_apply_bytes(M.nnzL, M.nnzU, nl)
+    apply_gbs = apply_b / (apply_ms * 1e-3) / 1e9
+
     # ---- BiCGSTAB steps ----
     def run(iters):
         return lssp_amd.solve(dev, A, M, x, b, solver=lssp_amd.BICGSTAB, tol_rel=0.0, tol_abs=0.0, tol_rb=0.0,
@@ -201,10 +236,15 @@ def main():
                        "rows": n, "partition": f"{world} z-slab row blocks", "reduction": "tree"},
             "spmv": {"gbps": round(spmv_gbs_total, 1), "frac_hbm_peak": round(spmv_gbs / HBM_PEAK_GBS, 4),
                      "ms_per_call": round(spmv_ms, 5)},
-            "roofline": {"bound": "hbm", "achieved": round(spmv_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(spmv_gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "k_spmv<EPI_MXY,0> (y = A x)",
-                         "bytes_per_launch": spmv_bytes(nnz_local, nl)},
+            "roofline": {"bound": "hbm", "achieved": round(apply_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(apply_gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("ilu_apply"),
+                         "kernel": "ILU(0) apply = k_perm<gather> + k_tri_pk6 (L) + k_tri_pk6 (U) + k_perm<scatter>; "
+                                   "latency-bound: 2 x 646 dependent levels",
+                         "bytes_per_launch": apply_b, "ms_per_launch": round(apply_ms, 5)},
+            "roofline_spmv": {"bound": "hbm", "achieved": round(spmv_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(spmv_gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("k_spmv3"),
+                              "kernel": "k_spmv3<EPI_MXY,0> (y = A x)",
+                              "bytes_per_launch": spmv_bytes(nnz_local, nl), "ms_per_launch": round(spmv_ms, 5)},
             "ilu": {"levels_L": M.levelsL, "levels_U": M.levelsU, "setup_s": round(M.setup_seconds, 3)},
             "setup_s": round(t_setup, 2),
         }

@@ -219,13 +219,23 @@ struct SpmvArgs {
     long pcap;
 };
 
-template <int EPI, int NRED>
-__global__ __launch_bounds__(256) void k_spmv(SpmvArgs a)
+// XCD != 0: the 256-row blocks are dealt so that each of the 8 XCDs owns one
+// contiguous eighth of the rows (dispatch round-robins workgroups over XCDs,
+// workgroup w runs on XCD w % 8); the x entries a block gathers are then
+// re-used by the neighbouring blocks of the same XCD out of its L2 (7-pt:
+// x is fetched once instead of ~1.3 times, rocprofv3 FETCH_SIZE).
+template <int EPI, int NRED, int XCD>
+__global__ __launch_bounds__(256) void k_spmv(SpmvArgs a, long nblk)
 {
     __shared__ int sj[SPMV_CAP];
     __shared__ double sx[SPMV_CAP];
     __shared__ double lds[MAX_SLOTS][4];
-    const long blk = blockIdx.x;
+    long blk = blockIdx.x;
+    if (XCD) {
+        const long per = gridDim.x / 8;
+        blk = (blockIdx.x % 8) * per + blockIdx.x / 8;
+        if (blk >= nblk) return;
+    }
     const int r0 = (int)(blk * 256);
     const int tid = threadIdx.x;
     const int r = r0 + tid;
@@ -347,28 +357,131 @@ __global__ __launch_bounds__(256) void k_spmv2(SpmvArgs a, long nblk)
     }
 }
 
-static int g_spmv_variant = -1;  // LSSP_AMD_SPMV: 0 k_spmv, 1 k_spmv2, 2 k_spmv2 + XCD order
+// Variant 3 of the staged SpMV: as k_spmv (XCD-ordered blocks), but every
+// global access a lane makes before the barrier is issued up front and
+// branch-free -- the block's Aj / Ax range as 16-byte loads (widened to 16-byte
+// boundaries, clamped to the padded arrays; entries outside the block are
+// dropped when landing in LDS) and the lane's own Ap[r], Ap[r+1] -- so one
+// memory round trip covers the staging and the row bounds.
+template <int EPI, int NRED>
+__global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_pad)
+{
+    constexpr int NX2 = (SPMV_CAP / 2 + 1 + 255) / 256;  // double2 loads per lane
+    constexpr int NJ4 = (SPMV_CAP / 4 + 1 + 255) / 256;  // int4 loads per lane
+    __shared__ __attribute__((aligned(16))) double sx[SPMV_CAP + 2];
+    __shared__ __attribute__((aligned(16))) int sj[SPMV_CAP + 4];
+    __shared__ double lds[MAX_SLOTS][4];
+    const long per = gridDim.x / 8;
+    const long blk = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    if (blk >= nblk) return;
+    const int r0 = (int)(blk * 256);
+    const int tid = threadIdx.x;
+    const int r = r0 + tid;
+    const int rend = min(r0 + 256, a.nrows);
+    const int base = a.Ap[r0];
+    const int cnt = a.Ap[rend] - base;
+    const int rr = min(r, a.nrows - 1);
+    const int rb = a.Ap[rr], re = a.Ap[rr + 1];
+    double sum = 0;
+    if (cnt <= SPMV_CAP) {
+        typedef double dbl2_t __attribute__((ext_vector_type(2)));
+        typedef int int4_t __attribute__((ext_vector_type(4)));
+        const long xb = base & ~1L, jb = base & ~3L;
+        // clamp to the block's last vector: lanes past the range re-read it
+        // (no extra lines), and the padded arrays keep it in bounds
+        const long last = cnt > 0 ? (long)base + cnt - 1 : (long)base;
+        const long xmax = min(last >> 1, (nnz_pad >> 1) - 1);
+        const long jmax = min(last >> 2, (nnz_pad >> 2) - 1);
+        const dbl2_t *X2 = reinterpret_cast<const dbl2_t *>(a.Ax);
+        const int4_t *J4 = reinterpret_cast<const int4_t *>(a.Aj);
+        dbl2_t vx[NX2];
+        int4_t vj[NJ4];
+#pragma unroll
+        for (int u = 0; u < NX2; u++) vx[u] = __builtin_nontemporal_load(X2 + min((xb >> 1) + tid + 256 * u, xmax));
+#pragma unroll
+        for (int u = 0; u < NJ4; u++) vj[u] = __builtin_nontemporal_load(J4 + min((jb >> 2) + tid + 256 * u, jmax));
+        const int xn = (int)(xmax - (xb >> 1)) + 1, jn = (int)(jmax - (jb >> 2)) + 1;  // vectors in range
+#pragma unroll
+        for (int u = 0; u < NX2; u++)
+            if (tid + 256 * u < xn) reinterpret_cast<dbl2_t *>(sx)[tid + 256 * u] = vx[u];
+#pragma unroll
+        for (int u = 0; u < NJ4; u++)
+            if (tid + 256 * u < jn) reinterpret_cast<int4_t *>(sj)[tid + 256 * u] = vj[u];
+        __syncthreads();
+        if (r < a.nrows) {
+            const int ox = (int)(base - xb) - base, oj = (int)(base - jb) - base;
+            const int len = re - rb;
+            if (len > 0 && len <= 8) {
+                // all x gathers of the row in flight at once; the products are
+                // then added in CSR order (clamped extra lanes are not added)
+                double pr[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int k = min(rb + u, re - 1);
+                    pr[u] = a.x[sj[k + oj]] * sx[k + ox];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (u < len) sum += pr[u];
+            } else {
+                for (int k = rb; k < re; k++) sum += a.x[sj[k + oj]] * sx[k + ox];
+            }
+        }
+    } else if (r < a.nrows) {
+        for (int k = rb; k < re; k++) sum += a.x[a.Aj[k]] * a.Ax[k];
+    }
+    double zv = 0;
+    if (r < a.nrows) {
+        if (EPI == EPI_MXY) zv = sum;
+        else if (EPI == EPI_AMXY) zv = sum * a.alpha;
+        else if (EPI == EPI_AXPBY) zv = a.y[r] * a.beta + a.alpha * sum;
+        else zv = a.alpha * sum;
+        a.z[r] = zv;
+    }
+    if (NRED > 0) {
+        double v[NRED > 0 ? NRED : 1];
+        if (r < a.nrows) {
+            v[0] = zv * a.w0[r];
+            if (NRED > 1) v[NRED > 1 ? 1 : 0] = zv * (a.w1 ? a.w1[r] : zv);
+        } else {
+#pragma unroll
+            for (int q = 0; q < NRED; q++) v[q] = 0.0;
+        }
+        chunk_reduce<NRED>(v, a.part, a.pcap, blk, lds);
+    }
+}
+
+static int g_spmv_variant = -1;  // LSSP_AMD_SPMV: 4 k_spmv3 (default), 3 k_spmv + XCD order,
+                                 // 0 k_spmv, 1 k_spmv2, 2 k_spmv2 + XCD order
 
 template <int EPI>
-static void spmv_dispatch(const SpmvArgs &a, int nred, long nblocks, hipStream_t s)
+static void spmv_dispatch(const SpmvArgs &a, int nred, long nblocks, hipStream_t s, long nnz_pad)
 {
     if (g_spmv_variant < 0) {
         const char *e = getenv("LSSP_AMD_SPMV");
-        g_spmv_variant = e ? atoi(e) : 0;
+        g_spmv_variant = e ? atoi(e) : 4;
     }
+    const long g = (nblocks + 7) / 8 * 8;
     if (g_spmv_variant == 0) {
-        if (nred == 0) k_spmv<EPI, 0><<<nblocks, 256, 0, s>>>(a);
-        else if (nred == 1) k_spmv<EPI, 1><<<nblocks, 256, 0, s>>>(a);
-        else k_spmv<EPI, 2><<<nblocks, 256, 0, s>>>(a);
+        if (nred == 0) k_spmv<EPI, 0, 0><<<nblocks, 256, 0, s>>>(a, nblocks);
+        else if (nred == 1) k_spmv<EPI, 1, 0><<<nblocks, 256, 0, s>>>(a, nblocks);
+        else k_spmv<EPI, 2, 0><<<nblocks, 256, 0, s>>>(a, nblocks);
     } else if (g_spmv_variant == 1) {
         if (nred == 0) k_spmv2<EPI, 0, 0><<<nblocks, 256, 0, s>>>(a, nblocks);
         else if (nred == 1) k_spmv2<EPI, 1, 0><<<nblocks, 256, 0, s>>>(a, nblocks);
         else k_spmv2<EPI, 2, 0><<<nblocks, 256, 0, s>>>(a, nblocks);
-    } else {
-        const long g = (nblocks + 7) / 8 * 8;
+    } else if (g_spmv_variant == 2) {
         if (nred == 0) k_spmv2<EPI, 0, 1><<<g, 256, 0, s>>>(a, nblocks);
         else if (nred == 1) k_spmv2<EPI, 1, 1><<<g, 256, 0, s>>>(a, nblocks);
         else k_spmv2<EPI, 2, 1><<<g, 256, 0, s>>>(a, nblocks);
+    } else if (g_spmv_variant == 4) {
+        if (nred == 0) k_spmv3<EPI, 0><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
+        else if (nred == 1) k_spmv3<EPI, 1><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
+        else k_spmv3<EPI, 2><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
+    } else {
+        if (nred == 0) k_spmv<EPI, 0, 1><<<g, 256, 0, s>>>(a, nblocks);
+        else if (nred == 1) k_spmv<EPI, 1, 1><<<g, 256, 0, s>>>(a, nblocks);
+        else k_spmv<EPI, 2, 1><<<g, 256, 0, s>>>(a, nblocks);
     }
 }
 
@@ -381,10 +494,10 @@ int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, c
     LSSP_TRY(ensure_part(c, nb));
     SpmvArgs a{A->nrows, A->Ap, A->Aj, A->Ax, x, y, z, alpha, beta, w0, w1, c->d_part, c->part_cap};
     switch (epi) {
-    case EPI_MXY: spmv_dispatch<EPI_MXY>(a, nred, nb, c->stream); break;
-    case EPI_AMXY: spmv_dispatch<EPI_AMXY>(a, nred, nb, c->stream); break;
-    case EPI_AXPBY: spmv_dispatch<EPI_AXPBY>(a, nred, nb, c->stream); break;
-    default: spmv_dispatch<EPI_AMX>(a, nred, nb, c->stream); break;
+    case EPI_MXY: spmv_dispatch<EPI_MXY>(a, nred, nb, c->stream, A->nnz + 4L); break;
+    case EPI_AMXY: spmv_dispatch<EPI_AMXY>(a, nred, nb, c->stream, A->nnz + 4L); break;
+    case EPI_AXPBY: spmv_dispatch<EPI_AXPBY>(a, nred, nb, c->stream, A->nnz + 4L); break;
+    default: spmv_dispatch<EPI_AMX>(a, nred, nb, c->stream, A->nnz + 4L); break;
     }
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;

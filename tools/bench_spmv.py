@@ -25,6 +25,9 @@ def main():
     y = dev.vec(n)
     for _ in range(5):
         A.mv_mxy(x, y)
+    if os.environ.get("LSSP_AMD_PROBE_COPY"):  # PMC calibration: n doubles read, n written
+        for _ in range(args.reps):
+            dev.L.lssp_amd_vec_copy(dev.h, y.ptr, x.ptr, n)
     s = torch.cuda.ExternalStream(dev.stream)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)

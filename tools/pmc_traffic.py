@@ -1,0 +1,46 @@
+"""Reduce rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of bench.py to HBM bytes
+per launch (tuning aid; writes profiles/pmc_traffic.json read by bench.py).
+
+    python tools/pmc_traffic.py <FETCH run dir> <WRITE run dir> [out.json]
+
+gfx950 correction (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE counts the
+fabric read requests at half their bytes -- checked on this code's 8-byte
+per-lane copy kernel (k_ew, 80.6 MB read: FETCH_SIZE 40.3 MB) -- so it is
+doubled; WRITE_SIZE is exact.  Units: KB.  The ILU apply entry sums the
+median per-launch bytes of its four kernels (2 permutations, 2 sweeps)."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_kernel(run_dir):
+    f = glob.glob(os.path.join(run_dir, "**", "*counter_collection.csv"), recursive=True)[0]
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(f)):
+        agg[r["Kernel_Name"]].append(float(r["Counter_Value"]) * 1000.0)
+    return {k: sorted(v)[len(v) // 2] for k, v in agg.items()}
+
+
+def main(fetch_dir, write_dir, out):
+    fe, wr = per_kernel(fetch_dir), per_kernel(write_dir)
+
+    def find(sub):
+        return [k for k in fe if sub in k]
+
+    res = {}
+    for k in find("k_spmv3<0, 0>"):
+        res["k_spmv3"] = int(2 * fe[k] + wr.get(k, 0))
+    tri = find("k_tri_pk6")
+    perm = find("k_perm")
+    if tri and perm:
+        res["ilu_apply"] = int(sum(2 * fe[k] + wr.get(k, 0) for k in perm) + 2 * sum(2 * fe[k] + wr.get(k, 0) for k in tri) / max(1, len(tri)))
+    res["_note"] = "HBM bytes per launch: 2 x FETCH_SIZE + WRITE_SIZE (rocprofv3 --pmc, medians over launches)"
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_traffic.json")
