@@ -108,6 +108,8 @@ int lssp_amd_ctx_create(int device, lssp_amd_ctx **out)
     if (td) c->tri_diag = atoi(td);
     const char *tdp = getenv("LSSP_AMD_TRI_DEPTH");
     if (tdp) c->tri_depth = std::min(3, std::max(1, atoi(tdp)));
+    const char *tpp = getenv("LSSP_AMD_TRI_PIPE");
+    if (tpp) c->tri_pipe = atoi(tpp);
     *out = c;
     return LSSP_AMD_OK;
 }

@@ -80,6 +80,7 @@ struct lssp_amd_ctx {
     int tri_mode = 9;
     int tri_diag = 0;  // LSSP_AMD_TRI_DIAG timing experiments (wrong results when != 0)
     int tri_depth = 2; // LSSP_AMD_TRI_DEPTH: tri_mode 6 prefetch depth S (2, 3), tri_mode 7 x lead KE (1, 2)
+    int tri_pipe = 0;  // LSSP_AMD_TRI_PIPE: tri_mode 9 prefetch depths (kernels.hip launch_pk6)
     // Krylov work vectors, kept across solves (no hipMalloc on the solve path)
     struct WsBuf {
         double *p;

@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstring>
+#include <string>
 #include <type_traits>
 
 #include "internal.h"
@@ -2045,6 +2047,8 @@ struct Pk6Args {
     int *err;
     int diag;
     unsigned long long *trace;
+    unsigned long long *trace2;  // diagnostics (LSSP_AMD_TRI_TRACE2): per-step clocks of blocks tb0, tb0+1
+    int tb0;
 };
 
 typedef unsigned v2u __attribute__((ext_vector_type(2)));
@@ -2060,12 +2064,28 @@ struct Pk6Rec {
 
 __device__ __forceinline__ int code16(int w, int hi) { return hi ? (w >> 16) : (int)(short)(w & 0xffff); }
 
-template <int EP, int KE, bool NAT, int NR>
+template <int I, typename T>
+__device__ __forceinline__ T &sel4(T &a, T &b, T &c, T &d)
+{
+    if constexpr (I == 0) return a;
+    else if constexpr (I == 1) return b;
+    else if constexpr (I == 2) return c;
+    else return d;
+}
+
+// KE: steps of lead of the x-operand and rhs gathers; IA: of the gather-index
+// loads (IA - KE of 1 or 2); D: of the compute lanes' record loads.  Register
+// sets rotate with period Q = 4 (packet p lives in set p mod 4), so D <= 3 and
+// IA <= 4.  Shallower prefetch keeps fewer requests in the CU's memory queue,
+// which is what a cross-CU hand-off waits behind (MI355X_MICROARCH.md,
+// handoff-1to1).
+template <int EP, int KE, int IA, int D, bool NAT, int NR>
 __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args a)
 {
-    constexpr int IA = KE + 2;
-    constexpr int D = KE + 2;
-    constexpr int Q = D + 1;
+    constexpr int Q = 4;
+    static_assert(D + 1 <= Q && IA <= Q && KE >= 1 && IA - KE >= 1 && IA - KE <= 2, "pipeline depths");
+    constexpr int S0 = (IA > D ? IA : D);
+    constexpr int J0 = -((S0 + Q - 1) / Q) * Q;  // first step, a multiple of Q
     __shared__ double ring[BP_RING + 1];
     __shared__ double rbuf[2][NR];
     __shared__ double xbuf[2][NR * PK3_EXT];
@@ -2101,9 +2121,16 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
         prev = b;
         const int q0 = a.blk[b], np = a.blk[b + 1] - q0;
         const int bbase = b * a.B;  // first schedule position of the block
+        const bool tr2 = a.trace2 && (b == a.tb0 || b == a.tb0 + 1);
+        auto mark = [&](int j, int k) {
+            if (tr2 && j >= -8 && j < 1016)
+                a.trace2[((long)(b - a.tb0) * 1024 + (j + 8)) * 4 + k] = __builtin_amdgcn_s_memrealtime();
+        };
         for (int i = tid; i < np; i += blockDim.x) sdesc[i] = a.desc[q0 + i];
         __syncthreads();
-        const int T = (np + D + Q - 1) / Q * Q;  // steps -D .. T-D-1, as in k_tri_pk5
+        // both roles run steps J0 .. J0+T-1 (T a multiple of Q); out-of-range
+        // packets turn into loads from valid dummy addresses
+        const int T = (np - J0 + Q - 1) / Q * Q;
         auto desc = [&](int p) {
             const int4 d = sdesc[p];
             return make_int4(__builtin_amdgcn_readfirstlane(d.x), __builtin_amdgcn_readfirstlane(d.y),
@@ -2138,7 +2165,7 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                 Rr.nr = nr;
                 Rr.pos0 = d.w;
             };
-            int4 dn = descc(-1);  // descriptor of packet j+D, read one step ahead
+            int4 dn = descc(J0 + D);  // descriptor of packet j+D, read one step ahead
             auto step = [&](int j, Pk6Rec<EP> &Rc, Pk6Rec<EP> &Rn) {
                 if (a.trace) c0 = __builtin_amdgcn_s_memtime();
                 issue(dn, Rn);
@@ -2168,6 +2195,7 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                     if (!(a.diag & 2)) st_agent(a.sh + pos, xi);
                 }
                 if (a.trace) c1 = __builtin_amdgcn_s_memtime();
+                if (tid == 0) mark(j, 0);
                 lds_barrier();
                 if (a.trace) {
                     const uint64_t c2 = __builtin_amdgcn_s_memtime();
@@ -2175,24 +2203,14 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                     acc_b += c2 - c1;
                 }
             };
-            Pk6Rec<EP> R0, R1, R2, R3, R4;
-            R0.nr = R1.nr = R2.nr = R3.nr = R4.nr = 0;
-            dn = descc(-D + D);  // packet 0 is issued at step -D
-            for (int j0 = -D; j0 < T - D; j0 += Q) {  // packet p in NR[(p+1) % Q], j0 == 1 (mod Q)
-                if constexpr (Q == 4) {
-                    step(j0, R2, R1);
-                    step(j0 + 1, R3, R2);
-                    step(j0 + 2, R0, R3);
-                    step(j0 + 3, R1, R0);
-                } else {
-                    step(j0, R2, R1);
-                    step(j0 + 1, R3, R2);
-                    step(j0 + 2, R4, R3);
-                    step(j0 + 3, R0, R4);
-                    step(j0 + 4, R1, R0);
-                }
+            Pk6Rec<EP> R0, R1, R2, R3;
+            R0.nr = R1.nr = R2.nr = R3.nr = 0;
+            for (int j0 = J0; j0 < J0 + T; j0 += Q) {  // j0 == 0 (mod Q): packet p in set p mod Q
+                step(j0, sel4<0>(R0, R1, R2, R3), sel4<(0 + D) % Q>(R0, R1, R2, R3));
+                step(j0 + 1, sel4<1>(R0, R1, R2, R3), sel4<(1 + D) % Q>(R0, R1, R2, R3));
+                step(j0 + 2, sel4<2>(R0, R1, R2, R3), sel4<(2 + D) % Q>(R0, R1, R2, R3));
+                step(j0 + 3, sel4<3>(R0, R1, R2, R3), sel4<(3 + D) % Q>(R0, R1, R2, R3));
             }
-            (void)R4;
             // arm the block's positions of the other shadow for the next apply
             if (!(a.diag & 1)) {
                 const long s0 = bbase, s1 = min(s0 + a.B, (long)a.n);
@@ -2213,7 +2231,8 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
             // use (issued at step j-2) have exactly 12 younger loads, and the
             // gathers landed at the end of step j (packet j+1, issued at step
             // j+1-KE) have 6 (KE 2) or 0 (KE 1) younger loads.
-            static_assert(PK3_EXT == 2 && IA - KE == 2, "wait counts below assume this layout");
+            static_assert(PK3_EXT == 2, "wait counts below assume 3 + 3 loads per step");
+            constexpr int WAIT_IDX = 6 * (IA - KE);  // younger than the indices the gathers use
             uint64_t acc_w = 0, acc_lb = 0, acc_is = 0, acc_ld = 0, m0 = 0;
             auto issue_idx = [&](const int4 d, Pk5Ld &L) {
                 const int nr = d.z & 0x3ff, nx = (d.z >> 10) & 0x7ff;
@@ -2228,7 +2247,7 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                 L.nx = nx;
             };
             auto gather = [&](Pk5Ld &L) {
-                asm volatile("s_waitcnt vmcnt(12)" : "+v"(L.row), "+v"(L.xi[0]), "+v"(L.xi[1]) :: "memory");
+                asm volatile("s_waitcnt vmcnt(%3)" : "+v"(L.row), "+v"(L.xi[0]), "+v"(L.xi[1]) : "n"(WAIT_IDX) : "memory");
                 const double *pr = a.rhs + ((a.diag & 4) ? t : L.row);
                 const double *px0 = a.sh + ((a.diag & 8) ? 0 : L.xi[0]);
                 const double *px1 = a.sh + ((a.diag & 8) ? 0 : L.xi[1]);
@@ -2236,7 +2255,7 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                 asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(L.ev[0]) : "v"(px0) : "memory");
                 asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(L.ev[1]) : "v"(px1) : "memory");
             };
-            int4 dl = descc(-D + IA);  // descriptor of packet j+IA, read one step ahead
+            int4 dl = descc(J0 + IA);  // descriptor of packet j+IA, read one step ahead
             auto step = [&](int j, Pk5Ld &Li, Pk5Ld &Lg, Pk5Ld &Ll) {
                 if (a.diag & 16) {  // timing experiment: loader idle
                     lds_barrier();
@@ -2251,15 +2270,14 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                     l0 = __builtin_amdgcn_s_memtime();
                     acc_is += l0 - m0;
                 }
-                if constexpr (KE == 2)
-                    asm volatile("s_waitcnt vmcnt(6)" : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]) :: "memory");
-                else
-                    asm volatile("s_waitcnt vmcnt(0)" : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]) :: "memory");
+                // gathers of packet j+1 were issued at step j+1-KE
+                asm volatile("s_waitcnt vmcnt(%3)" : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]) : "n"(6 * (KE - 1)) : "memory");
                 uint64_t l2 = 0;
                 if (a.trace) {
                     l2 = __builtin_amdgcn_s_memtime();
                     acc_w += l2 - l0;
                 }
+                if (tid == NR) mark(j, 2);
                 // land packet j+1 (nr = nx = 0 outside the block's packets)
                 if (t < Ll.nr) rbuf[(j + 1) & 1][t] = Ll.rh;
 #pragma unroll
@@ -2279,32 +2297,31 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                     l1 = __builtin_amdgcn_s_memtime();
                     acc_ld += l1 - l2;
                 }
+                if (tid == NR) {
+                    mark(j, 1);
+                    if (tr2 && j >= -8 && j < 1016) a.trace2[((long)(b - a.tb0) * 1024 + (j + 8)) * 4 + 3] = s_polls;
+                }
                 lds_barrier();
                 if (a.trace) acc_lb += __builtin_amdgcn_s_memtime() - l1;
             };
-            Pk5Ld L0, L1, L2, L3, L4;
-            L0.nr = L1.nr = L2.nr = L3.nr = L4.nr = 0;
-            L0.nx = L1.nx = L2.nx = L3.nx = L4.nx = 0;
-            L0.row = L1.row = L2.row = L3.row = L4.row = 0;
+            Pk5Ld L0, L1, L2, L3;
+            L0.nr = L1.nr = L2.nr = L3.nr = 0;
+            L0.nx = L1.nx = L2.nx = L3.nx = 0;
+            L0.row = L1.row = L2.row = L3.row = 0;
 #pragma unroll
-            for (int e = 0; e < PK3_EXT; e++) L0.xi[e] = L1.xi[e] = L2.xi[e] = L3.xi[e] = L4.xi[e] = 0;
-            L0.rh = L1.rh = L2.rh = L3.rh = L4.rh = 0;
-            for (int j0 = -D; j0 < T - D; j0 += Q) {  // as in k_tri_pk5
-                if constexpr (Q == 4) {
-                    step(j0, L1, L3, L3);
-                    step(j0 + 1, L2, L0, L0);
-                    step(j0 + 2, L3, L1, L1);
-                    step(j0 + 3, L0, L2, L2);
-                } else {
-                    step(j0, L1, L4, L3);
-                    step(j0 + 1, L2, L0, L4);
-                    step(j0 + 2, L3, L1, L0);
-                    step(j0 + 3, L4, L2, L1);
-                    step(j0 + 4, L0, L3, L2);
-                }
+            for (int e = 0; e < PK3_EXT; e++) L0.xi[e] = L1.xi[e] = L2.xi[e] = L3.xi[e] = 0;
+            L0.rh = L1.rh = L2.rh = L3.rh = 0;
+#define LSSP_PK6_LSTEP(u)                                                                          \
+    step(j0 + u, sel4<(u + IA) % Q>(L0, L1, L2, L3), sel4<(u + KE) % Q>(L0, L1, L2, L3), \
+         sel4<(u + 1) % Q>(L0, L1, L2, L3))
+            for (int j0 = J0; j0 < J0 + T; j0 += Q) {  // packet p in set p mod Q
+                LSSP_PK6_LSTEP(0);
+                LSSP_PK6_LSTEP(1);
+                LSSP_PK6_LSTEP(2);
+                LSSP_PK6_LSTEP(3);
             }
+#undef LSSP_PK6_LSTEP
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            (void)L4;
             (void)acc_lb;
             if (a.trace && tid == NR) {  // compute's barrier share is dropped here
                 a.trace[8 * b + 5] = acc_w;
@@ -2323,11 +2340,11 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                         a.nat[rowbuf[p & 1][k]] = ring[(d.w + k - bbase) % BP_RING];
                 }
             };
-            for (int j = -D; j < T - D; j++) {
+            for (int j = J0; j < J0 + T; j++) {
                 store(j - 1);
                 lds_barrier();
             }
-            store(T - D - 1);
+            store(J0 + T - 1);
         }
     }
 }
@@ -2474,22 +2491,51 @@ static int launch_pk6(lssp_amd_ctx *c, const TriSched &t, const double *rhs, dou
         LSSP_HIP(hipMalloc(&d_trace, sizeof(unsigned long long) * 8 * t.bp_nb));
         LSSP_HIP(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * 8 * t.bp_nb, c->stream));
     }
+    const char *t2 = getenv("LSSP_AMD_TRI_TRACE2");  // "path:block"
+    unsigned long long *d_t2 = nullptr;
+    int tb0 = 0;
+    if (t2) {
+        const char *colon = strrchr(t2, ':');
+        tb0 = colon ? atoi(colon + 1) : t.bp_nb / 2;
+        LSSP_HIP(hipMalloc(&d_t2, sizeof(unsigned long long) * 2 * 1024 * 4));
+        LSSP_HIP(hipMemsetAsync(d_t2, 0, sizeof(unsigned long long) * 2 * 1024 * 4, c->stream));
+    }
     Pk6Args g{t.bp_nb, t.pk6_blk, reinterpret_cast<const int4 *>(t.pk6_desc), t.pk6_rec, t.pk6_idx, rhs, sh,
-              sh_next, nat, t.n, t.bp_B, t.pk6_claim, t.pk6_base, c->d_err, c->tri_diag, d_trace};
+              sh_next, nat, t.n, t.bp_B, t.pk6_claim, t.pk6_base, c->d_err, c->tri_diag, d_trace, d_t2, tb0};
     // Instantiated: 256-row packets, x operands gathered 2 steps ahead (KE 2),
     // EP 4 or 8 -- the variants whose inline-asm loader tools/check_vmcnt.py
     // (tests/test_isa_vmcnt.py) verifies hazard-free
     if (t.pk6_rows != 256) return LSSP_AMD_EUNSUPPORTED;
+    // pipeline depths (LSSP_AMD_TRI_PIPE): 0 = (KE 2, IA 4, D 3), 1 = (2, 3, 3), 2 = (2, 3, 2)
+    const int pd = c->tri_pipe;
     if constexpr (NAT) {
         if (t.pk6_ep != 4) return LSSP_AMD_EUNSUPPORTED;
-        k_tri_pk6<4, 2, true, 256><<<grid, 2 * 256 + 64, 0, c->stream>>>(g);
+        k_tri_pk6<4, 2, 4, 3, true, 256><<<grid, 2 * 256 + 64, 0, c->stream>>>(g);
+    } else if (t.pk6_ep == 4) {
+        if (pd == 1) k_tri_pk6<4, 2, 3, 3, false, 256><<<grid, 512, 0, c->stream>>>(g);
+        else if (pd == 2) k_tri_pk6<4, 2, 3, 2, false, 256><<<grid, 512, 0, c->stream>>>(g);
+        else k_tri_pk6<4, 2, 4, 3, false, 256><<<grid, 512, 0, c->stream>>>(g);
     } else {
-        if (t.pk6_ep == 4) k_tri_pk6<4, 2, false, 256><<<grid, 512, 0, c->stream>>>(g);
-        else k_tri_pk6<8, 2, false, 256><<<grid, 512, 0, c->stream>>>(g);
+        k_tri_pk6<8, 2, 4, 3, false, 256><<<grid, 512, 0, c->stream>>>(g);
     }
     t.pk6_base += (unsigned long long)t.bp_nb + grid;
     LSSP_HIP(hipGetLastError());
     if (trace_path) LSSP_TRY(dump_trace(c, d_trace, t.bp_nb, t.n, t.pk6_n, grid, trace_path));
+    if (t2) {  // diagnostics only: per-step clocks of two consecutive blocks
+        std::vector<unsigned long long> h(2 * 1024 * 4);
+        LSSP_HIP(hipMemcpyAsync(h.data(), d_t2, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost,
+                                c->stream));
+        LSSP_HIP(hipStreamSynchronize(c->stream));
+        (void)hipFree(d_t2);
+        std::string path(t2, strrchr(t2, ':') ? strrchr(t2, ':') - t2 : strlen(t2));
+        FILE *f = fopen(path.c_str(), "a");
+        if (f) {
+            fprintf(f, "{\"tb0\": %d, \"steps\": [", tb0);
+            for (size_t i = 0; i < h.size(); i++) fprintf(f, "%s%llu", i ? ", " : "", h[i]);
+            fprintf(f, "]}\n");
+            fclose(f);
+        }
+    }
     return LSSP_AMD_OK;
 }
 
@@ -2534,7 +2580,8 @@ int launch_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const do
         LSSP_HIP(hipGetLastError());
         LSSP_TRY(launch_pk6<false>(c, M->lower, M->d_rperm, M->d_sh[e], M->d_sh[e ^ 1], nullptr));
         static const bool nat = getenv("LSSP_AMD_TRI_NAT") && atoi(getenv("LSSP_AMD_TRI_NAT"));
-        if (nat) return launch_pk6<true>(c, M->upper, M->d_sh[e], M->d_sh[2 + e], M->d_sh[2 + (e ^ 1)], x);
+        if (nat && M->upper.pk6_ep == 4)
+            return launch_pk6<true>(c, M->upper, M->d_sh[e], M->d_sh[2 + e], M->d_sh[2 + (e ^ 1)], x);
         LSSP_TRY(launch_pk6<false>(c, M->upper, M->d_sh[e], M->d_sh[2 + e], M->d_sh[2 + (e ^ 1)], nullptr));
         k_perm<false><<<pg, 256, 0, c->stream>>>(x, M->d_sh[2 + e], M->upper.bp_perm, n);
         LSSP_HIP(hipGetLastError());

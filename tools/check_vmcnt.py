@@ -1,17 +1,22 @@
-"""Static check of hand-placed vmcnt waits in a gfx950 kernel (tuning aid).
+"""Static check of hand-placed vmcnt waits in a gfx950 kernel (tuning aid and
+CPU test, tests/test_isa_vmcnt.py).
 
-Walks the assembly of one kernel linearly (a loop body is seen once per pass;
-run with --passes 2 to model one back-edge), keeps the in-order queue of
-outstanding VMEM operations, retires entries at every `s_waitcnt vmcnt(N)`,
-and reports any instruction that reads or overwrites a VGPR that is still the
-destination of an outstanding load -- the hazard of issuing loads from inline
-asm, where the compiler does not insert waits itself.
-    python tools/check_vmcnt.py kernels.s _ZN8lssp_amd9k_tri_pk6ILi4ELi2ELb0ELi256EEEvNS_7Pk6ArgsE
+Builds the control-flow graph of one kernel from its assembly and runs a
+forward dataflow over the in-order queue of outstanding VMEM operations:
+every load/store joins the queue, `s_waitcnt vmcnt(N)` retires all but the N
+youngest, and at a join the predecessor queues are merged conservatively
+(aligned at the young end, destination registers united, the longer length
+kept).  Any instruction that reads or overwrites a VGPR that may still be the
+destination of an outstanding load is reported -- the hazard of issuing loads
+from inline asm, where the compiler inserts no waits of its own.
+
+    python tools/check_vmcnt.py kernels.s <kernel symbol>
 """
 import re
 import sys
 
 VREG = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
+BRANCH = re.compile(r"^s_(c?branch\w*)\s+(\.\w+)")
 
 
 def regs(text):
@@ -21,67 +26,120 @@ def regs(text):
             out.add(int(m.group(3)))
         else:
             out.update(range(int(m.group(1)), int(m.group(2)) + 1))
-    return out
+    return frozenset(out)
 
 
-def main(path, name, passes=2):
-    lines = open(path).read().split("\n")
-    start = next(i for i, l in enumerate(lines) if l.startswith(name + ":"))
-    end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
-    body = [l.split(";")[0].strip() for l in lines[start:end]]
-    body = [l for l in body if l and not l.endswith(":") and not l.startswith(".")]
-    queue = []  # [(dest regs or empty set, index)]
-    issues = 0
-    for p in range(passes):
-        for i, ins in enumerate(body):
-            op = ins.split()[0]
-            args = ins[len(op):]
-            m = re.match(r"s_waitcnt\s+vmcnt\((\d+)\)", ins)
-            if m or (op == "s_waitcnt" and "vmcnt" in ins):
-                n = int(re.search(r"vmcnt\((\d+)\)", ins).group(1))
-                while len(queue) > n:
-                    queue.pop(0)
+def classify(ins):
+    op = ins.split()[0]
+    args = ins[len(op):]
+    parts = [x.strip() for x in args.split(",")]
+    is_vmem = op.startswith(("global_", "buffer_", "flat_", "scratch_"))
+    if is_vmem and "load" in op and "lds" not in op:
+        return op, True, regs(parts[0]), regs(",".join(parts[1:]))
+    if is_vmem:
+        return op, True, frozenset(), regs(args)
+    if op.startswith("ds_write") or op.startswith("ds_store"):
+        return op, False, frozenset(), regs(args)
+    if op.startswith(("v_", "ds_")) and parts and parts[0]:
+        return op, False, regs(parts[0]), regs(",".join(parts[1:]))
+    return op, False, frozenset(), regs(args)
+
+
+def merge(a, b):
+    if a is None:
+        return b
+    if b is None:
+        return a
+    n = max(len(a), len(b))
+    pa = [frozenset()] * (n - len(a)) + list(a)
+    pb = [frozenset()] * (n - len(b)) + list(b)
+    return tuple(x | y for x, y in zip(pa, pb))
+
+
+def blocks_of(lines):
+    blocks, cur, label = [], [], "__entry"
+    for raw in lines:
+        l = raw.split(";")[0].strip()
+        if not l:
+            continue
+        if l.endswith(":"):
+            blocks.append((label, cur))
+            label, cur = l[:-1], []
+            continue
+        if l.startswith("."):
+            continue
+        cur.append(l)
+    blocks.append((label, cur))
+    return blocks
+
+
+def analyse(lines, report=20):
+    blocks = blocks_of(lines)
+    index = {lab: i for i, (lab, _) in enumerate(blocks)}
+    succ = []
+    for i, (lab, ins) in enumerate(blocks):
+        s = []
+        last = ins[-1] if ins else ""
+        m = BRANCH.match(last)
+        if m:
+            if m.group(2) in index:
+                s.append(index[m.group(2)])
+            if m.group(1) != "branch" and i + 1 < len(blocks):
+                s.append(i + 1)
+        elif "s_endpgm" not in last and i + 1 < len(blocks):
+            s.append(i + 1)
+        succ.append(s)
+    state_in = [None] * len(blocks)
+    state_in[0] = ()
+    work = [0]
+    hazards = []
+    seen = set()
+    while work:
+        i = work.pop()
+        q = list(state_in[i])
+        for ins in blocks[i][1]:
+            m = re.search(r"vmcnt\((\d+)\)", ins) if ins.startswith("s_waitcnt") else None
+            if m:
+                n = int(m.group(1))
+                q = q[-n:] if n else []
                 continue
-            parts = [x.strip() for x in args.split(",")]
-            is_vmem = op.startswith(("global_", "buffer_", "flat_", "scratch_"))
-            if is_vmem and "load" in op and "lds" not in op:
-                dst, src = regs(parts[0]), regs(",".join(parts[1:]))
-            elif is_vmem:
-                dst, src = set(), regs(args)
-            elif op.startswith(("v_", "ds_")) and parts and parts[0]:
-                if op.startswith("ds_write") or op.startswith("ds_store"):
-                    dst, src = set(), regs(args)
-                else:
-                    dst, src = regs(parts[0]), regs(",".join(parts[1:]))
-            else:
-                dst, src = set(), regs(args)
-            pending = set().union(*[q[0] for q in queue]) if queue else set()
+            op, vmem, dst, src = classify(ins)
+            pending = frozenset().union(*q) if q else frozenset()
             bad = (src | dst) & pending
-            if bad and p == passes - 1:
-                issues += 1
-                if issues <= 20:
-                    print(f"hazard: {ins}   (pending v{sorted(bad)})")
-            if is_vmem:
-                queue.append((dst, i))
-    print(f"{name}: {issues} hazards")
-    return issues
+            if bad and (i, ins) not in seen:
+                seen.add((i, ins))
+                hazards.append(f"{blocks[i][0]}: {ins}   (pending v{sorted(bad)})")
+            if vmem:
+                q.append(dst)
+                if len(q) > 63:  # the hardware counter holds at most 63 outstanding
+                    q = q[-63:]
+        out = tuple(q)
+        for j in succ[i]:
+            new = merge(state_in[j], out)
+            if new != state_in[j]:
+                state_in[j] = new
+                work.append(j)
+    for h in hazards[:report]:
+        print("hazard:", h)
+    return len(hazards)
 
 
-def check_loader(path, name, repeat=3):
-    """Check the inline-asm loader loop of a k_tri_pk6 instantiation: the
-    region from its first asm index load to the vmcnt(0) after the loop,
-    unrolled `repeat` times to model the back-edge.  Returns the hazard count."""
+def kernel_lines(path, name):
     lines = open(path).read().split("\n")
     st = next(i for i, l in enumerate(lines) if l.startswith(name + ":"))
     en = next(i for i in range(st, len(lines)) if "s_endpgm" in lines[i])
-    seg = lines[st:en]
-    idx = [i for i, l in enumerate(seg) if re.match(r"\s*global_load_dword v\d+, v\[\d+:\d+\], off$", l)]
-    a = max(idx[0] - 5, 0)
-    b = max(i for i, l in enumerate(seg) if "s_waitcnt vmcnt(0)" in l and i > idx[-1])
-    import tempfile
-    with tempfile.NamedTemporaryFile("w", suffix=".s", delete=False) as f:
-        f.write(name + ":\n" + "\n".join(seg[a:b] * repeat) + "\n\ts_endpgm\n")
-    return main(f.name, name, passes=1)
+    return lines[st + 1:en + 1]
+
+
+def main(path, name):
+    n = analyse(kernel_lines(path, name))
+    print(f"{name}: {n} hazards")
+    return n
+
+
+def check_loader(path, name):
+    """kept for the test's interface: the whole kernel is analysed"""
+    return main(path, name)
 
 
 if __name__ == "__main__":
