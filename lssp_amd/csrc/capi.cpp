@@ -106,8 +106,6 @@ int lssp_amd_ctx_create(int device, lssp_amd_ctx **out)
     if (tm) c->tri_mode = atoi(tm);
     const char *td = getenv("LSSP_AMD_TRI_DIAG");
     if (td) c->tri_diag = atoi(td);
-    const char *tdp = getenv("LSSP_AMD_TRI_DEPTH");
-    if (tdp) c->tri_depth = std::min(3, std::max(1, atoi(tdp)));
     const char *tpp = getenv("LSSP_AMD_TRI_PIPE");
     if (tpp) c->tri_pipe = atoi(tpp);
     *out = c;

@@ -552,15 +552,9 @@ void free_trisched(TriSched &t)
     if (t.cols) (void)hipFree(t.cols);
     if (t.vals) (void)hipFree(t.vals);
     if (t.diag) (void)hipFree(t.diag);
-    for (void *p : {(void *)t.bp_perm, (void *)t.bp_rp, (void *)t.bp_cols, (void *)t.bp_vals, (void *)t.bp_diag,
-                    (void *)t.bp_step_pos, (void *)t.bp_step_need, (void *)t.bp_step_done,
-                    (void *)t.bp_step_flag, (void *)t.bp_blk_step, (void *)t.bp_prog, (void *)t.bp_claim,
-                    (void *)t.pk_blk, (void *)t.pk_off, t.pk_data, (void *)t.pk_claim,
-                    (void *)t.pk3_blk, (void *)t.pk3_off, t.pk3_data, (void *)t.pk3_claim,
-                    (void *)t.pk4_blk, (void *)t.pk4_off, t.pk4_data, (void *)t.pk4_claim,
-                    (void *)t.pk5_blk, (void *)t.pk5_desc, (void *)t.pk5_idx, (void *)t.pk5_rec,
-                    (void *)t.pk5_claim, (void *)t.pk6_blk, (void *)t.pk6_desc, (void *)t.pk6_idx,
-                    (void *)t.pk6_rec, (void *)t.pk6_claim})
+    for (void *p : {(void *)t.bp_perm, (void *)t.pk_blk, (void *)t.pk_off, t.pk_data, (void *)t.pk_claim,
+                    (void *)t.pk6_blk, (void *)t.pk6_desc, (void *)t.pk6_idx, (void *)t.pk6_rec,
+                    (void *)t.pk6_claim})
         if (p) (void)hipFree(p);
     t = TriSched();
 }

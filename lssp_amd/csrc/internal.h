@@ -73,14 +73,12 @@ struct lssp_amd_ctx {
     void *comm = nullptr;      // ncclComm_t
     double *d_gather = nullptr;  // [nranks][MAX_SLOTS]
     int tri_blocks_per_cu = 1;
-    // 0 sync-free + back-off, 1 one launch per level, 2 sync-free no back-off,
-    // 3 block pipeline with progress words, 4 packet-streamed block pipeline,
-    // 5-8 packet-pipeline experiments, 9 role-split packet sweeps through
-    // schedule-ordered shadows (default; kernels.hip k_tri_pk6)
+    // 0 sync-free + back-off, 1 one launch per level, 2 sync-free without
+    // back-off, 4 packet pipeline (v1 packets), 9 role-split packet sweeps
+    // through schedule-ordered shadows (default): trisolve.hip
     int tri_mode = 9;
     int tri_diag = 0;  // LSSP_AMD_TRI_DIAG timing experiments (wrong results when != 0)
-    int tri_depth = 2; // LSSP_AMD_TRI_DEPTH: tri_mode 6 prefetch depth S (2, 3), tri_mode 7 x lead KE (1, 2)
-    int tri_pipe = 0;  // LSSP_AMD_TRI_PIPE: tri_mode 9 prefetch depths (kernels.hip launch_pk6)
+    int tri_pipe = 0;  // LSSP_AMD_TRI_PIPE: tri_mode 9 prefetch depths (trisolve.hip launch_pk6)
     // Krylov work vectors, kept across solves (no hipMalloc on the solve path)
     struct WsBuf {
         double *p;
@@ -116,43 +114,18 @@ struct TriSched {
     double *diag = nullptr;  // per position (nullptr when unit)
     std::vector<int> level_ptr;  // host: schedule positions of each level
     int max_level_rows = 0;
-    // block-pipelined schedule (tri_mode 3): contiguous row blocks of B >=
-    // bandwidth rows in sweep order, each processed level by level by one
-    // workgroup; see kernels.hip k_tri_bp
+    // block-pipelined schedule (tri_bp.cpp): contiguous row blocks of B >=
+    // bandwidth rows in sweep order, each walked level by level by one workgroup
     int bp_B = 0, bp_nb = 0, bp_nsteps = 0;
-    int *bp_perm = nullptr, *bp_rp = nullptr, *bp_cols = nullptr;  // cols < 0: LDS ring slot
-    double *bp_vals = nullptr, *bp_diag = nullptr;
-    int *bp_step_pos = nullptr, *bp_step_need = nullptr, *bp_step_done = nullptr;
-    int *bp_step_flag = nullptr, *bp_blk_step = nullptr;
-    unsigned long long *bp_prog = nullptr, *bp_claim = nullptr;
-    mutable unsigned long long bp_base = 0;  // claim-ticket base of the next launch
-    mutable unsigned bp_epoch = 0;           // progress-word epoch of the last launch
-    // packet-streamed block pipeline (tri_mode 4): each block's steps cut into
-    // packets of <= PK_ROWS rows / PK_BYTES bytes, laid out contiguously
+    int *bp_perm = nullptr;  // schedule position -> row
+    // packets v1 (tri_mode 4): each block's steps cut into packets of <=
+    // PK_ROWS rows / PK_BYTES bytes, laid out contiguously
     int pk_n = 0;
     int *pk_blk = nullptr;        // [nb+1] first packet of each block
     int *pk_off = nullptr;        // [npk+1] packet offsets in 16-byte units
     void *pk_data = nullptr;
     mutable unsigned long long pk_base = 0;
     unsigned long long *pk_claim = nullptr;
-    // packets v3 (tri_mode 6: loader waves gather HBM operands ahead, tri_bp.cpp)
-    int pk3_n = 0;
-    int *pk3_blk = nullptr, *pk3_off = nullptr;
-    void *pk3_data = nullptr;
-    mutable unsigned long long pk3_base = 0;
-    unsigned long long *pk3_claim = nullptr;
-    // packets v4 (tri_mode 7: column-major fixed-width rows, register-prefetched)
-    int pk4_n = 0;
-    int *pk4_blk = nullptr, *pk4_off = nullptr;
-    void *pk4_data = nullptr;
-    mutable unsigned long long pk4_base = 0;
-    unsigned long long *pk4_claim = nullptr;
-    // packets v5 (tri_mode 8: register records straight from HBM, LDS only for values)
-    int pk5_n = 0, pk5_ep = 4;
-    int *pk5_blk = nullptr, *pk5_desc = nullptr, *pk5_idx = nullptr;
-    uint32_t *pk5_rec = nullptr;
-    mutable unsigned long long pk5_base = 0;
-    unsigned long long *pk5_claim = nullptr;
     // packets v6 (tri_mode 9: schedule-ordered shadow vectors between sweeps)
     int pk6_n = 0, pk6_ep = 4, pk6_rows = 256;
     int *pk6_blk = nullptr, *pk6_desc = nullptr, *pk6_idx = nullptr;
@@ -163,11 +136,10 @@ struct TriSched {
 };
 constexpr int PK_ROWS = 256;
 constexpr int PK_BYTES = 12288;
-constexpr int PK3_ROWS = 256;    // rows per packet = compute lanes = loader lanes
-constexpr int PK3_EXT = 2;       // HBM x operands per packet row (on average)
-constexpr int PK3_BYTES = 12288;
-constexpr int PK3_CAP = 4096;    // packets per block (offsets staged in LDS)
-constexpr int PK4_PAD = -1 - 4096;  // v4 padding code: the value-ring slot past the end (holds +0.0)
+constexpr int PK3_ROWS = 256;    // v6: rows per packet = compute lanes = loader lanes
+constexpr int PK3_EXT = 2;       // v6: HBM x operands per packet row (on average)
+constexpr int PK3_CAP = 4096;    // v6: packets per block (descriptors staged in LDS)
+constexpr int PK4_PAD = -1 - 4096;  // v6 padding code: the value-ring slot past the end (holds +0.0)
 
 }  // namespace lssp_amd
 
@@ -179,7 +151,7 @@ struct lssp_amd_ilu {
     lssp_amd::TriSched lower, upper;
     double *d_cache = nullptr;  // L sweep output, kept all-sentinel between applies
     // tri_mode 9: schedule-ordered shadows {L out, L out', U out, U out'} and the
-    // apply counter selecting the buffer pair (kernels.hip launch_ilu_apply)
+    // apply counter selecting the buffer pair (trisolve.hip launch_ilu_apply)
     mutable double *d_sh[4] = {nullptr, nullptr, nullptr, nullptr};
     mutable double *d_rperm = nullptr;  // the apply's rhs in L order
     mutable unsigned epoch = 0;
@@ -243,18 +215,6 @@ int build_packets(int n, const std::vector<int> &perm, const std::vector<int> &r
                   const std::vector<int> &cols, const std::vector<double> &vals,
                   const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
                   const std::vector<int> &blk_step, int nb, long B, TriSched &t);
-int build_packets3(int n, const std::vector<int> &perm, const std::vector<int> &rp,
-                   const std::vector<int> &cols, const std::vector<double> &vals,
-                   const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
-                   const std::vector<int> &blk_step, int nb, long B, TriSched &t);
-int build_packets4(int n, const std::vector<int> &perm, const std::vector<int> &rp,
-                   const std::vector<int> &cols, const std::vector<double> &vals,
-                   const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
-                   const std::vector<int> &blk_step, int nb, long B, TriSched &t);
-int build_packets5(int n, const std::vector<int> &perm, const std::vector<int> &rp,
-                   const std::vector<int> &cols, const std::vector<double> &vals,
-                   const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
-                   const std::vector<int> &blk_step, int nb, long B, TriSched &t);
 int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &pos, const std::vector<int> &rp,
                    const std::vector<int> &cols, const std::vector<double> &vals,
                    const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,

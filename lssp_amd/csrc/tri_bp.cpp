@@ -1,14 +1,16 @@
-// tri_bp.cpp -- host setup of the block-pipelined triangular sweep (tri_mode 3).
+// tri_bp.cpp -- host setup of the block-pipelined triangular sweeps
+// (tri_mode 9, k_tri_pk6; tri_mode 4, k_tri_pk: trisolve.hip).
 //
 // The factor's rows, in sweep order (q = r for L, q = n-1-r for U), are cut
 // into contiguous blocks of B rows with B >= the factor's bandwidth, so every
-// dependency of a row lies in its own block or in the previous one.  One
+// dependency of a row lies in its own block or in earlier ones.  One
 // workgroup takes a block and walks it level by level ("steps"); values it
 // needs from its own block come from an LDS ring of recent results, values
-// from the previous block are read once that block's progress word says the
-// needed level is complete.  Only one cross-CU hand-off per block boundary is
-// on the critical path instead of one per level.  The per-row arithmetic is
-// untouched (entries in the reference's order), so the sweep stays bitwise.
+// from earlier blocks from HBM, where value-as-flag (TRI_SENTINEL) makes a
+// not-yet-written value visible as such.  Only one cross-CU hand-off per block
+// boundary is on the critical path instead of one per level.  The per-row
+// arithmetic is untouched (entries in the reference's order), so the sweep
+// stays bitwise.
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
@@ -41,8 +43,6 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
     long B = std::max(64L, mult * (long)bw);
     if (B > n) B = n;
     const int nb = (int)((n + B - 1) / B);
-    const char *ep = getenv("LSSP_AMD_TRI_BP_PUBLISH");
-    const int publish_every = ep ? std::max(1, atoi(ep)) : 1;
 
     // rows of each block ordered by (level, q)
     std::vector<int> perm(n), pos(n);
@@ -80,13 +80,16 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
 
     // entries in summation order; intra-block dependencies still inside the
     // ring window come from LDS (code -1 - slot), everything else from HBM
-    std::vector<int> rp(n + 1, 0), cols, need(nsteps, -1), done(nsteps), flag(nsteps, 0);
+    std::vector<int> rp(n + 1, 0), cols;
     std::vector<double> vals, diag;
     if (!unit) diag.resize(n);
     cols.reserve(Tj.size());
     vals.reserve(Tj.size());
     for (int p = 0; p < n; p++) {
         const int i = perm[p], b = (int)(Q(i) / B), s = step_of[p];
+        // within the ring window (the last BP_RING positions of the block)
+        // the value comes from LDS; everything else (earlier blocks, far back
+        // in this one) from HBM
         auto take = [&](int k) {
             const int j = Tj[k];
             const int bj = (int)(Q(j) / B);
@@ -94,9 +97,6 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
             if (bj == b) {
                 const int pd = pos[j];
                 if (step_pos[s + 1] - pd <= BP_RING) code = -1 - (int)((pd - (long)b * B) % BP_RING);
-                else flag[step_of[pd]] |= 1;  // drain right after the producing step
-            } else {
-                need[s] = std::max(need[s], lev[j]);
             }
             cols.push_back(code);
             vals.push_back(Tx[k]);
@@ -108,27 +108,9 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
         if (!unit) diag[p] = upper ? Tx[Tp[i]] : Tx[Tp[i + 1] - 1];
         rp[p + 1] = (int)cols.size();
     }
-    for (int b = 0; b < nb; b++)
-        for (int s = blk_step[b], k = 0; s < blk_step[b + 1]; s++, k++) {
-            const bool last = s + 1 == blk_step[b + 1];
-            done[s] = last ? INT_MAX - 2 : step_lev[s + 1] - 1;
-            if (last || (k + 1) % publish_every == 0) flag[s] |= 1;
-        }
-
     {
-        const int st = build_packets(n, perm, rp, cols, vals, diag, unit, step_pos, blk_step, nb, B, t);
-        if (st == LSSP_AMD_EUNSUPPORTED) t.pk_n = -1;  // a row too long for a packet: mode 2 serves it
-        else if (st != LSSP_AMD_OK) return st;
-        const int st3 = build_packets3(n, perm, rp, cols, vals, diag, unit, step_pos, blk_step, nb, B, t);
-        if (st3 == LSSP_AMD_EUNSUPPORTED) t.pk3_n = -1;  // mode 6 falls back to mode 4
-        else if (st3 != LSSP_AMD_OK) return st3;
-        const int st4 = build_packets4(n, perm, rp, cols, vals, diag, unit, step_pos, blk_step, nb, B, t);
-        if (st4 == LSSP_AMD_EUNSUPPORTED) t.pk4_n = -1;  // mode 7 falls back to mode 4
-        else if (st4 != LSSP_AMD_OK) return st4;
-        const int st5 = build_packets5(n, perm, rp, cols, vals, diag, unit, step_pos, blk_step, nb, B, t);
-        if (st5 == LSSP_AMD_EUNSUPPORTED) t.pk5_n = -1;  // mode 8 falls back to mode 4
-        else if (st5 != LSSP_AMD_OK) return st5;
-        // v6: the rhs of the U sweep is the L sweep's output in L's schedule order
+        // v6 packets (tri_mode 9); the rhs of the U sweep is the L sweep's
+        // output, read in L's schedule order
         std::vector<int> rhs_index(n);
         for (int r = 0; r < n; r++) rhs_index[r] = prod && !prod->h_pos.empty() ? prod->h_pos[r] : pos[r];
         const int st6 = build_packets6(n, perm, pos, rp, cols, vals, diag, unit, step_pos, blk_step, nb, B,
@@ -136,6 +118,13 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
         if (st6 == LSSP_AMD_EUNSUPPORTED) t.pk6_n = -1;  // mode 9 falls back to mode 4
         else if (st6 != LSSP_AMD_OK) return st6;
         if (!upper) t.h_pos = pos;
+        // v1 packets (tri_mode 4): when selected, or as mode 9's fallback
+        t.pk_n = -1;
+        if (c->tri_mode == 4 || t.pk6_n < 0) {
+            const int st = build_packets(n, perm, rp, cols, vals, diag, unit, step_pos, blk_step, nb, B, t);
+            if (st == LSSP_AMD_EUNSUPPORTED) t.pk_n = -1;  // a row too long for a packet: mode 0 serves it
+            else if (st != LSSP_AMD_OK) return st;
+        }
     }
     t.bp_B = (int)B;
     t.upper = upper;
@@ -147,22 +136,7 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
         if (!h.empty()) LSSP_HIP(hipMemcpy(d, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
         return LSSP_AMD_OK;
     };
-    LSSP_TRY(up(t.bp_perm, perm));
-    LSSP_TRY(up(t.bp_rp, rp));
-    LSSP_TRY(up(t.bp_cols, cols));
-    LSSP_TRY(up(t.bp_vals, vals));
-    if (!unit) LSSP_TRY(up(t.bp_diag, diag));
-    LSSP_TRY(up(t.bp_step_pos, step_pos));
-    LSSP_TRY(up(t.bp_step_need, need));
-    LSSP_TRY(up(t.bp_step_done, done));
-    LSSP_TRY(up(t.bp_step_flag, flag));
-    LSSP_TRY(up(t.bp_blk_step, blk_step));
-    LSSP_HIP(hipMalloc(&t.bp_prog, sizeof(unsigned long long) * nb));
-    LSSP_HIP(hipMemset(t.bp_prog, 0, sizeof(unsigned long long) * nb));
-    LSSP_HIP(hipMalloc(&t.bp_claim, sizeof(unsigned long long)));
-    LSSP_HIP(hipMemset(t.bp_claim, 0, sizeof(unsigned long long)));
-    t.bp_base = 0;
-    t.bp_epoch = 0;
+    LSSP_TRY(up(t.bp_perm, perm));  // position -> row: the apply's permutation kernels
     return LSSP_AMD_OK;
 }
 
@@ -230,316 +204,10 @@ int build_packets(int n, const std::vector<int> &perm, const std::vector<int> &r
     return LSSP_AMD_OK;
 }
 
-// Packet layout v3 (tri_mode 6, kernels.hip k_tri_pk3), 4-byte words:
-//   [0] nrows  [1] nent  [2] block-local position of the first row  [3] nx
-//   rows[nrows]  rp[nrows+1]  codes[nent]  xidx[nx]  (pad to 8 bytes)
-//   vals[nent] (double)  diag[nrows] (double, only when the diagonal is not 1)
-// codes < 0 name an LDS ring slot (-1 - slot) as in v1; codes >= 0 index the
-// packet's list xidx of distinct x entries read from HBM, which the loader
-// waves gather ahead of time (at most PK3_ROWS * PK3_EXT per packet).  Each
-// block's packets are contiguous and at most PK3_CAP; the buffer is padded by
-// one packet so a fixed-size PK3_BYTES load from any packet start stays in bounds.
-int build_packets3(int n, const std::vector<int> &perm, const std::vector<int> &rp,
-                   const std::vector<int> &cols, const std::vector<double> &vals,
-                   const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
-                   const std::vector<int> &blk_step, int nb, long B, TriSched &t)
-{
-    auto words = [&](int nr, int ne, int nx) {
-        long w = 5 + 2L * nr + ne + nx;
-        w = (w + 1) & ~1L;
-        w += 2L * ne + (unit ? 0 : 2L * nr);
-        return (w + 3) & ~3L;
-    };
-    std::vector<int> blk(nb + 1, 0), off(1, 0);
-    std::vector<uint32_t> data;
-    std::vector<int> stamp(n, -1), slot(n, 0), xl;
-    int pid = 0;
-    for (int b = 0; b < nb; b++) {
-        blk[b] = (int)off.size() - 1;
-        for (int s = blk_step[b]; s < blk_step[b + 1]; s++) {
-            int p = step_pos[s];
-            while (p < step_pos[s + 1]) {
-                int nr = 0, ne = 0;
-                xl.clear();
-                while (p + nr < step_pos[s + 1] && nr < PK3_ROWS) {
-                    const int r = p + nr;
-                    const int e = rp[r + 1] - rp[r];
-                    int newx = 0;
-                    for (int k = rp[r]; k < rp[r + 1]; k++)
-                        if (cols[k] >= 0 && stamp[cols[k]] != pid) newx++;
-                    if ((long)xl.size() + newx > (long)PK3_ROWS * PK3_EXT) break;
-                    if (words(nr + 1, ne + e, (int)xl.size() + newx) * 4 > PK3_BYTES) break;
-                    for (int k = rp[r]; k < rp[r + 1]; k++) {
-                        const int g = cols[k];
-                        if (g >= 0 && stamp[g] != pid) {
-                            stamp[g] = pid;
-                            slot[g] = (int)xl.size();
-                            xl.push_back(g);
-                        }
-                    }
-                    nr++;
-                    ne += e;
-                }
-                if (nr == 0) return LSSP_AMD_EUNSUPPORTED;  // one row does not fit a packet
-                const int nx = (int)xl.size();
-                const size_t o = data.size();
-                data.resize(o + words(nr, ne, nx), 0u);
-                uint32_t *w = data.data() + o;
-                w[0] = nr;
-                w[1] = ne;
-                w[2] = (uint32_t)(p - (long)b * B);
-                w[3] = nx;
-                for (int r = 0; r < nr; r++) w[4 + r] = (uint32_t)perm[p + r];
-                for (int r = 0; r <= nr; r++) w[4 + nr + r] = (uint32_t)(rp[p + r] - rp[p]);
-                for (int e = 0; e < ne; e++) {
-                    const int g = cols[rp[p] + e];
-                    w[5 + 2 * nr + e] = (uint32_t)(g < 0 ? g : slot[g]);
-                }
-                for (int x = 0; x < nx; x++) w[5 + 2 * nr + ne + x] = (uint32_t)xl[x];
-                const long vo = (5 + 2L * nr + ne + nx + 1) & ~1L;
-                memcpy(w + vo, vals.data() + rp[p], sizeof(double) * ne);
-                if (!unit) memcpy(w + vo + 2L * ne, diag.data() + p, sizeof(double) * nr);
-                off.push_back((int)(data.size() / 4));
-                p += nr;
-                pid++;
-            }
-        }
-        if ((int)off.size() - 1 - blk[b] > PK3_CAP) return LSSP_AMD_EUNSUPPORTED;
-    }
-    blk[nb] = (int)off.size() - 1;
-    data.resize(data.size() + PK3_BYTES / 4, 0u);  // over-read pad
-    t.pk3_n = (int)off.size() - 1;
-    LSSP_HIP(hipMalloc(&t.pk3_blk, sizeof(int) * (nb + 1)));
-    LSSP_HIP(hipMemcpy(t.pk3_blk, blk.data(), sizeof(int) * (nb + 1), hipMemcpyHostToDevice));
-    LSSP_HIP(hipMalloc(&t.pk3_off, sizeof(int) * off.size()));
-    LSSP_HIP(hipMemcpy(t.pk3_off, off.data(), sizeof(int) * off.size(), hipMemcpyHostToDevice));
-    LSSP_HIP(hipMalloc(&t.pk3_data, sizeof(uint32_t) * data.size()));
-    LSSP_HIP(hipMemcpy(t.pk3_data, data.data(), sizeof(uint32_t) * data.size(), hipMemcpyHostToDevice));
-    LSSP_HIP(hipMalloc(&t.pk3_claim, sizeof(unsigned long long)));
-    LSSP_HIP(hipMemset(t.pk3_claim, 0, sizeof(unsigned long long)));
-    t.pk3_base = 0;
-    return LSSP_AMD_OK;
-}
 
-// Packet layout v4 (tri_mode 7, kernels.hip k_tri_pk4), 4-byte words:
-//   [0] nrows  [1] emax (entries of the longest row)  [2] block-local position
-//   of the first row  [3] nx
-//   rows[nrows]  codes[emax][nrows]  xidx[nx]  (pad to 8 bytes)
-//   vals[emax][nrows] (double)  diag[nrows] (double, only when not unit)
-// Entries are stored column-major (entry e of row t at e*nrows + t) so that a
-// compute lane reads its row with stride-1 LDS accesses; rows shorter than emax
-// are padded with code PK4_PAD (an LDS slot holding +0.0) and value +0.0, and
-// acc - (+0.0)*(+0.0) == acc bit for bit, so the padding leaves the reference's
-// summation untouched.  codes < 0 other than PK4_PAD name a value-ring slot,
-// codes >= 0 index xidx (HBM operands gathered by the loader waves).
-int build_packets4(int n, const std::vector<int> &perm, const std::vector<int> &rp,
-                   const std::vector<int> &cols, const std::vector<double> &vals,
-                   const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
-                   const std::vector<int> &blk_step, int nb, long B, TriSched &t)
-{
-    auto words = [&](long nr, long emax, long nx) {
-        long w = 4 + nr + emax * nr + nx;
-        w = (w + 1) & ~1L;
-        w += 2 * emax * nr + (unit ? 0 : 2 * nr);
-        return (w + 3) & ~3L;
-    };
-    std::vector<int> blk(nb + 1, 0), off(1, 0);
-    std::vector<uint32_t> data;
-    std::vector<int> stamp(n, -1), slot(n, 0), xl;
-    int pid = 0;
-    for (int b = 0; b < nb; b++) {
-        blk[b] = (int)off.size() - 1;
-        for (int s = blk_step[b]; s < blk_step[b + 1]; s++) {
-            int p = step_pos[s];
-            while (p < step_pos[s + 1]) {
-                int nr = 0, emax = 0;
-                xl.clear();
-                while (p + nr < step_pos[s + 1] && nr < PK3_ROWS) {
-                    const int r = p + nr;
-                    const int e = rp[r + 1] - rp[r];
-                    int newx = 0;
-                    for (int k = rp[r]; k < rp[r + 1]; k++)
-                        if (cols[k] >= 0 && stamp[cols[k]] != pid) newx++;
-                    if ((long)xl.size() + newx > (long)PK3_ROWS * PK3_EXT) break;
-                    if (words(nr + 1, std::max(emax, e), (long)xl.size() + newx) * 4 > PK3_BYTES) break;
-                    for (int k = rp[r]; k < rp[r + 1]; k++) {
-                        const int g = cols[k];
-                        if (g >= 0 && stamp[g] != pid) {
-                            stamp[g] = pid;
-                            slot[g] = (int)xl.size();
-                            xl.push_back(g);
-                        }
-                    }
-                    nr++;
-                    emax = std::max(emax, e);
-                }
-                if (nr == 0) return LSSP_AMD_EUNSUPPORTED;  // one row does not fit a packet
-                const int nx = (int)xl.size();
-                const size_t o = data.size();
-                data.resize(o + words(nr, emax, nx), 0u);
-                uint32_t *w = data.data() + o;
-                w[0] = nr;
-                w[1] = emax;
-                w[2] = (uint32_t)(p - (long)b * B);
-                w[3] = nx;
-                const long co = 4 + nr, xo = co + (long)emax * nr;
-                const long vo = (xo + nx + 1) & ~1L;
-                double *wv = reinterpret_cast<double *>(w + vo);
-                for (int r = 0; r < nr; r++) {
-                    w[4 + r] = (uint32_t)perm[p + r];
-                    const int k0 = rp[p + r], len = rp[p + r + 1] - k0;
-                    for (int e = 0; e < emax; e++) {
-                        int code = PK4_PAD;
-                        double v = 0.0;
-                        if (e < len) {
-                            const int g = cols[k0 + e];
-                            code = g < 0 ? g : slot[g];
-                            v = vals[k0 + e];
-                        }
-                        w[co + (long)e * nr + r] = (uint32_t)code;
-                        wv[(long)e * nr + r] = v;
-                    }
-                }
-                for (int x = 0; x < nx; x++) w[xo + x] = (uint32_t)xl[x];
-                if (!unit) memcpy(w + vo + 2L * emax * nr, diag.data() + p, sizeof(double) * nr);
-                off.push_back((int)(data.size() / 4));
-                p += nr;
-                pid++;
-            }
-        }
-        if ((int)off.size() - 1 - blk[b] > PK3_CAP) return LSSP_AMD_EUNSUPPORTED;
-    }
-    blk[nb] = (int)off.size() - 1;
-    data.resize(data.size() + PK3_BYTES / 4, 0u);  // over-read pad
-    t.pk4_n = (int)off.size() - 1;
-    LSSP_HIP(hipMalloc(&t.pk4_blk, sizeof(int) * (nb + 1)));
-    LSSP_HIP(hipMemcpy(t.pk4_blk, blk.data(), sizeof(int) * (nb + 1), hipMemcpyHostToDevice));
-    LSSP_HIP(hipMalloc(&t.pk4_off, sizeof(int) * off.size()));
-    LSSP_HIP(hipMemcpy(t.pk4_off, off.data(), sizeof(int) * off.size(), hipMemcpyHostToDevice));
-    LSSP_HIP(hipMalloc(&t.pk4_data, sizeof(uint32_t) * data.size()));
-    LSSP_HIP(hipMemcpy(t.pk4_data, data.data(), sizeof(uint32_t) * data.size(), hipMemcpyHostToDevice));
-    LSSP_HIP(hipMalloc(&t.pk4_claim, sizeof(unsigned long long)));
-    LSSP_HIP(hipMemset(t.pk4_claim, 0, sizeof(unsigned long long)));
-    t.pk4_base = 0;
-    return LSSP_AMD_OK;
-}
 
-// Packets v5 (tri_mode 8, kernels.hip k_tri_pk5): nothing is staged in LDS but
-// the per-block descriptor table.  Per packet:
-//   desc  int4 {record offset (16 B units), index offset (4 B units), nr | nx << 16, emax}
-//   records (compute lanes, read straight into registers, lane t -> element t):
-//     I0[nr] int4 {row, ring slot, c0, c1}   I1[nr] int4 {c2, c3, c4, c5}
-//     I2[nr] int4 {c6, c7, 0, 0} (EP == 8 only)
-//     V[EP/2][nr] double2 (entry values, +0.0 padded)   D[nr] double (+ pad to 16 B)
-//   indices (loader lanes): rows[nr] (rhs gathers), xidx[nx] (HBM x operands)
-// Codes as in v4 (ring slot -1-s, PK4_PAD, or an xidx index).  The diagonal of
-// a unit factor is stored as 1.0 (acc / 1.0 == acc exactly).
-int build_packets5(int n, const std::vector<int> &perm, const std::vector<int> &rp,
-                   const std::vector<int> &cols, const std::vector<double> &vals,
-                   const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
-                   const std::vector<int> &blk_step, int nb, long B, TriSched &t)
-{
-    int maxlen = 0;
-    for (int p = 0; p < n; p++) maxlen = std::max(maxlen, rp[p + 1] - rp[p]);
-    if (maxlen > 8) return LSSP_AMD_EUNSUPPORTED;
-    const int EP = maxlen <= 4 ? 4 : 8;
-    const int NI = EP == 4 ? 2 : 3;  // int4 arrays per record
-    std::vector<int> blk(nb + 1, 0);
-    std::vector<int> desc;
-    std::vector<uint32_t> rec;  // 4-byte words, 16-byte aligned packets
-    std::vector<int> idx;
-    std::vector<int> stamp(n, -1), slot(n, 0), xl;
-    int pid = 0;
-    for (int b = 0; b < nb; b++) {
-        blk[b] = (int)desc.size() / 4;
-        for (int s = blk_step[b]; s < blk_step[b + 1]; s++) {
-            int p = step_pos[s];
-            while (p < step_pos[s + 1]) {
-                int nr = 0, emax = 0;
-                xl.clear();
-                while (p + nr < step_pos[s + 1] && nr < PK3_ROWS) {
-                    const int r = p + nr;
-                    int newx = 0;
-                    for (int k = rp[r]; k < rp[r + 1]; k++)
-                        if (cols[k] >= 0 && stamp[cols[k]] != pid) newx++;
-                    if ((long)xl.size() + newx > (long)PK3_ROWS * PK3_EXT) break;
-                    for (int k = rp[r]; k < rp[r + 1]; k++) {
-                        const int g = cols[k];
-                        if (g >= 0 && stamp[g] != pid) {
-                            stamp[g] = pid;
-                            slot[g] = (int)xl.size();
-                            xl.push_back(g);
-                        }
-                    }
-                    emax = std::max(emax, rp[r + 1] - rp[r]);
-                    nr++;
-                }
-                const int nx = (int)xl.size();
-                const long ro = (long)rec.size() / 4, io = (long)idx.size();
-                if (ro > INT_MAX || io > INT_MAX) return LSSP_AMD_EUNSUPPORTED;
-                desc.push_back((int)ro);
-                desc.push_back((int)io);
-                desc.push_back(nr | (nx << 16));
-                desc.push_back(emax);
-                const long nwords = 4L * nr * (NI + EP / 2) + 2L * ((nr + 1) & ~1);
-                rec.resize(rec.size() + nwords, 0u);
-                uint32_t *w = rec.data() + 4 * ro;
-                double *V = reinterpret_cast<double *>(w + 4L * NI * nr);
-                double *D = V + (long)EP * nr;
-                const long pos0 = p - (long)b * B;
-                for (int r = 0; r < nr; r++) {
-                    const int k0 = rp[p + r], len = rp[p + r + 1] - k0;
-                    int c[8];
-                    for (int e = 0; e < 8; e++) c[e] = PK4_PAD;
-                    for (int e = 0; e < len; e++) {
-                        const int g = cols[k0 + e];
-                        c[e] = g < 0 ? g : slot[g];
-                        // V[e/2][r] = {v(2q), v(2q+1)}
-                        V[2L * ((long)(e / 2) * nr + r) + (e & 1)] = vals[k0 + e];
-                    }
-                    uint32_t *i0 = w + 4L * r, *i1 = w + 4L * (nr + r);
-                    i0[0] = (uint32_t)perm[p + r];
-                    i0[1] = (uint32_t)((pos0 + r) % BP_RING);
-                    i0[2] = (uint32_t)c[0];
-                    i0[3] = (uint32_t)c[1];
-                    for (int e = 0; e < 4; e++) i1[e] = (uint32_t)c[2 + e];
-                    if (NI == 3) {
-                        uint32_t *i2 = w + 4L * (2L * nr + r);
-                        i2[0] = (uint32_t)c[6];
-                        i2[1] = (uint32_t)c[7];
-                    }
-                    D[r] = unit ? 1.0 : diag[p + r];
-                }
-                for (int r = 0; r < nr; r++) idx.push_back(perm[p + r]);
-                for (int x = 0; x < nx; x++) idx.push_back(xl[x]);
-                p += nr;
-                pid++;
-            }
-        }
-        if ((int)desc.size() / 4 - blk[b] > PK3_CAP) return LSSP_AMD_EUNSUPPORTED;
-    }
-    blk[nb] = (int)desc.size() / 4;
-    rec.resize(rec.size() + 4, 0u);
-    idx.push_back(0);
-    t.pk5_n = blk[nb];
-    t.pk5_ep = EP;
-    auto up = [](auto *&d, const auto &h) -> int {
-        using T = typename std::remove_reference<decltype(h)>::type::value_type;
-        LSSP_HIP(hipMalloc(&d, sizeof(T) * std::max<size_t>(h.size(), 1)));
-        if (!h.empty()) LSSP_HIP(hipMemcpy(d, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
-        return LSSP_AMD_OK;
-    };
-    LSSP_TRY(up(t.pk5_blk, blk));
-    LSSP_TRY(up(t.pk5_desc, desc));
-    LSSP_TRY(up(t.pk5_rec, rec));
-    LSSP_TRY(up(t.pk5_idx, idx));
-    LSSP_HIP(hipMalloc(&t.pk5_claim, sizeof(unsigned long long)));
-    LSSP_HIP(hipMemset(t.pk5_claim, 0, sizeof(unsigned long long)));
-    t.pk5_base = 0;
-    return LSSP_AMD_OK;
-}
 
-// Packets v6 (tri_mode 9, kernels.hip k_tri_pk6).  The sweeps exchange values
+// Packets v6 (tri_mode 9, trisolve.hip k_tri_pk6).  The sweeps exchange values
 // through "shadow" vectors kept in schedule order (position p holds the value
 // of row perm[p]), so the cross-block operands of a packet and its output are
 // contiguous runs instead of one cache line per row.  Per packet:

@@ -1,0 +1,807 @@
+// trisolve.hip -- the ILU triangular sweeps (solver-tri.cxx:4-60) on gfx950.
+//
+// tri_mode 9 (default): role-split packet pipeline through schedule-ordered
+// shadow vectors (k_tri_pk6, packets from tri_bp.cpp build_packets6); tri_mode
+// 4: the first packet pipeline (k_tri_pk, build_packets), used when a factor
+// has rows longer than the v6 record holds; tri_mode 0 / 2: the sync-free
+// level-ordered sweep (also the single-sweep API's path); tri_mode 1: one
+// launch per level.  DESIGN.md 5 has the measurements behind the choice.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "internal.h"
+
+namespace lssp_amd {
+
+// ---------------------------------------------------------------------------
+// Sync-free level-ordered triangular sweep (solver-tri.cxx:4-46).
+//
+// Rows are visited in level order (host analysis, ilu_setup.cpp); 64
+// consecutive scheduled rows form a chunk and wave w of the persistent grid
+// takes chunks w, w+W, w+2W, ... in order.  x starts as TRI_SENTINEL
+// everywhere; a row's value is published by ONE 8-byte agent-scope store and
+// read by agent-scope (sc1, L1-bypassing) loads -- the data is the flag
+// (MI355X_MICROARCH: R2 granule).  Each lane consumes its row's entries in the
+// reference's order as they become available, so the arithmetic is exactly
+// result = result - val*x[col] ... ; x = result / diag.  The smallest
+// unfinished chunk can always progress (its dependencies lie in earlier chunks
+// or earlier in the same chunk, and its wave is resident), so the sweep
+// cannot deadlock; every wait is still bounded (4 s of s_memrealtime) and a
+// timeout raises ctx->d_err instead of hanging the GPU.
+// ---------------------------------------------------------------------------
+struct TriArgs {
+    int n;
+    long nchunks;
+    const int *perm, *rp, *cols;
+    const double *vals, *diag;
+    int unit;
+    const double *rhs;
+    double *x;
+    double *reset;  // if set: reset[row] = TRI_SENTINEL once rhs[row] has been read
+    int *err;
+};
+
+__device__ __forceinline__ uint64_t ld_agent(const double *p)
+{
+    return __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void st_agent(double *p, double v)
+{
+    __hip_atomic_store(reinterpret_cast<uint64_t *>(p), (uint64_t)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Sync-free sweep.  First pass over a row's entries loads them in batches of
+// four; once a dependency is found missing, the lane re-polls only that one
+// entry (one load per lane per poll) with an exponential back-off, so waves
+// far ahead of the wavefront do not flood the memory system with polls.
+template <int BACKOFF>
+__global__ __launch_bounds__(256) void k_trisolve(TriArgs a)
+{
+    const int lane = threadIdx.x & 63;
+    const long wave = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const long nwaves = (long)gridDim.x * (blockDim.x >> 6);
+    for (long c = wave; c < a.nchunks; c += nwaves) {
+        const long p = c * 64 + lane;
+        bool active = p < a.n;
+        int row = 0, k = 0, end = 0;
+        double acc = 0;
+        if (active) {
+            row = a.perm[p];
+            k = a.rp[p];
+            end = a.rp[p + 1];
+            acc = a.rhs[row];
+            if (a.reset) a.reset[row] = __longlong_as_double((long long)TRI_SENTINEL);
+        }
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        int nap = 1;
+        int mcap = 4;
+        for (;;) {
+            if (active) {
+                while (k < end) {
+                    const int m = end - k < mcap ? end - k : mcap;
+                    uint64_t bits[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (u < m) bits[u] = ld_agent(a.x + a.cols[k + u]);
+                    int u = 0;
+                    for (; u < m; u++) {
+                        if (bits[u] == TRI_SENTINEL) break;
+                        acc = acc - a.vals[k] * __longlong_as_double((long long)bits[u]);
+                        k++;
+                    }
+                    if (u < m) {
+                        mcap = 1;  // re-poll just the first missing dependency
+                        break;
+                    }
+                    mcap = 4;
+                }
+                if (k == end) {
+                    const double xi = a.unit ? acc : acc / a.diag[p];
+                    st_agent(a.x + row, xi);
+                    active = false;
+                }
+            }
+            if (!__any(active)) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s at 100 MHz
+                if (active) {
+                    atomicOr(a.err, 1);
+                    st_agent(a.x + row, __longlong_as_double(0x7FF8000000000000ll));
+                }
+                break;
+            }
+            for (int q = 0; q < nap; q++) __builtin_amdgcn_s_sleep(2);
+            if (BACKOFF && nap < 32) nap <<= 1;
+        }
+    }
+}
+
+// Level-synchronous alternative: one launch per level, every dependency lies in
+// an earlier launch, so plain loads suffice and nothing waits.
+__global__ __launch_bounds__(256) void k_trisolve_level(TriArgs a, int lo, int hi)
+{
+    const int p = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= hi) return;
+    const int row = a.perm[p];
+    double acc = a.rhs[row];
+    if (a.reset) a.reset[row] = __longlong_as_double((long long)TRI_SENTINEL);
+    for (int k = a.rp[p]; k < a.rp[p + 1]; k++) acc = acc - a.vals[k] * a.x[a.cols[k]];
+    a.x[row] = a.unit ? acc : acc / a.diag[p];
+}
+
+// Packet-streamed block pipeline (tri_mode 4, packets from tri_bp.cpp).
+// Blocks are claimed in sweep order as in k_tri_bp.  Inside a block the
+// workgroup streams its packets (one level's rows each) through a 3-slot LDS
+// ring: while it computes packet q it loads packet q+2 with 16-byte loads and
+// gathers the right-hand side of packet q+1, so only the x dependencies are
+// on the critical path.  Same-block values of the last BP_RING positions come
+// from the LDS value ring; all other x values are read with agent-scope loads
+// and, because x is armed with TRI_SENTINEL before the sweep, a value that is
+// not yet visible is simply re-read (value-as-flag): no store drains, no
+// progress words.  A block only ever waits on the block before it, which was
+// claimed earlier by a running workgroup, so the sweep always drains.
+struct PkArgs {
+    int nb;
+    const int *blk, *off;
+    const int4 *data;
+    int unit;
+    const double *rhs;
+    double *x;
+    double *reset;
+    unsigned long long *claim;
+    unsigned long long base;
+    int *err;
+    int diag;  // diagnostics only (LSSP_AMD_TRI_DIAG): 1 = no waiting, 2 = no cross-block loads
+};
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a
+// workgroup-scope fence + s_barrier, which on gfx950 also waits vmcnt(0): every
+// in-flight global load AND every x store would be waited for at each step.
+// Here only LDS traffic must be complete; global loads are waited for where
+// their registers are used, the sc1 x stores are never waited for.
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ double ld_ready(const double *p, int *err)
+{
+    uint64_t bits = ld_agent(p);
+    if (bits == TRI_SENTINEL) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        do {
+            __builtin_amdgcn_s_sleep(1);
+            bits = ld_agent(p);
+            if (bits != TRI_SENTINEL) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s
+                atomicOr(err, 4);
+                return __longlong_as_double(0x7FF8000000000000ll);
+            }
+        } while (true);
+    }
+    return __longlong_as_double((long long)bits);
+}
+
+constexpr int PK_VEC = PK_BYTES / 16;         // int4 per packet slot
+constexpr int PK_LD = (PK_VEC + 255) / 256;   // int4 loads per thread to stage one packet
+
+__global__ __launch_bounds__(256) void k_tri_pk(PkArgs a)
+{
+    __shared__ double ring[BP_RING];
+    __shared__ int4 pbuf[3][PK_VEC];
+    __shared__ double rbuf[3][PK_ROWS];
+    __shared__ int s_blk;
+    const int tid = threadIdx.x;
+    for (;;) {
+        __syncthreads();
+        if (tid == 0) s_blk = (int)(atomicAdd(a.claim, 1ull) - a.base);
+        __syncthreads();
+        const int b = s_blk;
+        if (b >= a.nb) break;
+        const int q0 = a.blk[b], q1 = a.blk[b + 1];
+        // prologue: packets q0, q0+1 into slots 0, 1; rhs of q0 into rbuf[0]
+        for (int j = 0; j < 2 && q0 + j < q1; j++) {
+            const int o = a.off[q0 + j], len = a.off[q0 + j + 1] - o;
+            for (int i = tid; i < len; i += 256) pbuf[j][i] = a.data[o + i];
+        }
+        __syncthreads();
+        {
+            const int *w = reinterpret_cast<const int *>(pbuf[0]);
+            if (tid < w[0]) rbuf[0][tid] = a.rhs[w[4 + tid]];
+        }
+        __syncthreads();
+        for (int q = q0; q < q1; q++) {
+            const int cur = (q - q0) % 3, nxt = (cur + 1) % 3, nn = (cur + 2) % 3;
+            // (1) stage packet q+2
+            int4 st[PK_LD];
+            int o2 = 0, len2 = 0;
+            if (q + 2 < q1) {
+                o2 = a.off[q + 2];
+                len2 = a.off[q + 3] - o2;
+#pragma unroll
+                for (int u = 0; u < PK_LD; u++) {
+                    const int i = tid + 256 * u;
+                    if (i < len2) st[u] = a.data[o2 + i];
+                }
+            }
+            // (2) gather the right-hand side of packet q+1
+            double rh = 0;
+            bool have_rh = false;
+            if (q + 1 < q1) {
+                const int *w = reinterpret_cast<const int *>(pbuf[nxt]);
+                if (tid < w[0]) {
+                    rh = a.rhs[w[4 + tid]];
+                    have_rh = true;
+                }
+            }
+            // (3) packet q
+            {
+                const int *w = reinterpret_cast<const int *>(pbuf[cur]);
+                const int nr = w[0], ne = w[1], pos0 = w[2];
+                if (tid < nr) {
+                    const int *rows = w + 4, *rp = w + 4 + nr, *codes = w + 5 + 2 * nr;
+                    const int vo = (5 + 2 * nr + ne + 1) & ~1;
+                    const double *vals = reinterpret_cast<const double *>(w + vo);
+                    const int row = rows[tid];
+                    double acc = rbuf[cur][tid];
+                    if (a.reset) a.reset[row] = __longlong_as_double((long long)TRI_SENTINEL);
+                    for (int k = rp[tid]; k < rp[tid + 1]; k++) {
+                        const int code = codes[k];
+                        double xv;
+                        if (code < 0) xv = ring[-1 - code];
+                        else if (a.diag == 0) xv = ld_ready(a.x + code, a.err);
+                        else if (a.diag == 1) xv = __longlong_as_double((long long)ld_agent(a.x + code));
+                        else xv = 0.0;
+                        acc = acc - vals[k] * xv;
+                    }
+                    const double xi = a.unit ? acc : acc / reinterpret_cast<const double *>(w + vo + 2 * ne)[tid];
+                    ring[(pos0 + tid) % BP_RING] = xi;
+                    st_agent(a.x + row, xi);
+                }
+            }
+            // (4) land the staged data
+            if (q + 2 < q1) {
+#pragma unroll
+                for (int u = 0; u < PK_LD; u++) {
+                    const int i = tid + 256 * u;
+                    if (i < len2) pbuf[nn][i] = st[u];
+                }
+            }
+            if (have_rh) rbuf[nxt][tid] = rh;
+            lds_barrier();
+        }
+    }
+}
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint64_t poll_ready(const double *p, int *err)
+{
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const uint64_t bits = ld_agent(p);
+        if (bits != TRI_SENTINEL) return bits;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s
+            atomicOr(err, 4);
+            return 0x7FF8000000000000ull;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+struct PkLd {
+    int row, xi[PK3_EXT];
+    int nr, nx;
+    double rh;
+    uint64_t ev[PK3_EXT];
+};
+
+// tri_mode 9: packets v6 (tri_bp.cpp build_packets6) with schedule-ordered
+// shadow vectors.  the loader/compute role split of the earlier packet kernels, plus:
+//   * the sweep's output goes to a shadow vector in schedule order with
+//     coalesced agent-scope stores (position pos0+t), and the HBM operands of
+//     a packet are read from that shadow by schedule position: for a stencil
+//     both are contiguous runs (one line per 8 rows instead of one per row);
+//   * when the natural-order output is wanted too (the U sweep), a store wave
+//     (wave 8) writes it from the LDS value ring one step later with plain
+//     stores; it never waits on its vmcnt, so neither do the compute waves;
+//   * arming for the next apply: the shadows are double-buffered, and every
+//     block fills its own position range of the other buffer with
+//     TRI_SENTINEL when it is done (coalesced).
+// The compute waves' only VMEM traffic is the coalesced record loads and the
+// coalesced shadow stores, so their in-order vmcnt wait for the record of the
+// current packet never waits for a slow scattered store.
+struct Pk6Args {
+    int nb;
+    const int *blk;
+    const int4 *desc;
+    const uint32_t *rec;
+    const int *idx;
+    const double *rhs;   // rhs entries, indexed by the packet's rhs indices
+    double *sh;          // this sweep's shadow (schedule order), armed with TRI_SENTINEL
+    double *sh_next;     // the other shadow buffer: armed here for the next apply
+    double *nat;         // natural-order output (nullptr: none)
+    int n, B;
+    unsigned long long *claim;
+    unsigned long long base;
+    int *err;
+    int diag;
+    unsigned long long *trace;
+    unsigned long long *trace2;  // diagnostics (LSSP_AMD_TRI_TRACE2): per-step clocks of blocks tb0, tb0+1
+    int tb0;
+};
+
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+template <int EP>
+struct Pk6Rec {
+    typename std::conditional<EP == 4, v2u, v4u>::type c;  // int16 code pairs
+    double v[EP];
+    double dg;
+    int row;
+    int nr, pos0;
+};
+
+__device__ __forceinline__ int code16(int w, int hi) { return hi ? (w >> 16) : (int)(short)(w & 0xffff); }
+
+template <int I, typename T>
+__device__ __forceinline__ T &sel4(T &a, T &b, T &c, T &d)
+{
+    if constexpr (I == 0) return a;
+    else if constexpr (I == 1) return b;
+    else if constexpr (I == 2) return c;
+    else return d;
+}
+
+// KE: steps of lead of the x-operand and rhs gathers; IA: of the gather-index
+// loads (IA - KE of 1 or 2); D: of the compute lanes' record loads.  Register
+// sets rotate with period Q = 4 (packet p lives in set p mod 4), so D <= 3 and
+// IA <= 4.  Shallower prefetch keeps fewer requests in the CU's memory queue,
+// which is what a cross-CU hand-off waits behind (MI355X_MICROARCH.md,
+// handoff-1to1).
+template <int EP, int KE, int IA, int D, bool NAT, int NR>
+__global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args a)
+{
+    constexpr int Q = 4;
+    static_assert(D + 1 <= Q && IA <= Q && KE >= 1 && IA - KE >= 1 && IA - KE <= 2, "pipeline depths");
+    constexpr int S0 = (IA > D ? IA : D);
+    constexpr int J0 = -((S0 + Q - 1) / Q) * Q;  // first step, a multiple of Q
+    __shared__ double ring[BP_RING + 1];
+    __shared__ double rbuf[2][NR];
+    __shared__ double xbuf[2][NR * PK3_EXT];
+    __shared__ int rowbuf[2][NR];
+    __shared__ int4 sdesc[PK3_CAP];
+    __shared__ int s_blk;
+    __shared__ unsigned s_polls;
+    const int tid = threadIdx.x;
+    const int role = __builtin_amdgcn_readfirstlane(tid) / NR;  // 0 compute, 1 loader, 2 store
+    static_assert(!NAT || NR == 256, "the store wave needs a 256-row packet");
+    const int t = tid & (NR - 1);
+    if (tid == 0) ring[BP_RING] = 0.0;
+    int prev = -1;
+    for (;;) {
+        __syncthreads();
+        if (tid == 0) {
+            if (a.trace && prev >= 0) {
+                a.trace[8 * prev + 1] = __builtin_amdgcn_s_memrealtime();
+                a.trace[8 * prev + 2] = s_polls;
+            }
+            s_polls = 0;
+            s_blk = (int)(atomicAdd(a.claim, 1ull) - a.base);
+        }
+        __syncthreads();
+        const int b = s_blk;
+        if (b >= a.nb) break;
+        if (a.trace && tid == 0) {
+            unsigned xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            a.trace[8 * b] = __builtin_amdgcn_s_memrealtime();
+            a.trace[8 * b + 3] = xcc;
+        }
+        prev = b;
+        const int q0 = a.blk[b], np = a.blk[b + 1] - q0;
+        const int bbase = b * a.B;  // first schedule position of the block
+        const bool tr2 = a.trace2 && (b == a.tb0 || b == a.tb0 + 1);
+        auto mark = [&](int j, int k) {
+            if (tr2 && j >= -8 && j < 1016)
+                a.trace2[((long)(b - a.tb0) * 1024 + (j + 8)) * 4 + k] = __builtin_amdgcn_s_memrealtime();
+        };
+        for (int i = tid; i < np; i += blockDim.x) sdesc[i] = a.desc[q0 + i];
+        __syncthreads();
+        // both roles run steps J0 .. J0+T-1 (T a multiple of Q); out-of-range
+        // packets turn into loads from valid dummy addresses
+        const int T = (np - J0 + Q - 1) / Q * Q;
+        auto desc = [&](int p) {
+            const int4 d = sdesc[p];
+            return make_int4(__builtin_amdgcn_readfirstlane(d.x), __builtin_amdgcn_readfirstlane(d.y),
+                             __builtin_amdgcn_readfirstlane(d.z), __builtin_amdgcn_readfirstlane(d.w));
+        };
+
+        // descriptor of a packet, clamped: out-of-range packets get nr = nx = 0
+        // and read valid dummy records (no branches around the loads)
+        auto descc = [&](int p) {
+            int4 d = desc(min(max(p, 0), max(np - 1, 0)));
+            if (p < 0 || p >= np) d.z = 0;
+            return d;
+        };
+        if (role == 0) {
+            uint64_t c0 = 0, c1 = 0, acc_c = 0, acc_b = 0;
+            auto issue = [&](const int4 d, Pk6Rec<EP> &Rr) {
+                const int nr = d.z & 0x3ff;
+                const int n1 = nr > 0 ? nr : 1, tt = min(t, n1 - 1);
+                const uint32_t *base = a.rec + 4L * d.x;
+                const int wc = ((EP / 2) * n1 + 3) & ~3, wd = (2 * n1 + 3) & ~3;
+                Rr.c = reinterpret_cast<const decltype(Rr.c) *>(base)[tt];
+                typedef double v2d __attribute__((ext_vector_type(2)));
+                const v2d *vb = reinterpret_cast<const v2d *>(base + wc);
+#pragma unroll
+                for (int q = 0; q < EP / 2; q++) {
+                    const v2d v = vb[q * n1 + tt];
+                    Rr.v[2 * q] = v.x;
+                    Rr.v[2 * q + 1] = v.y;
+                }
+                Rr.dg = reinterpret_cast<const double *>(vb + (EP / 2) * n1)[tt];
+                if (NAT) Rr.row = reinterpret_cast<const int *>(base + wc + 2 * EP * n1 + wd)[tt];
+                Rr.nr = nr;
+                Rr.pos0 = d.w;
+            };
+            int4 dn = descc(J0 + D);  // descriptor of packet j+D, read one step ahead
+            auto step = [&](int j, Pk6Rec<EP> &Rc, Pk6Rec<EP> &Rn) {
+                if (a.trace) c0 = __builtin_amdgcn_s_memtime();
+                issue(dn, Rn);
+                dn = descc(j + D + 1);
+                if constexpr (EP == 4)
+                    asm volatile("" ::"v"(Rc.c), "v"(Rc.v[0]), "v"(Rc.v[1]), "v"(Rc.v[2]), "v"(Rc.v[3]), "v"(Rc.dg));
+                else
+                    asm volatile("" ::"v"(Rc.c), "v"(Rc.v[0]), "v"(Rc.v[1]), "v"(Rc.v[2]), "v"(Rc.v[3]), "v"(Rc.v[4]),
+                                 "v"(Rc.v[5]), "v"(Rc.v[6]), "v"(Rc.v[7]), "v"(Rc.dg));
+                if (NAT) asm volatile("" ::"v"(Rc.row));
+                if (t < Rc.nr) {  // nr == 0 outside the block's packets
+                    const double *xb = xbuf[j & 1];
+                    double acc = rbuf[j & 1][t];
+                    double xv[EP];
+                    // all EP entries: padded ones read +0.0 and subtract +0.0*+0.0
+#pragma unroll
+                    for (int e = 0; e < EP; e++) {
+                        const int cd = code16((int)Rc.c[e / 2], e & 1);
+                        xv[e] = cd < 0 ? ring[-1 - cd] : xb[cd];
+                    }
+#pragma unroll
+                    for (int e = 0; e < EP; e++) acc = acc - Rc.v[e] * xv[e];
+                    const double xi = acc / Rc.dg;
+                    const int pos = Rc.pos0 + t;
+                    ring[(pos - bbase) & (BP_RING - 1)] = xi;
+                    if (NAT) rowbuf[j & 1][t] = Rc.row;
+                    if (!(a.diag & 2)) st_agent(a.sh + pos, xi);
+                }
+                if (a.trace) c1 = __builtin_amdgcn_s_memtime();
+                if (tid == 0) mark(j, 0);
+                lds_barrier();
+                if (a.trace) {
+                    const uint64_t c2 = __builtin_amdgcn_s_memtime();
+                    acc_c += c1 - c0;
+                    acc_b += c2 - c1;
+                }
+            };
+            Pk6Rec<EP> R0, R1, R2, R3;
+            R0.nr = R1.nr = R2.nr = R3.nr = 0;
+            for (int j0 = J0; j0 < J0 + T; j0 += Q) {  // j0 == 0 (mod Q): packet p in set p mod Q
+                step(j0, sel4<0>(R0, R1, R2, R3), sel4<(0 + D) % Q>(R0, R1, R2, R3));
+                step(j0 + 1, sel4<1>(R0, R1, R2, R3), sel4<(1 + D) % Q>(R0, R1, R2, R3));
+                step(j0 + 2, sel4<2>(R0, R1, R2, R3), sel4<(2 + D) % Q>(R0, R1, R2, R3));
+                step(j0 + 3, sel4<3>(R0, R1, R2, R3), sel4<(3 + D) % Q>(R0, R1, R2, R3));
+            }
+            // arm the block's positions of the other shadow for the next apply
+            if (!(a.diag & 1)) {
+                const long s0 = bbase, s1 = min(s0 + a.B, (long)a.n);
+                uint64_t *rs = reinterpret_cast<uint64_t *>(a.sh_next);
+                for (long i = s0 + t; i < s1; i += NR) rs[i] = TRI_SENTINEL;
+            }
+            if (a.trace && tid == 0) {
+                a.trace[8 * b + 4] = acc_c;
+                a.trace[8 * b + 5] = acc_b;
+            }
+        } else if (role == 1) {
+            // The loader's loads are issued from inline asm with explicit
+            // vmcnt waits: its register sets rotate across the loop back-edge,
+            // where the compiler's own wait counting turns conservative and
+            // waited for the previous step's gathers before issuing new ones.
+            // Per step, in issue order: 3 index loads (packet j+IA), then 3
+            // gathers (packet j+KE) -- so before the gathers, the indices they
+            // use (issued at step j-2) have exactly 12 younger loads, and the
+            // gathers landed at the end of step j (packet j+1, issued at step
+            // j+1-KE) have 6 (KE 2) or 0 (KE 1) younger loads.
+            static_assert(PK3_EXT == 2, "wait counts below assume 3 + 3 loads per step");
+            constexpr int WAIT_IDX = 6 * (IA - KE);  // younger than the indices the gathers use
+            uint64_t acc_w = 0, acc_lb = 0, acc_is = 0, acc_ld = 0, m0 = 0;
+            auto issue_idx = [&](const int4 d, PkLd &L) {
+                const int nr = d.z & 0x3ff, nx = (d.z >> 10) & 0x7ff;
+                const int *base = a.idx + d.y;
+                const int *p0 = base + max(min(t, nr - 1), 0);
+                const int *p1 = base + nr + max(min(t, nx - 1), 0);
+                const int *p2 = base + nr + max(min(t + NR, nx - 1), 0);
+                asm volatile("global_load_dword %0, %1, off" : "=v"(L.row) : "v"(p0) : "memory");
+                asm volatile("global_load_dword %0, %1, off" : "=v"(L.xi[0]) : "v"(p1) : "memory");
+                asm volatile("global_load_dword %0, %1, off" : "=v"(L.xi[1]) : "v"(p2) : "memory");
+                L.nr = nr;
+                L.nx = nx;
+            };
+            auto gather = [&](PkLd &L) {
+                asm volatile("s_waitcnt vmcnt(%3)" : "+v"(L.row), "+v"(L.xi[0]), "+v"(L.xi[1]) : "n"(WAIT_IDX) : "memory");
+                const double *pr = a.rhs + ((a.diag & 4) ? t : L.row);
+                const double *px0 = a.sh + ((a.diag & 8) ? 0 : L.xi[0]);
+                const double *px1 = a.sh + ((a.diag & 8) ? 0 : L.xi[1]);
+                asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(L.rh) : "v"(pr) : "memory");
+                asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(L.ev[0]) : "v"(px0) : "memory");
+                asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(L.ev[1]) : "v"(px1) : "memory");
+            };
+            int4 dl = descc(J0 + IA);  // descriptor of packet j+IA, read one step ahead
+            auto step = [&](int j, PkLd &Li, PkLd &Lg, PkLd &Ll) {
+                if (a.diag & 16) {  // timing experiment: loader idle
+                    lds_barrier();
+                    return;
+                }
+                if (a.trace) m0 = __builtin_amdgcn_s_memtime();
+                issue_idx(dl, Li);
+                gather(Lg);
+                dl = descc(j + IA + 1);
+                uint64_t l0 = 0;
+                if (a.trace) {
+                    l0 = __builtin_amdgcn_s_memtime();
+                    acc_is += l0 - m0;
+                }
+                // gathers of packet j+1 were issued at step j+1-KE
+                asm volatile("s_waitcnt vmcnt(%3)" : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]) : "n"(6 * (KE - 1)) : "memory");
+                uint64_t l2 = 0;
+                if (a.trace) {
+                    l2 = __builtin_amdgcn_s_memtime();
+                    acc_w += l2 - l0;
+                }
+                if (tid == NR) mark(j, 2);
+                // land packet j+1 (nr = nx = 0 outside the block's packets)
+                if (t < Ll.nr) rbuf[(j + 1) & 1][t] = Ll.rh;
+#pragma unroll
+                for (int e = 0; e < PK3_EXT; e++) {
+                    const int k = t + NR * e;
+                    if (k < Ll.nx) {
+                        uint64_t bits = Ll.ev[e];
+                        if (bits == TRI_SENTINEL && !(a.diag & 8)) {
+                            bits = poll_ready(a.sh + Ll.xi[e], a.err);
+                            if (a.trace) atomicAdd(&s_polls, 1u);
+                        }
+                        xbuf[(j + 1) & 1][k] = __longlong_as_double((long long)bits);
+                    }
+                }
+                uint64_t l1 = 0;
+                if (a.trace) {
+                    l1 = __builtin_amdgcn_s_memtime();
+                    acc_ld += l1 - l2;
+                }
+                if (tid == NR) {
+                    mark(j, 1);
+                    if (tr2 && j >= -8 && j < 1016) a.trace2[((long)(b - a.tb0) * 1024 + (j + 8)) * 4 + 3] = s_polls;
+                }
+                lds_barrier();
+                if (a.trace) acc_lb += __builtin_amdgcn_s_memtime() - l1;
+            };
+            PkLd L0, L1, L2, L3;
+            L0.nr = L1.nr = L2.nr = L3.nr = 0;
+            L0.nx = L1.nx = L2.nx = L3.nx = 0;
+            L0.row = L1.row = L2.row = L3.row = 0;
+#pragma unroll
+            for (int e = 0; e < PK3_EXT; e++) L0.xi[e] = L1.xi[e] = L2.xi[e] = L3.xi[e] = 0;
+            L0.rh = L1.rh = L2.rh = L3.rh = 0;
+#define LSSP_PK6_LSTEP(u)                                                                          \
+    step(j0 + u, sel4<(u + IA) % Q>(L0, L1, L2, L3), sel4<(u + KE) % Q>(L0, L1, L2, L3), \
+         sel4<(u + 1) % Q>(L0, L1, L2, L3))
+            for (int j0 = J0; j0 < J0 + T; j0 += Q) {  // packet p in set p mod Q
+                LSSP_PK6_LSTEP(0);
+                LSSP_PK6_LSTEP(1);
+                LSSP_PK6_LSTEP(2);
+                LSSP_PK6_LSTEP(3);
+            }
+#undef LSSP_PK6_LSTEP
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            (void)acc_lb;
+            if (a.trace && tid == NR) {  // compute's barrier share is dropped here
+                a.trace[8 * b + 5] = acc_w;
+                a.trace[8 * b + 6] = acc_is;
+                a.trace[8 * b + 7] = acc_ld;
+            }
+        } else {
+            // store wave: at step j write packet j-1's values in natural order
+            // (the last step's packet after the loop)
+            const int lane = tid & 63;
+            auto store = [&](int p) {
+                if (NAT && p >= 0 && p < np) {
+                    const int4 d = desc(p);
+                    const int nr = d.z & 0x3ff;
+                    for (int k = lane; k < nr; k += 64)
+                        a.nat[rowbuf[p & 1][k]] = ring[(d.w + k - bbase) % BP_RING];
+                }
+            };
+            for (int j = J0; j < J0 + T; j++) {
+                store(j - 1);
+                lds_barrier();
+            }
+            store(J0 + T - 1);
+        }
+    }
+}
+
+// diagnostics only (LSSP_AMD_TRI_TRACE): synchronous dump of the per-block
+// trace of one packet sweep, one JSON line (tools/tri_trace.py)
+static int dump_trace(lssp_amd_ctx *c, unsigned long long *d_trace, int nb, int n, int npk, int grid,
+                      const char *path, int width = 8)
+{
+    std::vector<unsigned long long> h(width * (size_t)nb);
+    LSSP_HIP(hipMemcpyAsync(h.data(), d_trace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost,
+                            c->stream));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    (void)hipFree(d_trace);
+    FILE *f = fopen(path, "a");
+    if (!f) return LSSP_AMD_OK;
+    fprintf(f, "{\"n\": %d, \"nb\": %d, \"npk\": %d, \"grid\": %d, \"blocks\": [", n, nb, npk, grid);
+    for (int b = 0; b < nb; b++) {
+        fprintf(f, "%s[", b ? ", " : "");
+        for (int k = 0; k < width; k++) fprintf(f, "%s%llu", k ? ", " : "", h[(size_t)width * b + k]);
+        fprintf(f, "]");
+    }
+    fprintf(f, "]}\n");
+    fclose(f);
+    return LSSP_AMD_OK;
+}
+
+int launch_trisolve(lssp_amd_ctx *c, const TriSched &t, const double *rhs, double *x, double *reset)
+{
+    if (t.n == 0) return LSSP_AMD_OK;
+    long nchunks = (t.n + 63) / 64;
+    TriArgs a{t.n, nchunks, t.perm, t.rp, t.cols, t.vals, t.diag, t.unit, rhs, x, reset, c->d_err};
+    if (c->tri_mode == 4 && t.pk_n >= 0) {
+        const int grid = std::min(t.bp_nb, c->num_cus);
+        PkArgs g{t.bp_nb, t.pk_blk, t.pk_off, reinterpret_cast<const int4 *>(t.pk_data), t.unit, rhs, x, reset,
+                 t.pk_claim, t.pk_base, c->d_err, c->tri_diag};
+        k_tri_pk<<<grid, 256, 0, c->stream>>>(g);
+        t.pk_base += (unsigned long long)t.bp_nb + grid;
+        LSSP_HIP(hipGetLastError());
+        return LSSP_AMD_OK;
+    }
+    if (c->tri_mode == 1) {
+        for (int l = 0; l < t.nlevels; l++) {
+            const int lo = t.level_ptr[l], hi = t.level_ptr[l + 1];
+            k_trisolve_level<<<(hi - lo + 255) / 256, 256, 0, c->stream>>>(a, lo, hi);
+        }
+    } else {
+        long grid = (long)c->num_cus * c->tri_blocks_per_cu;
+        long need = (nchunks + 3) / 4;
+        if (grid > need) grid = need;
+        if (c->tri_mode == 2) k_trisolve<0><<<grid, 256, 0, c->stream>>>(a);
+        else k_trisolve<1><<<grid, 256, 0, c->stream>>>(a);
+    }
+    LSSP_HIP(hipGetLastError());
+    return LSSP_AMD_OK;
+}
+
+// tri_mode 9 apply: cache = L^-1 rhs, x = U^-1 cache through the shadows
+template <bool NAT>
+static int launch_pk6(lssp_amd_ctx *c, const TriSched &t, const double *rhs, double *sh, double *sh_next,
+                      double *nat)
+{
+    const int grid = std::min(t.bp_nb, c->num_cus);
+    const char *trace_path = getenv("LSSP_AMD_TRI_TRACE");
+    unsigned long long *d_trace = nullptr;
+    if (trace_path) {
+        LSSP_HIP(hipMalloc(&d_trace, sizeof(unsigned long long) * 8 * t.bp_nb));
+        LSSP_HIP(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * 8 * t.bp_nb, c->stream));
+    }
+    const char *t2 = getenv("LSSP_AMD_TRI_TRACE2");  // "path:block"
+    unsigned long long *d_t2 = nullptr;
+    int tb0 = 0;
+    if (t2) {
+        const char *colon = strrchr(t2, ':');
+        tb0 = colon ? atoi(colon + 1) : t.bp_nb / 2;
+        LSSP_HIP(hipMalloc(&d_t2, sizeof(unsigned long long) * 2 * 1024 * 4));
+        LSSP_HIP(hipMemsetAsync(d_t2, 0, sizeof(unsigned long long) * 2 * 1024 * 4, c->stream));
+    }
+    Pk6Args g{t.bp_nb, t.pk6_blk, reinterpret_cast<const int4 *>(t.pk6_desc), t.pk6_rec, t.pk6_idx, rhs, sh,
+              sh_next, nat, t.n, t.bp_B, t.pk6_claim, t.pk6_base, c->d_err, c->tri_diag, d_trace, d_t2, tb0};
+    // Instantiated: 256-row packets, x operands gathered 2 steps ahead (KE 2),
+    // EP 4 or 8 -- the variants whose inline-asm loader tools/check_vmcnt.py
+    // (tests/test_isa_vmcnt.py) verifies hazard-free
+    if (t.pk6_rows != 256) return LSSP_AMD_EUNSUPPORTED;
+    // pipeline depths (LSSP_AMD_TRI_PIPE): 0 = (KE 2, IA 4, D 3), 1 = (2, 3, 3), 2 = (2, 3, 2)
+    const int pd = c->tri_pipe;
+    if constexpr (NAT) {
+        if (t.pk6_ep != 4) return LSSP_AMD_EUNSUPPORTED;
+        k_tri_pk6<4, 2, 4, 3, true, 256><<<grid, 2 * 256 + 64, 0, c->stream>>>(g);
+    } else if (t.pk6_ep == 4) {
+        if (pd == 1) k_tri_pk6<4, 2, 3, 3, false, 256><<<grid, 512, 0, c->stream>>>(g);
+        else if (pd == 2) k_tri_pk6<4, 2, 3, 2, false, 256><<<grid, 512, 0, c->stream>>>(g);
+        else k_tri_pk6<4, 2, 4, 3, false, 256><<<grid, 512, 0, c->stream>>>(g);
+    } else {
+        k_tri_pk6<8, 2, 4, 3, false, 256><<<grid, 512, 0, c->stream>>>(g);
+    }
+    t.pk6_base += (unsigned long long)t.bp_nb + grid;
+    LSSP_HIP(hipGetLastError());
+    if (trace_path) LSSP_TRY(dump_trace(c, d_trace, t.bp_nb, t.n, t.pk6_n, grid, trace_path));
+    if (t2) {  // diagnostics only: per-step clocks of two consecutive blocks
+        std::vector<unsigned long long> h(2 * 1024 * 4);
+        LSSP_HIP(hipMemcpyAsync(h.data(), d_t2, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost,
+                                c->stream));
+        LSSP_HIP(hipStreamSynchronize(c->stream));
+        (void)hipFree(d_t2);
+        std::string path(t2, strrchr(t2, ':') ? strrchr(t2, ':') - t2 : strlen(t2));
+        FILE *f = fopen(path.c_str(), "a");
+        if (f) {
+            fprintf(f, "{\"tb0\": %d, \"steps\": [", tb0);
+            for (size_t i = 0; i < h.size(); i++) fprintf(f, "%s%llu", i ? ", " : "", h[i]);
+            fprintf(f, "]}\n");
+            fclose(f);
+        }
+    }
+    return LSSP_AMD_OK;
+}
+
+// permutations between natural order and a sweep's schedule order (positions).
+// XCD-aware: workgroup w runs on XCD w % 8 (round-robin dispatch) and walks
+// the XCD's contiguous eighth of the positions, so the natural-order lines a
+// position range touches (the same few z-planes for a stencil) are reused
+// inside one XCD's L2 instead of being fetched once per XCD.
+template <bool GATHER>
+__global__ __launch_bounds__(256) void k_perm(double *dst, const double *src, const int *perm, int n)
+{
+    const int nx = 8, per = gridDim.x / nx;
+    const int xcd = blockIdx.x % nx, k = blockIdx.x / nx;
+    const long chunk = ((long)n + nx - 1) / nx;
+    const long lo = xcd * chunk, hi = min((long)n, lo + chunk);
+    for (long p = lo + (long)k * 256 + threadIdx.x; p < hi; p += (long)per * 256) {
+        if (GATHER) dst[p] = src[perm[p]];
+        else dst[perm[p]] = src[p];
+    }
+}
+
+// tri_mode 9 apply.  The scattered halves of the work -- reading the rhs in L
+// order and writing x in natural order -- run as fully parallel permutation
+// kernels around the two sweeps, so the pipelined sweeps only touch
+// contiguous runs of HBM.  LSSP_AMD_TRI_NAT=1 instead writes x from the U
+// sweep's store wave (timing experiments).
+int launch_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const double *rhs)
+{
+    if (c->tri_mode == 9 && M->lower.pk6_n > 0 && M->upper.pk6_n > 0) {
+        const int n = M->n;
+        if (!M->d_sh[0]) {
+            for (int k = 0; k < 4; k++) {
+                LSSP_HIP(hipMalloc(&M->d_sh[k], sizeof(double) * n));
+                LSSP_TRY(launch_fill(c, M->d_sh[k], n, TRI_SENTINEL));
+            }
+            LSSP_HIP(hipMalloc(&M->d_rperm, sizeof(double) * n));
+        }
+        const int e = M->epoch & 1;
+        M->epoch++;
+        const int pg = 8 * std::max(1, std::min((n + 2047) / 2048, c->num_cus));  // multiple of 8
+        k_perm<true><<<pg, 256, 0, c->stream>>>(M->d_rperm, rhs, M->lower.bp_perm, n);
+        LSSP_HIP(hipGetLastError());
+        LSSP_TRY(launch_pk6<false>(c, M->lower, M->d_rperm, M->d_sh[e], M->d_sh[e ^ 1], nullptr));
+        static const bool nat = getenv("LSSP_AMD_TRI_NAT") && atoi(getenv("LSSP_AMD_TRI_NAT"));
+        if (nat && M->upper.pk6_ep == 4)
+            return launch_pk6<true>(c, M->upper, M->d_sh[e], M->d_sh[2 + e], M->d_sh[2 + (e ^ 1)], x);
+        LSSP_TRY(launch_pk6<false>(c, M->upper, M->d_sh[e], M->d_sh[2 + e], M->d_sh[2 + (e ^ 1)], nullptr));
+        k_perm<false><<<pg, 256, 0, c->stream>>>(x, M->d_sh[2 + e], M->upper.bp_perm, n);
+        LSSP_HIP(hipGetLastError());
+        return LSSP_AMD_OK;
+    }
+    LSSP_TRY(launch_trisolve(c, M->lower, rhs, M->d_cache, x));
+    return launch_trisolve(c, M->upper, M->d_cache, x, M->d_cache);
+}
+
+}  // namespace lssp_amd

@@ -1,5 +1,5 @@
 """The packet sweep's loader issues its loads from inline asm with explicit
-vmcnt waits (kernels.hip k_tri_pk6).  Compile the device code for gfx950 and
+vmcnt waits (trisolve.hip k_tri_pk6).  Compile the device code for gfx950 and
 check, on the generated assembly, that no instruction touches a VGPR that is
 still the destination of an outstanding load, and that no instantiation spills
 (a spill of an in-flight register would store garbage).  CPU-only: hipcc
@@ -25,7 +25,7 @@ def device_asm(tmp_path_factory):
     out = tmp_path_factory.mktemp("isa") / "kernels.s"
     cmd = [HIPCC, "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950",
            "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-S", "-x", "hip",
-           os.path.join(ROOT, "lssp_amd", "csrc", "kernels.hip"), "-o", str(out)]
+           os.path.join(ROOT, "lssp_amd", "csrc", "trisolve.hip"), "-o", str(out)]
     subprocess.run(cmd, check=True, capture_output=True)
     return str(out)
 
