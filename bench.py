@@ -124,6 +124,9 @@ def main():
     ap.add_argument("--apply-reps", type=int, default=10)
     ap.add_argument("--cpu-iters", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal: every rank on device 0, collectives over the host-staged gloo transport "
+                         "(RCCL refuses two ranks on one GPU); not a scaling measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -133,11 +136,15 @@ def main():
     import torch.distributed as dist
     if world > 1:
         dist.init_process_group("gloo")  # control plane only; the data path is RCCL in the library
-    torch.cuda.set_device(local_rank)
+    gpu = 0 if args.share_gpu else local_rank
+    torch.cuda.set_device(gpu)
 
     import lssp_amd
-    dev = lssp_amd.Device(local_rank)
-    if world > 1:
+    dev = lssp_amd.Device(gpu)
+    if world > 1 and args.share_gpu:
+        from lssp_amd.dist import GlooTransport
+        dev.comm_init_host(world, rank, GlooTransport())
+    elif world > 1:
         uid = [lssp_amd.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         dev.comm_init(world, rank, uid[0])
@@ -233,7 +240,9 @@ def main():
             "config": {"workload": f"7-pt Poisson {N}^3 (n={n}, nnz={int(7 * N ** 3 - 6 * N ** 2)}), "
                                    f"BiCGSTAB + ILUK(0){' block-Jacobi per rank' if world > 1 else ''}, "
                                    "b=1, x0=0, fp64 CSR int32",
-                       "rows": n, "partition": f"{world} z-slab row blocks", "reduction": "tree"},
+                       "rows": n, "partition": f"{world} z-slab row blocks", "reduction": "tree",
+                       "transport": ("host-staged gloo, all ranks on GPU 0 (rehearsal, not a scaling number)"
+                                     if args.share_gpu and world > 1 else "rccl" if world > 1 else "none")},
             "spmv": {"gbps": round(spmv_gbs_total, 1), "frac_hbm_peak": round(spmv_gbs / HBM_PEAK_GBS, 4),
                      "ms_per_call": round(spmv_ms, 5)},
             "roofline": {"bound": "hbm", "achieved": round(apply_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -154,6 +154,25 @@ int lssp_amd_comm_unique_id_size(void);
 int lssp_amd_comm_get_unique_id(void *id_out);
 int lssp_amd_comm_init(lssp_amd_ctx *ctx, int nranks, int rank, const void *id);
 int lssp_amd_comm_barrier(lssp_amd_ctx *ctx);
+
+/* Host-staged transport: the same protocol with the collective carried by the
+ * caller (an MPI library, a torch.distributed gloo group, ...) instead of
+ * RCCL.  The library copies the bytes to host memory, calls the hook and
+ * copies the result back; used where RCCL is unavailable and to exercise the
+ * multi-rank path with several ranks on ONE device (RCCL refuses that).
+ * Every hook returns 0 on success; buffers are host memory. */
+typedef struct {
+    void *user;
+    /* recv[q*bytes .. (q+1)*bytes) = rank q's send, for q = 0 .. nranks-1 */
+    int (*allgather)(void *user, const void *send, void *recv, long bytes);
+    /* one grouped round: nsend messages to peers send_peer[i], nrecv from
+     * recv_peer[i]; a rank sends at most one message to each peer per round */
+    int (*sendrecv)(void *user, int nsend, const int *send_peer, const void *const *send_buf,
+                    const long *send_bytes, int nrecv, const int *recv_peer, void *const *recv_buf,
+                    const long *recv_bytes);
+} lssp_amd_host_transport;
+int lssp_amd_comm_init_host(lssp_amd_ctx *ctx, int nranks, int rank, const lssp_amd_host_transport *t);
+
 /* rows [row0, row0 + nlocal) of a global n x n CSR given by its local rows */
 int lssp_amd_mat_upload_dist(lssp_amd_ctx *ctx, int n_global, int row0, int nlocal,
                              const int *Ap, const int *Aj, const double *Ax, lssp_amd_mat **A);

@@ -16,6 +16,16 @@ _vp, _ci, _cd, _cl = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_lo
 _pvp = ctypes.POINTER(ctypes.c_void_p)
 
 
+ALLGATHER_FN = ctypes.CFUNCTYPE(_ci, _vp, _vp, _vp, _cl)
+SENDRECV_FN = ctypes.CFUNCTYPE(_ci, _vp, _ci, ctypes.POINTER(_ci), ctypes.POINTER(_vp), ctypes.POINTER(_cl),
+                               _ci, ctypes.POINTER(_ci), ctypes.POINTER(_vp), ctypes.POINTER(_cl))
+
+
+class HostTransport(ctypes.Structure):
+    """lssp_amd_host_transport (include/lssp_amd.h)"""
+    _fields_ = [("user", _vp), ("allgather", ALLGATHER_FN), ("sendrecv", SENDRECV_FN)]
+
+
 class SolveParams(ctypes.Structure):
     _fields_ = [("solver", _ci), ("tol_rel", _cd), ("tol_abs", _cd), ("tol_rb", _cd),
                 ("maxit", _ci), ("restart", _ci), ("verb", _ci)]
@@ -62,6 +72,7 @@ SIGNATURES = {
     "lssp_amd_comm_get_unique_id": (_ci, [_vp]),
     "lssp_amd_comm_init": (_ci, [_vp, _ci, _ci, _vp]),
     "lssp_amd_comm_barrier": (_ci, [_vp]),
+    "lssp_amd_comm_init_host": (_ci, [_vp, _ci, _ci, _vp]),
     "lssp_amd_mat_upload_dist": (_ci, [_vp, _ci, _ci, _ci, _vp, _vp, _vp, _pvp]),
     "lssp_amd_mat_local_rows": (_ci, [_vp, _vp, _vp, _vp]),
     "lssp_amd_poisson_nnz": (_cl, [_ci, _ci]),

@@ -1,4 +1,5 @@
-// comm.cpp -- multi-GPU layer: one process per GPU, RCCL over xGMI.
+// comm.cpp -- multi-GPU layer: one process per GPU, RCCL over xGMI (or the
+// caller's host-staged transport, lssp_amd_comm_init_host).
 //
 // The reference is serial (README.md:3); this is the SURVEY 8(e) extension of
 // the hot path.  Rows are partitioned in contiguous blocks of ceil(n/P) (the
@@ -31,11 +32,77 @@ namespace lssp_amd {
         }                                                                                          \
     } while (0)
 
+// ---- transport: RCCL, or the caller's host-staged hooks --------------------
+struct Msg {
+    int peer;
+    void *dbuf;  // device buffer
+    long bytes;
+};
+
+static bool host_mode(const lssp_amd_ctx *c) { return c->comm == nullptr && c->host.allgather != nullptr; }
+
+// recv (device, nranks * bytes) = every rank's send (device, bytes), rank order
+static int xfer_allgather(lssp_amd_ctx *c, const void *dsend, void *drecv, long bytes)
+{
+    if (!host_mode(c)) {
+        LSSP_NCCL(ncclAllGather(dsend, drecv, (size_t)bytes, ncclInt8, (ncclComm_t)c->comm, c->stream));
+        return LSSP_AMD_OK;
+    }
+    std::vector<char> hs(std::max<long>(bytes, 1)), hr(std::max<long>(bytes * c->nranks, 1));
+    if (bytes) LSSP_HIP(hipMemcpyAsync(hs.data(), dsend, bytes, hipMemcpyDeviceToHost, c->stream));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    if (c->host.allgather(c->host.user, hs.data(), hr.data(), bytes) != 0) return LSSP_AMD_ECOMM;
+    if (bytes) LSSP_HIP(hipMemcpyAsync(drecv, hr.data(), bytes * c->nranks, hipMemcpyHostToDevice, c->stream));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    return LSSP_AMD_OK;
+}
+
+// one grouped point-to-point round
+static int xfer_group(lssp_amd_ctx *c, const std::vector<Msg> &sends, const std::vector<Msg> &recvs)
+{
+    if (!host_mode(c)) {
+        LSSP_NCCL(ncclGroupStart());
+        for (const Msg &m : sends)
+            LSSP_NCCL(ncclSend(m.dbuf, (size_t)m.bytes, ncclInt8, m.peer, (ncclComm_t)c->comm, c->stream));
+        for (const Msg &m : recvs)
+            LSSP_NCCL(ncclRecv(m.dbuf, (size_t)m.bytes, ncclInt8, m.peer, (ncclComm_t)c->comm, c->stream));
+        LSSP_NCCL(ncclGroupEnd());
+        return LSSP_AMD_OK;
+    }
+    const int ns = (int)sends.size(), nr = (int)recvs.size();
+    std::vector<std::vector<char>> hs(ns), hr(nr);
+    std::vector<int> sp(ns), rp(nr);
+    std::vector<const void *> sb(ns);
+    std::vector<void *> rb(nr);
+    std::vector<long> sl(ns), rl(nr);
+    for (int i = 0; i < ns; i++) {
+        hs[i].resize(std::max<long>(sends[i].bytes, 1));
+        if (sends[i].bytes)
+            LSSP_HIP(hipMemcpyAsync(hs[i].data(), sends[i].dbuf, sends[i].bytes, hipMemcpyDeviceToHost, c->stream));
+        sp[i] = sends[i].peer;
+        sb[i] = hs[i].data();
+        sl[i] = sends[i].bytes;
+    }
+    for (int i = 0; i < nr; i++) {
+        hr[i].resize(std::max<long>(recvs[i].bytes, 1));
+        rp[i] = recvs[i].peer;
+        rb[i] = hr[i].data();
+        rl[i] = recvs[i].bytes;
+    }
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    if (c->host.sendrecv(c->host.user, ns, sp.data(), sb.data(), sl.data(), nr, rp.data(), rb.data(), rl.data()) != 0)
+        return LSSP_AMD_ECOMM;
+    for (int i = 0; i < nr; i++)
+        if (recvs[i].bytes)
+            LSSP_HIP(hipMemcpyAsync(recvs[i].dbuf, hr[i].data(), recvs[i].bytes, hipMemcpyHostToDevice, c->stream));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    return LSSP_AMD_OK;
+}
+
 int comm_allgather_sums(lssp_amd_ctx *c, int nslot)
 {
     (void)nslot;
-    LSSP_NCCL(ncclAllGather(c->d_sums, c->d_gather, MAX_SLOTS, ncclDouble, (ncclComm_t)c->comm, c->stream));
-    return LSSP_AMD_OK;
+    return xfer_allgather(c, c->d_sums, c->d_gather, (long)sizeof(double) * MAX_SLOTS);
 }
 
 int halo_exchange(const lssp_amd_mat *A, double *x)
@@ -44,15 +111,12 @@ int halo_exchange(const lssp_amd_mat *A, double *x)
     if (A->send_peer.empty() && A->recv_peer.empty()) return LSSP_AMD_OK;
     lssp_amd_ctx *c = A->ctx;
     LSSP_TRY(launch_pack(c, A->d_send_idx, x, A->d_send_buf, A->nsend));
-    LSSP_NCCL(ncclGroupStart());
+    std::vector<Msg> s, r;
     for (size_t q = 0; q < A->send_peer.size(); q++)
-        LSSP_NCCL(ncclSend(A->d_send_buf + A->send_off[q], A->send_cnt[q], ncclDouble, A->send_peer[q],
-                           (ncclComm_t)c->comm, c->stream));
+        s.push_back({A->send_peer[q], A->d_send_buf + A->send_off[q], (long)sizeof(double) * A->send_cnt[q]});
     for (size_t q = 0; q < A->recv_peer.size(); q++)
-        LSSP_NCCL(ncclRecv(x + A->nrows + A->recv_off[q], A->recv_cnt[q], ncclDouble, A->recv_peer[q],
-                           (ncclComm_t)c->comm, c->stream));
-    LSSP_NCCL(ncclGroupEnd());
-    return LSSP_AMD_OK;
+        r.push_back({A->recv_peer[q], x + A->nrows + A->recv_off[q], (long)sizeof(double) * A->recv_cnt[q]});
+    return xfer_group(c, s, r);
 }
 
 int comm_destroy(lssp_amd_ctx *c)
@@ -65,6 +129,7 @@ int comm_destroy(lssp_amd_ctx *c)
         (void)hipFree(c->d_gather);
         c->d_gather = nullptr;
     }
+    c->host = lssp_amd_host_transport{};
     c->nranks = 1;
     c->rank = 0;
     return LSSP_AMD_OK;
@@ -104,16 +169,26 @@ int lssp_amd_comm_init(lssp_amd_ctx *c, int nranks, int rank, const void *idp)
     return LSSP_AMD_OK;
 }
 
+int lssp_amd_comm_init_host(lssp_amd_ctx *c, int nranks, int rank, const lssp_amd_host_transport *t)
+{
+    if (!c || nranks < 1 || rank < 0 || rank >= nranks) return LSSP_AMD_EINVAL;
+    if (nranks > 1 && (!t || !t->allgather || !t->sendrecv)) return LSSP_AMD_EINVAL;
+    LSSP_HIP(hipSetDevice(c->device));
+    comm_destroy(c);
+    if (nranks == 1) return LSSP_AMD_OK;
+    c->host = *t;
+    c->nranks = nranks;
+    c->rank = rank;
+    LSSP_HIP(hipMalloc(&c->d_gather, sizeof(double) * MAX_SLOTS * nranks));
+    return LSSP_AMD_OK;
+}
+
 int lssp_amd_comm_barrier(lssp_amd_ctx *c)
 {
     if (!c) return LSSP_AMD_EINVAL;
     if (c->nranks > 1) {
-        LSSP_NCCL(ncclAllReduce(c->d_sums, c->d_sums, 0, ncclDouble, ncclSum, (ncclComm_t)c->comm, c->stream));
-        double *tmp;
-        LSSP_HIP(hipMalloc(&tmp, sizeof(double)));
-        LSSP_NCCL(ncclAllReduce(tmp, tmp, 1, ncclDouble, ncclSum, (ncclComm_t)c->comm, c->stream));
-        LSSP_HIP(hipStreamSynchronize(c->stream));
-        LSSP_HIP(hipFree(tmp));
+        // an all-gather of one double per rank: returns on a rank only once every rank has entered
+        LSSP_TRY(xfer_allgather(c, c->d_sums, c->d_gather, (long)sizeof(double)));
     }
     LSSP_HIP(hipStreamSynchronize(c->stream));
     return LSSP_AMD_OK;
@@ -172,7 +247,7 @@ int lssp_amd_mat_upload_dist(lssp_amd_ctx *c, int n_global, int row0, int nlocal
     LSSP_HIP(hipMalloc(&d_cnt_mine, sizeof(int) * P));
     LSSP_HIP(hipMalloc(&d_cnt_all, sizeof(int) * P * P));
     LSSP_HIP(hipMemcpy(d_cnt_mine, need.data(), sizeof(int) * P, hipMemcpyHostToDevice));
-    LSSP_NCCL(ncclAllGather(d_cnt_mine, d_cnt_all, P, ncclInt32, (ncclComm_t)c->comm, c->stream));
+    LSSP_TRY(xfer_allgather(c, d_cnt_mine, d_cnt_all, (long)sizeof(int) * P));
     std::vector<int> all(P * P);
     LSSP_HIP(hipMemcpyAsync(all.data(), d_cnt_all, sizeof(int) * P * P, hipMemcpyDeviceToHost, c->stream));
     LSSP_HIP(hipStreamSynchronize(c->stream));
@@ -192,14 +267,14 @@ int lssp_amd_mat_upload_dist(lssp_amd_ctx *c, int n_global, int row0, int nlocal
     LSSP_HIP(hipMalloc(&d_sendg, sizeof(int) * std::max(nsend, 1)));
     if (!hcols.empty())
         LSSP_HIP(hipMemcpy(d_hcols, hcols.data(), sizeof(int) * hcols.size(), hipMemcpyHostToDevice));
-    LSSP_NCCL(ncclGroupStart());
-    for (size_t q = 0; q < M->recv_peer.size(); q++)
-        LSSP_NCCL(ncclSend(d_hcols + M->recv_off[q], M->recv_cnt[q], ncclInt32, M->recv_peer[q],
-                           (ncclComm_t)c->comm, c->stream));
-    for (size_t q = 0; q < M->send_peer.size(); q++)
-        LSSP_NCCL(ncclRecv(d_sendg + M->send_off[q], M->send_cnt[q], ncclInt32, M->send_peer[q],
-                           (ncclComm_t)c->comm, c->stream));
-    LSSP_NCCL(ncclGroupEnd());
+    {
+        std::vector<Msg> s, r;  // my halo columns to their owners; the columns peers need from me
+        for (size_t q = 0; q < M->recv_peer.size(); q++)
+            s.push_back({M->recv_peer[q], d_hcols + M->recv_off[q], (long)sizeof(int) * M->recv_cnt[q]});
+        for (size_t q = 0; q < M->send_peer.size(); q++)
+            r.push_back({M->send_peer[q], d_sendg + M->send_off[q], (long)sizeof(int) * M->send_cnt[q]});
+        LSSP_TRY(xfer_group(c, s, r));
+    }
     std::vector<int> sendg(nsend);
     if (nsend)
         LSSP_HIP(hipMemcpyAsync(sendg.data(), d_sendg, sizeof(int) * nsend, hipMemcpyDeviceToHost, c->stream));

@@ -71,6 +71,7 @@ struct lssp_amd_ctx {
     // multi-GPU (RCCL)
     int nranks = 1, rank = 0;
     void *comm = nullptr;      // ncclComm_t
+    lssp_amd_host_transport host{};  // host-staged transport (comm == nullptr, nranks > 1)
     double *d_gather = nullptr;  // [nranks][MAX_SLOTS]
     int tri_blocks_per_cu = 1;
     // 0 sync-free + back-off, 1 one launch per level, 2 sync-free without

@@ -94,6 +94,12 @@ class Device:
         buf = ctypes.create_string_buffer(uid, len(uid))
         _ck(self.L.lssp_amd_comm_init(self.h, nranks, rank, buf), "comm_init")
 
+    def comm_init_host(self, nranks: int, rank: int, transport):
+        """multi-rank protocol over a host-staged transport (e.g. lssp_amd.dist.GlooTransport)"""
+        self._transport = transport  # keeps the ctypes callbacks alive
+        _ck(self.L.lssp_amd_comm_init_host(self.h, nranks, rank, ctypes.byref(transport.struct)),
+            "comm_init_host")
+
     def barrier(self):
         _ck(self.L.lssp_amd_comm_barrier(self.h), "barrier")
 

@@ -1,0 +1,97 @@
+"""The multi-rank path of the library on the GPU, with several ranks on ONE device.
+
+RCCL refuses two ranks on one GPU, so these tests carry the protocol's
+collectives over the host-staged transport (lssp_amd_comm_init_host, hooks
+implemented with torch.distributed gloo in lssp_amd.dist).  Everything else
+is the production multi-GPU code: lssp_amd_mat_upload_dist's halo plan (built
+through the transport), the pack kernel and halo placement before every SpMV,
+rank-local canonical tree partials summed in rank order (k_sum_ranks), and
+block-Jacobi ILU(0) per rank (pc-iluk.cxx:411-552 with blk = ceil(n/P)).
+Results must equal, bit for bit, the oracle's single-process P-rank mode --
+the same check tests/test_dist_cpu.py pins on the CPU.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, N, maxit, seed, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import lssp_amd
+        from bench import local_block
+        from inputs import uniform
+        from lssp_amd.dist import GlooTransport
+        dev = lssp_amd.Device(0)
+        dev.comm_init_host(world, rank, GlooTransport())
+        n = N ** 3
+        blk = (n + world - 1) // world
+        r0 = min(rank * blk, n)
+        nl = min(blk, n - r0)
+        Ap, Aj, Ax = lssp_amd.poisson(3, N, r0, nl)
+        A = lssp_amd.DMat(dev, Ap, Aj, Ax, dist=(n, r0))
+        bp, bj, bx = local_block(Ap, Aj, Ax, r0, nl)
+        M = lssp_amd.DILU.create(dev, bp, bj, bx, kind=lssp_amd.ILUK, level=0)
+        # SpMV with a halo: y = A x for a seeded global x
+        xg = uniform(seed, n)
+        xv = dev.vec(A.nx, np.concatenate([xg[r0:r0 + nl], np.zeros(A.nhalo)]))
+        yv = dev.vec(A.nx)
+        A.mv_mxy(xv, yv)
+        y = yv.download(nl)
+        # BiCGSTAB + block-Jacobi ILU(0), b = 1, x0 = 0, tree reductions
+        x = dev.vec(A.nx, np.zeros(A.nx))
+        b = dev.vec(A.nx, np.ones(A.nx))
+        r = lssp_amd.solve(dev, A, M, x, b, solver=lssp_amd.BICGSTAB, maxit=maxit, trace_cap=100000)
+        xl = x.download(nl)
+        dev.barrier()
+        parts = [None] * world
+        dist.all_gather_object(parts, (y, xl))
+        if rank == 0:
+            out.put((r.nits, r.residual, r.trace, np.concatenate([p[0] for p in parts]),
+                     np.concatenate([p[1] for p in parts])))
+        dev.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N", [(2, 12), (3, 10), (4, 16)])
+def test_multirank_on_one_gpu_equals_oracle_prank_mode(world, N):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, 500, 0x5EED, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        nits, res, trace, y, x = q.get(timeout=100)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+    assert all(p.exitcode == 0 for p in procs)
+    from inputs import uniform
+    A = O.poisson(3, N)
+    assert np.array_equal(y, O.spmv(0, A, uniform(0x5EED, A.n)))
+    Lg, Ug = O.ilu(A, "iluk", level=0, blk=(A.n + world - 1) // world)
+    o = O.solve(O.BICGSTAB, A, np.ones(A.n), L=Lg, U=Ug, mode=O.TREE, nranks=world, maxit=500)
+    assert nits == o.nits
+    assert res == o.residual
+    assert np.array_equal(trace, o.trace)
+    assert np.array_equal(x, o.x)
