@@ -1,0 +1,114 @@
+// amd_backend.cxx -- the reference-side binding: route LSSP's Krylov hot path
+// (BiCGSTAB / GMRES(m) / CG with PC_NON, ILUK or ILUT) to lssp_amd on MI355X.
+//
+// This is the translation unit a maintainer adds to huiscliu/lssp (as
+// src/amd-backend.cxx); INTEGRATION.md describes it.  It compiles against the
+// reference's own headers and replaces, at link time, the three drivers that
+// lssp_solver_solve dispatches to (lssp.cxx:259-289):
+//
+//     -Wl,--wrap=<mangled lssp_solver_bicgstab / _gmres / _cg>
+//
+// so lssp.cxx, the drivers and every caller (example/exam.cxx) stay unchanged.
+// Everything else (assemble, the column sort, the ILU setup of pc-iluk.cxx /
+// pc-ilut.cxx, other solvers and preconditioners) is the reference's own code.
+//
+// Per solve: A (the sorted copy lssp_solver_assemble made, lssp.cxx:166-173)
+// and the factors pc.L / pc.U the reference built are uploaded, x0 and b too;
+// the whole iteration runs in HBM (lssp_amd_solve); x is downloaded into the
+// caller's view s.x.d (lssp.cxx:175-176) and s.residual / s.nits are set as the
+// drivers set them (solver-bicgstab.cxx:156-157, :174).  A non-zero lssp_amd
+// status becomes lssp_error(1, ...) -> exit(1), the reference's fatal path
+// (utils.cxx:114-135).  LSSP_AMD_REDUCE=serial selects the reference's
+// sequential dot order (bitwise-identical runs).
+#include "lssp.h"
+#include "lssp_amd.h"
+
+// the linker's --wrap names are the mangled symbols with a prefix: declare them unmangled
+extern "C" {
+int __real__Z20lssp_solver_bicgstabR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
+int __real__Z17lssp_solver_gmresR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
+int __real__Z14lssp_solver_cgR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
+int __wrap__Z20lssp_solver_bicgstabR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
+int __wrap__Z17lssp_solver_gmresR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
+int __wrap__Z14lssp_solver_cgR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
+}
+
+static lssp_amd_ctx *amd_ctx()
+{
+    static lssp_amd_ctx *c = NULL;
+    if (c == NULL) {
+        const char *d = getenv("LSSP_AMD_DEVICE");
+        int st = lssp_amd_ctx_create(d ? atoi(d) : 0, &c);
+        if (st != LSSP_AMD_OK) lssp_error(1, "amd: cannot open the device: %s\n", lssp_amd_strerror(st));
+    }
+    return c;
+}
+
+#define AMD_CK(call)                                                                    \
+    do {                                                                                \
+        int st_ = (call);                                                               \
+        if (st_ != LSSP_AMD_OK) lssp_error(1, "amd: %s: %s\n", #call, lssp_amd_strerror(st_)); \
+    } while (0)
+
+static bool amd_handles(const LSSP_PC &pc)
+{
+    return pc.type == LSSP_PC_NON || pc.type == LSSP_PC_ILUK || pc.type == LSSP_PC_ILUT;
+}
+
+static int amd_solve(LSSP_SOLVER &s, LSSP_PC &pc, int solver)
+{
+    lssp_amd_ctx *c = amd_ctx();
+    const int n = s.A.num_rows;
+    lssp_amd_mat *A = NULL;
+    lssp_amd_ilu *M = NULL;
+    double *x = NULL, *b = NULL;
+
+    AMD_CK(lssp_amd_mat_upload(c, n, s.A.num_cols, s.A.num_nnzs, s.A.Ap, s.A.Aj, s.A.Ax, &A));
+    if (pc.type != LSSP_PC_NON)
+        AMD_CK(lssp_amd_ilu_from_factors(c, n, pc.L.Ap, pc.L.Aj, pc.L.Ax, pc.U.Ap, pc.U.Aj, pc.U.Ax, &M));
+    AMD_CK(lssp_amd_vec_alloc(c, n, &x));
+    AMD_CK(lssp_amd_vec_alloc(c, n, &b));
+    AMD_CK(lssp_amd_vec_upload(c, x, s.x.d, n));
+    AMD_CK(lssp_amd_vec_upload(c, b, s.rhs.d, n));
+
+    lssp_amd_solve_params p;
+    p.solver = solver;
+    p.tol_rel = s.tol_rel;
+    p.tol_abs = s.tol_abs;
+    p.tol_rb = s.tol_rb;
+    p.maxit = s.maxit;
+    p.restart = s.restart;
+    p.verb = s.verb;
+    int nits = 0;
+    double res = 0.;
+    fflush(stdout);  // the device driver prints with stdio too: keep the line order
+    AMD_CK(lssp_amd_solve(c, A, M, &p, x, b, &nits, &res, NULL, 0, NULL));
+    fflush(stdout);
+    AMD_CK(lssp_amd_vec_download(c, s.x.d, x, n));
+
+    s.residual = res;
+    s.nits = nits;
+    lssp_amd_vec_free(c, x);
+    lssp_amd_vec_free(c, b);
+    if (M) lssp_amd_ilu_destroy(M);
+    lssp_amd_mat_destroy(A);
+    return nits;
+}
+
+int __wrap__Z20lssp_solver_bicgstabR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &s, LSSP_PC &pc)
+{
+    if (!amd_handles(pc)) return __real__Z20lssp_solver_bicgstabR12LSSP_SOLVER_R8LSSP_PC_(s, pc);
+    return amd_solve(s, pc, LSSP_AMD_BICGSTAB);
+}
+
+int __wrap__Z17lssp_solver_gmresR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &s, LSSP_PC &pc)
+{
+    if (!amd_handles(pc)) return __real__Z17lssp_solver_gmresR12LSSP_SOLVER_R8LSSP_PC_(s, pc);
+    return amd_solve(s, pc, LSSP_AMD_GMRES);
+}
+
+int __wrap__Z14lssp_solver_cgR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &s, LSSP_PC &pc)
+{
+    if (!amd_handles(pc)) return __real__Z14lssp_solver_cgR12LSSP_SOLVER_R8LSSP_PC_(s, pc);
+    return amd_solve(s, pc, LSSP_AMD_CG);
+}

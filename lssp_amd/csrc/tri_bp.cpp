@@ -214,7 +214,7 @@ int build_packets(int n, const std::vector<int> &perm, const std::vector<int> &r
 //   desc  int4 {record offset (16 B units), index offset (4 B units),
 //               nr | nx << 10 | emax << 21, schedule position of the first row}
 //   records (compute lanes), arrays over the packet's rows, 16-byte aligned:
-//     C  codes as int16 pairs: uint2 {c0|c1<<16, c2|c3<<16} (EP 4) or uint4 (EP 8)
+//     C  codes as int16 pairs, EP/2 words per row: uint2 (EP 4) or uint4 chunks (EP 8, 16, 24)
 //        -- -1-slot (value ring), PK4_PAD, or an xidx index
 //     V[EP/2] double2 entry values, D double diagonal, ROW int (natural row)
 //   indices (loader lanes): rhs[nr] (the rhs entry of each row: its L-schedule
@@ -230,8 +230,8 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
     const int ROWS = 256;  // rows per packet = compute lanes (512 measured slower)
     int maxlen = 0;
     for (int p = 0; p < n; p++) maxlen = std::max(maxlen, rp[p + 1] - rp[p]);
-    if (maxlen > 8) return LSSP_AMD_EUNSUPPORTED;
-    const int EP = maxlen <= 4 ? 4 : 8;
+    if (maxlen > 24) return LSSP_AMD_EUNSUPPORTED;  // ILUT(tol, p <= 24), ILU(k) of stencils
+    const int EP = maxlen <= 4 ? 4 : maxlen <= 8 ? 8 : maxlen <= 16 ? 16 : 24;
     std::vector<int> blk(nb + 1, 0);
     std::vector<int> desc;
     std::vector<uint32_t> rec;  // 4-byte words, 16-byte aligned packets
@@ -280,8 +280,8 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
                 uint32_t *ROW = w + wc + wv + wd;
                 for (int r = 0; r < nr; r++) {
                     const int k0 = rp[p + r], len = rp[p + r + 1] - k0;
-                    int c[8];
-                    for (int e = 0; e < 8; e++) c[e] = PK4_PAD;
+                    int c[24];
+                    for (int e = 0; e < 24; e++) c[e] = PK4_PAD;
                     for (int e = 0; e < len; e++) {
                         const int g = cols[k0 + e];
                         c[e] = g < 0 ? g : slot[g];

@@ -345,14 +345,21 @@ typedef unsigned v2u __attribute__((ext_vector_type(2)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 template <int EP>
 struct Pk6Rec {
-    typename std::conditional<EP == 4, v2u, v4u>::type c;  // int16 code pairs
+    // int16 code pairs: EP/2 words, loaded as uint2 (EP 4) or uint4 chunks
+    typedef typename std::conditional<EP == 4, v2u, v4u>::type CW;
+    static constexpr int NCW = EP == 4 ? 1 : EP / 8;
+    CW c[NCW];
     double v[EP];
     double dg;
     int row;
     int nr, pos0;
+    __device__ __forceinline__ int code(int e) const
+    {
+        const unsigned w = EP == 4 ? c[0][e / 2] : c[e / 8][(e / 2) & 3];
+        return (e & 1) ? ((int)w >> 16) : (int)(short)(w & 0xffff);
+    }
 };
 
-__device__ __forceinline__ int code16(int w, int hi) { return hi ? (w >> 16) : (int)(short)(w & 0xffff); }
 
 template <int I, typename T>
 __device__ __forceinline__ T &sel4(T &a, T &b, T &c, T &d)
@@ -441,7 +448,9 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                 const int n1 = nr > 0 ? nr : 1, tt = min(t, n1 - 1);
                 const uint32_t *base = a.rec + 4L * d.x;
                 const int wc = ((EP / 2) * n1 + 3) & ~3, wd = (2 * n1 + 3) & ~3;
-                Rr.c = reinterpret_cast<const decltype(Rr.c) *>(base)[tt];
+#pragma unroll
+                for (int q = 0; q < Pk6Rec<EP>::NCW; q++)
+                    Rr.c[q] = reinterpret_cast<const typename Pk6Rec<EP>::CW *>(base)[Pk6Rec<EP>::NCW * tt + q];
                 typedef double v2d __attribute__((ext_vector_type(2)));
                 const v2d *vb = reinterpret_cast<const v2d *>(base + wc);
 #pragma unroll
@@ -460,11 +469,12 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                 if (a.trace) c0 = __builtin_amdgcn_s_memtime();
                 issue(dn, Rn);
                 dn = descc(j + D + 1);
-                if constexpr (EP == 4)
-                    asm volatile("" ::"v"(Rc.c), "v"(Rc.v[0]), "v"(Rc.v[1]), "v"(Rc.v[2]), "v"(Rc.v[3]), "v"(Rc.dg));
-                else
-                    asm volatile("" ::"v"(Rc.c), "v"(Rc.v[0]), "v"(Rc.v[1]), "v"(Rc.v[2]), "v"(Rc.v[3]), "v"(Rc.v[4]),
-                                 "v"(Rc.v[5]), "v"(Rc.v[6]), "v"(Rc.v[7]), "v"(Rc.dg));
+                // the current record must be complete here, at one fixed point
+#pragma unroll
+                for (int q = 0; q < Pk6Rec<EP>::NCW; q++) asm volatile("" ::"v"(Rc.c[q]));
+#pragma unroll
+                for (int e = 0; e < EP; e++) asm volatile("" ::"v"(Rc.v[e]));
+                asm volatile("" ::"v"(Rc.dg));
                 if (NAT) asm volatile("" ::"v"(Rc.row));
                 if (t < Rc.nr) {  // nr == 0 outside the block's packets
                     const double *xb = xbuf[j & 1];
@@ -473,7 +483,7 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                     // all EP entries: padded ones read +0.0 and subtract +0.0*+0.0
 #pragma unroll
                     for (int e = 0; e < EP; e++) {
-                        const int cd = code16((int)Rc.c[e / 2], e & 1);
+                        const int cd = Rc.code(e);
                         xv[e] = cd < 0 ? ring[-1 - cd] : xb[cd];
                     }
 #pragma unroll
@@ -728,8 +738,12 @@ static int launch_pk6(lssp_amd_ctx *c, const TriSched &t, const double *rhs, dou
         if (pd == 1) k_tri_pk6<4, 2, 3, 3, false, 256><<<grid, 512, 0, c->stream>>>(g);
         else if (pd == 2) k_tri_pk6<4, 2, 3, 2, false, 256><<<grid, 512, 0, c->stream>>>(g);
         else k_tri_pk6<4, 2, 4, 3, false, 256><<<grid, 512, 0, c->stream>>>(g);
-    } else {
+    } else if (t.pk6_ep == 8) {
         k_tri_pk6<8, 2, 4, 3, false, 256><<<grid, 512, 0, c->stream>>>(g);
+    } else if (t.pk6_ep == 16) {
+        k_tri_pk6<16, 2, 4, 3, false, 256><<<grid, 512, 0, c->stream>>>(g);
+    } else {
+        k_tri_pk6<24, 2, 4, 1, false, 256><<<grid, 512, 0, c->stream>>>(g);
     }
     t.pk6_base += (unsigned long long)t.bp_nb + grid;
     LSSP_HIP(hipGetLastError());

@@ -1,0 +1,220 @@
+"""Measurement + full-size parity of BASELINE.json's other single-GPU configs.
+
+    python tools/bench_configs.py cg-thermal   [--iters 1000] [--ref-iters 1000]
+    python tools/bench_configs.py gmres-ilut   [--grid 256]   [--ref-iters 30]
+    python tools/bench_configs.py bicgstab-iluk --grid 512     (config 4's matrix on one GPU)
+
+Each prints ONE JSON line: GPU throughput (Krylov it/s with HIP-event SpMV
+and ILU-apply rooflines), the reference's own CPU timing on a bounded sample
+(oracle/_ref/libref.so, 1 core), and a FULL-SIZE parity check: the library in
+SERIAL reduction mode is run for the same number of iterations as the
+reference and every dot/norm the driver evaluates must be bitwise equal
+(trace), plus the final x.  The tree-mode (fast path) run to convergence is
+compared with the reference's iteration count.
+
+config 5 (cg-thermal): thermal2-like SPD matrix (lssp_amd.synthetic), CG,
+PC_NON, b = 1, x0 = 0, fixed 1000 iterations.
+config 3 (gmres-ilut): 7-pt Poisson 256^3, GMRES(30) + ILUT(1e-4, p=20).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0
+T0 = time.perf_counter()
+
+
+def log(msg):
+    """progress on stderr (long host setups must not look like a hang)"""
+    print(f"[{time.perf_counter() - T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
+def _events(dev):
+    import torch
+    s = torch.cuda.ExternalStream(dev.stream)
+    return s, torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+
+def spmv_leg(dev, A, nnz, n, reps=50):
+    x = dev.vec(n, np.random.default_rng(1).uniform(-1, 1, n))
+    y = dev.vec(n)
+    for _ in range(5):
+        A.mv_mxy(x, y)
+    s, e0, e1 = _events(dev)
+    e0.record(s)
+    for _ in range(reps):
+        A.mv_mxy(x, y)
+    e1.record(s)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    b = 12 * nnz + 20 * n + 4
+    return {"ms": round(ms, 5), "GBps": round(b / ms / 1e6, 1), "frac_hbm_peak": round(b / ms / 1e6 / HBM_PEAK_GBS, 4),
+            "bytes": b}
+
+
+def apply_leg(dev, M, n, reps=5):
+    x = dev.vec(n, np.random.default_rng(2).uniform(-1, 1, n))
+    z = dev.vec(n)
+    M.apply(z, x)
+    s, e0, e1 = _events(dev)
+    e0.record(s)
+    for _ in range(reps):
+        M.apply(z, x)
+    e1.record(s)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    b = 12 * (M.nnzL + M.nnzU) + 8 * (n + 1) + 32 * n
+    return {"ms": round(ms, 4), "GBps": round(b / ms / 1e6, 1), "bytes": b, "levels_L": M.levelsL,
+            "levels_U": M.levelsU}
+
+
+def timed_solve(dev, A, M, n, solver, iters, restart=30, reduction=None):
+    import lssp_amd
+    if reduction is not None:
+        dev.set_reduction(reduction)
+    x = dev.vec(n, np.zeros(n))
+    b = dev.vec(n, np.ones(n))
+    dev.sync()
+    t0 = time.perf_counter()
+    r = lssp_amd.solve(dev, A, M, x, b, solver=solver, tol_rel=0.0, tol_abs=0.0, tol_rb=0.0, maxit=iters,
+                       restart=restart)
+    dev.sync()
+    return r, time.perf_counter() - t0
+
+
+def parity(dev, A, M, n, Ao, solver, ref_kw, iters, restart, out):
+    """SERIAL mode vs the reference itself, same iteration count, bitwise"""
+    import lssp_amd
+    import oracle as O
+    log(f"reference: {iters} iterations (setup included)")
+    t0 = time.perf_counter()
+    ref = O.ref_solve(solver, Ao, np.ones(n), rtol=0.0, atol=0.0, rbtol=0.0, maxit=iters, restart=restart,
+                      **ref_kw)
+    t_ref = time.perf_counter() - t0
+    log("serial-mode run on the GPU")
+    dev.set_reduction(lssp_amd.SERIAL)
+    x = dev.vec(n, np.zeros(n))
+    b = dev.vec(n, np.ones(n))
+    r = lssp_amd.solve(dev, A, M, x, b, solver=solver, tol_rel=0.0, tol_abs=0.0, tol_rb=0.0, maxit=iters,
+                       restart=restart, trace_cap=ref.trace.size + 16)
+    dev.set_reduction(lssp_amd.TREE)
+    xs = x.download()
+    same = lambda a, b_: bool(np.array_equal(np.asarray(a), np.asarray(b_), equal_nan=True))
+    out["parity_serial_vs_reference"] = {
+        "iterations": iters, "nits": [r.nits, ref.nits], "trace_len": [int(r.trace.size), int(ref.trace.size)],
+        "trace_bitwise": same(r.trace, ref.trace), "x_bitwise": same(xs, ref.x),
+        "residual": [r.residual, ref.residual]}
+    out["cpu_baseline"] = {"value": round(ref.nits / ref.t_solve, 4), "unit": "iters/s", "cores": 1,
+                           "kind": "reference",
+                           "sample": f"reference lssp_solver_solve, {ref.nits} iterations in {ref.t_solve:.2f} s "
+                                     f"(PC setup {ref.t_setup:.2f} s, wall {t_ref:.1f} s)"}
+    return ref
+
+
+def cg_thermal(args):
+    import lssp_amd
+    import oracle as O
+    from lssp_amd.synthetic import thermal_like
+    Ap, Aj, Ax = thermal_like()
+    n, nnz = Ap.size - 1, int(Ap[-1])
+    dev = lssp_amd.Device(0)
+    A = lssp_amd.DMat(dev, Ap, Aj, Ax)
+    out = {"config": "thermal2-like SPD (SURVEY 8(d)), CG, PC_NON, b=1, x0=0", "rows": n, "nnz": nnz,
+           "spmv": spmv_leg(dev, A, nnz, n)}
+    timed_solve(dev, A, None, n, lssp_amd.CG, 20)
+    r, t = timed_solve(dev, A, None, n, lssp_amd.CG, args.iters)
+    out["gpu"] = {"iters": r.nits, "seconds": round(t, 4), "iters_per_s": round(r.nits / t, 2),
+                  "ms_per_iter": round(t / r.nits * 1e3, 4), "residual": r.residual, "reduction": "tree"}
+    if O.ref_available():
+        ref = parity(dev, A, None, n, O.CSR(n, Ap, Aj, Ax), O.CG, dict(pc=O.PC_NON), args.ref_iters, 30, out)
+        out["tree_vs_reference_residual_rel"] = (abs(r.residual - ref.residual) / ref.residual
+                                                 if args.ref_iters == args.iters else None)
+    dev.close()
+    print(json.dumps(out), flush=True)
+
+
+def gmres_ilut(args):
+    import lssp_amd
+    import oracle as O
+    N = args.grid
+    Ap, Aj, Ax = lssp_amd.poisson(3, N)
+    n, nnz = Ap.size - 1, int(Ap[-1])
+    dev = lssp_amd.Device(0)
+    A = lssp_amd.DMat(dev, Ap, Aj, Ax)
+    log("ILUT setup")
+    t0 = time.perf_counter()
+    M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUT, tol=1e-4, p=20)
+    t_pc = time.perf_counter() - t0
+    out = {"config": f"7-pt Poisson {N}^3, GMRES(30) + ILUT(1e-4, p=20), b=1, x0=0", "rows": n, "nnz": nnz,
+           "ilut": {"nnzL": M.nnzL, "nnzU": M.nnzU, "setup_s": round(t_pc, 2)},
+           "spmv": spmv_leg(dev, A, nnz, n), "ilu_apply": apply_leg(dev, M, n)}
+    log("GMRES to convergence")
+    # to convergence, default tolerances (lssp.cxx:11-13), tree reductions
+    x = dev.vec(n, np.zeros(n))
+    b = dev.vec(n, np.ones(n))
+    dev.sync()
+    t0 = time.perf_counter()
+    r = lssp_amd.solve(dev, A, M, x, b, solver=lssp_amd.GMRES, maxit=5000, restart=30)
+    dev.sync()
+    t = time.perf_counter() - t0
+    out["gpu"] = {"nits": r.nits, "residual": r.residual, "seconds": round(t, 3),
+                  "iters_per_s": round(r.nits / t, 2), "reduction": "tree",
+                  "reference_nits_survey": 162 if N == 256 else None}
+    if O.ref_available() and args.ref_iters > 0:
+        parity(dev, A, M, n, O.CSR(n, Ap, Aj, Ax), O.GMRES, dict(pc=O.PC_ILUT, ilut_tol=1e-4, ilut_p=20),
+               args.ref_iters, 30, out)
+    dev.close()
+    print(json.dumps(out), flush=True)
+
+
+def bicgstab_iluk(args):
+    import lssp_amd
+    N = args.grid
+    Ap, Aj, Ax = lssp_amd.poisson(3, N)
+    n, nnz = Ap.size - 1, int(Ap[-1])
+    dev = lssp_amd.Device(0)
+    A = lssp_amd.DMat(dev, Ap, Aj, Ax)
+    log("ILUK(0) setup")
+    t0 = time.perf_counter()
+    M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=0)
+    t_pc = time.perf_counter() - t0
+    out = {"config": f"7-pt Poisson {N}^3, BiCGSTAB + ILUK(0), b=1, x0=0, one GPU", "rows": n, "nnz": nnz,
+           "ilu_setup_s": round(t_pc, 2), "spmv": spmv_leg(dev, A, nnz, n), "ilu_apply": apply_leg(dev, M, n)}
+    timed_solve(dev, A, M, n, lssp_amd.BICGSTAB, 3)
+    r, t = timed_solve(dev, A, M, n, lssp_amd.BICGSTAB, args.iters)
+    out["gpu"] = {"iters": r.nits, "iters_per_s": round(r.nits / t, 2), "ms_per_iter": round(t / r.nits * 1e3, 4)}
+    x = dev.vec(n, np.zeros(n))
+    b = dev.vec(n, np.ones(n))
+    r = lssp_amd.solve(dev, A, M, x, b, solver=lssp_amd.BICGSTAB, maxit=5000)
+    out["converged"] = {"nits": r.nits, "residual": r.residual}
+    dev.close()
+    print(json.dumps(out), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("which", choices=["cg-thermal", "gmres-ilut", "bicgstab-iluk"])
+    ap.add_argument("--iters", type=int, default=1000)
+    ap.add_argument("--ref-iters", type=int, default=None)
+    ap.add_argument("--grid", type=int, default=256)
+    args = ap.parse_args()
+    if args.which == "cg-thermal":
+        args.ref_iters = args.iters if args.ref_iters is None else args.ref_iters
+        cg_thermal(args)
+    elif args.which == "gmres-ilut":
+        args.ref_iters = 30 if args.ref_iters is None else args.ref_iters
+        gmres_ilut(args)
+    else:
+        args.iters = min(args.iters, 50)
+        bicgstab_iluk(args)
+
+
+if __name__ == "__main__":
+    main()
