@@ -159,26 +159,51 @@ struct SerialArgs {
     const double *b[MAX_SLOTS];
 };
 
-__global__ void k_dot_serial(SerialArgs g, long n, int nslot, double *sums, double *scal,
-                             double *trace, Fin f, int do_fin)
+// SERIAL reduction mode: sum += x[i]*y[i] for i = 0 .. n-1 from 0.0, exactly
+// vector.cxx:123-133.  The additions are one dependent chain per slot, run by
+// lane 0 of wave 0 out of LDS; waves 1..15 stream the products (each rounded
+// as the reference rounds it) of the next 2048-element chunk into the other
+// LDS buffer meanwhile, so the chain never waits on HBM latency.
+constexpr int SER_C = 2048;
+__global__ __launch_bounds__(1024) void k_dot_serial(SerialArgs g, long n, int nslot, double *sums, double *scal,
+                                                     double *trace, Fin f, int do_fin)
 {
-    double r[MAX_SLOTS] = {0, 0, 0, 0};
-    for (int s = 0; s < nslot; s++) {
-        const double *x = g.a[s], *y = g.b[s];
-        double acc = 0;
-        long i = 0;
-        for (; i + 8 <= n; i += 8) {
-            double p[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) p[u] = x[i + u] * y[i + u];
-#pragma unroll
-            for (int u = 0; u < 8; u++) acc += p[u];
+    __shared__ double buf[2][MAX_SLOTS][SER_C];
+    const int tid = threadIdx.x;
+    const long nch = (n + SER_C - 1) / SER_C;
+    auto fill = [&](long k, int b) {
+        if (tid < 64) return;
+        for (int s = 0; s < nslot; s++) {
+            const double *x = g.a[s], *y = g.b[s];
+            for (int i = tid - 64; i < SER_C; i += 1024 - 64) {
+                const long e = k * SER_C + i;
+                if (e < n) buf[b][s][i] = x[e] * y[e];
+            }
         }
-        for (; i < n; i++) acc += x[i] * y[i];
-        r[s] = acc;
-        sums[s] = acc;
+    };
+    double acc[MAX_SLOTS] = {0, 0, 0, 0};
+    if (nch > 0) fill(0, 0);
+    __syncthreads();
+    for (long k = 0; k < nch; k++) {
+        if (k + 1 < nch) fill(k + 1, (k + 1) & 1);
+        if (tid == 0) {
+            const int m = (int)min((long)SER_C, n - k * SER_C);
+            const double(*B)[SER_C] = buf[k & 1];
+            if (nslot == 1) {
+                for (int i = 0; i < m; i++) acc[0] += B[0][i];
+            } else {
+                for (int i = 0; i < m; i++)
+#pragma unroll
+                    for (int s = 0; s < MAX_SLOTS; s++)
+                        if (s < nslot) acc[s] += B[s][i];
+            }
+        }
+        __syncthreads();
     }
-    if (do_fin) finalize(f, r, scal, trace);
+    if (tid == 0) {
+        for (int s = 0; s < nslot; s++) sums[s] = acc[s];
+        if (do_fin) finalize(f, acc, scal, trace);
+    }
 }
 
 __global__ void k_finalize(const double *sums, double *scal, double *trace, Fin f)
@@ -638,7 +663,7 @@ int launch_reduce_serial(lssp_amd_ctx *c, long n, int nslot, const double *const
         g.b[s] = b[s];
     }
     int do_fin = c->nranks > 1 ? 0 : 1;
-    k_dot_serial<<<1, 1, 0, c->stream>>>(g, n, nslot, c->d_sums, c->d_scal, c->d_trace, f, do_fin);
+    k_dot_serial<<<1, 1024, 0, c->stream>>>(g, n, nslot, c->d_sums, c->d_scal, c->d_trace, f, do_fin);
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;
 }

@@ -232,6 +232,13 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
     for (int p = 0; p < n; p++) maxlen = std::max(maxlen, rp[p + 1] - rp[p]);
     if (maxlen > 24) return LSSP_AMD_EUNSUPPORTED;  // ILUT(tol, p <= 24), ILU(k) of stencils
     const int EP = maxlen <= 4 ? 4 : maxlen <= 8 ? 8 : maxlen <= 16 ? 16 : 24;
+    // record words of a packet of n rows (C, V, D, ROW, each padded to 4 words);
+    // EP >= 16 records are staged through a 16 KB LDS slot (trisolve.hip LREC)
+    auto rec_words = [&](long nrow) {
+        auto p4 = [](long w) { return (w + 3) & ~3L; };
+        return p4((long)(EP / 2) * nrow) + 2L * EP * nrow + p4(2 * nrow) + p4(nrow);
+    };
+    constexpr long PK6_REC_WORDS16 = 1024;  // 16-byte units (trisolve.hip PK6_REC16)
     std::vector<int> blk(nb + 1, 0);
     std::vector<int> desc;
     std::vector<uint32_t> rec;  // 4-byte words, 16-byte aligned packets
@@ -248,6 +255,7 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
                 xl.clear();
                 while (p + nr < step_pos[s + 1] && nr < ROWS) {
                     const int r = p + nr;
+                    if (EP >= 16 && rec_words(nr + 1) > 4 * PK6_REC_WORDS16) break;  // LDS record slot
                     int newx = 0;
                     for (int k = rp[r]; k < rp[r + 1]; k++)
                         if (cols[k] >= 0 && stamp[cols[k]] != pid) newx++;

@@ -299,11 +299,26 @@ __device__ __forceinline__ uint64_t poll_ready(const double *p, int *err)
     }
 }
 
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+// v6 record length of a packet of n1 rows, in 16-byte units (tri_bp.cpp
+// build_packets6: C, V, D, ROW arrays, each padded to 4 words)
+template <int EP>
+__device__ __forceinline__ int rec16(int n1)
+{
+    auto pad4 = [](int w) { return (w + 3) & ~3; };
+    return (pad4((EP / 2) * n1) + 2 * EP * n1 + pad4(2 * n1) + pad4(n1)) / 4;
+}
+constexpr int PK6_REC16 = 1024;  // LREC: record bytes per packet <= 16 KB (4 loads x 256 loader lanes)
+
 struct PkLd {
     int row, xi[PK3_EXT];
     int nr, nx;
     double rh;
     uint64_t ev[PK3_EXT];
+    v4u rw[4];  // LREC: the packet's compute record, 4 x 16 B per loader lane
+    int rlen;   // record length in 16-byte units (0: none)
 };
 
 // tri_mode 9: packets v6 (tri_bp.cpp build_packets6) with schedule-ordered
@@ -332,6 +347,7 @@ struct Pk6Args {
     double *sh_next;     // the other shadow buffer: armed here for the next apply
     double *nat;         // natural-order output (nullptr: none)
     int n, B;
+    int unit;  // unit diagonal (ILUK / ILUT L): x / 1.0 == x, the division is skipped
     unsigned long long *claim;
     unsigned long long base;
     int *err;
@@ -341,8 +357,6 @@ struct Pk6Args {
     int tb0;
 };
 
-typedef unsigned v2u __attribute__((ext_vector_type(2)));
-typedef unsigned v4u __attribute__((ext_vector_type(4)));
 template <int EP>
 struct Pk6Rec {
     // int16 code pairs: EP/2 words, loaded as uint2 (EP 4) or uint4 chunks
@@ -376,7 +390,11 @@ __device__ __forceinline__ T &sel4(T &a, T &b, T &c, T &d)
 // IA <= 4.  Shallower prefetch keeps fewer requests in the CU's memory queue,
 // which is what a cross-CU hand-off waits behind (MI355X_MICROARCH.md,
 // handoff-1to1).
-template <int EP, int KE, int IA, int D, bool NAT, int NR>
+// LREC (long rows, EP 16 / 24): the compute record does not fit in rotating
+// registers; the loader lanes fetch it KE steps ahead with the gathers and land
+// it in an LDS slot at the end of the step before, and the compute lanes read
+// it from there (D unused).
+template <int EP, int KE, int IA, int D, bool NAT, int NR, bool LREC = false>
 __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args a)
 {
     constexpr int Q = 4;
@@ -388,6 +406,7 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
     __shared__ double xbuf[2][NR * PK3_EXT];
     __shared__ int rowbuf[2][NR];
     __shared__ int4 sdesc[PK3_CAP];
+    __shared__ v4u recbuf[LREC ? 2 : 1][LREC ? PK6_REC16 : 1];
     __shared__ int s_blk;
     __shared__ unsigned s_polls;
     const int tid = threadIdx.x;
@@ -441,7 +460,51 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
             if (p < 0 || p >= np) d.z = 0;
             return d;
         };
-        if (role == 0) {
+        if (LREC && role == 0) {
+            // compute lanes, record from LDS (landed by the loaders one step ahead)
+            for (int j = J0; j < J0 + T; j++) {
+                const int4 d = descc(j);
+                const int nr = d.z & 0x3ff;
+                if (t < nr) {
+                    const unsigned *w = reinterpret_cast<const unsigned *>(recbuf[j & 1]);
+                    const int wc = ((EP / 2) * nr + 3) & ~3;
+                    typedef double v2d __attribute__((ext_vector_type(2)));
+                    const v2d *V = reinterpret_cast<const v2d *>(w + wc);
+                    const double dg = reinterpret_cast<const double *>(V + (EP / 2) * nr)[t];
+                    const double *xb = xbuf[j & 1];
+                    double acc = rbuf[j & 1][t];
+                    double xv[EP], vv[EP];
+#pragma unroll
+                    for (int q = 0; q < EP / 8; q++) {
+                        const v4u cw = reinterpret_cast<const v4u *>(w)[(EP / 8) * t + q];
+#pragma unroll
+                        for (int h = 0; h < 8; h++) {
+                            const unsigned ww = cw[h / 2];
+                            const int cd = (h & 1) ? ((int)ww >> 16) : (int)(short)(ww & 0xffff);
+                            xv[8 * q + h] = cd < 0 ? ring[-1 - cd] : xb[cd];
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < EP / 2; q++) {
+                        const v2d v = V[q * nr + t];
+                        vv[2 * q] = v.x;
+                        vv[2 * q + 1] = v.y;
+                    }
+#pragma unroll
+                    for (int e = 0; e < EP; e++) acc = acc - vv[e] * xv[e];
+                    const double xi = a.unit ? acc : acc / dg;
+                    const int pos = d.w + t;
+                    ring[(pos - bbase) & (BP_RING - 1)] = xi;
+                    if (!(a.diag & 2)) st_agent(a.sh + pos, xi);
+                }
+                lds_barrier();
+            }
+            if (!(a.diag & 1)) {
+                const long s0 = bbase, s1 = min(s0 + a.B, (long)a.n);
+                uint64_t *rs = reinterpret_cast<uint64_t *>(a.sh_next);
+                for (long i = s0 + t; i < s1; i += NR) rs[i] = TRI_SENTINEL;
+            }
+        } else if (role == 0) {
             uint64_t c0 = 0, c1 = 0, acc_c = 0, acc_b = 0;
             auto issue = [&](const int4 d, Pk6Rec<EP> &Rr) {
                 const int nr = d.z & 0x3ff;
@@ -488,7 +551,7 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                     }
 #pragma unroll
                     for (int e = 0; e < EP; e++) acc = acc - Rc.v[e] * xv[e];
-                    const double xi = acc / Rc.dg;
+                    const double xi = a.unit ? acc : acc / Rc.dg;
                     const int pos = Rc.pos0 + t;
                     ring[(pos - bbase) & (BP_RING - 1)] = xi;
                     if (NAT) rowbuf[j & 1][t] = Rc.row;
@@ -531,8 +594,26 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
             // use (issued at step j-2) have exactly 12 younger loads, and the
             // gathers landed at the end of step j (packet j+1, issued at step
             // j+1-KE) have 6 (KE 2) or 0 (KE 1) younger loads.
+            // LREC: RL record loads (packet j+KE) open every step, so per step
+            // the queue grows by RL + 3 + 3 in the order records, indices, gathers
             static_assert(PK3_EXT == 2, "wait counts below assume 3 + 3 loads per step");
-            constexpr int WAIT_IDX = 6 * (IA - KE);  // younger than the indices the gathers use
+            constexpr int RL = LREC ? 4 : 0;
+            static_assert(!LREC || PK6_REC16 == RL * NR, "record loads cover one LDS slot");
+            constexpr int WAIT_IDX = 3 + (IA - KE - 1) * (RL + 6) + RL + 3;  // younger than the indices the gathers use
+            constexpr int WAIT_G = (KE - 1) * (RL + 6);  // younger than packet j+1's gathers (and records)
+            auto issue_rec = [&](const int4 d, PkLd &L) {
+                if constexpr (LREC) {
+                    const int nr = d.z & 0x3ff, n1 = nr > 0 ? nr : 1;
+                    const int len = rec16<EP>(n1);
+                    const v4u *base = reinterpret_cast<const v4u *>(a.rec) + d.x;
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const v4u *p = base + min(t + NR * u, len - 1);
+                        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(L.rw[u]) : "v"(p) : "memory");
+                    }
+                    L.rlen = nr > 0 ? len : 0;
+                }
+            };
             uint64_t acc_w = 0, acc_lb = 0, acc_is = 0, acc_ld = 0, m0 = 0;
             auto issue_idx = [&](const int4 d, PkLd &L) {
                 const int nr = d.z & 0x3ff, nx = (d.z >> 10) & 0x7ff;
@@ -562,6 +643,7 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                     return;
                 }
                 if (a.trace) m0 = __builtin_amdgcn_s_memtime();
+                issue_rec(descc(j + KE), Lg);
                 issue_idx(dl, Li);
                 gather(Lg);
                 dl = descc(j + IA + 1);
@@ -571,7 +653,14 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                     acc_is += l0 - m0;
                 }
                 // gathers of packet j+1 were issued at step j+1-KE
-                asm volatile("s_waitcnt vmcnt(%3)" : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]) : "n"(6 * (KE - 1)) : "memory");
+                if constexpr (LREC)
+                    asm volatile("s_waitcnt vmcnt(%7)"
+                                 : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]), "+v"(Ll.rw[0]), "+v"(Ll.rw[1]),
+                                   "+v"(Ll.rw[2]), "+v"(Ll.rw[3])
+                                 : "n"(WAIT_G)
+                                 : "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(%3)" : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]) : "n"(WAIT_G) : "memory");
                 uint64_t l2 = 0;
                 if (a.trace) {
                     l2 = __builtin_amdgcn_s_memtime();
@@ -580,6 +669,11 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                 if (tid == NR) mark(j, 2);
                 // land packet j+1 (nr = nx = 0 outside the block's packets)
                 if (t < Ll.nr) rbuf[(j + 1) & 1][t] = Ll.rh;
+                if constexpr (LREC) {
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (t + NR * u < Ll.rlen) recbuf[(j + 1) & 1][t + NR * u] = Ll.rw[u];
+                }
 #pragma unroll
                 for (int e = 0; e < PK3_EXT; e++) {
                     const int k = t + NR * e;
@@ -611,6 +705,7 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
 #pragma unroll
             for (int e = 0; e < PK3_EXT; e++) L0.xi[e] = L1.xi[e] = L2.xi[e] = L3.xi[e] = 0;
             L0.rh = L1.rh = L2.rh = L3.rh = 0;
+            L0.rlen = L1.rlen = L2.rlen = L3.rlen = 0;
 #define LSSP_PK6_LSTEP(u)                                                                          \
     step(j0 + u, sel4<(u + IA) % Q>(L0, L1, L2, L3), sel4<(u + KE) % Q>(L0, L1, L2, L3), \
          sel4<(u + 1) % Q>(L0, L1, L2, L3))
@@ -724,7 +819,7 @@ static int launch_pk6(lssp_amd_ctx *c, const TriSched &t, const double *rhs, dou
         LSSP_HIP(hipMemsetAsync(d_t2, 0, sizeof(unsigned long long) * 2 * 1024 * 4, c->stream));
     }
     Pk6Args g{t.bp_nb, t.pk6_blk, reinterpret_cast<const int4 *>(t.pk6_desc), t.pk6_rec, t.pk6_idx, rhs, sh,
-              sh_next, nat, t.n, t.bp_B, t.pk6_claim, t.pk6_base, c->d_err, c->tri_diag, d_trace, d_t2, tb0};
+              sh_next, nat, t.n, t.bp_B, t.unit, t.pk6_claim, t.pk6_base, c->d_err, c->tri_diag, d_trace, d_t2, tb0};
     // Instantiated: 256-row packets, x operands gathered 2 steps ahead (KE 2),
     // EP 4 or 8 -- the variants whose inline-asm loader tools/check_vmcnt.py
     // (tests/test_isa_vmcnt.py) verifies hazard-free
@@ -741,9 +836,9 @@ static int launch_pk6(lssp_amd_ctx *c, const TriSched &t, const double *rhs, dou
     } else if (t.pk6_ep == 8) {
         k_tri_pk6<8, 2, 4, 3, false, 256><<<grid, 512, 0, c->stream>>>(g);
     } else if (t.pk6_ep == 16) {
-        k_tri_pk6<16, 2, 4, 3, false, 256><<<grid, 512, 0, c->stream>>>(g);
+        k_tri_pk6<16, 3, 4, 1, false, 256, true><<<grid, 512, 0, c->stream>>>(g);
     } else {
-        k_tri_pk6<24, 2, 4, 1, false, 256><<<grid, 512, 0, c->stream>>>(g);
+        k_tri_pk6<24, 3, 4, 1, false, 256, true><<<grid, 512, 0, c->stream>>>(g);
     }
     t.pk6_base += (unsigned long long)t.bp_nb + grid;
     LSSP_HIP(hipGetLastError());

@@ -40,6 +40,7 @@ def main():
         os.environ["LSSP_AMD_TRI_DEPTH"] = f[2] if len(f) > 2 else "2"
         os.environ["LSSP_AMD_TRI_PK_ROWS"] = f[3] if len(f) > 3 else "256"
         os.environ["LSSP_AMD_TRI_BP_MULT"] = f[4] if len(f) > 4 else "1"
+        os.environ["LSSP_AMD_TRI_DIAG"] = f[5] if len(f) > 5 else "0"  # timing experiments (wrong results)
         dev = lssp_amd.Device(0)
         kind = lssp_amd.ILUK if args.kind == "iluk" else lssp_amd.ILUT
         if M is None:
@@ -63,7 +64,8 @@ def main():
         ms = e0.elapsed_time(e1) / args.reps
         ok = bool(np.array_equal(x.download(), ref))
         out.append({"mode": int(mode), "blocks_per_cu": int(bpc), "depth": int(os.environ["LSSP_AMD_TRI_DEPTH"]),
-                    "rows": int(os.environ["LSSP_AMD_TRI_PK_ROWS"]), "mult": int(os.environ["LSSP_AMD_TRI_BP_MULT"]), "apply_ms": round(ms, 4),
+                    "rows": int(os.environ["LSSP_AMD_TRI_PK_ROWS"]), "mult": int(os.environ["LSSP_AMD_TRI_BP_MULT"]),
+                    "diag": int(os.environ["LSSP_AMD_TRI_DIAG"]), "apply_ms": round(ms, 4),
                     "us_per_level": round(ms * 1e3 / (levels[0] + levels[1]), 3), "stable": ok})
         print(json.dumps(out[-1]), flush=True)
         dev.close()
