@@ -397,7 +397,9 @@ int lssp_amd_ilu_create(lssp_amd_ctx *c, int kind, int n, const int *Ap, const i
     sort_columns(A);  // lssp.cxx:173
     if (kind == LSSP_AMD_ILUK && level < 0) level = 1;  // pc-iluk.cxx:583-592
     HostCSR L, U;
-    ilu_factor(kind, A, level, tol < 0 ? 1e-3 : tol, p, blk, L, U);
+    int fst = LSSP_AMD_OK;
+    ilu_factor(c, kind, A, level, tol < 0 ? 1e-3 : tol, p, blk, L, U, &fst);
+    if (fst != LSSP_AMD_OK) return fst;
     lssp_amd_ilu *M = new lssp_amd_ilu();
     M->ctx = c;
     M->n = n;

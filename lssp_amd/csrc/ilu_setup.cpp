@@ -376,9 +376,10 @@ void sort_columns(HostCSR &A)
 // pc-iluk.cxx:411-581 / pc-ilut.cxx:288-456: adjust_zero_diag, optional
 // symbolic ILU(k), block-diagonal extraction, per-block factorization, split
 // into L (unit diagonal LAST) and U (pivot FIRST).
-void ilu_factor(int kind, const HostCSR &A0, int level, double tol, int p, int blk, HostCSR &L,
-                HostCSR &U)
+void ilu_factor(lssp_amd_ctx *c, int kind, const HostCSR &A0, int level, double tol, int p, int blk, HostCSR &L,
+                HostCSR &U, int *status)
 {
+    *status = LSSP_AMD_OK;
     const int n = A0.n;
     if (kind == LSSP_AMD_ILUT && p <= 0) p = (A0.Ap[n] + n - 1) / n;  // pc-ilut.cxx:436-438
     HostCSR Az = adjust_zero_diag(A0, ZERO_DIAG_TOL);
@@ -393,7 +394,15 @@ void ilu_factor(int kind, const HostCSR &A0, int level, double tol, int p, int b
     Az = HostCSR();
 
     HostCSR F;
+    static const bool host_ilu0 = getenv("LSSP_AMD_ILU_HOST") && atoi(getenv("LSSP_AMD_ILU_HOST"));
+    if (kind == LSSP_AMD_ILUK && c && !host_ilu0) {
+        // the numeric ILU(0) of every block at once, on the GPU (ilu_factor.hip)
+        *status = ilu0_factor_gpu(c, n, blk, M.Ap, M.Aj, M.Ax);
+        if (*status != LSSP_AMD_OK) return;
+        F = std::move(M);
+    }
     F.n = F.ncols = n;
+    if (F.Ap.empty()) {
     F.Ap.assign(n + 1, 0);
     F.Aj.reserve(M.Aj.size());
     F.Ax.reserve(M.Ax.size());
@@ -413,6 +422,7 @@ void ilu_factor(int kind, const HostCSR &A0, int level, double tol, int p, int b
             }
             F.Ap[s + i + 1] = (int)F.Aj.size();
         }
+    }
     }
     M = HostCSR();
 

@@ -236,8 +236,13 @@ struct HostCSR {
     std::vector<double> Ax;
 };
 void sort_columns(HostCSR &A);
-void ilu_factor(int kind, const HostCSR &A, int level, double tol, int p, int blk, HostCSR &L,
-                HostCSR &U);
+// c != nullptr: ILUK's numeric ILU(0) runs on c's GPU (ilu_factor.hip), bitwise
+// the host restatement (LSSP_AMD_ILU_HOST=1 selects the host one); ILUT stays
+// on the host (pc-ilut.cxx:51-286 is sequential by row)
+void ilu_factor(lssp_amd_ctx *c, int kind, const HostCSR &A, int level, double tol, int p, int blk, HostCSR &L,
+                HostCSR &U, int *status);
+int ilu0_factor_gpu(lssp_amd_ctx *c, int n, int blk, const std::vector<int> &Ap, const std::vector<int> &Aj,
+                    std::vector<double> &Ax);
 int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std::vector<int> &Tj,
                    const std::vector<double> &Tx, bool upper, TriSched &t, const TriSched *prod = nullptr);
 void free_trisched(TriSched &t);
