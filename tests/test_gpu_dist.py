@@ -29,7 +29,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, N, maxit, seed, out):
+def _worker(rank, world, port, N, maxit, seed, out, solver="bicgstab"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -55,10 +55,12 @@ def _worker(rank, world, port, N, maxit, seed, out):
         yv = dev.vec(A.nx)
         A.mv_mxy(xv, yv)
         y = yv.download(nl)
-        # BiCGSTAB + block-Jacobi ILU(0), b = 1, x0 = 0, tree reductions
+        # b = 1, x0 = 0, tree reductions; block-Jacobi ILU(0) except for CG (PC_NON)
         x = dev.vec(A.nx, np.zeros(A.nx))
         b = dev.vec(A.nx, np.ones(A.nx))
-        r = lssp_amd.solve(dev, A, M, x, b, solver=lssp_amd.BICGSTAB, maxit=maxit, trace_cap=100000)
+        sol = {"bicgstab": lssp_amd.BICGSTAB, "gmres": lssp_amd.GMRES, "cg": lssp_amd.CG}[solver]
+        r = lssp_amd.solve(dev, A, None if solver == "cg" else M, x, b, solver=sol, maxit=maxit, restart=30,
+                           trace_cap=100000)
         xl = x.download(nl)
         dev.barrier()
         parts = [None] * world
@@ -71,13 +73,14 @@ def _worker(rank, world, port, N, maxit, seed, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,N", [(2, 12), (3, 10), (4, 16)])
-def test_multirank_on_one_gpu_equals_oracle_prank_mode(world, N):
+@pytest.mark.parametrize("world,N,solver", [(2, 12, "bicgstab"), (3, 10, "bicgstab"), (4, 16, "bicgstab"),
+                                             (2, 12, "gmres"), (3, 11, "gmres"), (2, 12, "cg"), (4, 13, "cg")])
+def test_multirank_on_one_gpu_equals_oracle_prank_mode(world, N, solver):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, N, 500, 0x5EED, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, 500, 0x5EED, q, solver)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -89,8 +92,11 @@ def test_multirank_on_one_gpu_equals_oracle_prank_mode(world, N):
     from inputs import uniform
     A = O.poisson(3, N)
     assert np.array_equal(y, O.spmv(0, A, uniform(0x5EED, A.n)))
-    Lg, Ug = O.ilu(A, "iluk", level=0, blk=(A.n + world - 1) // world)
-    o = O.solve(O.BICGSTAB, A, np.ones(A.n), L=Lg, U=Ug, mode=O.TREE, nranks=world, maxit=500)
+    L = U = None
+    if solver != "cg":
+        L, U = O.ilu(A, "iluk", level=0, blk=(A.n + world - 1) // world)
+    sol = {"bicgstab": O.BICGSTAB, "gmres": O.GMRES, "cg": O.CG}[solver]
+    o = O.solve(sol, A, np.ones(A.n), L=L, U=U, mode=O.TREE, nranks=world, maxit=500, restart=30)
     assert nits == o.nits
     assert res == o.residual
     assert np.array_equal(trace, o.trace)
