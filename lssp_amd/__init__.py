@@ -1,8 +1,12 @@
 """lssp_amd -- MI355X-native hot path of LSSP (CSR SpMV, fused BLAS-1, ILU
 trisolves, BiCGSTAB / GMRES / CG) behind the reference's API.
 
-    from lssp_amd import api          # lssp_solver_create / _assemble / _solve ...
-    from lssp_amd.device import ...   # raw C-ABI handles (include/lssp_amd.h)
+    from lssp_amd.device import ...   # C-ABI handles (include/lssp_amd.h): Device, DMat, DILU, solve
+    from lssp_amd.dist import GlooTransport   # host-staged multi-rank transport
+    from lssp_amd.synthetic import thermal_like   # config 5's matrix
+
+The reference's own C++ API (lssp_solver_create / _assemble / _solve) reaches
+this library through integration/amd_backend.cxx.
 
 The compute lives in lssp_amd/lib/liblssp_amd.so (hand-written HIP for
 gfx950).  Importing the package loads it and fails loudly if it is missing.
