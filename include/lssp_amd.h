@@ -4,9 +4,9 @@
  * Plain pointers and sizes only (no torch, no C++ types).  Device vectors are
  * raw `double *` obtained from lssp_amd_vec_alloc; host arrays are the
  * caller's.  Every entry point returns an int status (LSSP_AMD_OK == 0) and
- * never exits the process; the reference-compatible C++ layer
- * (include/lssp/lssp.h) maps a non-zero status to lssp_error(1, ...), which
- * reproduces the reference's exit-on-fatal (utils.cxx:114-135).
+ * never exits the process; the reference-side binding
+ * (integration/amd_backend.cxx) maps a non-zero status to lssp_error(1, ...),
+ * which reproduces the reference's exit-on-fatal (utils.cxx:114-135).
  *
  * Each group cites the reference interface it replaces (paths relative to the
  * huiscliu/lssp tree).  The binding a maintainer would add on the reference
@@ -37,7 +37,7 @@ enum {
 };
 
 /* LSSP_SOLVER_TYPE values of the reference (type-defs.h:157-178) */
-enum { LSSP_AMD_GMRES = 0, LSSP_AMD_BICGSTAB = 4, LSSP_AMD_CG = 7 };
+enum { LSSP_AMD_GMRES = 0, LSSP_AMD_RGMRES = 2, LSSP_AMD_BICGSTAB = 4, LSSP_AMD_CG = 7 };
 /* ILU kinds (LSSP_PC_TYPE, type-defs.h:63-101) */
 enum { LSSP_AMD_ILUK = 1, LSSP_AMD_ILUT = 2 };
 
@@ -123,11 +123,12 @@ int lssp_amd_ilu_get_factors(const lssp_amd_ilu *M, int *Lp, int *Lj, double *Lx
                              int *Uj, double *Ux);
 
 /* ---- Krylov solve: lssp_solver_solve (lssp.cxx:250-414) for BiCGSTAB
- *      (solver-bicgstab.cxx:10-175), GMRES(m) (solver-gmres.cxx:12-255) and
- *      CG (solver-cg.cxx:8-136).  Same recurrences, guards, defaults and
+ *      (solver-bicgstab.cxx:10-175), GMRES(m) (solver-gmres.cxx:12-255),
+ *      right-preconditioned GMRES(m) (solver-gmres.cxx:257-479) and CG
+ *      (solver-cg.cxx:8-136).  Same recurrences, guards, defaults and
  *      iteration counting; vectors stay in HBM. ------------------------- */
 typedef struct {
-    int solver;     /* LSSP_AMD_GMRES / _BICGSTAB / _CG */
+    int solver;     /* LSSP_AMD_GMRES / _RGMRES / _BICGSTAB / _CG */
     double tol_rel; /* < 0: default 1e-7 (lssp.cxx:11-13) */
     double tol_abs;
     double tol_rb;

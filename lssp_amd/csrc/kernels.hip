@@ -552,6 +552,8 @@ enum EwKind {
     EW_CG_XR,      // out0(x) = out0 + alpha*x ; out1(r) = out1 - alpha*y   (:101-104)
     EW_GM_MGS,     // out0 = out0 * 1 + x * (-scal[sidx])  (solver-gmres.cxx:144)
     EW_GM_X,       // out0[q] += sum_{i<k} vbase[i][q] * scal[S_H..]  (:196-204); ym passed in u
+    EW_GMR_Z,      // out0 = v_{k-1}*y_{k-1}, then out0 = out0*1 + v_i*y_i, i = k-2 .. 0
+                   // (solver-gmres.cxx:417-423, right-preconditioned GMRES); ym in u
 };
 
 struct EwArgs {
@@ -616,6 +618,13 @@ __global__ __launch_bounds__(256) void k_ew(EwArgs g)
                 double acc = 0;
                 for (int q = 0; q < g.k; q++) acc += g.vbase[(long)q * ld + i] * g.u[q];
                 g.out0[i] += acc;
+                break;
+            }
+            case EW_GMR_Z: {
+                const long ld = (long)g.b;
+                double z = g.vbase[(long)(g.k - 1) * ld + i] * g.u[g.k - 1];
+                for (int q = g.k - 2; q >= 0; q--) z = z * 1 + g.vbase[(long)q * ld + i] * g.u[q];
+                g.out0[i] = z;
                 break;
             }
             }

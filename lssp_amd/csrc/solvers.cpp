@@ -28,7 +28,7 @@ constexpr double DEF_TOL = 1e-7;     // lssp.cxx:11-13
 
 enum EwK {  // mirror of kernels.hip EwKind
     K_FILL = 0, K_COPY, K_AXY, K_AXPBY, K_AXPBYZ, K_SCALE, K_DIVS, K_DOT,
-    K_BICG_P, K_BICG_S, K_BICG_XR, K_CG_P, K_CG_XR, K_GM_MGS, K_GM_X
+    K_BICG_P, K_BICG_S, K_BICG_XR, K_CG_P, K_CG_XR, K_GM_MGS, K_GM_X, K_GMR_Z
 };
 
 struct Run {
@@ -531,6 +531,164 @@ int gmres(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, in
     return LSSP_AMD_OK;
 }
 
+// ---------------------------------------------------------------------------
+// GMRES(m), right preconditioned (solver-gmres.cxx:257-479): A M^-1 u = b,
+// x = x0 + M^-1 (V y).  The residual reported is the Givens estimate |g_{i+1}|
+// (:370, :427); a true residual b - A x is formed only to restart (:433).
+// ---------------------------------------------------------------------------
+int gmres_r(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
+{
+    lssp_amd_ctx *c = R.c;
+    double tol_rel, tol_abs, tol_rb = P.tol_rb;
+    int maxit;
+    defaults(P, tol_rel, tol_abs, maxit);
+    int m = P.restart < 0 ? DEF_RESTART : P.restart;
+    if (tol_rb < 0) tol_rb = DEF_TOL;
+    if (m <= 0) return LSSP_AMD_EINVAL;
+    if (S_H + 2 * m + 2 > NSCAL) return LSSP_AMD_EUNSUPPORTED;
+    if (P.verb >= 2 && R.rank == 0) {
+        printf("gmres: restart parameter m: %d\n", m);
+        printf("gmres: maximal iteration: %d\n", maxit);
+        printf("gmres: tolerance abs: %g\n", tol_abs);
+        printf("gmres: tolerance rel: %g\n", tol_rel);
+        printf("gmres: tolerance rbn: %g\n", tol_rb);
+    }
+    double *wj = R.vec(), *rg = R.vec();
+    double *V = R.vec(R.nx * (long)m);
+    double *d_ym = R.vec(m);
+    if (!wj || !rg || !V || !d_ym) return LSSP_AMD_ENOMEM;
+    auto Vi = [&](int i) { return V + (long)i * R.nx; };
+    std::vector<double> H((size_t)(m + 1) * m), gg(m + 1), cs(m), sn(m), ym(m);
+    auto HG = [&](int row, int col) -> double & { return H[(size_t)row * m + col]; };
+
+    LSSP_TRY(R.dot1(b, b, R.fin(FIN_NORM, 1, R.T(), -1, S_BNORM)));  // :324
+    LSSP_TRY(R.spmv(EPI_AXPBY, -1, x, 1, b, rg));                     // :327
+    LSSP_TRY(R.dot1(rg, rg, R.fin(FIN_NORM, 1, R.T(), -1, S_RES)));  // :328
+    LSSP_TRY(R.sync(0, 16));
+    const double b_norm = R.h(S_BNORM);
+    tol_rb *= b_norm;
+    double beta = R.h(S_RES);
+    int inner = 0;
+    if (beta <= tol_abs) {  // :330-333
+        *nits = 0;
+        *res_out = beta;
+        return LSSP_AMD_OK;
+    }
+    const double err_rel = beta;
+    double tol = tol_rel * err_rel;
+    if (tol < tol_abs) tol = tol_abs;
+    if (tol < tol_rb) tol = tol_rb;
+
+    while (inner < maxit) {
+        int i, kk;
+        std::fill(gg.begin(), gg.end(), 0.0);  // :345-351
+        std::fill(H.begin(), H.end(), 0.0);
+        LSSP_TRY(R.dot1(rg, rg, R.fin(FIN_NORM, 1, R.T(), -1, S_TMP)));  // :354
+        LSSP_TRY(R.sync(0, 16));
+        gg[0] = beta = R.h(S_TMP);
+        {
+            Ew e;
+            e.kind = K_AXY;  // :355, a multiply by 1/beta
+            e.a = 1 / beta;
+            e.x = rg;
+            e.out0 = Vi(0);
+            LSSP_TRY(R.ew(e));
+        }
+        bool converged = false;
+        for (i = 0; i < m && inner < maxit; i++) {
+            inner++;
+            LSSP_TRY(R.pc(rg, Vi(i)));                              // :362-363
+            LSSP_TRY(R.spmv(EPI_MXY, 1, rg, 0, nullptr, wj));      // :364
+            LSSP_TRY(R.dot1(wj, Vi(0), R.fin(FIN_STORE, 1, R.T(), -1, S_H)));  // :367, j = 0
+            for (int j = 0; j <= i; j++) {  // :366-371, axpy fused with the next dot / the norm
+                Ew e;
+                e.kind = K_GM_MGS;
+                e.out0 = wj;
+                e.x = Vi(j);
+                e.sidx = S_H + j;
+                e.nred = 1;
+                e.r0a = wj;
+                e.r0b = j < i ? Vi(j + 1) : wj;
+                LSSP_TRY(R.ew(e));
+                if (j < i)
+                    LSSP_TRY(R.fin1(wj, Vi(j + 1), R.fin(FIN_STORE, 1, R.T(), -1, S_H + j + 1)));
+                else
+                    LSSP_TRY(R.fin1(wj, wj, R.fin(FIN_NORM, 1, R.T(), -1, S_H + i + 1)));  // :373
+            }
+            LSSP_TRY(R.sync(0, S_H + i + 2));
+            for (int j = 0; j <= i; j++) HG(j, i) = R.h(S_H + j);
+            const double hij = R.h(S_H + i + 1);
+            HG(i + 1, i) = hij;
+            if (std::fabs(hij) <= BREAKDOWN) {  // :377-380
+                i--;
+                break;
+            } else if (i + 1 < m) {
+                Ew e;
+                e.kind = K_AXY;  // :382
+                e.a = 1 / hij;
+                e.x = wj;
+                e.out0 = Vi(i + 1);
+                LSSP_TRY(R.ew(e));
+            }
+            for (int j = 0; j < i; j++) {  // :385-391
+                const double h1 = cs[j] * HG(j, i) + sn[j] * HG(j + 1, i);
+                const double h2 = -sn[j] * HG(j, i) + cs[j] * HG(j + 1, i);
+                HG(j, i) = h1;
+                HG(j + 1, i) = h2;
+            }
+            double gma = std::sqrt(HG(i, i) * HG(i, i) + HG(i + 1, i) * HG(i + 1, i));  // :393
+            if (std::fabs(gma) == 0.) gma = 1e-20;
+            cs[i] = HG(i, i) / gma;
+            sn[i] = HG(i + 1, i) / gma;
+            gg[i + 1] = -sn[i] * gg[i];
+            gg[i] = cs[i] * gg[i];
+            HG(i, i) = cs[i] * HG(i, i) + sn[i] * HG(i + 1, i);
+            beta = std::fabs(gg[i + 1]);
+            if (P.verb >= 1 && R.rank == 0)
+                printf("rgmres: itr: %4d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", inner, beta,
+                       (err_rel == 0 ? 0 : beta / err_rel), (b_norm == 0 ? 0 : beta / b_norm));
+            if (beta <= tol) {  // :409-411 (goto solve: i is not advanced)
+                converged = true;
+                break;
+            }
+        }
+        (void)converged;
+        kk = i == m ? m : i + 1;  // :414
+        for (i = kk - 1; i >= 0; i--) {  // :415-420
+            ym[i] = gg[i] / HG(i, i);
+            for (int j = 0; j < i; j++) gg[j] = gg[j] - ym[i] * HG(j, i);
+        }
+        if (kk > 0) {  // :423-431
+            memcpy(c->h_scal + NSCAL - m, ym.data(), sizeof(double) * kk);
+            LSSP_HIP(hipMemcpyAsync(d_ym, c->h_scal + NSCAL - m, sizeof(double) * kk, hipMemcpyHostToDevice,
+                                    c->stream));
+            Ew e;
+            e.kind = K_GMR_Z;
+            e.out0 = rg;
+            e.vbase = V;
+            e.k = kk;
+            e.u = d_ym;
+            e.b = (double)R.nx;  // basis stride
+            LSSP_TRY(R.ew(e));
+            LSSP_TRY(R.pc(wj, rg));  // :429
+            Ew xa;
+            xa.kind = K_AXPBY;  // :430: x = x*1 + wj*1
+            xa.a = 1;
+            xa.b = 1;
+            xa.x = wj;
+            xa.out0 = x;
+            LSSP_TRY(R.ew(xa));
+        }
+        if (beta <= tol) break;                          // :433-435
+        LSSP_TRY(R.spmv(EPI_AXPBY, -1, x, 1, b, rg));    // :437
+    }
+    if (P.verb >= 2 && R.rank == 0) printf("gmres: total iteration: %d\n", inner);
+    LSSP_TRY(R.sync(0, 1));  // the last x update is complete when the call returns
+    *nits = inner;
+    *res_out = beta;
+    return LSSP_AMD_OK;
+}
+
 }  // namespace
 }  // namespace lssp_amd
 
@@ -569,6 +727,7 @@ extern "C" int lssp_amd_solve(lssp_amd_ctx *c, const lssp_amd_mat *A, const lssp
     case LSSP_AMD_BICGSTAB: st = bicgstab(R, *prm, x, b, &it, &res); break;
     case LSSP_AMD_CG: st = cg(R, *prm, x, b, &it, &res); break;
     case LSSP_AMD_GMRES: st = gmres(R, *prm, x, b, &it, &res); break;
+    case LSSP_AMD_RGMRES: st = gmres_r(R, *prm, x, b, &it, &res); break;
     default: st = LSSP_AMD_EUNSUPPORTED;
     }
     c->d_trace = saved_trace;

@@ -14,7 +14,7 @@ import numpy as np
 
 from . import _lib
 
-GMRES, BICGSTAB, CG = 0, 4, 7      # LSSP_SOLVER_TYPE (type-defs.h:157-178)
+GMRES, RGMRES, BICGSTAB, CG = 0, 2, 4, 7  # LSSP_SOLVER_TYPE (type-defs.h:157-178)
 ILUK, ILUT = 1, 2                  # LSSP_PC_TYPE (type-defs.h:63-101)
 SERIAL, TREE = 0, 1                # reduction order
 

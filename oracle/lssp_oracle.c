@@ -838,7 +838,7 @@ EXPORT void orc_ilu_free(void *hp)
 /* Krylov drivers                                                           */
 /* ------------------------------------------------------------------------ */
 
-enum { SOLVER_GMRES = 0, SOLVER_BICGSTAB = 4, SOLVER_CG = 7 }; /* type-defs.h:157-178 */
+enum { SOLVER_GMRES = 0, SOLVER_RGMRES = 2, SOLVER_BICGSTAB = 4, SOLVER_CG = 7 }; /* type-defs.h:157-178 */
 
 typedef struct {
     const csr_t *A;
@@ -1104,6 +1104,106 @@ done:
     return inner;
 }
 
+/* solver-gmres.cxx:257-479: right-preconditioned GMRES(m).  The residual it
+ * reports is the Givens estimate |g_{i+1}|; b - A x is formed only to restart. */
+static int gmres_r(ctx_t *c, double *x, const double *b, double tol_rel, double tol_abs,
+                   double tol_rb, int maxit, int m, double *res_out)
+{
+    const csr_t *A = c->A;
+    int n = A->nrows, inner = 0;
+    if (m < 0) m = DEF_RESTART;
+    if (maxit <= 0) maxit = DEF_MAXIT;
+    if (tol_abs < 0) tol_abs = DEF_TOL;
+    if (tol_rel < 0) tol_rel = DEF_TOL;
+    if (tol_rb < 0) tol_rb = DEF_TOL;
+    size_t bytes = sizeof(double) * (size_t)n;
+    double *wj = malloc(bytes), *rg = malloc(bytes);
+    double **v = malloc(sizeof(double *) * (size_t)m);
+    for (int i = 0; i < m; i++) v[i] = malloc(bytes);
+    double *gg = malloc(sizeof(double) * (size_t)(m + 1)), *ym = malloc(sizeof(double) * (size_t)m);
+    double *H = malloc(sizeof(double) * (size_t)(m + 1) * (size_t)m);
+    double *cs = malloc(sizeof(double) * (size_t)m), *sn = malloc(sizeof(double) * (size_t)m);
+#define HG(r, col) H[(size_t)(r) * (size_t)m + (size_t)(col)]
+    double tol = 0, err_rel = 0, beta;
+
+    double bnorm = tnorm(c, b);
+    tol_rb *= bnorm;
+    mv_amxpbyz(-1, A, x, 1, b, rg);
+    beta = tnorm(c, rg);
+    if (beta <= tol_abs) goto done;
+    err_rel = beta;
+    tol = tol_rel * err_rel;
+    if (tol < tol_abs) tol = tol_abs;
+    if (tol < tol_rb) tol = tol_rb;
+
+    while (inner < maxit) {
+        int i, kk;
+        for (kk = 1; kk <= m; kk++) gg[kk] = 0;
+        for (size_t q = 0; q < (size_t)(m + 1) * (size_t)m; q++) H[q] = 0;
+        gg[0] = beta = tnorm(c, rg);
+        {
+            double a = 1 / beta;
+            for (int q = 0; q < n; q++) v[0][q] = rg[q] * a; /* vector.cxx:86-95 */
+        }
+        for (i = 0; i < m && inner < maxit; i++) {
+            double h;
+            inner++;
+            pc_apply(c, rg, v[i]);
+            mv_mxy(A, rg, wj);
+            for (int j = 0; j <= i; j++) {
+                h = tdot(c, wj, v[j]);
+                for (int q = 0; q < n; q++) wj[q] = wj[q] * 1 + v[j][q] * (-h);
+                HG(j, i) = h;
+            }
+            h = tnorm(c, wj);
+            HG(i + 1, i) = h;
+            if (fabs(h) <= BREAKDOWN) {
+                i--;
+                break;
+            } else if (i + 1 < m) {
+                double a = 1 / h;
+                for (int q = 0; q < n; q++) v[i + 1][q] = wj[q] * a;
+            }
+            for (int j = 0; j < i; j++) {
+                double h1 = cs[j] * HG(j, i) + sn[j] * HG(j + 1, i);
+                double h2 = -sn[j] * HG(j, i) + cs[j] * HG(j + 1, i);
+                HG(j, i) = h1;
+                HG(j + 1, i) = h2;
+            }
+            double gma = sqrt(HG(i, i) * HG(i, i) + HG(i + 1, i) * HG(i + 1, i));
+            if (fabs(gma) == 0.) gma = 1e-20;
+            cs[i] = HG(i, i) / gma;
+            sn[i] = HG(i + 1, i) / gma;
+            gg[i + 1] = -sn[i] * gg[i];
+            gg[i] = cs[i] * gg[i];
+            HG(i, i) = cs[i] * HG(i, i) + sn[i] * HG(i + 1, i);
+            beta = fabs(gg[i + 1]);
+            if (beta <= tol) break; /* goto solve: i not advanced */
+        }
+        kk = (i == m) ? m : i + 1;
+        for (i = kk - 1; i >= 0; i--) {
+            ym[i] = gg[i] / HG(i, i);
+            for (int j = 0; j < i; j++) gg[j] = gg[j] - ym[i] * HG(j, i);
+        }
+        if (kk > 0) {
+            for (int q = 0; q < n; q++) rg[q] = v[kk - 1][q] * ym[kk - 1];
+            for (i = kk - 2; i >= 0; i--)
+                for (int q = 0; q < n; q++) rg[q] = rg[q] * 1 + v[i][q] * ym[i];
+            pc_apply(c, wj, rg);
+            for (int q = 0; q < n; q++) x[q] = x[q] * 1 + wj[q] * 1;
+        }
+        if (beta <= tol) break;
+        mv_amxpbyz(-1, A, x, 1, b, rg);
+    }
+#undef HG
+done:
+    *res_out = beta;
+    free(wj); free(rg);
+    for (int i = 0; i < m; i++) free(v[i]);
+    free(v); free(gg); free(ym); free(H); free(cs); free(sn);
+    return inner;
+}
+
 /* Solve A x = b (x holds x0 on entry).  L/U == NULL => PC_NON.
  * trace receives every dot/norm the driver computes, in call order (the same
  * sequence tests/golden records from the reference). */
@@ -1134,6 +1234,7 @@ EXPORT int orc_solve(int solver, int n, const int *Ap, const int *Aj, const doub
     case SOLVER_BICGSTAB: it = bicgstab(&c, x, b, tol_rel, tol_abs, tol_rb, maxit, &res); break;
     case SOLVER_CG: it = cg(&c, x, b, tol_rel, tol_abs, tol_rb, maxit, &res); break;
     case SOLVER_GMRES: it = gmres(&c, x, b, tol_rel, tol_abs, tol_rb, maxit, restart, &res); break;
+    case SOLVER_RGMRES: it = gmres_r(&c, x, b, tol_rel, tol_abs, tol_rb, maxit, restart, &res); break;
     default: it = -1;
     }
     if (trace_len) *trace_len = c.len;

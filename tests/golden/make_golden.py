@@ -118,7 +118,7 @@ def main():
                             "apply_from_ref": applied is not None})
 
     # 4/5. solver traces (every dot/norm the driver computed, in order)
-    B, G, C = O.BICGSTAB, O.GMRES, O.CG
+    B, G, C, RG = O.BICGSTAB, O.GMRES, O.CG, O.RGMRES
     solves = [
         (B, {"kind": "iluk", "level": 0}, P7(32), "ones", None, {}),
         (B, {"kind": "iluk", "level": 0}, P7(64), "ones", None, {}),
@@ -145,6 +145,15 @@ def main():
         (B, {"kind": "bj", "nblk": 8}, P7(64), "ones", None, {}),
         (G, {"kind": "bj", "nblk": 4}, P7(32), "ones", None, {"restart": 30}),
         (C, {"kind": "bj", "nblk": 4}, P7(32), "ones", None, {}),
+        # right-preconditioned GMRES (solver-gmres.cxx:257-479)
+        (RG, {"kind": "ilut", "tol": 1e-4, "p": 20}, P7(32), "ones", None, {"restart": 30}),
+        (RG, {"kind": "iluk", "level": 0}, P7(32), "ones", None, {"restart": 30}),
+        (RG, {"kind": "iluk", "level": 1}, P5(100), "ones", None, {"restart": 60, "maxit": 3000}),
+        (RG, {"kind": "none"}, P7(16), "ones", None, {"restart": 10}),
+        (RG, {"kind": "iluk", "level": 0}, P7(16), "ones", None, {"maxit": 13, "restart": 5}),
+        (RG, {"kind": "ilut", "tol": 1e-3, "p": 5}, RND2, 0x5EED, 0xB0B, {"restart": 20}),
+        (RG, {"kind": "bj", "nblk": 4}, P7(32), "ones", None, {"restart": 30}),
+        (RG, {"kind": "iluk", "level": 0}, P7(16), "zeros", None, {}),
     ]
     pcmap = {"none": O.PC_NON, "iluk": O.PC_ILUK, "ilut": O.PC_ILUT}
     for solver, pc, mat, bspec, x0spec, kw in solves:

@@ -126,7 +126,9 @@ def test_solver_tree_mode_bitwise_vs_oracle(dev, c):
     assert r.nits == o.nits
     assert r.residual == o.residual
     assert np.array_equal(r.trace, o.trace)
-    assert np.array_equal(x.download(), o.x)
+    # NaN compared as NaN: GMRES-R hitting maxit mid-cycle divides 0/0 in the
+    # reference (solver-gmres.cxx:414-418 use a zeroed Hessenberg column)
+    assert np.array_equal(x.download(), o.x, equal_nan=True)
     assert abs(r.nits - c["nits"]) <= max(1, c["nits"] // 20)
 
 
