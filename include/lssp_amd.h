@@ -37,7 +37,7 @@ enum {
 };
 
 /* LSSP_SOLVER_TYPE values of the reference (type-defs.h:157-178) */
-enum { LSSP_AMD_GMRES = 0, LSSP_AMD_RGMRES = 2, LSSP_AMD_BICGSTAB = 4, LSSP_AMD_CG = 7 };
+enum { LSSP_AMD_GMRES = 0, LSSP_AMD_LGMRES = 1, LSSP_AMD_RGMRES = 2, LSSP_AMD_BICGSTAB = 4, LSSP_AMD_CG = 7 };
 /* ILU kinds (LSSP_PC_TYPE, type-defs.h:63-101) */
 enum { LSSP_AMD_ILUK = 1, LSSP_AMD_ILUT = 2 };
 
@@ -124,17 +124,18 @@ int lssp_amd_ilu_get_factors(const lssp_amd_ilu *M, int *Lp, int *Lj, double *Lx
 
 /* ---- Krylov solve: lssp_solver_solve (lssp.cxx:250-414) for BiCGSTAB
  *      (solver-bicgstab.cxx:10-175), GMRES(m) (solver-gmres.cxx:12-255),
- *      right-preconditioned GMRES(m) (solver-gmres.cxx:257-479) and CG
- *      (solver-cg.cxx:8-136).  Same recurrences, guards, defaults and
+ *      right-preconditioned GMRES(m) (solver-gmres.cxx:257-479), LGMRES(m, k)
+ *      (solver-lgmres.cxx:12-312) and CG (solver-cg.cxx:8-136).  Same recurrences, guards, defaults and
  *      iteration counting; vectors stay in HBM. ------------------------- */
 typedef struct {
-    int solver;     /* LSSP_AMD_GMRES / _RGMRES / _BICGSTAB / _CG */
+    int solver;     /* LSSP_AMD_GMRES / _LGMRES / _RGMRES / _BICGSTAB / _CG */
     double tol_rel; /* < 0: default 1e-7 (lssp.cxx:11-13) */
     double tol_abs;
     double tol_rb;
     int maxit;      /* <= 0: default 1000 */
     int restart;    /* GMRES m; < 0: default 50 */
     int verb;       /* >= 1 prints the reference's per-iteration line */
+    int aug_k;      /* LGMRES augmentation vectors k; <= 0: default 3 (lssp.cxx:6) */
 } lssp_amd_solve_params;
 
 /* x: device, x0 on entry, solution on exit; b: device.  M == NULL is PC_NON

@@ -1,13 +1,13 @@
 // amd_backend.cxx -- the reference-side binding: route LSSP's Krylov hot path
-// (BiCGSTAB / GMRES(m) / right-preconditioned GMRES(m) / CG with PC_NON, ILUK
-// or ILUT) to lssp_amd on MI355X.
+// (BiCGSTAB / GMRES(m) / right-preconditioned GMRES(m) / LGMRES(m, k) / CG with
+// PC_NON, ILUK or ILUT) to lssp_amd on MI355X.
 //
 // This is the translation unit a maintainer adds to huiscliu/lssp (as
 // src/amd-backend.cxx); INTEGRATION.md describes it.  It compiles against the
-// reference's own headers and replaces, at link time, the four drivers that
+// reference's own headers and replaces, at link time, the five drivers that
 // lssp_solver_solve dispatches to (lssp.cxx:259-289):
 //
-//     -Wl,--wrap=<mangled lssp_solver_bicgstab / _gmres / _gmres_r / _cg>
+//     -Wl,--wrap=<mangled lssp_solver_bicgstab / _gmres / _gmres_r / _lgmres / _cg>
 //
 // so lssp.cxx, the drivers and every caller (example/exam.cxx) stay unchanged.
 // Everything else (assemble, the column sort, the ILU setup of pc-iluk.cxx /
@@ -30,6 +30,8 @@ int __real__Z20lssp_solver_bicgstabR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP
 int __real__Z17lssp_solver_gmresR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
 int __real__Z14lssp_solver_cgR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
 int __real__Z19lssp_solver_gmres_rR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
+int __real__Z18lssp_solver_lgmresR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
+int __wrap__Z18lssp_solver_lgmresR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
 int __wrap__Z19lssp_solver_gmres_rR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
 int __wrap__Z20lssp_solver_bicgstabR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
 int __wrap__Z17lssp_solver_gmresR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
@@ -82,6 +84,7 @@ static int amd_solve(LSSP_SOLVER &s, LSSP_PC &pc, int solver)
     p.maxit = s.maxit;
     p.restart = s.restart;
     p.verb = s.verb;
+    p.aug_k = s.aug_k;
     int nits = 0;
     double res = 0.;
     fflush(stdout);  // the device driver prints with stdio too: keep the line order
@@ -120,4 +123,10 @@ int __wrap__Z19lssp_solver_gmres_rR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &s, LSSP
 {
     if (!amd_handles(pc)) return __real__Z19lssp_solver_gmres_rR12LSSP_SOLVER_R8LSSP_PC_(s, pc);
     return amd_solve(s, pc, LSSP_AMD_RGMRES);
+}
+
+int __wrap__Z18lssp_solver_lgmresR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &s, LSSP_PC &pc)
+{
+    if (!amd_handles(pc)) return __real__Z18lssp_solver_lgmresR12LSSP_SOLVER_R8LSSP_PC_(s, pc);
+    return amd_solve(s, pc, LSSP_AMD_LGMRES);
 }

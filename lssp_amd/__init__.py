@@ -15,8 +15,8 @@ from . import _lib
 
 _lib.load()
 
-from .device import (BICGSTAB, CG, GMRES, RGMRES, ILUK, ILUT, SERIAL, TREE, DILU, DMat,  # noqa: E402,F401
+from .device import (BICGSTAB, CG, GMRES, LGMRES, RGMRES, ILUK, ILUT, SERIAL, TREE, DILU, DMat,  # noqa: E402,F401
                      Device, DVec, LsspError, comm_unique_id, poisson, solve, sort_columns)
 
 __all__ = ["Device", "DVec", "DMat", "DILU", "solve", "poisson", "sort_columns", "LsspError",
-           "comm_unique_id", "GMRES", "RGMRES", "BICGSTAB", "CG", "ILUK", "ILUT", "SERIAL", "TREE"]
+           "comm_unique_id", "GMRES", "LGMRES", "RGMRES", "BICGSTAB", "CG", "ILUK", "ILUT", "SERIAL", "TREE"]

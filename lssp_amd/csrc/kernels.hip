@@ -554,6 +554,9 @@ enum EwKind {
     EW_GM_X,       // out0[q] += sum_{i<k} vbase[i][q] * scal[S_H..]  (:196-204); ym passed in u
     EW_GMR_Z,      // out0 = v_{k-1}*y_{k-1}, then out0 = out0*1 + v_i*y_i, i = k-2 .. 0
                    // (solver-gmres.cxx:417-423, right-preconditioned GMRES); ym in u
+    EW_LGM_X,      // t = sum_{i<min(k,mk)} v_i*y_i (+ sum_{i<nz} z_i*y_{mk+i} when k > mk);
+                   // out0 += t; out1 = t  (solver-lgmres.cxx:224-251); ym in u, mk in sidx,
+                   // nz in k >> 16, z basis in v (stride as vbase)
 };
 
 struct EwArgs {
@@ -618,6 +621,20 @@ __global__ __launch_bounds__(256) void k_ew(EwArgs g)
                 double acc = 0;
                 for (int q = 0; q < g.k; q++) acc += g.vbase[(long)q * ld + i] * g.u[q];
                 g.out0[i] += acc;
+                break;
+            }
+            case EW_LGM_X: {
+                const long ld = (long)g.b;
+                const int kk = (short)(g.k & 0xffff), nz = g.k >> 16, mk = g.sidx;
+                double t = 0;
+                if (kk <= mk) {
+                    for (int q = 0; q < kk; q++) t += g.vbase[(long)q * ld + i] * g.u[q];
+                } else {
+                    for (int q = 0; q < mk; q++) t += g.vbase[(long)q * ld + i] * g.u[q];
+                    for (int q = 0; q < nz; q++) t += g.v[(long)q * ld + i] * g.u[q + mk];
+                }
+                g.out0[i] += t;
+                g.out1[i] = t;
                 break;
             }
             case EW_GMR_Z: {

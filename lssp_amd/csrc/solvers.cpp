@@ -28,7 +28,7 @@ constexpr double DEF_TOL = 1e-7;     // lssp.cxx:11-13
 
 enum EwK {  // mirror of kernels.hip EwKind
     K_FILL = 0, K_COPY, K_AXY, K_AXPBY, K_AXPBYZ, K_SCALE, K_DIVS, K_DOT,
-    K_BICG_P, K_BICG_S, K_BICG_XR, K_CG_P, K_CG_XR, K_GM_MGS, K_GM_X, K_GMR_Z
+    K_BICG_P, K_BICG_S, K_BICG_XR, K_CG_P, K_CG_XR, K_GM_MGS, K_GM_X, K_GMR_Z, K_LGM_X
 };
 
 struct Run {
@@ -689,6 +689,179 @@ int gmres_r(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, 
     return LSSP_AMD_OK;
 }
 
+// ---------------------------------------------------------------------------
+// LGMRES(m, k) (solver-lgmres.cxx:12-312): left-preconditioned GMRES(m)
+// augmented with the last k corrections z; the cycle's basis grows by one z per
+// cycle up to m + k.  Kept exactly as the reference has it:
+//   * v_{i+1} = w / h and v_0 /= beta are true divisions (:192-194, :149-151);
+//   * the solve uses kk = i columns (:216), so a gstol exit drops the last one;
+//   * the x update sums min(kk, m) basis terms, then -- when kk > m -- the
+//     first min(cycle, k) z terms with y[m + i] (:226-245), whether or not this
+//     cycle set them (y persists across cycles; it starts at zero here).
+// ---------------------------------------------------------------------------
+int lgmres(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
+{
+    lssp_amd_ctx *c = R.c;
+    double tol_rel, tol_abs, tol_rb = P.tol_rb;
+    int maxit;
+    defaults(P, tol_rel, tol_abs, maxit);
+    const int mk = P.restart < 0 ? DEF_RESTART : P.restart;
+    const int auk = P.aug_k <= 0 ? 3 : P.aug_k;  // lssp.cxx:6
+    if (tol_rb < 0) tol_rb = DEF_TOL;
+    if (mk <= 0) return LSSP_AMD_EINVAL;
+    const int mmax = mk + auk;
+    if (S_H + 2 * mmax + 2 > NSCAL || mmax > 0x7fff || auk > 0x7fff) return LSSP_AMD_EUNSUPPORTED;
+    if (P.verb >= 2 && R.rank == 0) {
+        printf("lgmres: restart parameter m: %d\n", mk);
+        printf("lgmres: aug k: %d\n", auk);
+        printf("lgmres: maximal iteration: %d\n", maxit);
+        printf("lgmres: tolerance abs: %g\n", tol_abs);
+        printf("lgmres: tolerance rel: %g\n", tol_rel);
+        printf("lgmres: tolerance rbn: %g\n", tol_rb);
+    }
+    double *wj = R.vec(), *rg = R.vec();
+    double *V = R.vec(R.nx * (long)mmax);
+    double *Z = R.vec(R.nx * (long)auk);
+    double *d_ym = R.vec(mmax);
+    if (!wj || !rg || !V || !Z || !d_ym) return LSSP_AMD_ENOMEM;
+    auto Vi = [&](int i) { return V + (long)i * R.nx; };
+    auto Zi = [&](int i) { return Z + (long)i * R.nx; };
+    std::vector<double> H((size_t)(mmax + 1) * mmax), gg(mmax + 1), cs(mmax), sn(mmax), ym(mmax, 0.0);
+    auto HG = [&](int row, int col) -> double & { return H[(size_t)row * mmax + col]; };
+
+    LSSP_TRY(R.dot1(b, b, R.fin(FIN_NORM, 1, R.T(), -1, S_BNORM)));  // :108
+    LSSP_TRY(R.spmv(EPI_AXPBY, -1, x, 1, b, rg));                     // :111
+    LSSP_TRY(R.dot1(rg, rg, R.fin(FIN_NORM, 1, R.T(), -1, S_RES)));  // :112
+    LSSP_TRY(R.sync(0, 16));
+    const double b_norm = R.h(S_BNORM);
+    tol_rb *= b_norm;
+    double beta = R.h(S_RES);
+    int inner = 0, outer = 0;
+    if (beta <= tol_abs) {
+        *nits = 0;
+        *res_out = beta;
+        return LSSP_AMD_OK;
+    }
+    const double err_rel = beta;
+    double tol = tol_rel * err_rel;
+    if (tol < tol_abs) tol = tol_abs;
+    if (tol < tol_rb) tol = tol_rb;
+    const double rtol = tol / beta;
+    double gstol = 0.;
+
+    while (inner < maxit) {
+        int i, kk;
+        double gs_norm = 0.;
+        LSSP_TRY(R.pc(Vi(0), rg));                                             // :130-131
+        LSSP_TRY(R.dot1(Vi(0), Vi(0), R.fin(FIN_NORM, 1, R.T(), -1, S_TMP)));  // :133
+        LSSP_TRY(R.sync(0, 16));
+        beta = R.h(S_TMP);
+        const int m = outer < auk ? mk + outer : mk + auk;  // :136-141
+        std::fill(gg.begin(), gg.end(), 0.0);
+        gg[0] = beta;
+        if (outer == 0) gstol = rtol * beta * 0.5;  // :148-150
+        std::fill(H.begin(), H.end(), 0.0);
+        {
+            Ew e;
+            e.kind = K_DIVS;  // :156-158
+            e.out0 = Vi(0);
+            e.sidx = S_TMP;
+            LSSP_TRY(R.ew(e));
+        }
+        for (i = 0; i < m; i++) {
+            inner++;
+            LSSP_TRY(R.spmv(EPI_MXY, 1, i < mk ? Vi(i) : Zi(i - mk), 0, nullptr, rg));  // :165-171
+            LSSP_TRY(R.pc(wj, rg));                                                    // :173-174
+            LSSP_TRY(R.dot1(wj, Vi(0), R.fin(FIN_STORE, 1, R.T(), -1, S_H)));         // :177, j = 0
+            for (int j = 0; j <= i; j++) {  // :176-181
+                Ew e;
+                e.kind = K_GM_MGS;
+                e.out0 = wj;
+                e.x = Vi(j);
+                e.sidx = S_H + j;
+                e.nred = 1;
+                e.r0a = wj;
+                e.r0b = j < i ? Vi(j + 1) : wj;
+                LSSP_TRY(R.ew(e));
+                if (j < i)
+                    LSSP_TRY(R.fin1(wj, Vi(j + 1), R.fin(FIN_STORE, 1, R.T(), -1, S_H + j + 1)));
+                else
+                    LSSP_TRY(R.fin1(wj, wj, R.fin(FIN_NORM, 1, R.T(), -1, S_H + i + 1)));  // :183
+            }
+            LSSP_TRY(R.sync(0, S_H + i + 2));
+            for (int j = 0; j <= i; j++) HG(j, i) = R.h(S_H + j);
+            const double hij = R.h(S_H + i + 1);
+            HG(i + 1, i) = hij;
+            if (std::fabs(hij) <= BREAKDOWN) {  // :186-189
+                i--;
+                break;
+            } else if (i + 1 < m) {  // :191-195: v_{i+1} = w / h, a true division
+                Ew cp;
+                cp.kind = K_COPY;
+                cp.x = wj;
+                cp.out0 = Vi(i + 1);
+                LSSP_TRY(R.ew(cp));
+                Ew e;
+                e.kind = K_DIVS;
+                e.out0 = Vi(i + 1);
+                e.sidx = S_H + i + 1;
+                LSSP_TRY(R.ew(e));
+            }
+            for (int j = 0; j < i; j++) {  // :197-203
+                const double h1 = cs[j] * HG(j, i) + sn[j] * HG(j + 1, i);
+                const double h2 = -sn[j] * HG(j, i) + cs[j] * HG(j + 1, i);
+                HG(j, i) = h1;
+                HG(j + 1, i) = h2;
+            }
+            double gma = std::sqrt(HG(i, i) * HG(i, i) + HG(i + 1, i) * HG(i + 1, i));  // :205
+            if (std::fabs(gma) == 0.) gma = 1e-20;
+            cs[i] = HG(i, i) / gma;
+            sn[i] = HG(i + 1, i) / gma;
+            gg[i + 1] = -sn[i] * gg[i];
+            gg[i] = cs[i] * gg[i];
+            HG(i, i) = cs[i] * HG(i, i) + sn[i] * HG(i + 1, i);
+            gs_norm = std::fabs(gg[i + 1]);
+            if (gs_norm <= gstol) break;  // :216-218 (goto solve: i not advanced)
+        }
+        kk = i;  // :221
+        for (i = kk - 1; i >= 0; i--) {  // :222-230
+            ym[i] = gg[i] / HG(i, i);
+            for (int j = 0; j < i; j++) gg[j] = gg[j] - ym[i] * HG(j, i);
+        }
+        memcpy(c->h_scal + NSCAL - mmax, ym.data(), sizeof(double) * mmax);
+        LSSP_HIP(hipMemcpyAsync(d_ym, c->h_scal + NSCAL - mmax, sizeof(double) * mmax, hipMemcpyHostToDevice,
+                                c->stream));
+        {
+            const int zn = outer % auk, nz = outer <= auk ? outer : auk;  // :233, :240-246
+            Ew e;
+            e.kind = K_LGM_X;  // :234-251
+            e.out0 = x;
+            e.out1 = Zi(zn);
+            e.vbase = V;
+            e.v = Z;
+            e.u = d_ym;
+            e.sidx = mk;
+            e.k = (kk & 0xffff) | (nz << 16);
+            e.b = (double)R.nx;  // basis stride
+            LSSP_TRY(R.ew(e));
+        }
+        LSSP_TRY(R.spmv(EPI_AXPBY, -1, x, 1, b, rg));                     // :253
+        LSSP_TRY(R.dot1(rg, rg, R.fin(FIN_NORM, 1, R.T(), -1, S_RES)));  // :254
+        LSSP_TRY(R.sync(0, 16));
+        beta = R.h(S_RES);
+        if (P.verb >= 1 && R.rank == 0)
+            printf("lgmres: itr: %4d / %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", outer, inner, beta,
+                   (err_rel == 0 ? 0 : beta / err_rel), (b_norm == 0 ? 0 : beta / b_norm));
+        if (beta <= tol) break;                                  // :262
+        gstol = rtol * gs_norm / (beta / err_rel) * 0.5;          // :265
+        outer++;
+    }
+    if (P.verb >= 2 && R.rank == 0) printf("lgmres: total iteration: %d\n", inner);
+    *nits = inner;
+    *res_out = beta;
+    return LSSP_AMD_OK;
+}
+
 }  // namespace
 }  // namespace lssp_amd
 
@@ -728,6 +901,7 @@ extern "C" int lssp_amd_solve(lssp_amd_ctx *c, const lssp_amd_mat *A, const lssp
     case LSSP_AMD_CG: st = cg(R, *prm, x, b, &it, &res); break;
     case LSSP_AMD_GMRES: st = gmres(R, *prm, x, b, &it, &res); break;
     case LSSP_AMD_RGMRES: st = gmres_r(R, *prm, x, b, &it, &res); break;
+    case LSSP_AMD_LGMRES: st = lgmres(R, *prm, x, b, &it, &res); break;
     default: st = LSSP_AMD_EUNSUPPORTED;
     }
     c->d_trace = saved_trace;

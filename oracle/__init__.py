@@ -28,7 +28,7 @@ ORACLE_SO = os.path.join(HERE, "_build", "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libref.so")
 
 # LSSP_SOLVER_TYPE / LSSP_PC_TYPE values (type-defs.h:63-101, :157-178)
-GMRES, RGMRES, BICGSTAB, CG = 0, 2, 4, 7
+GMRES, LGMRES, RGMRES, BICGSTAB, CG = 0, 1, 2, 4, 7
 PC_NON, PC_ILUK, PC_ILUT = 0, 1, 2
 SERIAL, TREE = 0, 1
 

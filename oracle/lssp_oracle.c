@@ -838,7 +838,7 @@ EXPORT void orc_ilu_free(void *hp)
 /* Krylov drivers                                                           */
 /* ------------------------------------------------------------------------ */
 
-enum { SOLVER_GMRES = 0, SOLVER_RGMRES = 2, SOLVER_BICGSTAB = 4, SOLVER_CG = 7 }; /* type-defs.h:157-178 */
+enum { SOLVER_GMRES = 0, SOLVER_LGMRES = 1, SOLVER_RGMRES = 2, SOLVER_BICGSTAB = 4, SOLVER_CG = 7 }; /* type-defs.h:157-178 */
 
 typedef struct {
     const csr_t *A;
@@ -1204,6 +1204,125 @@ done:
     return inner;
 }
 
+/* solver-lgmres.cxx:12-312: LGMRES(m, k), left preconditioned, augmented with
+ * the last k corrections (k = LSSP_AUG_K = 3, lssp.cxx:6).  Quirks kept: true
+ * divisions for v_0 and v_{i+1}; the solve uses kk = i columns; the x update
+ * reads y[m + i] for the first min(cycle, k) z vectors whenever kk > m (y
+ * persists across cycles; the reference mallocs it uninitialised, zero here). */
+static int lgmres(ctx_t *c, double *x, const double *b, double tol_rel, double tol_abs,
+                  double tol_rb, int maxit, int mk, double *res_out)
+{
+    const csr_t *A = c->A;
+    int n = A->nrows, inner = 0, outer = 0, auk = 3;
+    if (mk < 0) mk = DEF_RESTART;
+    if (maxit <= 0) maxit = DEF_MAXIT;
+    if (tol_abs < 0) tol_abs = DEF_TOL;
+    if (tol_rel < 0) tol_rel = DEF_TOL;
+    if (tol_rb < 0) tol_rb = DEF_TOL;
+    int mmax = mk + auk;
+    size_t bytes = sizeof(double) * (size_t)n;
+    double *wj = malloc(bytes), *rg = malloc(bytes);
+    double **v = malloc(sizeof(double *) * (size_t)mmax);
+    for (int i = 0; i < mmax; i++) v[i] = malloc(bytes);
+    double **z = malloc(sizeof(double *) * (size_t)auk);
+    for (int i = 0; i < auk; i++) z[i] = malloc(bytes);
+    double *gg = malloc(sizeof(double) * (size_t)(mmax + 1)), *ym = calloc((size_t)mmax, sizeof(double));
+    double *H = malloc(sizeof(double) * (size_t)(mmax + 1) * (size_t)mmax);
+    double *cs = malloc(sizeof(double) * (size_t)mmax), *sn = malloc(sizeof(double) * (size_t)mmax);
+#define HG(r, col) H[(size_t)(r) * (size_t)mmax + (size_t)(col)]
+    double tol = 0, err_rel = 0, beta, rtol, gstol = 0.;
+
+    double bnorm = tnorm(c, b);
+    tol_rb *= bnorm;
+    mv_amxpbyz(-1, A, x, 1, b, rg);
+    beta = tnorm(c, rg);
+    if (beta <= tol_abs) goto done;
+    err_rel = beta;
+    tol = tol_rel * err_rel;
+    if (tol < tol_abs) tol = tol_abs;
+    if (tol < tol_rb) tol = tol_rb;
+    rtol = tol / beta;
+
+    while (inner < maxit) {
+        int i, kk, m;
+        double gs_norm = 0.;
+        pc_apply(c, v[0], rg);
+        beta = tnorm(c, v[0]);
+        m = outer < auk ? mk + outer : mk + auk;
+        gg[0] = beta;
+        for (kk = 1; kk <= m; kk++) gg[kk] = 0;
+        if (outer == 0) gstol = rtol * beta * 0.5;
+        for (size_t q = 0; q < (size_t)(mmax + 1) * (size_t)mmax; q++) H[q] = 0;
+        for (int q = 0; q < n; q++) v[0][q] /= beta;
+        for (i = 0; i < m; i++) {
+            double h;
+            inner++;
+            mv_mxy(A, i < mk ? v[i] : z[i - mk], rg);
+            pc_apply(c, wj, rg);
+            for (int j = 0; j <= i; j++) {
+                h = tdot(c, wj, v[j]);
+                for (int q = 0; q < n; q++) wj[q] = wj[q] * 1 + v[j][q] * (-h);
+                HG(j, i) = h;
+            }
+            h = tnorm(c, wj);
+            HG(i + 1, i) = h;
+            if (fabs(h) <= BREAKDOWN) {
+                i--;
+                break;
+            } else if (i + 1 < m) {
+                for (int q = 0; q < n; q++) v[i + 1][q] = wj[q] / h;
+            }
+            for (int j = 0; j < i; j++) {
+                double h1 = cs[j] * HG(j, i) + sn[j] * HG(j + 1, i);
+                double h2 = -sn[j] * HG(j, i) + cs[j] * HG(j + 1, i);
+                HG(j, i) = h1;
+                HG(j + 1, i) = h2;
+            }
+            double gma = sqrt(HG(i, i) * HG(i, i) + HG(i + 1, i) * HG(i + 1, i));
+            if (fabs(gma) == 0.) gma = 1e-20;
+            cs[i] = HG(i, i) / gma;
+            sn[i] = HG(i + 1, i) / gma;
+            gg[i + 1] = -sn[i] * gg[i];
+            gg[i] = cs[i] * gg[i];
+            HG(i, i) = cs[i] * HG(i, i) + sn[i] * HG(i + 1, i);
+            gs_norm = fabs(gg[i + 1]);
+            if (gs_norm <= gstol) break;
+        }
+        kk = i;
+        for (i = kk - 1; i >= 0; i--) {
+            ym[i] = gg[i] / HG(i, i);
+            for (int j = 0; j < i; j++) gg[j] = gg[j] - ym[i] * HG(j, i);
+        }
+        {
+            int zn = outer % auk, nz = outer <= auk ? outer : auk;
+            for (int q = 0; q < n; q++) {
+                double t = 0;
+                if (kk <= mk) {
+                    for (i = 0; i < kk; i++) t += v[i][q] * ym[i];
+                } else {
+                    for (i = 0; i < mk; i++) t += v[i][q] * ym[i];
+                    for (i = 0; i < nz; i++) t += z[i][q] * ym[i + mk];
+                }
+                x[q] += t;
+                z[zn][q] = t;
+            }
+        }
+        mv_amxpbyz(-1, A, x, 1, b, rg);
+        beta = tnorm(c, rg);
+        if (beta <= tol) break;
+        gstol = rtol * gs_norm / (beta / err_rel) * 0.5;
+        outer++;
+    }
+#undef HG
+done:
+    *res_out = beta;
+    free(wj); free(rg);
+    for (int i = 0; i < mmax; i++) free(v[i]);
+    for (int i = 0; i < auk; i++) free(z[i]);
+    free(v); free(z); free(gg); free(ym); free(H); free(cs); free(sn);
+    return inner;
+}
+
 /* Solve A x = b (x holds x0 on entry).  L/U == NULL => PC_NON.
  * trace receives every dot/norm the driver computes, in call order (the same
  * sequence tests/golden records from the reference). */
@@ -1235,6 +1354,7 @@ EXPORT int orc_solve(int solver, int n, const int *Ap, const int *Aj, const doub
     case SOLVER_CG: it = cg(&c, x, b, tol_rel, tol_abs, tol_rb, maxit, &res); break;
     case SOLVER_GMRES: it = gmres(&c, x, b, tol_rel, tol_abs, tol_rb, maxit, restart, &res); break;
     case SOLVER_RGMRES: it = gmres_r(&c, x, b, tol_rel, tol_abs, tol_rb, maxit, restart, &res); break;
+    case SOLVER_LGMRES: it = lgmres(&c, x, b, tol_rel, tol_abs, tol_rb, maxit, restart, &res); break;
     default: it = -1;
     }
     if (trace_len) *trace_len = c.len;

@@ -118,7 +118,7 @@ def main():
                             "apply_from_ref": applied is not None})
 
     # 4/5. solver traces (every dot/norm the driver computed, in order)
-    B, G, C, RG = O.BICGSTAB, O.GMRES, O.CG, O.RGMRES
+    B, G, C, RG, LG = O.BICGSTAB, O.GMRES, O.CG, O.RGMRES, O.LGMRES
     solves = [
         (B, {"kind": "iluk", "level": 0}, P7(32), "ones", None, {}),
         (B, {"kind": "iluk", "level": 0}, P7(64), "ones", None, {}),
@@ -154,6 +154,15 @@ def main():
         (RG, {"kind": "ilut", "tol": 1e-3, "p": 5}, RND2, 0x5EED, 0xB0B, {"restart": 20}),
         (RG, {"kind": "bj", "nblk": 4}, P7(32), "ones", None, {"restart": 30}),
         (RG, {"kind": "iluk", "level": 0}, P7(16), "zeros", None, {}),
+        # LGMRES(m, k = 3) (solver-lgmres.cxx:12-312)
+        (LG, {"kind": "ilut", "tol": 1e-4, "p": 20}, P7(32), "ones", None, {"restart": 30}),
+        (LG, {"kind": "iluk", "level": 0}, P7(32), "ones", None, {"restart": 10}),
+        (LG, {"kind": "iluk", "level": 1}, P5(100), "ones", None, {"restart": 20}),
+        (LG, {"kind": "none"}, P7(16), "ones", None, {"restart": 8}),
+        (LG, {"kind": "iluk", "level": 0}, P7(16), "ones", None, {"maxit": 13, "restart": 5}),
+        (LG, {"kind": "ilut", "tol": 1e-3, "p": 5}, RND2, 0x5EED, 0xB0B, {"restart": 6}),
+        (LG, {"kind": "bj", "nblk": 4}, P7(32), "ones", None, {"restart": 12}),
+        (LG, {"kind": "iluk", "level": 0}, P7(16), "zeros", None, {}),
     ]
     pcmap = {"none": O.PC_NON, "iluk": O.PC_ILUK, "ilut": O.PC_ILUT}
     for solver, pc, mat, bspec, x0spec, kw in solves:
