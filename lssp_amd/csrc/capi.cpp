@@ -219,6 +219,7 @@ int lssp_amd_mat_upload(lssp_amd_ctx *c, int nrows, int ncols, int nnz, const in
     M->nnz = nnz;
     M->n_global = nrows;
     int st = upload_csr(M, Ap, Aj, Ax);
+    if (st == LSSP_AMD_OK) st = plan_spmv_xt(M, Ap, Aj);
     if (st != LSSP_AMD_OK) {
         lssp_amd_mat_destroy(M);
         return st;
@@ -236,6 +237,8 @@ int lssp_amd_mat_destroy(lssp_amd_mat *M)
     if (M->Ax) (void)hipFree(M->Ax);
     if (M->d_send_idx) (void)hipFree(M->d_send_idx);
     if (M->d_send_buf) (void)hipFree(M->d_send_buf);
+    if (M->d_xt_lo) (void)hipFree(M->d_xt_lo);
+    if (M->d_xt_span) (void)hipFree(M->d_xt_span);
     delete M;
     return LSSP_AMD_OK;
 }

@@ -102,6 +102,11 @@ struct lssp_amd_mat {
     int *d_send_idx = nullptr;
     double *d_send_buf = nullptr;
     int nsend = 0;
+    // x-tile SpMV plan (kernels.hip k_spmv_xt): per XT_ROWS-row block the first
+    // column and the column span; set only when the gathers are scattered and
+    // every block's span fits the LDS tile
+    int *d_xt_lo = nullptr, *d_xt_span = nullptr;
+    bool xt = false;
 };
 
 namespace lssp_amd {
@@ -223,6 +228,8 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
                    TriSched &t);
 int launch_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const double *rhs);
 int launch_pack(lssp_amd_ctx *c, const int *idx, const double *x, double *buf, int n);
+// x-tile SpMV plan for a host CSR (capi.cpp upload): decides and uploads
+int plan_spmv_xt(lssp_amd_mat *M, const int *Ap, const int *Aj);
 int launch_sum_ranks(lssp_amd_ctx *c, int nslot, const Fin &f);
 
 long num_chunks(long n);

@@ -15,6 +15,10 @@
 // oracle/lssp_oracle.c (dot_tree) restates this order on the CPU.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <climits>
+#include <vector>
+
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -478,6 +482,109 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
     }
 }
 
+// x-tile SpMV for matrices whose x gathers are scattered (unstructured rows,
+// e.g. config 5): a gather instruction whose 64 lanes hit 64 different cache
+// lines costs ~64 L1/TA cycles, so instead each 1024-row block first copies
+// the x range its rows touch, [lo, lo + span), into LDS with coalesced loads,
+// and its rows then gather from LDS.  One row per thread, entries in CSR
+// order from 0.0 (mvops.cxx:55-58) -- bitwise the same sums as k_spmv3.  A
+// block's four 256-row quarters are the canonical reduction chunks.
+constexpr int XT_ROWS = 1024;
+constexpr int XT_CAP = 16384;  // doubles in the LDS tile (128 KB)
+template <int EPI, int NRED>
+__global__ __launch_bounds__(XT_ROWS) void k_spmv_xt(SpmvArgs a, const int *xt_lo, const int *xt_span, long nblk)
+{
+    __shared__ double tile[XT_CAP];
+    __shared__ double lds[4][MAX_SLOTS][4];
+    const long per = gridDim.x / 8;
+    const long blk = (blockIdx.x % 8) * per + blockIdx.x / 8;  // XCD-contiguous, as k_spmv3
+    if (blk >= nblk) return;
+    const int tid = threadIdx.x;
+    const int r = (int)(blk * XT_ROWS) + tid;
+    const int lo = xt_lo[blk], span = xt_span[blk];
+    for (int i = tid; i < span; i += XT_ROWS) tile[i] = a.x[lo + i];
+    __syncthreads();
+    double sum = 0;
+    if (r < a.nrows) {
+        const int rb = a.Ap[r], re = a.Ap[r + 1], len = re - rb;
+        if (len > 0 && len <= 12) {
+            double pr[12];
+#pragma unroll
+            for (int u = 0; u < 12; u++) {
+                const int k = min(rb + u, re - 1);
+                pr[u] = tile[a.Aj[k] - lo] * a.Ax[k];
+            }
+#pragma unroll
+            for (int u = 0; u < 12; u++)
+                if (u < len) sum += pr[u];
+        } else {
+            for (int k = rb; k < re; k++) sum += tile[a.Aj[k] - lo] * a.Ax[k];
+        }
+    }
+    double zv = 0;
+    if (r < a.nrows) {
+        if (EPI == EPI_MXY) zv = sum;
+        else if (EPI == EPI_AMXY) zv = sum * a.alpha;
+        else if (EPI == EPI_AXPBY) zv = a.y[r] * a.beta + a.alpha * sum;
+        else zv = a.alpha * sum;
+        a.z[r] = zv;
+    }
+    if (NRED > 0) {
+        double v[NRED > 0 ? NRED : 1];
+        if (r < a.nrows) {
+            v[0] = zv * a.w0[r];
+            if (NRED > 1) v[NRED > 1 ? 1 : 0] = zv * (a.w1 ? a.w1[r] : zv);
+        } else {
+#pragma unroll
+            for (int q = 0; q < NRED; q++) v[q] = 0.0;
+        }
+        const int lane = tid & 63, wave = (tid >> 6) & 3, quarter = tid >> 8;
+#pragma unroll
+        for (int q = 0; q < NRED; q++) {
+            const double w = wave_sum(v[q]);
+            if (lane == 0) lds[quarter][q][wave] = w;
+        }
+        __syncthreads();
+        if ((tid & 255) == 0 && blk * 4 + quarter < (a.nrows + CHUNK - 1) / CHUNK) {
+#pragma unroll
+            for (int q = 0; q < NRED; q++)
+                a.part[q * a.pcap + blk * 4 + quarter] =
+                    (lds[quarter][q][0] + lds[quarter][q][1]) + (lds[quarter][q][2] + lds[quarter][q][3]);
+        }
+    }
+}
+
+// Decide and upload the x-tile plan: every 1024-row block's column span
+// must fit the LDS tile.
+int plan_spmv_xt(lssp_amd_mat *M, const int *Ap, const int *Aj)
+{
+    const int n = M->nrows;
+    // opt-in (LSSP_AMD_SPMV_XT=1): measured no faster than k_spmv3 on the
+    // thermal-like matrix of config 5 (40.9 vs 40.2 us per call)
+    const char *e = getenv("LSSP_AMD_SPMV_XT");
+    if (!e || atoi(e) == 0 || n <= 0 || M->nnz <= 0) return LSSP_AMD_OK;
+    const long nb = (n + XT_ROWS - 1) / XT_ROWS;
+    std::vector<int> lo(nb), span(nb);
+    for (long b = 0; b < nb; b++) {
+        const int r0 = (int)(b * XT_ROWS), r1 = std::min<int>(n, r0 + XT_ROWS);
+        int mn = INT_MAX, mx = -1;
+        for (int k = Ap[r0]; k < Ap[r1]; k++) {
+            mn = std::min(mn, Aj[k]);
+            mx = std::max(mx, Aj[k]);
+        }
+        if (mx < 0) mn = mx = 0;
+        lo[b] = mn;
+        span[b] = mx - mn + 1;
+        if (span[b] > XT_CAP) return LSSP_AMD_OK;  // some block does not fit: k_spmv3
+    }
+    LSSP_HIP(hipMalloc(&M->d_xt_lo, sizeof(int) * nb));
+    LSSP_HIP(hipMalloc(&M->d_xt_span, sizeof(int) * nb));
+    LSSP_HIP(hipMemcpy(M->d_xt_lo, lo.data(), sizeof(int) * nb, hipMemcpyHostToDevice));
+    LSSP_HIP(hipMemcpy(M->d_xt_span, span.data(), sizeof(int) * nb, hipMemcpyHostToDevice));
+    M->xt = true;
+    return LSSP_AMD_OK;
+}
+
 static int g_spmv_variant = -1;  // LSSP_AMD_SPMV: 4 k_spmv3 (default), 3 k_spmv + XCD order,
                                  // 0 k_spmv, 1 k_spmv2, 2 k_spmv2 + XCD order
 
@@ -520,6 +627,24 @@ int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, c
     long nb = num_chunks(A->nrows);
     LSSP_TRY(ensure_part(c, nb));
     SpmvArgs a{A->nrows, A->Ap, A->Aj, A->Ax, x, y, z, alpha, beta, w0, w1, c->d_part, c->part_cap};
+    if (A->xt) {
+        const long nxb = (A->nrows + XT_ROWS - 1) / XT_ROWS, g = (nxb + 7) / 8 * 8;
+#define LSSP_XT(E)                                                                                            \
+    do {                                                                                                      \
+        if (nred == 0) k_spmv_xt<E, 0><<<g, XT_ROWS, 0, c->stream>>>(a, A->d_xt_lo, A->d_xt_span, nxb);      \
+        else if (nred == 1) k_spmv_xt<E, 1><<<g, XT_ROWS, 0, c->stream>>>(a, A->d_xt_lo, A->d_xt_span, nxb); \
+        else k_spmv_xt<E, 2><<<g, XT_ROWS, 0, c->stream>>>(a, A->d_xt_lo, A->d_xt_span, nxb);               \
+    } while (0)
+        switch (epi) {
+        case EPI_MXY: LSSP_XT(EPI_MXY); break;
+        case EPI_AMXY: LSSP_XT(EPI_AMXY); break;
+        case EPI_AXPBY: LSSP_XT(EPI_AXPBY); break;
+        default: LSSP_XT(EPI_AMX); break;
+        }
+#undef LSSP_XT
+        LSSP_HIP(hipGetLastError());
+        return LSSP_AMD_OK;
+    }
     switch (epi) {
     case EPI_MXY: spmv_dispatch<EPI_MXY>(a, nred, nb, c->stream, A->nnz + 4L); break;
     case EPI_AMXY: spmv_dispatch<EPI_AMXY>(a, nred, nb, c->stream, A->nnz + 4L); break;

@@ -207,3 +207,57 @@ def test_gpu_ilu0_factorization_bitwise_vs_oracle(dev, seed, n, per_row, missing
         assert np.array_equal(Lp, L.Ap) and np.array_equal(Lj, L.Aj) and np.array_equal(Lx, L.Ax, equal_nan=True)
         assert np.array_equal(Up, U.Ap) and np.array_equal(Uj, U.Aj) and np.array_equal(Ux, U.Ax, equal_nan=True)
         M.close()
+
+
+def _scattered(n, seed, maxlen=20, reach=3000):
+    """random CSR whose columns scatter within +-reach of the row: rows of 0..maxlen
+    entries (empty rows and rows longer than the 12-entry unrolled path included)"""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, maxlen + 1, n)
+    lens[::97] = 0
+    Ap = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=Ap[1:])
+    Aj = np.empty(Ap[-1], np.int64)
+    for r in range(n):
+        lo, hi = max(0, r - reach), min(n, r + reach + 1)
+        Aj[Ap[r]:Ap[r + 1]] = np.sort(rng.choice(np.arange(lo, hi), lens[r], replace=False))
+    Ax = uniform(seed + 7, int(Ap[-1]))
+    return O.CSR(n, Ap.astype(np.int32), Aj.astype(np.int32), Ax)
+
+
+@pytest.mark.parametrize("xt", ["0", "1", None])
+@pytest.mark.parametrize("which", ["thermal", "scattered"])
+def test_spmv_xtile_bitwise_vs_oracle(dev, monkeypatch, xt, which):
+    """k_spmv_xt (x range staged in LDS per 1024-row block) and k_spmv3 give
+    the oracle's sums bit for bit (mvops.cxx:42-78, 118-150) on scattered-
+    column matrices; LSSP_AMD_SPMV_XT=1 selects the x-tile plan, None is the default."""
+    import lssp_amd
+    from lssp_amd.synthetic import thermal_like
+    if xt is None:
+        monkeypatch.delenv("LSSP_AMD_SPMV_XT", raising=False)
+    else:
+        monkeypatch.setenv("LSSP_AMD_SPMV_XT", xt)
+    if which == "thermal":
+        Ap, Aj, Ax = thermal_like(m=150, window=512)
+        A = O.CSR(Ap.size - 1, Ap, Aj, Ax)
+    else:
+        A = _scattered(5000, 11)
+    M = lssp_amd.DMat(dev, A.Ap, A.Aj, A.Ax)
+    xh, yh = uniform(0x5EED, A.n), uniform(3, A.n)
+    x, y, z = dev.vec(A.n, xh), dev.vec(A.n, yh), dev.vec(A.n, yh)
+    M.mv_mxy(x, z)
+    assert np.array_equal(z.download(), O.spmv(0, A, xh))
+    M.mv_amxy(-0.75, x, z)
+    assert np.array_equal(z.download(), O.spmv(1, A, xh, alpha=-0.75))
+    M.mv_amxpbyz(-1.0, x, 1.0, y, z)
+    assert np.array_equal(z.download(), O.spmv(3, A, xh, alpha=-1.0, beta=1.0, y=yh))
+    M.mv_amxpby(1.5, x, 0.25, y)
+    assert np.array_equal(y.download(), O.spmv(2, A, xh, alpha=1.5, beta=0.25, z=yh.copy()))
+    # CG (fused q.p in the SpMV epilogue) in tree mode vs the oracle
+    if which == "thermal":
+        b = dev.vec(A.n, np.ones(A.n))
+        xs = dev.vec(A.n, np.zeros(A.n))
+        r = lssp_amd.solve(dev, M, None, xs, b, solver=lssp_amd.CG, maxit=60, trace_cap=100000)
+        o = O.solve(lssp_amd.CG, A, np.ones(A.n), maxit=60, mode=O.TREE)
+        assert r.nits == o.nits and np.array_equal(r.trace, o.trace)
+        assert np.array_equal(xs.download(), o.x)
