@@ -139,6 +139,7 @@ struct TriSched {
     mutable unsigned long long pk6_base = 0;
     unsigned long long *pk6_claim = nullptr;
     std::vector<int> h_pos;  // L factor: row -> schedule position (for the U factor's build)
+    bool rhs_nat = false;    // L factor, v6: the loader gathers the rhs in natural order
 };
 constexpr int PK_ROWS = 256;
 constexpr int PK_BYTES = 12288;

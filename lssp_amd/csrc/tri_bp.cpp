@@ -111,12 +111,19 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
     {
         // v6 packets (tri_mode 9); the rhs of the U sweep is the L sweep's
         // output, read in L's schedule order
+        // LSSP_AMD_TRI_RNAT=1: the L sweep's loader gathers the rhs straight
+        // from the caller's natural-order vector (rhs_nat) instead of the
+        // permutation kernel into L order -- measured slower
+        const char *en = getenv("LSSP_AMD_TRI_RNAT");
+        const bool rnat = !upper && !prod && en && atoi(en) != 0;
         std::vector<int> rhs_index(n);
-        for (int r = 0; r < n; r++) rhs_index[r] = prod && !prod->h_pos.empty() ? prod->h_pos[r] : pos[r];
+        for (int r = 0; r < n; r++)
+            rhs_index[r] = prod && !prod->h_pos.empty() ? prod->h_pos[r] : rnat ? r : pos[r];
         const int st6 = build_packets6(n, perm, pos, rp, cols, vals, diag, unit, step_pos, blk_step, nb, B,
                                        rhs_index, t);
         if (st6 == LSSP_AMD_EUNSUPPORTED) t.pk6_n = -1;  // mode 9 falls back to mode 4
         else if (st6 != LSSP_AMD_OK) return st6;
+        t.rhs_nat = rnat && t.pk6_n > 0;
         if (!upper) t.h_pos = pos;
         // v1 packets (tri_mode 4): when selected, or as mode 9's fallback
         t.pk_n = -1;

@@ -898,9 +898,12 @@ int launch_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const do
         const int e = M->epoch & 1;
         M->epoch++;
         const int pg = 8 * std::max(1, std::min((n + 2047) / 2048, c->num_cus));  // multiple of 8
-        k_perm<true><<<pg, 256, 0, c->stream>>>(M->d_rperm, rhs, M->lower.bp_perm, n);
-        LSSP_HIP(hipGetLastError());
-        LSSP_TRY(launch_pk6<false>(c, M->lower, M->d_rperm, M->d_sh[e], M->d_sh[e ^ 1], nullptr));
+        if (!M->lower.rhs_nat) {
+            k_perm<true><<<pg, 256, 0, c->stream>>>(M->d_rperm, rhs, M->lower.bp_perm, n);
+            LSSP_HIP(hipGetLastError());
+        }
+        LSSP_TRY(launch_pk6<false>(c, M->lower, M->lower.rhs_nat ? rhs : M->d_rperm, M->d_sh[e], M->d_sh[e ^ 1],
+                                   nullptr));
         static const bool nat = getenv("LSSP_AMD_TRI_NAT") && atoi(getenv("LSSP_AMD_TRI_NAT"));
         if (nat && M->upper.pk6_ep == 4)
             return launch_pk6<true>(c, M->upper, M->d_sh[e], M->d_sh[2 + e], M->d_sh[2 + (e ^ 1)], x);
