@@ -37,7 +37,12 @@ enum {
 };
 
 /* LSSP_SOLVER_TYPE values of the reference (type-defs.h:157-178) */
-enum { LSSP_AMD_GMRES = 0, LSSP_AMD_LGMRES = 1, LSSP_AMD_RGMRES = 2, LSSP_AMD_BICGSTAB = 4, LSSP_AMD_CG = 7 };
+enum {
+    LSSP_AMD_GMRES = 0, LSSP_AMD_LGMRES = 1, LSSP_AMD_RGMRES = 2, LSSP_AMD_BICGSTAB = 4,
+    LSSP_AMD_BICGSAFE = 6, LSSP_AMD_CG = 7, LSSP_AMD_CGS = 8, LSSP_AMD_GPBICG = 9, LSSP_AMD_CR = 10,
+    LSSP_AMD_CRS = 11, LSSP_AMD_BICRSTAB = 12, LSSP_AMD_BICRSAFE = 13, LSSP_AMD_GPBICR = 14,
+    LSSP_AMD_QMRCGSTAB = 15, LSSP_AMD_TFQMR = 16, LSSP_AMD_ORTHOMIN = 17
+};
 /* ILU kinds (LSSP_PC_TYPE, type-defs.h:63-101) */
 enum { LSSP_AMD_ILUK = 1, LSSP_AMD_ILUT = 2 };
 
@@ -128,7 +133,7 @@ int lssp_amd_ilu_get_factors(const lssp_amd_ilu *M, int *Lp, int *Lj, double *Lx
  *      (solver-lgmres.cxx:12-312) and CG (solver-cg.cxx:8-136).  Same recurrences, guards, defaults and
  *      iteration counting; vectors stay in HBM. ------------------------- */
 typedef struct {
-    int solver;     /* LSSP_AMD_GMRES / _LGMRES / _RGMRES / _BICGSTAB / _CG */
+    int solver;     /* LSSP_AMD_* above (LSSP_SOLVER_TYPE) */
     double tol_rel; /* < 0: default 1e-7 (lssp.cxx:11-13) */
     double tol_abs;
     double tol_rb;

@@ -16,7 +16,9 @@ from . import _lib
 _lib.load()
 
 from .device import (BICGSTAB, CG, GMRES, LGMRES, RGMRES, ILUK, ILUT, SERIAL, TREE, DILU, DMat,  # noqa: E402,F401
-                     Device, DVec, LsspError, comm_unique_id, poisson, solve, sort_columns)
+                     Device, DVec, LsspError, comm_unique_id, poisson, solve, sort_columns,
+                     BICGSAFE, CGS, GPBICG, CR, CRS, BICRSTAB, BICRSAFE, GPBICR, QMRCGSTAB, TFQMR, ORTHOMIN)
 
 __all__ = ["Device", "DVec", "DMat", "DILU", "solve", "poisson", "sort_columns", "LsspError",
-           "comm_unique_id", "GMRES", "LGMRES", "RGMRES", "BICGSTAB", "CG", "ILUK", "ILUT", "SERIAL", "TREE"]
+           "comm_unique_id", "GMRES", "LGMRES", "RGMRES", "BICGSTAB", "CG", "ILUK", "ILUT", "SERIAL", "TREE",
+           "BICGSAFE", "CGS", "GPBICG", "CR", "CRS", "BICRSTAB", "BICRSAFE", "GPBICR", "QMRCGSTAB", "TFQMR", "ORTHOMIN"]

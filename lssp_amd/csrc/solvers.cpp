@@ -862,6 +862,754 @@ int lgmres(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, i
     return LSSP_AMD_OK;
 }
 
+
+// ===========================================================================
+// The remaining Krylov drivers.  Unlike BiCGSTAB / CG / GMRES, the reference
+// writes these purely as sequences of its L1 calls (lssp_vec_* vector.cxx,
+// lssp_mv_* mvops.cxx, pc.solve) with host scalars, so each is restated here
+// call for call over L1K below: the same kernels, operand order and aliasing,
+// every dot / norm returned to the host where the reference branches on it.
+// Work vectors start zeroed: three drivers read vectors lssp_vec_create left
+// uninitialised (malloc, vector.cxx:4-20) before writing them (BiCGSafe y/u/z,
+// BiCRSafe u/y/z/my, GPBiCG/GPBiCR mr/u/z/mt_old); the golden runs of the
+// reference are made with zero-initialising malloc (oracle/ref_shim.cxx).
+// ===========================================================================
+struct L1K {
+    Run &R;
+    int st = LSSP_AMD_OK;  // first failure; every later call is a no-op
+    explicit L1K(Run &r) : R(r) {}
+    bool ok() const { return st == LSSP_AMD_OK; }
+    void chk(int s)
+    {
+        if (st == LSSP_AMD_OK && s != LSSP_AMD_OK) st = s;
+    }
+    double *vec()
+    {
+        double *p = R.vec();
+        if (!p) chk(LSSP_AMD_ENOMEM);
+        else set(p, 0.0);
+        return p;
+    }
+    void ew(int kind, double a, double b, const double *x, const double *y, double *out)
+    {
+        if (!ok()) return;
+        Ew e;
+        e.kind = kind;
+        e.a = a;
+        e.b = b;
+        e.x = x;
+        e.y = y;
+        e.out0 = out;
+        chk(R.ew(e));
+    }
+    // vector.cxx:98-107 y = y*b + x*a;  :110-120 z = y*b + x*a
+    void axpby(double a, const double *x, double b, double *y) { ew(K_AXPBY, a, b, x, nullptr, y); }
+    void axpbyz(double a, const double *x, double b, const double *y, double *z) { ew(K_AXPBYZ, a, b, x, y, z); }
+    void copy(double *dst, const double *src) { ew(K_COPY, 0, 0, src, nullptr, dst); }  // :73-83
+    void set(double *x, double v) { ew(K_FILL, v, 0, nullptr, nullptr, x); }          // :31-38
+    void scale(double *x, double a) { ew(K_SCALE, a, 0, nullptr, nullptr, x); }       // :141-146
+    void mxy(double *x, double *y)  // mvops.cxx:118-150
+    {
+        if (ok()) chk(R.spmv(EPI_MXY, 1, x, 0, nullptr, y));
+    }
+    void resid(double *x, const double *b, double *r)  // lssp_mv_amxpbyz(-1, A, x, 1, b, r), :42-78
+    {
+        if (ok()) chk(R.spmv(EPI_AXPBY, -1, x, 1, b, r));
+    }
+    void pc(double *x, const double *rhs)
+    {
+        if (ok()) chk(R.pc(x, rhs));
+    }
+    double fetch(int op, const double *x, const double *y)
+    {
+        if (!ok()) return NAN;
+        chk(R.dot1(x, y, R.fin(op, 1, R.T(), -1, S_TMP)));
+        if (ok()) chk(R.sync(0, 16));
+        return ok() ? R.h(S_TMP) : NAN;
+    }
+    double dot(const double *x, const double *y) { return fetch(FIN_STORE, x, y); }  // vector.cxx:123-133
+    double norm(const double *x) { return fetch(FIN_NORM, x, x); }                    // :135-139
+};
+
+void tol_setup(const lssp_amd_solve_params &P, double nrm2, double bnorm_rb, double &tol)
+{
+    // tol = nrm2*rtol; alpha = ||b||*rb; tol = max(tol, atol, alpha)  (e.g. solver-cgs.cxx:41-44)
+    double tol_rel, tol_abs;
+    int maxit;
+    defaults(P, tol_rel, tol_abs, maxit);
+    tol = nrm2 * tol_rel;
+    if (tol < tol_abs) tol = tol_abs;
+    if (tol < bnorm_rb) tol = bnorm_rb;
+}
+
+#define L1_DONE()                      \
+    do {                               \
+        if (!K.ok()) return K.st;      \
+        *nits = iter;                  \
+        *res_out = nrm2;               \
+        return LSSP_AMD_OK;            \
+    } while (0)
+
+// CGS (solver-cgs.cxx:4-133); vhat aliases uhat (:25)
+int cgs(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
+{
+    L1K K(R);
+    double tol_rel, tol_abs, tol;
+    int maxiter, iter;
+    defaults(P, tol_rel, tol_abs, maxiter);
+    double *r = K.vec(), *rtld = K.vec(), *p = K.vec(), *phat = K.vec(), *q = K.vec(), *qhat = K.vec();
+    double *u = K.vec(), *uhat = K.vec(), *vhat = uhat;
+    double alpha = 1.0, beta, rho, rho_old = 1.0, tdot1, nrm2, ires;
+    K.resid(x, b, r);
+    iter = 0;
+    nrm2 = ires = K.norm(r);
+    if (!K.ok() || nrm2 <= tol_abs) L1_DONE();
+    alpha = K.norm(b) * P.tol_rb;
+    tol_setup(P, nrm2, alpha, tol);
+    K.copy(rtld, r);
+    K.set(q, 0);
+    K.set(p, 0);
+    for (iter = 1; iter <= maxiter; iter++) {
+        rho = K.dot(rtld, r);
+        if (!K.ok() || rho == 0.0) L1_DONE();
+        beta = rho / rho_old;
+        K.axpbyz(beta, q, 1, r, u);
+        K.axpby(1, q, beta, p);
+        K.axpby(1, u, beta, p);
+        K.pc(phat, p);
+        K.mxy(phat, vhat);
+        tdot1 = K.dot(rtld, vhat);
+        if (!K.ok() || tdot1 == 0.0) L1_DONE();
+        alpha = rho / tdot1;
+        K.axpbyz(-alpha, vhat, 1, u, q);
+        K.axpbyz(1, u, 1, q, phat);
+        K.pc(uhat, phat);
+        K.axpby(alpha, uhat, 1, x);
+        K.mxy(uhat, qhat);
+        K.axpby(-alpha, qhat, 1, r);
+        nrm2 = K.norm(r);
+        if (P.verb >= 1 && R.rank == 0)
+            printf("cgs: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+        if (!K.ok() || tol >= nrm2) L1_DONE();
+        rho_old = rho;
+    }
+    L1_DONE();
+}
+
+// CR (solver-cr.cxx:3-115)
+int cr(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
+{
+    L1K K(R);
+    double tol_rel, tol_abs, tol;
+    int maxiter, iter;
+    defaults(P, tol_rel, tol_abs, maxiter);
+    double *r = K.vec(), *z = K.vec(), *p = K.vec(), *q = K.vec(), *qtld = K.vec(), *az = K.vec();
+    double alpha, beta, rho, dot_rq, dot_zq, nrm2, ires;
+    K.resid(x, b, r);
+    nrm2 = ires = K.norm(r);
+    iter = 1;
+    if (!K.ok() || nrm2 <= tol_abs) L1_DONE();  // nits = iter = 1 (:31-35, :105)
+    alpha = K.norm(b) * P.tol_rb;
+    tol_setup(P, nrm2, alpha, tol);
+    K.pc(p, r);
+    K.mxy(p, q);
+    K.copy(z, p);
+    for (iter = 1; iter <= maxiter; iter++) {
+        K.pc(qtld, q);
+        rho = K.dot(qtld, q);
+        if (!K.ok() || rho == 0.0) L1_DONE();
+        dot_rq = K.dot(r, qtld);
+        alpha = dot_rq / rho;
+        K.axpby(alpha, p, 1, x);
+        K.axpby(-alpha, q, 1, r);
+        nrm2 = K.norm(r);
+        if (P.verb >= 1 && R.rank == 0)
+            printf("cr: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+        if (!K.ok() || tol >= nrm2) L1_DONE();
+        K.axpby(-alpha, qtld, 1, z);
+        K.mxy(z, az);
+        dot_zq = K.dot(az, qtld);
+        beta = -dot_zq / rho;
+        K.axpby(1, z, beta, p);
+        K.axpby(1, az, beta, q);
+    }
+    L1_DONE();
+}
+
+// CRS (solver-crs.cxx:3-109); u = uq = z, ap = q, auq = map (:20-25)
+int crs(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
+{
+    L1K K(R);
+    double tol_rel, tol_abs, tol;
+    int maxiter, iter;
+    defaults(P, tol_rel, tol_abs, maxiter);
+    double *r = K.vec(), *rtld = K.vec(), *p = K.vec(), *z = K.vec(), *q = K.vec(), *map = K.vec();
+    double *u = z, *uq = z, *ap = q, *auq = map;
+    double alpha, beta, rho, rho_old, tdot1, nrm2, ires;
+    K.resid(x, b, r);
+    nrm2 = ires = K.norm(r);
+    iter = 1;
+    if (!K.ok() || nrm2 <= tol_abs) L1_DONE();
+    alpha = K.norm(b) * P.tol_rb;
+    tol_setup(P, nrm2, alpha, tol);
+    K.copy(p, r);
+    K.mxy(p, rtld);
+    rho_old = 1.0;
+    K.set(q, 0.);
+    K.set(p, 0.);
+    for (iter = 1; iter <= maxiter; iter++) {
+        K.pc(z, r);
+        rho = K.dot(rtld, z);
+        if (!K.ok() || rho == 0.0) L1_DONE();
+        beta = rho / rho_old;
+        K.axpbyz(beta, q, 1, z, u);
+        K.axpby(1, q, beta, p);
+        K.axpby(1, u, beta, p);
+        K.mxy(p, ap);
+        K.pc(map, ap);
+        tdot1 = K.dot(rtld, map);
+        if (!K.ok() || tdot1 == 0.0) L1_DONE();
+        alpha = rho / tdot1;
+        K.axpbyz(-alpha, map, 1, u, q);
+        K.axpbyz(1, u, 1, q, uq);
+        K.mxy(uq, auq);
+        K.axpby(alpha, uq, 1, x);
+        K.axpby(-alpha, auq, 1, r);
+        nrm2 = K.norm(r);
+        if (P.verb >= 1 && R.rank == 0)
+            printf("crs: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+        if (!K.ok() || tol >= nrm2) L1_DONE();
+        rho_old = rho;
+    }
+    L1_DONE();
+}
+
+// BiCRSTAB (solver-bicrstab.cxx:3-114)
+int bicrstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
+{
+    L1K K(R);
+    double tol_rel, tol_abs, tol;
+    int maxiter, iter;
+    defaults(P, tol_rel, tol_abs, maxiter);
+    double *rtld = K.vec(), *r = K.vec(), *s = K.vec(), *ms = K.vec(), *ams = K.vec(), *p = K.vec();
+    double *ap = K.vec(), *map = K.vec(), *z = K.vec();
+    double alpha, beta, omega, rho, rho_old, tdot1, tdot2, nrm2, ires;
+    K.resid(x, b, r);
+    nrm2 = ires = K.norm(r);
+    iter = 1;
+    if (!K.ok() || nrm2 <= tol_abs) L1_DONE();
+    alpha = K.norm(b) * P.tol_rb;
+    tol_setup(P, nrm2, alpha, tol);
+    K.copy(p, r);
+    K.mxy(p, rtld);
+    K.pc(z, r);
+    K.copy(p, z);
+    rho_old = K.dot(rtld, z);
+    for (iter = 1; iter <= maxiter; iter++) {
+        K.mxy(p, ap);
+        K.pc(map, ap);
+        tdot1 = K.dot(rtld, map);
+        alpha = rho_old / tdot1;
+        K.axpbyz(-alpha, ap, 1, r, s);
+        nrm2 = K.norm(s);
+        if (!K.ok()) L1_DONE();
+        if (nrm2 <= tol) {
+            K.axpby(alpha, p, 1, x);
+            L1_DONE();
+        }
+        K.axpbyz(-alpha, map, 1, z, ms);
+        K.mxy(ms, ams);
+        tdot1 = K.dot(ams, s);
+        tdot2 = K.dot(ams, ams);
+        omega = tdot1 / tdot2;
+        K.axpby(alpha, p, 1, x);
+        K.axpby(omega, ms, 1, x);
+        K.axpbyz(-omega, ams, 1, s, r);
+        nrm2 = K.norm(r);
+        if (P.verb >= 2 && R.rank == 0)
+            printf("bicrstab: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+        if (!K.ok() || tol >= nrm2) L1_DONE();
+        K.pc(z, r);
+        rho = K.dot(rtld, z);
+        if (!K.ok() || rho == 0.0) L1_DONE();
+        beta = (rho / rho_old) * (alpha / omega);
+        K.axpby(-omega, map, 1, p);
+        K.axpby(1, z, beta, p);
+        rho_old = rho;
+    }
+    L1_DONE();
+}
+
+// the (qsi, eta) pair of BiCGSafe / BiCRSafe / GPBiCG / GPBiCR
+// (e.g. solver-bicgsafe.cxx:61-75): five dots, then the 2x2 solve
+static void safe_coef(L1K &K, int iter, const double *y, const double *a, const double *r, double &qsi,
+                      double &eta)
+{
+    double tdot[5], tmp;
+    tdot[0] = K.dot(y, y);
+    tdot[1] = K.dot(a, r);
+    tdot[2] = K.dot(y, r);
+    tdot[3] = K.dot(a, y);
+    tdot[4] = K.dot(a, a);
+    if (iter == 1) {
+        qsi = tdot[1] / tdot[4];
+        eta = 0.0;
+    } else {
+        tmp = tdot[4] * tdot[0] - tdot[3] * tdot[3];
+        qsi = (tdot[0] * tdot[1] - tdot[2] * tdot[3]) / tmp;
+        eta = (tdot[4] * tdot[2] - tdot[3] * tdot[1]) / tmp;
+    }
+}
+
+// BiCGSafe (solver-bicgsafe.cxx:3-155)
+int bicgsafe(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
+{
+    L1K K(R);
+    double tol_rel, tol_abs, tol;
+    int maxiter, iter;
+    defaults(P, tol_rel, tol_abs, maxiter);
+    double *rtld = K.vec(), *r = K.vec(), *mr = K.vec(), *amr = K.vec(), *p = K.vec(), *ap = K.vec();
+    double *t = K.vec(), *mt = K.vec(), *y = K.vec(), *u = K.vec(), *z = K.vec(), *au = K.vec();
+    double alpha, beta, rho, rho_old, qsi, eta, nrm2, ires;
+    K.resid(x, b, r);
+    nrm2 = ires = K.norm(r);
+    iter = 1;
+    if (!K.ok() || nrm2 <= tol_abs) L1_DONE();
+    alpha = K.norm(b) * P.tol_rb;
+    tol_setup(P, nrm2, alpha, tol);
+    K.copy(rtld, r);
+    K.pc(mr, r);
+    K.mxy(mr, amr);
+    rho_old = K.dot(rtld, r);
+    K.copy(ap, amr);
+    K.copy(p, mr);
+    beta = 0.0;
+    for (iter = 1; iter <= maxiter; iter++) {
+        alpha = rho_old / K.dot(rtld, ap);
+        safe_coef(K, iter, y, amr, r, qsi, eta);
+        K.copy(t, y);
+        K.scale(t, eta);
+        K.axpby(qsi, ap, 1, t);
+        K.pc(mt, t);
+        K.axpby(1, mt, eta * beta, u);
+        K.mxy(u, au);
+        K.scale(z, eta);
+        K.axpby(qsi, mr, 1, z);
+        K.axpby(-alpha, u, 1, z);
+        K.scale(y, eta);
+        K.axpby(qsi, amr, 1, y);
+        K.axpby(-alpha, au, 1, y);
+        K.axpby(alpha, p, 1, x);
+        K.axpby(1, z, 1, x);
+        K.axpby(-alpha, ap, 1, r);
+        K.axpby(-1, y, 1.0, r);
+        nrm2 = K.norm(r);
+        if (P.verb >= 1 && R.rank == 0)
+            printf("bicgsafe: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+        if (!K.ok() || tol >= nrm2) L1_DONE();
+        rho = K.dot(rtld, r);
+        if (!K.ok() || rho == 0.0) L1_DONE();
+        beta = (rho / rho_old) * (alpha / qsi);
+        K.pc(mr, r);
+        K.mxy(mr, amr);
+        K.axpby(-1, u, 1.0, p);
+        K.axpby(1, mr, beta, p);
+        K.axpby(-1, au, 1.0, ap);
+        K.axpby(1, amr, beta, ap);
+        rho_old = rho;
+    }
+    L1_DONE();
+}
+
+// BiCRSafe (solver-bicrsafe.cxx:3-151)
+int bicrsafe(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
+{
+    L1K K(R);
+    double tol_rel, tol_abs, tol;
+    int maxiter, iter;
+    defaults(P, tol_rel, tol_abs, maxiter);
+    double *rtld = K.vec(), *r = K.vec(), *mr = K.vec(), *amr = K.vec(), *p = K.vec(), *ap = K.vec();
+    double *map = K.vec(), *my = K.vec(), *y = K.vec(), *u = K.vec(), *z = K.vec(), *au = K.vec();
+    double *artld = K.vec();
+    double alpha, beta, rho, rho_old, qsi, eta, nrm2, ires;
+    K.resid(x, b, r);
+    nrm2 = ires = K.norm(r);
+    iter = 1;
+    if (!K.ok() || nrm2 <= tol_abs) L1_DONE();
+    alpha = K.norm(b) * P.tol_rb;
+    tol_setup(P, nrm2, alpha, tol);
+    K.copy(rtld, r);
+    K.mxy(rtld, artld);
+    K.pc(mr, r);
+    K.mxy(mr, amr);
+    rho_old = K.dot(rtld, amr);
+    K.copy(ap, amr);
+    K.copy(p, mr);
+    beta = 0.0;
+    for (iter = 1; iter <= maxiter; iter++) {
+        K.pc(map, ap);
+        alpha = rho_old / K.dot(artld, map);
+        safe_coef(K, iter, y, amr, r, qsi, eta);
+        K.scale(u, eta * beta);
+        K.axpby(qsi, map, 1, u);
+        K.axpby(eta, my, 1, u);
+        K.mxy(u, au);
+        K.scale(z, eta);
+        K.axpby(qsi, mr, 1, z);
+        K.axpby(-alpha, u, 1, z);
+        K.scale(y, eta);
+        K.axpby(qsi, amr, 1, y);
+        K.axpby(-alpha, au, 1, y);
+        K.pc(my, y);
+        K.axpby(alpha, p, 1, x);
+        K.axpby(1, z, 1, x);
+        K.axpby(-alpha, ap, 1, r);
+        K.axpby(-1, y, 1, r);
+        nrm2 = K.norm(r);
+        if (P.verb >= 2 && R.rank == 0)
+            printf("bicrsafe: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+        if (!K.ok() || tol >= nrm2) L1_DONE();
+        K.axpby(-alpha, map, 1, mr);
+        K.axpby(-1, my, 1, mr);
+        K.mxy(mr, amr);
+        rho = K.dot(rtld, amr);
+        if (!K.ok() || rho == 0.0) L1_DONE();
+        beta = (rho / rho_old) * (alpha / qsi);
+        K.axpby(-1, u, 1., p);
+        K.axpby(1, mr, beta, p);
+        K.axpby(-1, au, 1.0, ap);
+        K.axpby(1, amr, beta, ap);
+        rho_old = rho;
+    }
+    L1_DONE();
+}
+
+// GPBiCG (solver-gpbicg.cxx:3-163) and GPBiCR (solver-gpbicr.cxx:3-164): the
+// same recurrence; GPBiCR shadows with A r0 and tests <rtld, M^-1 A p> and
+// <rtld, M^-1 r> (gpbicr.cxx:49-54, :62, :129)
+int gpbi(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out, bool cr_)
+{
+    L1K K(R);
+    double tol_rel, tol_abs, tol;
+    int maxiter, iter;
+    defaults(P, tol_rel, tol_abs, maxiter);
+    double *rtld = K.vec(), *r = K.vec(), *mr = K.vec(), *p = K.vec(), *ap = K.vec(), *map = K.vec();
+    double *t = K.vec(), *mt = K.vec(), *amt = K.vec(), *u = K.vec(), *y = K.vec(), *w = K.vec();
+    double *z = K.vec(), *mt_old = K.vec();
+    double alpha, beta, rho, rho_old, qsi, eta, tdot0, nrm2, ires;
+    const char *name = cr_ ? "gpbicr" : "gpbicg";
+    K.resid(x, b, r);
+    nrm2 = ires = K.norm(r);
+    iter = 1;
+    if (!K.ok()) L1_DONE();
+    if (nrm2 <= tol_abs) {
+        iter = 0;
+        L1_DONE();
+    }
+    alpha = K.norm(b) * P.tol_rb;
+    tol_setup(P, nrm2, alpha, tol);
+    if (cr_) {
+        K.copy(p, r);
+        K.mxy(p, rtld);
+        K.pc(p, r);
+        rho_old = K.dot(rtld, p);
+    } else {
+        K.copy(rtld, r);
+        K.pc(p, r);
+        rho_old = K.dot(rtld, r);
+    }
+    K.set(t, 0.);
+    K.set(w, 0.);
+    beta = 0.0;
+    for (iter = 1; iter <= maxiter; iter++) {
+        K.mxy(p, ap);
+        K.pc(map, ap);
+        tdot0 = K.dot(rtld, cr_ ? map : ap);
+        if (!K.ok() || tdot0 == 0.0) L1_DONE();
+        alpha = rho_old / tdot0;
+        K.axpbyz(-1, w, 1, ap, y);
+        K.axpby(1, t, alpha, y);
+        K.axpby(-1, r, 1, y);
+        K.axpbyz(-alpha, ap, 1, r, t);
+        nrm2 = K.norm(t);
+        if (P.verb >= 1 && R.rank == 0)
+            printf("%s: itr: %5d, abs res: %.6e, rel res: %.6e\n", name, iter, nrm2, nrm2 / ires);
+        if (!K.ok()) L1_DONE();
+        if (nrm2 <= tol) {
+            K.axpby(alpha, p, 1, x);
+            L1_DONE();
+        }
+        K.axpbyz(-alpha, map, 1, mr, mt);
+        K.mxy(mt, amt);
+        safe_coef(K, iter, y, amt, t, qsi, eta);
+        K.axpby(1., mt_old, beta, u);
+        K.axpby(-1, mr, 1, u);
+        K.scale(u, eta);
+        K.axpby(qsi, map, 1, u);
+        K.scale(z, eta);
+        K.axpby(qsi, mr, 1, z);
+        K.axpby(-alpha, u, 1, z);
+        K.axpby(alpha, p, 1, x);
+        K.axpby(1, z, 1., x);
+        K.axpbyz(-qsi, amt, 1, t, r);
+        K.axpby(-eta, y, 1, r);
+        nrm2 = K.norm(r);
+        if (P.verb >= 1 && R.rank == 0)
+            printf("%s: itr: %5d, abs res: %.6e, rel res: %.6e\n", name, iter, nrm2, nrm2 / ires);
+        if (!K.ok() || tol >= nrm2) L1_DONE();
+        K.pc(mr, r);
+        rho = K.dot(rtld, cr_ ? mr : r);
+        if (!K.ok() || rho == 0.0) L1_DONE();
+        beta = (rho / rho_old) * (alpha / qsi);
+        K.axpbyz(beta, ap, 1, amt, w);
+        K.axpby(-1, u, 1, p);
+        K.axpby(1., mr, beta, p);
+        K.copy(mt_old, mt);
+        rho_old = rho;
+    }
+    L1_DONE();
+}
+
+// QMRCGSTAB (solver-qmrcgstab.cxx:10-186)
+int qmrcgstab(Run &R, const lssp_amd_solve_params &P, double *xk, const double *bg, int *nits, double *res_out)
+{
+    L1K K(R);
+    double tol_rel, tol_abs, tol_rb = P.tol_rb;
+    int itr_max, itr_out;
+    defaults(P, tol_rel, tol_abs, itr_max);
+    if (P.verb >= 2 && R.rank == 0) {
+        printf("qmrcgstab: maximal iteration: %d\n", itr_max);
+        printf("qmrcgstab: tolerance abs: %g\n", tol_abs);
+        printf("qmrcgstab: tolerance rel: %g\n", tol_rel);
+        printf("qmrcgstab: tolerance rbn: %g\n", tol_rb);
+    }
+    double *rk = K.vec(), *r = K.vec(), *br0 = K.vec(), *pk = K.vec(), *vk = K.vec(), *sk = K.vec();
+    double *dk = K.vec(), *tk = K.vec(), *bdk = K.vec(), *bxk = K.vec();
+    double rho = 1, prho, alpha = 1, beta, omega = 1, theta = 0., btheta, b_eta, eta = 0., tau, btau;
+    double residual, c, ires, rerror, tol;
+    const double b_norm = K.norm(bg);
+    tol_rb *= b_norm;
+    K.resid(xk, bg, tk);
+    residual = K.norm(tk);
+    if (!K.ok()) return K.st;
+    if (residual <= tol_abs) {
+        *nits = 0;
+        *res_out = residual;
+        return LSSP_AMD_OK;
+    }
+    tol = residual * tol_rel;
+    if (tol < tol_abs) tol = tol_abs;
+    if (tol < tol_rb) tol = tol_rb;
+    tol = tol / residual;
+    K.pc(rk, tk);
+    K.copy(br0, rk);
+    K.set(pk, 0);
+    K.set(dk, 0);
+    K.set(vk, 0);
+    tau = ires = K.norm(rk);
+    prho = rho;
+    for (itr_out = 0; itr_out < itr_max; itr_out++) {
+        rho = K.dot(br0, rk);
+        beta = rho * alpha / prho / omega;
+        prho = rho;
+        K.axpbyz(1, pk, -omega, vk, r);
+        K.axpbyz(beta, r, 1, rk, pk);
+        K.mxy(pk, r);
+        K.pc(vk, r);
+        alpha = rho / K.dot(br0, vk);
+        K.axpbyz(-alpha, vk, 1, rk, sk);
+        btheta = K.norm(sk) / tau;
+        c = 1 / sqrt(1. + btheta * btheta);
+        btau = tau * btheta * c;
+        b_eta = c * c * alpha;
+        K.axpbyz(1., pk, theta * theta * eta / alpha, dk, bdk);
+        K.axpbyz(1, xk, b_eta, bdk, bxk);
+        K.mxy(sk, r);
+        K.pc(tk, r);
+        {
+            // :146 -- operand evaluation order as g++ -O2 built it (the golden traces)
+            const double num = K.dot(sk, tk);
+            omega = num / K.dot(tk, tk);
+        }
+        K.axpbyz(1., sk, -omega, tk, rk);
+        theta = K.norm(rk) / btau;
+        c = 1. / sqrt(1. + theta * theta);
+        tau = btau * theta * c;
+        eta = c * c * omega;
+        K.axpbyz(1, sk, btheta * btheta * b_eta / omega, bdk, dk);
+        K.axpbyz(1, bxk, eta, dk, xk);
+        rerror = K.norm(rk) / ires;
+        if (!K.ok()) return K.st;
+        if (P.verb >= 1 && R.rank == 0) printf("qmrcgstab: itr: %4d, rel res: %.6e\n", itr_out, rerror);
+        if (rerror <= tol) {
+            K.resid(xk, bg, tk);
+            residual = K.norm(tk);
+            break;
+        }
+    }
+    if (!K.ok()) return K.st;
+    if (itr_out < itr_max) itr_out += 1;
+    *nits = itr_out;
+    *res_out = residual;
+    return LSSP_AMD_OK;
+}
+
+// TFQMR (solver-tfqmr.cxx:3-149)
+int tfqmr(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
+{
+    L1K K(R);
+    double tol_rel, tol_abs, tol;
+    int maxiter, iter;
+    defaults(P, tol_rel, tol_abs, maxiter);
+    double *r = K.vec(), *rtld = K.vec(), *u = K.vec(), *p = K.vec(), *d = K.vec(), *t = K.vec();
+    double *t1 = K.vec(), *q = K.vec(), *v = K.vec();
+    double alpha, beta, rho, rhoold, s, tau, theta, eta, c, w, wold, ww, nrm2, ires;
+    K.resid(x, b, r);
+    nrm2 = ires = K.norm(r);
+    iter = 1;
+    if (!K.ok()) L1_DONE();
+    if (nrm2 <= tol_abs) {
+        iter = 0;
+        L1_DONE();
+    }
+    alpha = K.norm(b) * P.tol_rb;
+    tol_setup(P, nrm2, alpha, tol);
+    K.copy(rtld, r);
+    K.copy(p, r);
+    K.copy(u, r);
+    K.set(d, 0.);
+    K.pc(t, p);
+    K.mxy(t, v);
+    rhoold = K.dot(r, rtld);
+    tau = K.norm(r);
+    wold = tau;
+    theta = 0.0;
+    eta = 0.0;
+    while (iter <= maxiter) {
+        s = K.dot(v, rtld);
+        if (!K.ok() || fabs(s) == 0.0) L1_DONE();
+        alpha = rhoold / s;
+        K.axpbyz(-alpha, v, 1, u, q);
+        K.axpbyz(1, u, 1., q, t);
+        K.pc(t1, t);
+        K.mxy(t1, v);
+        K.axpby(-alpha, v, 1, r);
+        w = K.norm(r);
+        for (int m = 0; m < 2; m++) {
+            if (m == 0) {
+                ww = sqrt(w * wold);
+                K.axpby(1, u, theta * theta * eta / alpha, d);
+            } else {
+                ww = w;
+                K.axpby(1, q, theta * theta * eta / alpha, d);
+            }
+            theta = ww / tau;
+            c = 1.0 / sqrt(1.0 + theta * theta);
+            eta = c * c * alpha;
+            tau = tau * theta * c;
+            K.pc(t1, d);
+            K.axpby(eta, t1, 1, x);
+            nrm2 = tau * sqrt(1.0 + m);
+            if (P.verb >= 1 && R.rank == 0)
+                printf("tfqmr: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+            if (!K.ok() || tol >= nrm2) L1_DONE();
+        }
+        rho = K.dot(r, rtld);
+        if (!K.ok() || fabs(rho) == 0.0) L1_DONE();
+        beta = rho / rhoold;
+        K.axpbyz(beta, q, 1, r, u);
+        K.axpby(1, q, beta, p);
+        K.axpby(1, u, beta, p);
+        K.pc(t1, p);
+        K.mxy(t1, v);
+        rhoold = rho;
+        wold = w;
+        iter++;
+    }
+    L1_DONE();
+}
+
+// ORTHOMIN(k), k = restart (solver-orthomin.cxx:12-180)
+int orthomin(Run &R, const lssp_amd_solve_params &P, double *x, const double *rhs, int *nits, double *res_out)
+{
+    L1K K(R);
+    double tol_rel, tol_abs, tol_rb = P.tol_rb < 0 ? DEF_TOL : P.tol_rb;
+    int itr_max, itr_out, i, j;
+    defaults(P, tol_rel, tol_abs, itr_max);
+    int k = P.restart < 0 ? DEF_RESTART : P.restart;
+    if (k == 0) return LSSP_AMD_EINVAL;  // the reference divides by it (:102)
+    if (P.verb >= 2 && R.rank == 0) {
+        printf("orthomin: k parameter m: %d\n", k);
+        printf("orthomin: maximal iteration: %d\n", itr_max);
+        printf("orthomin: tolerance abs: %g\n", tol_abs);
+        printf("orthomin: tolerance rel: %g\n", tol_rel);
+        printf("orthomin: tolerance rbn: %g\n", tol_rb);
+    }
+    double *z = K.vec(), *r = K.vec(), *s = K.vec(), *sd = K.vec();
+    std::vector<double *> p(k), q(k);
+    std::vector<double> b_j(k), c_j(k);
+    for (i = 0; i < k; i++) {
+        p[i] = K.vec();
+        q[i] = K.vec();
+    }
+    double tol = -1, err_rel = 0, beta, a_j;
+    K.resid(x, rhs, z);
+    K.set(r, 0.);
+    K.pc(r, z);
+    K.copy(p[0], r);
+    K.copy(sd, r);
+    const double b_norm = K.norm(rhs);
+    tol_rb *= b_norm;
+    beta = K.norm(z);
+    if (!K.ok()) return K.st;
+    if (beta <= tol_abs) {
+        *nits = 0;
+        *res_out = beta;
+        return LSSP_AMD_OK;
+    }
+    err_rel = beta;
+    tol = tol_rel * err_rel;
+    if (tol < tol_abs) tol = tol_abs;
+    if (tol < tol_rb) tol = tol_rb;
+    for (itr_out = 0; itr_out < itr_max; itr_out++) {
+        K.mxy(sd, s);
+        j = itr_out % k;
+        K.set(q[j], 0.);
+        K.pc(q[j], s);
+        a_j = K.dot(r, q[j]);
+        c_j[j] = K.dot(q[j], q[j]);
+        if (!K.ok()) return K.st;
+        if (fabs(c_j[j]) <= BREAKDOWN) break;
+        a_j = a_j / c_j[j];
+        K.axpby(a_j, p[j], 1, x);
+        K.axpby(-a_j, q[j], 1, r);
+        K.copy(sd, r);
+        K.mxy(r, s);
+        K.set(z, 0.);
+        K.pc(z, s);
+        const int ni = itr_out >= k - 1 ? k : itr_out + 1;  // :120-136
+        for (i = 0; i < ni; i++) {
+            beta = K.dot(z, q[i]);
+            b_j[i] = -beta / c_j[i];
+            K.axpby(b_j[i], p[i], 1, sd);
+        }
+        j = (itr_out + 1) % k;
+        K.copy(p[j], sd);
+        K.resid(x, rhs, z);
+        beta = K.norm(z);
+        if (!K.ok()) return K.st;
+        if (P.verb >= 1 && R.rank == 0)
+            printf("orthomin: itr: %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", itr_out, beta,
+                   (err_rel == 0 ? 0 : beta / err_rel), (b_norm == 0 ? 0 : beta / b_norm));
+        if (beta <= tol) break;
+    }
+    if (itr_out < itr_max) itr_out += 1;
+    if (P.verb >= 2 && R.rank == 0) printf("orthomin: total iteration: %d\n", itr_out);
+    *nits = itr_out;
+    *res_out = beta;
+    return LSSP_AMD_OK;
+}
+
 }  // namespace
 }  // namespace lssp_amd
 
@@ -902,6 +1650,17 @@ extern "C" int lssp_amd_solve(lssp_amd_ctx *c, const lssp_amd_mat *A, const lssp
     case LSSP_AMD_GMRES: st = gmres(R, *prm, x, b, &it, &res); break;
     case LSSP_AMD_RGMRES: st = gmres_r(R, *prm, x, b, &it, &res); break;
     case LSSP_AMD_LGMRES: st = lgmres(R, *prm, x, b, &it, &res); break;
+    case LSSP_AMD_BICGSAFE: st = bicgsafe(R, *prm, x, b, &it, &res); break;
+    case LSSP_AMD_CGS: st = cgs(R, *prm, x, b, &it, &res); break;
+    case LSSP_AMD_GPBICG: st = gpbi(R, *prm, x, b, &it, &res, false); break;
+    case LSSP_AMD_CR: st = cr(R, *prm, x, b, &it, &res); break;
+    case LSSP_AMD_CRS: st = crs(R, *prm, x, b, &it, &res); break;
+    case LSSP_AMD_BICRSTAB: st = bicrstab(R, *prm, x, b, &it, &res); break;
+    case LSSP_AMD_BICRSAFE: st = bicrsafe(R, *prm, x, b, &it, &res); break;
+    case LSSP_AMD_GPBICR: st = gpbi(R, *prm, x, b, &it, &res, true); break;
+    case LSSP_AMD_QMRCGSTAB: st = qmrcgstab(R, *prm, x, b, &it, &res); break;
+    case LSSP_AMD_TFQMR: st = tfqmr(R, *prm, x, b, &it, &res); break;
+    case LSSP_AMD_ORTHOMIN: st = orthomin(R, *prm, x, b, &it, &res); break;
     default: st = LSSP_AMD_EUNSUPPORTED;
     }
     c->d_trace = saved_trace;

@@ -14,7 +14,9 @@ import numpy as np
 
 from . import _lib
 
-GMRES, LGMRES, RGMRES, BICGSTAB, CG = 0, 1, 2, 4, 7  # LSSP_SOLVER_TYPE (type-defs.h:157-178)
+GMRES, LGMRES, RGMRES, BICGSTAB, CG = 0, 1, 2, 4, 7
+BICGSAFE, CGS, GPBICG, CR, CRS, BICRSTAB, BICRSAFE, GPBICR, QMRCGSTAB, TFQMR, ORTHOMIN = (
+    6, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17)  # LSSP_SOLVER_TYPE (type-defs.h:157-178)
 ILUK, ILUT = 1, 2                  # LSSP_PC_TYPE (type-defs.h:63-101)
 SERIAL, TREE = 0, 1                # reduction order
 

@@ -29,6 +29,8 @@ REF_SO = os.path.join(HERE, "_ref", "libref.so")
 
 # LSSP_SOLVER_TYPE / LSSP_PC_TYPE values (type-defs.h:63-101, :157-178)
 GMRES, LGMRES, RGMRES, BICGSTAB, CG = 0, 1, 2, 4, 7
+BICGSAFE, CGS, GPBICG, CR, CRS, BICRSTAB, BICRSAFE, GPBICR, QMRCGSTAB, TFQMR, ORTHOMIN = (
+    6, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17)
 PC_NON, PC_ILUK, PC_ILUT = 0, 1, 2
 SERIAL, TREE = 0, 1
 

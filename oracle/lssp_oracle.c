@@ -1323,6 +1323,637 @@ done:
     return inner;
 }
 
+/* ------------------------------------------------------------------------ */
+/* The L1-composed drivers: the reference writes these purely as calls of     */
+/* its vector API, restated here call for call.  Work vectors are calloc'ed:  */
+/* BiCGSafe/BiCRSafe/GPBiCG/GPBiCR read some before writing them (the golden  */
+/* runs use zero-initialising malloc, oracle/ref_shim.cxx).                   */
+/* ------------------------------------------------------------------------ */
+
+enum { SOLVER_BICGSAFE = 6, SOLVER_CGS = 8, SOLVER_GPBICG = 9, SOLVER_CR = 10, SOLVER_CRS = 11,
+       SOLVER_BICRSTAB = 12, SOLVER_BICRSAFE = 13, SOLVER_GPBICR = 14, SOLVER_QMRCGSTAB = 15,
+       SOLVER_TFQMR = 16, SOLVER_ORTHOMIN = 17 };
+
+typedef struct {
+    ctx_t *c;
+    int n;
+    double tol_rel, tol_abs, tol_rb;
+    int maxit;
+} l1_t;
+
+static void v_axpby(int n, double a, const double *x, double b, double *y) /* vector.cxx:98-107 */
+{
+    for (int i = 0; i < n; i++) y[i] = y[i] * b + x[i] * a;
+}
+static void v_axpbyz(int n, double a, const double *x, double b, const double *y, double *z) /* :110-120 */
+{
+    for (int i = 0; i < n; i++) z[i] = y[i] * b + x[i] * a;
+}
+static void v_copy(int n, double *d, const double *s) { memcpy(d, s, sizeof(double) * (size_t)n); }
+static void v_set(int n, double *x, double v) { for (int i = 0; i < n; i++) x[i] = v; }
+static void v_scale(int n, double *x, double a) { for (int i = 0; i < n; i++) x[i] = x[i] * a; } /* :141-146 */
+static double *v_new(int n) { return (double *)calloc((size_t)(n > 0 ? n : 1), sizeof(double)); }
+
+#define NV(k) double *k = v_new(n)
+#define AXPBY(a, x, b, y) v_axpby(n, a, x, b, y)
+#define AXPBYZ(a, x, b, y, z) v_axpbyz(n, a, x, b, y, z)
+#define MXY(x, y) mv_mxy(S->c->A, x, y)
+#define RESID(x, b, r) mv_amxpbyz(-1, S->c->A, x, 1, b, r)
+#define PC(x, r) pc_apply(S->c, x, r)
+#define DOT(x, y) tdot(S->c, x, y)
+#define NORM(x) tnorm(S->c, x)
+
+static void l1_tol(const l1_t *S, double nrm2, double bnrb, double *tol)
+{
+    *tol = nrm2 * S->tol_rel;
+    if (*tol < S->tol_abs) *tol = S->tol_abs;
+    if (*tol < bnrb) *tol = bnrb;
+}
+
+/* solver-cgs.cxx:4-133 (vhat aliases uhat, :25) */
+static int l1_cgs(l1_t *S, double *x, const double *b, double *res)
+{
+    int n = S->n, iter;
+    NV(r); NV(rtld); NV(p); NV(phat); NV(q); NV(qhat); NV(u); NV(uhat);
+    double *vhat = uhat, alpha, beta, rho, rho_old = 1.0, tdot1, nrm2, ires, tol;
+    RESID(x, b, r);
+    iter = 0;
+    nrm2 = ires = NORM(r);
+    if (nrm2 <= S->tol_abs) goto end;
+    alpha = NORM(b) * S->tol_rb;
+    l1_tol(S, nrm2, alpha, &tol);
+    v_copy(n, rtld, r);
+    v_set(n, q, 0);
+    v_set(n, p, 0);
+    for (iter = 1; iter <= S->maxit; iter++) {
+        rho = DOT(rtld, r);
+        if (rho == 0.0) goto end;
+        beta = rho / rho_old;
+        AXPBYZ(beta, q, 1, r, u);
+        AXPBY(1, q, beta, p);
+        AXPBY(1, u, beta, p);
+        PC(phat, p);
+        MXY(phat, vhat);
+        tdot1 = DOT(rtld, vhat);
+        if (tdot1 == 0.0) goto end;
+        alpha = rho / tdot1;
+        AXPBYZ(-alpha, vhat, 1, u, q);
+        AXPBYZ(1, u, 1, q, phat);
+        PC(uhat, phat);
+        AXPBY(alpha, uhat, 1, x);
+        MXY(uhat, qhat);
+        AXPBY(-alpha, qhat, 1, r);
+        nrm2 = NORM(r);
+        if (tol >= nrm2) goto end;
+        rho_old = rho;
+    }
+end:
+    free(r); free(rtld); free(p); free(phat); free(q); free(qhat); free(u); free(uhat);
+    *res = nrm2;
+    return iter;
+}
+
+/* solver-cr.cxx:3-115 */
+static int l1_cr(l1_t *S, double *x, const double *b, double *res)
+{
+    int n = S->n, iter;
+    NV(r); NV(z); NV(p); NV(q); NV(qtld); NV(az);
+    double alpha, beta, rho, dot_rq, dot_zq, nrm2, ires, tol;
+    RESID(x, b, r);
+    nrm2 = ires = NORM(r);
+    iter = 1;
+    if (nrm2 <= S->tol_abs) goto end;
+    alpha = NORM(b) * S->tol_rb;
+    l1_tol(S, nrm2, alpha, &tol);
+    PC(p, r);
+    MXY(p, q);
+    v_copy(n, z, p);
+    for (iter = 1; iter <= S->maxit; iter++) {
+        PC(qtld, q);
+        rho = DOT(qtld, q);
+        if (rho == 0.0) goto end;
+        dot_rq = DOT(r, qtld);
+        alpha = dot_rq / rho;
+        AXPBY(alpha, p, 1, x);
+        AXPBY(-alpha, q, 1, r);
+        nrm2 = NORM(r);
+        if (tol >= nrm2) goto end;
+        AXPBY(-alpha, qtld, 1, z);
+        MXY(z, az);
+        dot_zq = DOT(az, qtld);
+        beta = -dot_zq / rho;
+        AXPBY(1, z, beta, p);
+        AXPBY(1, az, beta, q);
+    }
+end:
+    free(r); free(z); free(p); free(q); free(qtld); free(az);
+    *res = nrm2;
+    return iter;
+}
+
+/* solver-crs.cxx:3-109 (u = uq = z, ap = q, auq = map, :20-25) */
+static int l1_crs(l1_t *S, double *x, const double *b, double *res)
+{
+    int n = S->n, iter;
+    NV(r); NV(rtld); NV(p); NV(z); NV(q); NV(map);
+    double *u = z, *uq = z, *ap = q, *auq = map;
+    double alpha, beta, rho, rho_old, tdot1, nrm2, ires, tol;
+    RESID(x, b, r);
+    nrm2 = ires = NORM(r);
+    iter = 1;
+    if (nrm2 <= S->tol_abs) goto end;
+    alpha = NORM(b) * S->tol_rb;
+    l1_tol(S, nrm2, alpha, &tol);
+    v_copy(n, p, r);
+    MXY(p, rtld);
+    rho_old = 1.0;
+    v_set(n, q, 0.);
+    v_set(n, p, 0.);
+    for (iter = 1; iter <= S->maxit; iter++) {
+        PC(z, r);
+        rho = DOT(rtld, z);
+        if (rho == 0.0) goto end;
+        beta = rho / rho_old;
+        AXPBYZ(beta, q, 1, z, u);
+        AXPBY(1, q, beta, p);
+        AXPBY(1, u, beta, p);
+        MXY(p, ap);
+        PC(map, ap);
+        tdot1 = DOT(rtld, map);
+        if (tdot1 == 0.0) goto end;
+        alpha = rho / tdot1;
+        AXPBYZ(-alpha, map, 1, u, q);
+        AXPBYZ(1, u, 1, q, uq);
+        MXY(uq, auq);
+        AXPBY(alpha, uq, 1, x);
+        AXPBY(-alpha, auq, 1, r);
+        nrm2 = NORM(r);
+        if (tol >= nrm2) goto end;
+        rho_old = rho;
+    }
+end:
+    free(r); free(rtld); free(p); free(z); free(q); free(map);
+    *res = nrm2;
+    return iter;
+}
+
+/* solver-bicrstab.cxx:3-114 */
+static int l1_bicrstab(l1_t *S, double *x, const double *b, double *res)
+{
+    int n = S->n, iter;
+    NV(rtld); NV(r); NV(s); NV(ms); NV(ams); NV(p); NV(ap); NV(map); NV(z);
+    double alpha, beta, omega, rho, rho_old, tdot1, tdot2, nrm2, ires, tol;
+    RESID(x, b, r);
+    nrm2 = ires = NORM(r);
+    iter = 1;
+    if (nrm2 <= S->tol_abs) goto end;
+    alpha = NORM(b) * S->tol_rb;
+    l1_tol(S, nrm2, alpha, &tol);
+    v_copy(n, p, r);
+    MXY(p, rtld);
+    PC(z, r);
+    v_copy(n, p, z);
+    rho_old = DOT(rtld, z);
+    for (iter = 1; iter <= S->maxit; iter++) {
+        MXY(p, ap);
+        PC(map, ap);
+        tdot1 = DOT(rtld, map);
+        alpha = rho_old / tdot1;
+        AXPBYZ(-alpha, ap, 1, r, s);
+        nrm2 = NORM(s);
+        if (nrm2 <= tol) {
+            AXPBY(alpha, p, 1, x);
+            goto end;
+        }
+        AXPBYZ(-alpha, map, 1, z, ms);
+        MXY(ms, ams);
+        tdot1 = DOT(ams, s);
+        tdot2 = DOT(ams, ams);
+        omega = tdot1 / tdot2;
+        AXPBY(alpha, p, 1, x);
+        AXPBY(omega, ms, 1, x);
+        AXPBYZ(-omega, ams, 1, s, r);
+        nrm2 = NORM(r);
+        if (tol >= nrm2) goto end;
+        PC(z, r);
+        rho = DOT(rtld, z);
+        if (rho == 0.0) goto end;
+        beta = (rho / rho_old) * (alpha / omega);
+        AXPBY(-omega, map, 1, p);
+        AXPBY(1, z, beta, p);
+        rho_old = rho;
+    }
+end:
+    free(rtld); free(r); free(s); free(ms); free(ams); free(p); free(ap); free(map); free(z);
+    *res = nrm2;
+    return iter;
+}
+
+/* the (qsi, eta) pair, e.g. solver-bicgsafe.cxx:61-75 */
+static void l1_safe(l1_t *S, int iter, const double *y, const double *a, const double *r, double *qsi,
+                    double *eta)
+{
+    double td[5], tmp;
+    td[0] = DOT(y, y);
+    td[1] = DOT(a, r);
+    td[2] = DOT(y, r);
+    td[3] = DOT(a, y);
+    td[4] = DOT(a, a);
+    if (iter == 1) {
+        *qsi = td[1] / td[4];
+        *eta = 0.0;
+    } else {
+        tmp = td[4] * td[0] - td[3] * td[3];
+        *qsi = (td[0] * td[1] - td[2] * td[3]) / tmp;
+        *eta = (td[4] * td[2] - td[3] * td[1]) / tmp;
+    }
+}
+
+/* solver-bicgsafe.cxx:3-155 (cr_ = 0) and solver-bicrsafe.cxx:3-151 (cr_ = 1) */
+static int l1_safe_drv(l1_t *S, double *x, const double *b, double *res, int cr_)
+{
+    int n = S->n, iter;
+    NV(rtld); NV(r); NV(mr); NV(amr); NV(p); NV(ap); NV(t); NV(mt); NV(y); NV(u); NV(z); NV(au);
+    NV(map); NV(my); NV(artld);
+    double alpha, beta, rho, rho_old, qsi, eta, nrm2, ires, tol;
+    RESID(x, b, r);
+    nrm2 = ires = NORM(r);
+    iter = 1;
+    if (nrm2 <= S->tol_abs) goto end;
+    alpha = NORM(b) * S->tol_rb;
+    l1_tol(S, nrm2, alpha, &tol);
+    v_copy(n, rtld, r);
+    if (cr_) MXY(rtld, artld);
+    PC(mr, r);
+    MXY(mr, amr);
+    rho_old = cr_ ? DOT(rtld, amr) : DOT(rtld, r);
+    v_copy(n, ap, amr);
+    v_copy(n, p, mr);
+    beta = 0.0;
+    for (iter = 1; iter <= S->maxit; iter++) {
+        if (cr_) {
+            PC(map, ap);
+            alpha = rho_old / DOT(artld, map);
+        } else {
+            alpha = rho_old / DOT(rtld, ap);
+        }
+        l1_safe(S, iter, y, amr, r, &qsi, &eta);
+        if (cr_) {
+            v_scale(n, u, eta * beta);
+            AXPBY(qsi, map, 1, u);
+            AXPBY(eta, my, 1, u);
+        } else {
+            v_copy(n, t, y);
+            v_scale(n, t, eta);
+            AXPBY(qsi, ap, 1, t);
+            PC(mt, t);
+            AXPBY(1, mt, eta * beta, u);
+        }
+        MXY(u, au);
+        v_scale(n, z, eta);
+        AXPBY(qsi, mr, 1, z);
+        AXPBY(-alpha, u, 1, z);
+        v_scale(n, y, eta);
+        AXPBY(qsi, amr, 1, y);
+        AXPBY(-alpha, au, 1, y);
+        if (cr_) PC(my, y);
+        AXPBY(alpha, p, 1, x);
+        AXPBY(1, z, 1, x);
+        AXPBY(-alpha, ap, 1, r);
+        AXPBY(-1, y, 1.0, r);
+        nrm2 = NORM(r);
+        if (tol >= nrm2) goto end;
+        if (cr_) {
+            AXPBY(-alpha, map, 1, mr);
+            AXPBY(-1, my, 1, mr);
+            MXY(mr, amr);
+            rho = DOT(rtld, amr);
+            if (rho == 0.0) goto end;
+            beta = (rho / rho_old) * (alpha / qsi);
+        } else {
+            rho = DOT(rtld, r);
+            if (rho == 0.0) goto end;
+            beta = (rho / rho_old) * (alpha / qsi);
+            PC(mr, r);
+            MXY(mr, amr);
+        }
+        AXPBY(-1, u, 1.0, p);
+        AXPBY(1, mr, beta, p);
+        AXPBY(-1, au, 1.0, ap);
+        AXPBY(1, amr, beta, ap);
+        rho_old = rho;
+    }
+end:
+    free(rtld); free(r); free(mr); free(amr); free(p); free(ap); free(t); free(mt); free(y); free(u);
+    free(z); free(au); free(map); free(my); free(artld);
+    *res = nrm2;
+    return iter;
+}
+
+/* solver-gpbicg.cxx:3-163 (cr_ = 0) and solver-gpbicr.cxx:3-164 (cr_ = 1) */
+static int l1_gpbi(l1_t *S, double *x, const double *b, double *res, int cr_)
+{
+    int n = S->n, iter;
+    NV(rtld); NV(r); NV(mr); NV(p); NV(ap); NV(map); NV(t); NV(mt); NV(amt); NV(u); NV(y); NV(w);
+    NV(z); NV(mt_old);
+    double alpha, beta, rho, rho_old, qsi, eta, tdot0, nrm2, ires, tol;
+    RESID(x, b, r);
+    nrm2 = ires = NORM(r);
+    iter = 1;
+    if (nrm2 <= S->tol_abs) {
+        iter = 0;
+        goto end;
+    }
+    alpha = NORM(b) * S->tol_rb;
+    l1_tol(S, nrm2, alpha, &tol);
+    if (cr_) {
+        v_copy(n, p, r);
+        MXY(p, rtld);
+        PC(p, r);
+        rho_old = DOT(rtld, p);
+    } else {
+        v_copy(n, rtld, r);
+        PC(p, r);
+        rho_old = DOT(rtld, r);
+    }
+    v_set(n, t, 0.);
+    v_set(n, w, 0.);
+    beta = 0.0;
+    for (iter = 1; iter <= S->maxit; iter++) {
+        MXY(p, ap);
+        PC(map, ap);
+        tdot0 = DOT(rtld, cr_ ? map : ap);
+        if (tdot0 == 0.0) goto end;
+        alpha = rho_old / tdot0;
+        AXPBYZ(-1, w, 1, ap, y);
+        AXPBY(1, t, alpha, y);
+        AXPBY(-1, r, 1, y);
+        AXPBYZ(-alpha, ap, 1, r, t);
+        nrm2 = NORM(t);
+        if (nrm2 <= tol) {
+            AXPBY(alpha, p, 1, x);
+            goto end;
+        }
+        AXPBYZ(-alpha, map, 1, mr, mt);
+        MXY(mt, amt);
+        l1_safe(S, iter, y, amt, t, &qsi, &eta);
+        AXPBY(1., mt_old, beta, u);
+        AXPBY(-1, mr, 1, u);
+        v_scale(n, u, eta);
+        AXPBY(qsi, map, 1, u);
+        v_scale(n, z, eta);
+        AXPBY(qsi, mr, 1, z);
+        AXPBY(-alpha, u, 1, z);
+        AXPBY(alpha, p, 1, x);
+        AXPBY(1, z, 1., x);
+        AXPBYZ(-qsi, amt, 1, t, r);
+        AXPBY(-eta, y, 1, r);
+        nrm2 = NORM(r);
+        if (tol >= nrm2) goto end;
+        PC(mr, r);
+        rho = DOT(rtld, cr_ ? mr : r);
+        if (rho == 0.0) goto end;
+        beta = (rho / rho_old) * (alpha / qsi);
+        AXPBYZ(beta, ap, 1, amt, w);
+        AXPBY(-1, u, 1, p);
+        AXPBY(1., mr, beta, p);
+        v_copy(n, mt_old, mt);
+        rho_old = rho;
+    }
+end:
+    free(rtld); free(r); free(mr); free(p); free(ap); free(map); free(t); free(mt); free(amt); free(u);
+    free(y); free(w); free(z); free(mt_old);
+    *res = nrm2;
+    return iter;
+}
+
+/* solver-qmrcgstab.cxx:10-186 */
+static int l1_qmrcgstab(l1_t *S, double *xk, const double *bg, double *res)
+{
+    int n = S->n, itr_out;
+    NV(rk); NV(r); NV(br0); NV(pk); NV(vk); NV(sk); NV(dk); NV(tk); NV(bdk); NV(bxk);
+    double rho = 1, prho, alpha = 1, beta, omega = 1, theta = 0., btheta, b_eta, eta = 0., tau, btau;
+    double residual, c, ires, rerror, tol, tol_rb = S->tol_rb;
+    double b_norm = NORM(bg);
+    tol_rb *= b_norm;
+    RESID(xk, bg, tk);
+    residual = NORM(tk);
+    if (residual <= S->tol_abs) {
+        itr_out = 0;
+        goto end;
+    }
+    tol = residual * S->tol_rel;
+    if (tol < S->tol_abs) tol = S->tol_abs;
+    if (tol < tol_rb) tol = tol_rb;
+    tol = tol / residual;
+    PC(rk, tk);
+    v_copy(n, br0, rk);
+    v_set(n, pk, 0);
+    v_set(n, dk, 0);
+    v_set(n, vk, 0);
+    tau = ires = NORM(rk);
+    prho = rho;
+    for (itr_out = 0; itr_out < S->maxit; itr_out++) {
+        rho = DOT(br0, rk);
+        beta = rho * alpha / prho / omega;
+        prho = rho;
+        AXPBYZ(1, pk, -omega, vk, r);
+        AXPBYZ(beta, r, 1, rk, pk);
+        MXY(pk, r);
+        PC(vk, r);
+        alpha = rho / DOT(br0, vk);
+        AXPBYZ(-alpha, vk, 1, rk, sk);
+        btheta = NORM(sk) / tau;
+        c = 1 / sqrt(1. + btheta * btheta);
+        btau = tau * btheta * c;
+        b_eta = c * c * alpha;
+        AXPBYZ(1., pk, theta * theta * eta / alpha, dk, bdk);
+        AXPBYZ(1, xk, b_eta, bdk, bxk);
+        MXY(sk, r);
+        PC(tk, r);
+        {
+            double num = DOT(sk, tk); /* :146, operands in g++'s evaluation order */
+            omega = num / DOT(tk, tk);
+        }
+        AXPBYZ(1., sk, -omega, tk, rk);
+        theta = NORM(rk) / btau;
+        c = 1. / sqrt(1. + theta * theta);
+        tau = btau * theta * c;
+        eta = c * c * omega;
+        AXPBYZ(1, sk, btheta * btheta * b_eta / omega, bdk, dk);
+        AXPBYZ(1, bxk, eta, dk, xk);
+        rerror = NORM(rk) / ires;
+        if (rerror <= tol) {
+            RESID(xk, bg, tk);
+            residual = NORM(tk);
+            break;
+        }
+    }
+    if (itr_out < S->maxit) itr_out += 1;
+end:
+    free(rk); free(r); free(br0); free(pk); free(vk); free(sk); free(dk); free(tk); free(bdk); free(bxk);
+    *res = residual;
+    return itr_out;
+}
+
+/* solver-tfqmr.cxx:3-149 */
+static int l1_tfqmr(l1_t *S, double *x, const double *b, double *res)
+{
+    int n = S->n, iter;
+    NV(r); NV(rtld); NV(u); NV(p); NV(d); NV(t); NV(t1); NV(q); NV(v);
+    double alpha, beta, rho, rhoold, s, tau, theta, eta, c, w, wold, ww, nrm2, ires, tol;
+    RESID(x, b, r);
+    nrm2 = ires = NORM(r);
+    iter = 1;
+    if (nrm2 <= S->tol_abs) {
+        iter = 0;
+        goto end;
+    }
+    alpha = NORM(b) * S->tol_rb;
+    l1_tol(S, nrm2, alpha, &tol);
+    v_copy(n, rtld, r);
+    v_copy(n, p, r);
+    v_copy(n, u, r);
+    v_set(n, d, 0.);
+    PC(t, p);
+    MXY(t, v);
+    rhoold = DOT(r, rtld);
+    tau = NORM(r);
+    wold = tau;
+    theta = 0.0;
+    eta = 0.0;
+    while (iter <= S->maxit) {
+        s = DOT(v, rtld);
+        if (fabs(s) == 0.0) goto end;
+        alpha = rhoold / s;
+        AXPBYZ(-alpha, v, 1, u, q);
+        AXPBYZ(1, u, 1., q, t);
+        PC(t1, t);
+        MXY(t1, v);
+        AXPBY(-alpha, v, 1, r);
+        w = NORM(r);
+        for (int m = 0; m < 2; m++) {
+            if (m == 0) {
+                ww = sqrt(w * wold);
+                AXPBY(1, u, theta * theta * eta / alpha, d);
+            } else {
+                ww = w;
+                AXPBY(1, q, theta * theta * eta / alpha, d);
+            }
+            theta = ww / tau;
+            c = 1.0 / sqrt(1.0 + theta * theta);
+            eta = c * c * alpha;
+            tau = tau * theta * c;
+            PC(t1, d);
+            AXPBY(eta, t1, 1, x);
+            nrm2 = tau * sqrt(1.0 + m);
+            if (tol >= nrm2) goto end;
+        }
+        rho = DOT(r, rtld);
+        if (fabs(rho) == 0.0) goto end;
+        beta = rho / rhoold;
+        AXPBYZ(beta, q, 1, r, u);
+        AXPBY(1, q, beta, p);
+        AXPBY(1, u, beta, p);
+        PC(t1, p);
+        MXY(t1, v);
+        rhoold = rho;
+        wold = w;
+        iter++;
+    }
+end:
+    free(r); free(rtld); free(u); free(p); free(d); free(t); free(t1); free(q); free(v);
+    *res = nrm2;
+    return iter;
+}
+
+/* solver-orthomin.cxx:12-180: ORTHOMIN(k), k = restart */
+static int l1_orthomin(l1_t *S, int k, double *x, const double *rhs, double *res)
+{
+    int n = S->n, itr_out, i, j;
+    double tol = -1, err_rel = 0, beta, a_j, tol_rb = S->tol_rb;
+    if (k < 0) k = DEF_RESTART;
+    NV(z); NV(r); NV(s); NV(sd);
+    double *b_j = v_new(k), *c_j = v_new(k), **p = calloc((size_t)k, sizeof(double *));
+    double **q = calloc((size_t)k, sizeof(double *));
+    for (i = 0; i < k; i++) {
+        p[i] = v_new(n);
+        q[i] = v_new(n);
+    }
+    RESID(x, rhs, z);
+    v_set(n, r, 0.);
+    PC(r, z);
+    v_copy(n, p[0], r);
+    v_copy(n, sd, r);
+    double b_norm = NORM(rhs);
+    tol_rb *= b_norm;
+    beta = NORM(z);
+    if (beta <= S->tol_abs) {
+        itr_out = 0;
+        goto end;
+    }
+    err_rel = beta;
+    tol = S->tol_rel * err_rel;
+    if (tol < S->tol_abs) tol = S->tol_abs;
+    if (tol < tol_rb) tol = tol_rb;
+    for (itr_out = 0; itr_out < S->maxit; itr_out++) {
+        MXY(sd, s);
+        j = itr_out % k;
+        v_set(n, q[j], 0.);
+        PC(q[j], s);
+        a_j = DOT(r, q[j]);
+        c_j[j] = DOT(q[j], q[j]);
+        if (fabs(c_j[j]) <= BREAKDOWN) break;
+        a_j = a_j / c_j[j];
+        AXPBY(a_j, p[j], 1, x);
+        AXPBY(-a_j, q[j], 1, r);
+        v_copy(n, sd, r);
+        MXY(r, s);
+        v_set(n, z, 0.);
+        PC(z, s);
+        for (i = 0; i < (itr_out >= k - 1 ? k : itr_out + 1); i++) {
+            beta = DOT(z, q[i]);
+            b_j[i] = -beta / c_j[i];
+            AXPBY(b_j[i], p[i], 1, sd);
+        }
+        j = (itr_out + 1) % k;
+        v_copy(n, p[j], sd);
+        RESID(x, rhs, z);
+        beta = NORM(z);
+        if (beta <= tol) break;
+    }
+    if (itr_out < S->maxit) itr_out += 1;
+end:
+    for (i = 0; i < k; i++) {
+        free(p[i]);
+        free(q[i]);
+    }
+    free(p); free(q); free(b_j); free(c_j); free(z); free(r); free(s); free(sd);
+    *res = beta;
+    return itr_out;
+}
+
+static int l1_solve(ctx_t *c, int solver, double *x, const double *b, double tol_rel, double tol_abs,
+                    double tol_rb, int maxit, int restart, double *res)
+{
+    l1_t S = {c, c->A->nrows, tol_rel < 0 ? DEF_TOL : tol_rel, tol_abs < 0 ? DEF_TOL : tol_abs, tol_rb,
+              maxit <= 0 ? DEF_MAXIT : maxit};
+    switch (solver) {
+    case SOLVER_ORTHOMIN: return restart == 0 ? -1 : l1_orthomin(&S, restart, x, b, res);
+    case SOLVER_CGS: return l1_cgs(&S, x, b, res);
+    case SOLVER_CR: return l1_cr(&S, x, b, res);
+    case SOLVER_CRS: return l1_crs(&S, x, b, res);
+    case SOLVER_BICRSTAB: return l1_bicrstab(&S, x, b, res);
+    case SOLVER_BICGSAFE: return l1_safe_drv(&S, x, b, res, 0);
+    case SOLVER_BICRSAFE: return l1_safe_drv(&S, x, b, res, 1);
+    case SOLVER_GPBICG: return l1_gpbi(&S, x, b, res, 0);
+    case SOLVER_GPBICR: return l1_gpbi(&S, x, b, res, 1);
+    case SOLVER_QMRCGSTAB: return l1_qmrcgstab(&S, x, b, res);
+    case SOLVER_TFQMR: return l1_tfqmr(&S, x, b, res);
+    default: return -1;
+    }
+}
+
 /* Solve A x = b (x holds x0 on entry).  L/U == NULL => PC_NON.
  * trace receives every dot/norm the driver computes, in call order (the same
  * sequence tests/golden records from the reference). */
@@ -1355,7 +1986,7 @@ EXPORT int orc_solve(int solver, int n, const int *Ap, const int *Aj, const doub
     case SOLVER_GMRES: it = gmres(&c, x, b, tol_rel, tol_abs, tol_rb, maxit, restart, &res); break;
     case SOLVER_RGMRES: it = gmres_r(&c, x, b, tol_rel, tol_abs, tol_rb, maxit, restart, &res); break;
     case SOLVER_LGMRES: it = lgmres(&c, x, b, tol_rel, tol_abs, tol_rb, maxit, restart, &res); break;
-    default: it = -1;
+    default: it = l1_solve(&c, solver, x, b, tol_rel, tol_abs, tol_rb, maxit, restart, &res);
     }
     if (trace_len) *trace_len = c.len;
     if (residual) *residual = res;

@@ -9,6 +9,8 @@
 // lssp_vec_norm.  Used to generate tests/golden/ and as the CPU baseline.
 #include "lssp.h"
 
+#include <malloc.h>
+
 #include <vector>
 
 static bool g_trace_on = false;
@@ -164,6 +166,11 @@ int ref_solve(int solver, int pc_type, int level, double ilut_tol, int ilut_p, i
     LSSP_PC pc;
     lssp_mat_csr A = view(n, Ap, Aj, Ax);
     lssp_verbosity = 0;
+    // BiCGSafe, BiCRSafe, GPBiCG and GPBiCR read work vectors lssp_vec_create
+    // left uninitialised (malloc) before writing them; make malloc hand out
+    // zeroed bytes (glibc M_PERTURB: allocations filled with ~0xff) so those
+    // runs are deterministic -- the device drivers start from zeroed vectors.
+    mallopt(M_PERTURB, 0xff);
     lssp_solver_create(s, (LSSP_SOLVER_TYPE)solver, pc, (LSSP_PC_TYPE)pc_type);
     if (pc_type == LSSP_PC_ILUK) lssp_pc_iluk_set_level(pc, level);
     if (pc_type == LSSP_PC_ILUT) {
@@ -295,6 +302,7 @@ extern "C" int ref_solve_bj(void *hp, int solver, int n, const int *Ap, const in
     LSSP_PC pc;
     lssp_mat_csr A = view(n, Ap, Aj, Ax);
     lssp_verbosity = 0;
+    mallopt(M_PERTURB, 0xff);  // as in ref_solve
     lssp_solver_create(s, (LSSP_SOLVER_TYPE)solver, pc, LSSP_PC_USER);
     g_bjL = h->pc.L;
     g_bjU = h->pc.U;

@@ -164,6 +164,21 @@ def main():
         (LG, {"kind": "bj", "nblk": 4}, P7(32), "ones", None, {"restart": 12}),
         (LG, {"kind": "iluk", "level": 0}, P7(16), "zeros", None, {}),
     ]
+    # the L1-composed drivers (solver-{bicgsafe,cgs,gpbicg,cr,crs,bicrstab,bicrsafe,gpbicr,qmrcgstab,
+    # tfqmr}.cxx): SPD and nonsymmetric systems, each PC kind, maxit hit, immediate exit
+    for sv in (O.BICGSAFE, O.CGS, O.GPBICG, O.CR, O.CRS, O.BICRSTAB, O.BICRSAFE, O.GPBICR, O.QMRCGSTAB,
+               O.TFQMR, O.ORTHOMIN):
+        solves += [
+            (sv, {"kind": "iluk", "level": 0}, P7(16), "ones", None, {}),
+            (sv, {"kind": "none"}, P5(48), "ones", None, {}),
+            (sv, {"kind": "ilut", "tol": 1e-3, "p": 5}, RND2, 0x5EED, 0xB0B, {}),
+            (sv, {"kind": "iluk", "level": 1}, P7(12), "ones", None, {"maxit": 4}),
+            (sv, {"kind": "iluk", "level": 0}, P7(12), "zeros", None, {}),
+            (sv, {"kind": "bj", "nblk": 4}, P7(16), "ones", None, {}),
+        ]
+    # ORTHOMIN(k) with k = restart small enough to cycle its direction ring (solver-orthomin.cxx:102, :120)
+    solves += [(O.ORTHOMIN, {"kind": "iluk", "level": 0}, P7(16), "ones", None, {"restart": 3}),
+               (O.ORTHOMIN, {"kind": "ilut", "tol": 1e-3, "p": 5}, RND2, 0x5EED, 0xB0B, {"restart": 2})]
     pcmap = {"none": O.PC_NON, "iluk": O.PC_ILUK, "ilut": O.PC_ILUT}
     for solver, pc, mat, bspec, x0spec, kw in solves:
         A = build_matrix(mat)

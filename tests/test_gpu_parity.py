@@ -106,6 +106,7 @@ def test_solver_serial_mode_trace_bitwise_vs_reference(dev, c):
 
 
 TREE_CASES = [c for c in SOLVE if c["mat"].get("N", 0) <= 64 or c["mat"]["type"] == "rand"]
+L1_SOLVERS = (O.BICGSAFE, O.CGS, O.GPBICG, O.CR, O.CRS, O.BICRSTAB, O.BICRSAFE, O.GPBICR, O.QMRCGSTAB, O.TFQMR)
 
 
 @pytest.mark.parametrize("c", TREE_CASES, ids=[case_id(c) for c in TREE_CASES])
