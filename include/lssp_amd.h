@@ -41,7 +41,8 @@ enum {
     LSSP_AMD_GMRES = 0, LSSP_AMD_LGMRES = 1, LSSP_AMD_RGMRES = 2, LSSP_AMD_BICGSTAB = 4,
     LSSP_AMD_BICGSAFE = 6, LSSP_AMD_CG = 7, LSSP_AMD_CGS = 8, LSSP_AMD_GPBICG = 9, LSSP_AMD_CR = 10,
     LSSP_AMD_CRS = 11, LSSP_AMD_BICRSTAB = 12, LSSP_AMD_BICRSAFE = 13, LSSP_AMD_GPBICR = 14,
-    LSSP_AMD_QMRCGSTAB = 15, LSSP_AMD_TFQMR = 16, LSSP_AMD_ORTHOMIN = 17
+    LSSP_AMD_QMRCGSTAB = 15, LSSP_AMD_TFQMR = 16, LSSP_AMD_ORTHOMIN = 17,
+    LSSP_AMD_BICGSTABL = 5, LSSP_AMD_IDRS = 18
 };
 /* ILU kinds (LSSP_PC_TYPE, type-defs.h:63-101) */
 enum { LSSP_AMD_ILUK = 1, LSSP_AMD_ILUT = 2 };
@@ -130,7 +131,9 @@ int lssp_amd_ilu_get_factors(const lssp_amd_ilu *M, int *Lp, int *Lj, double *Lx
 /* ---- Krylov solve: lssp_solver_solve (lssp.cxx:250-414) for BiCGSTAB
  *      (solver-bicgstab.cxx:10-175), GMRES(m) (solver-gmres.cxx:12-255),
  *      right-preconditioned GMRES(m) (solver-gmres.cxx:257-479), LGMRES(m, k)
- *      (solver-lgmres.cxx:12-312) and CG (solver-cg.cxx:8-136).  Same recurrences, guards, defaults and
+ *      (solver-lgmres.cxx:12-312), CG (solver-cg.cxx:8-136), and the other internal
+ *      drivers (solver-{bicgstabl,bicgsafe,cgs,gpbicg,cr,crs,bicrstab,bicrsafe,
+ *      gpbicr,qmrcgstab,tfqmr,orthomin,idrs}.cxx).  Same recurrences, guards, defaults and
  *      iteration counting; vectors stay in HBM. ------------------------- */
 typedef struct {
     int solver;     /* LSSP_AMD_* above (LSSP_SOLVER_TYPE) */
@@ -141,6 +144,8 @@ typedef struct {
     int restart;    /* GMRES m; < 0: default 50 */
     int verb;       /* >= 1 prints the reference's per-iteration line */
     int aug_k;      /* LGMRES augmentation vectors k; <= 0: default 3 (lssp.cxx:6) */
+    int bgsl;       /* BiCGSTAB(l) l; <= 0: default 4 (LSSP_SOLVER.bgsl, lssp.cxx:7, :495-503) */
+    int idrs;       /* IDR(s) s; <= 0: default 4 (LSSP_SOLVER.idrs, lssp.cxx:8, :505-513) */
 } lssp_amd_solve_params;
 
 /* x: device, x0 on entry, solution on exit; b: device.  M == NULL is PC_NON

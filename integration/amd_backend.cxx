@@ -1,13 +1,14 @@
 // amd_backend.cxx -- the reference-side binding: route LSSP's Krylov hot path
-// (BiCGSTAB / GMRES(m) / right-preconditioned GMRES(m) / LGMRES(m, k) / CG with
-// PC_NON, ILUK or ILUT) to lssp_amd on MI355X.
+// (all 18 internal Krylov drivers: BiCGSTAB, BiCGSTAB(l), GMRES(m), GMRES-R(m),
+// LGMRES(m, k), CG, CGS, CR, CRS, BiCGSafe, BiCRSTAB, BiCRSafe, GPBiCG, GPBiCR,
+// QMRCGSTAB, TFQMR, ORTHOMIN, IDR(s), with PC_NON, ILUK or ILUT) to lssp_amd on MI355X.
 //
 // This is the translation unit a maintainer adds to huiscliu/lssp (as
 // src/amd-backend.cxx); INTEGRATION.md describes it.  It compiles against the
-// reference's own headers and replaces, at link time, the five drivers that
-// lssp_solver_solve dispatches to (lssp.cxx:259-289):
+// reference's own headers and replaces, at link time, the drivers that
+// lssp_solver_solve dispatches to (lssp.cxx:259-336):
 //
-//     -Wl,--wrap=<mangled lssp_solver_bicgstab / _gmres / _gmres_r / _lgmres / _cg>
+//     -Wl,--wrap=<mangled lssp_solver_*>   (one per AMD_DRIVER line below)
 //
 // so lssp.cxx, the drivers and every caller (example/exam.cxx) stay unchanged.
 // Everything else (assemble, the column sort, the ILU setup of pc-iluk.cxx /
@@ -23,20 +24,6 @@
 // sequential dot order (bitwise-identical runs).
 #include "lssp.h"
 #include "lssp_amd.h"
-
-// the linker's --wrap names are the mangled symbols with a prefix: declare them unmangled
-extern "C" {
-int __real__Z20lssp_solver_bicgstabR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
-int __real__Z17lssp_solver_gmresR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
-int __real__Z14lssp_solver_cgR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
-int __real__Z19lssp_solver_gmres_rR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
-int __real__Z18lssp_solver_lgmresR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
-int __wrap__Z18lssp_solver_lgmresR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
-int __wrap__Z19lssp_solver_gmres_rR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
-int __wrap__Z20lssp_solver_bicgstabR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
-int __wrap__Z17lssp_solver_gmresR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
-int __wrap__Z14lssp_solver_cgR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &, LSSP_PC &);
-}
 
 static lssp_amd_ctx *amd_ctx()
 {
@@ -85,6 +72,8 @@ static int amd_solve(LSSP_SOLVER &s, LSSP_PC &pc, int solver)
     p.restart = s.restart;
     p.verb = s.verb;
     p.aug_k = s.aug_k;
+    p.bgsl = s.bgsl;
+    p.idrs = s.idrs;
     int nits = 0;
     double res = 0.;
     fflush(stdout);  // the device driver prints with stdio too: keep the line order
@@ -101,32 +90,33 @@ static int amd_solve(LSSP_SOLVER &s, LSSP_PC &pc, int solver)
     return nits;
 }
 
-int __wrap__Z20lssp_solver_bicgstabR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &s, LSSP_PC &pc)
-{
-    if (!amd_handles(pc)) return __real__Z20lssp_solver_bicgstabR12LSSP_SOLVER_R8LSSP_PC_(s, pc);
-    return amd_solve(s, pc, LSSP_AMD_BICGSTAB);
-}
+// One wrapper per driver: the linker's --wrap=SYM sends every call of SYM here
+// and names the original __real_SYM; PCs this library does not hold (BILUK,
+// ITSOL, AMG, user PCs) fall through to the reference's own driver.
+#define AMD_DRIVER(SYM, KIND)                                                   \
+    extern "C" int __real_##SYM(LSSP_SOLVER &, LSSP_PC &);                      \
+    extern "C" int __wrap_##SYM(LSSP_SOLVER &s, LSSP_PC &pc)                    \
+    {                                                                           \
+        if (!amd_handles(pc)) return __real_##SYM(s, pc);                       \
+        return amd_solve(s, pc, KIND);                                          \
+    }
 
-int __wrap__Z17lssp_solver_gmresR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &s, LSSP_PC &pc)
-{
-    if (!amd_handles(pc)) return __real__Z17lssp_solver_gmresR12LSSP_SOLVER_R8LSSP_PC_(s, pc);
-    return amd_solve(s, pc, LSSP_AMD_GMRES);
-}
-
-int __wrap__Z14lssp_solver_cgR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &s, LSSP_PC &pc)
-{
-    if (!amd_handles(pc)) return __real__Z14lssp_solver_cgR12LSSP_SOLVER_R8LSSP_PC_(s, pc);
-    return amd_solve(s, pc, LSSP_AMD_CG);
-}
-
-int __wrap__Z19lssp_solver_gmres_rR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &s, LSSP_PC &pc)
-{
-    if (!amd_handles(pc)) return __real__Z19lssp_solver_gmres_rR12LSSP_SOLVER_R8LSSP_PC_(s, pc);
-    return amd_solve(s, pc, LSSP_AMD_RGMRES);
-}
-
-int __wrap__Z18lssp_solver_lgmresR12LSSP_SOLVER_R8LSSP_PC_(LSSP_SOLVER &s, LSSP_PC &pc)
-{
-    if (!amd_handles(pc)) return __real__Z18lssp_solver_lgmresR12LSSP_SOLVER_R8LSSP_PC_(s, pc);
-    return amd_solve(s, pc, LSSP_AMD_LGMRES);
-}
+// lssp.cxx:259-336 dispatch targets (mangled names of the drivers in src/solver-*.cxx)
+AMD_DRIVER(_Z17lssp_solver_gmresR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_GMRES)
+AMD_DRIVER(_Z18lssp_solver_lgmresR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_LGMRES)
+AMD_DRIVER(_Z19lssp_solver_gmres_rR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_RGMRES)
+AMD_DRIVER(_Z20lssp_solver_bicgstabR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_BICGSTAB)
+AMD_DRIVER(_Z21lssp_solver_bicgstablR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_BICGSTABL)
+AMD_DRIVER(_Z20lssp_solver_bicgsafeR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_BICGSAFE)
+AMD_DRIVER(_Z14lssp_solver_cgR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_CG)
+AMD_DRIVER(_Z15lssp_solver_cgsR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_CGS)
+AMD_DRIVER(_Z18lssp_solver_gpbicgR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_GPBICG)
+AMD_DRIVER(_Z14lssp_solver_crR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_CR)
+AMD_DRIVER(_Z15lssp_solver_crsR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_CRS)
+AMD_DRIVER(_Z20lssp_solver_bicrstabR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_BICRSTAB)
+AMD_DRIVER(_Z20lssp_solver_bicrsafeR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_BICRSAFE)
+AMD_DRIVER(_Z18lssp_solver_gpbicrR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_GPBICR)
+AMD_DRIVER(_Z21lssp_solver_qmrcgstabR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_QMRCGSTAB)
+AMD_DRIVER(_Z17lssp_solver_tfqmrR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_TFQMR)
+AMD_DRIVER(_Z20lssp_solver_orthominR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_ORTHOMIN)
+AMD_DRIVER(_Z16lssp_solver_idrsR12LSSP_SOLVER_R8LSSP_PC_, LSSP_AMD_IDRS)

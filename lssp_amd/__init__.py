@@ -17,8 +17,10 @@ _lib.load()
 
 from .device import (BICGSTAB, CG, GMRES, LGMRES, RGMRES, ILUK, ILUT, SERIAL, TREE, DILU, DMat,  # noqa: E402,F401
                      Device, DVec, LsspError, comm_unique_id, poisson, solve, sort_columns,
-                     BICGSAFE, CGS, GPBICG, CR, CRS, BICRSTAB, BICRSAFE, GPBICR, QMRCGSTAB, TFQMR, ORTHOMIN)
+                     BICGSAFE, CGS, GPBICG, CR, CRS, BICRSTAB, BICRSAFE, GPBICR, QMRCGSTAB, TFQMR, ORTHOMIN,
+                     BICGSTABL, IDRS)
 
 __all__ = ["Device", "DVec", "DMat", "DILU", "solve", "poisson", "sort_columns", "LsspError",
            "comm_unique_id", "GMRES", "LGMRES", "RGMRES", "BICGSTAB", "CG", "ILUK", "ILUT", "SERIAL", "TREE",
-           "BICGSAFE", "CGS", "GPBICG", "CR", "CRS", "BICRSTAB", "BICRSAFE", "GPBICR", "QMRCGSTAB", "TFQMR", "ORTHOMIN"]
+           "BICGSAFE", "CGS", "GPBICG", "CR", "CRS", "BICRSTAB", "BICRSAFE", "GPBICR", "QMRCGSTAB", "TFQMR", "ORTHOMIN",
+           "BICGSTABL", "IDRS"]

@@ -28,7 +28,8 @@ class HostTransport(ctypes.Structure):
 
 class SolveParams(ctypes.Structure):
     _fields_ = [("solver", _ci), ("tol_rel", _cd), ("tol_abs", _cd), ("tol_rb", _cd),
-                ("maxit", _ci), ("restart", _ci), ("verb", _ci), ("aug_k", _ci)]
+                ("maxit", _ci), ("restart", _ci), ("verb", _ci), ("aug_k", _ci),
+                ("bgsl", _ci), ("idrs", _ci)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/lssp_amd.h

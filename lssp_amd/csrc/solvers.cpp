@@ -1610,6 +1610,294 @@ int orthomin(Run &R, const lssp_amd_solve_params &P, double *x, const double *rh
     return LSSP_AMD_OK;
 }
 
+// BiCGSTAB(l) (solver-bicgstabl.cxx:4-217).  x accumulates the right-
+// preconditioned iterate; on every converged / breakdown exit the reference
+// maps it back as x = M^-1 x + x0 (:84-86, :131-133, :190-192) -- not when
+// the outer loop runs out of iterations (iter is tested only there, :73).
+int bicgstabl(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
+{
+    L1K K(R);
+    double tol_rel, tol_abs, tol_rb = P.tol_rb < 0 ? DEF_TOL : P.tol_rb, tol = 0;
+    int maxiter, iter, i, j;
+    defaults(P, tol_rel, tol_abs, maxiter);
+    const int l = P.bgsl <= 0 ? 4 : P.bgsl;  // :27-29; LSSP_BGSL = 4 (lssp.cxx:7)
+    const int zd = l + 1;
+    double *rtld = K.vec(), *xp = K.vec(), *bp = K.vec(), *t = K.vec();
+    std::vector<double *> r(l + 1), u(l + 1);
+    for (i = 0; i <= l; i++) r[i] = K.vec();
+    for (i = 0; i <= l; i++) u[i] = K.vec();
+    std::vector<double> tau(zd * zd, 0.), gamma(zd, 0.), gamma1(zd, 0.), gamma2(zd, 0.), sigma(zd, 0.);
+    double alpha, beta, omega, rho0, rho1, nu, nrm2, ires;
+    auto unprecondition = [&]() {  // pc.solve(t, x); copy(x, t); x = x + xp
+        K.pc(t, x);
+        K.copy(x, t);
+        K.axpby(1, xp, 1, x);
+    };
+    K.resid(x, b, r[0]);
+    K.copy(rtld, r[0]);
+    K.copy(bp, r[0]);
+    K.copy(xp, x);
+    K.set(u[0], 0.);
+    iter = 0;
+    nrm2 = ires = K.norm(r[0]);
+    if (!K.ok() || nrm2 <= tol_abs) L1_DONE();
+    tol = nrm2 * tol_rel;
+    alpha = K.norm(b) * tol_rb;
+    if (tol < tol_abs) tol = tol_abs;
+    if (tol < alpha) tol = alpha;
+    alpha = 0.0;
+    omega = 1.0;
+    rho0 = 1.0;
+    while (iter <= maxiter) {
+        rho0 = -omega * rho0;
+        for (j = 0; j < l; j++) {
+            iter++;
+            rho1 = K.dot(rtld, r[j]);
+            if (!K.ok()) return K.st;
+            if (rho1 == 0.0) {
+                unprecondition();
+                L1_DONE();
+            }
+            beta = alpha * (rho1 / rho0);
+            rho0 = rho1;
+            for (i = 0; i <= j; i++) K.axpby(1, r[i], -beta, u[i]);
+            K.pc(t, u[j]);
+            K.mxy(t, u[j + 1]);
+            nu = K.dot(rtld, u[j + 1]);
+            if (!K.ok()) return K.st;
+            if (fabs(nu) == 0.0) {
+                unprecondition();
+                L1_DONE();
+            }
+            alpha = rho1 / nu;
+            K.axpby(alpha, u[0], 1, x);
+            for (i = 0; i <= j; i++) K.axpby(-alpha, u[i + 1], 1, r[i]);
+            nrm2 = K.norm(r[0]);
+            if (!K.ok()) return K.st;
+            if (P.verb >= 1 && R.rank == 0)
+                printf("bicgstabl: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+            if (nrm2 <= tol) {
+                unprecondition();
+                L1_DONE();
+            }
+            K.pc(t, r[j]);
+            K.mxy(t, r[j + 1]);
+        }
+        // MR part (:143-171): modified Gram-Schmidt on r[1..l], then the small triangular solves
+        for (j = 1; j <= l; j++) {
+            for (i = 1; i <= j - 1; i++) {
+                nu = K.dot(r[j], r[i]);
+                nu = nu / sigma[i];
+                tau[i * zd + j] = nu;
+                K.axpby(-nu, r[i], 1, r[j]);
+            }
+            sigma[j] = K.dot(r[j], r[j]);
+            nu = K.dot(r[0], r[j]);
+            gamma1[j] = nu / sigma[j];
+        }
+        if (!K.ok()) return K.st;
+        gamma[l] = gamma1[l];
+        omega = gamma[l];
+        for (j = l - 1; j >= 1; j--) {
+            nu = 0.0;
+            for (i = j + 1; i <= l; i++) nu += tau[j * zd + i] * gamma[i];
+            gamma[j] = gamma1[j] - nu;
+        }
+        for (j = 1; j <= l - 1; j++) {
+            nu = 0.0;
+            for (i = j + 1; i <= l - 1; i++) nu += tau[j * zd + i] * gamma[i + 1];
+            gamma2[j] = gamma[j + 1] + nu;
+        }
+        // UPDATE (:174-182)
+        K.axpby(gamma[1], r[0], 1, x);
+        K.axpby(-gamma1[l], r[l], 1, r[0]);
+        K.axpby(-gamma[l], u[l], 1, u[0]);
+        for (j = 1; j <= l - 1; j++) {
+            K.axpby(-gamma[j], u[j], 1, u[0]);
+            K.axpby(gamma2[j], r[j], 1, x);
+            K.axpby(-gamma1[j], r[j], 1, r[0]);
+        }
+        nrm2 = K.norm(r[0]);
+        if (!K.ok()) return K.st;
+        if (P.verb >= 1 && R.rank == 0)
+            printf("bicgstabl: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+        if (nrm2 < tol) {
+            unprecondition();
+            L1_DONE();
+        }
+    }
+    L1_DONE();
+}
+
+// solver-idrs.cxx:23-84: solve the s x s system M c = m (read column-major),
+// LU without pivoting; the s = 1 and s = 2 cases are the reference's own
+// unrolled forms.
+static void idrs_array_solve(int n, const double *a, const double *b, double *x, double *w)
+{
+    int i, j, k;
+    double t;
+    for (i = 0; i < n * n; i++) w[i] = a[i];
+    switch (n) {
+    case 1: x[0] = b[0] / w[0]; break;
+    case 2:
+        w[0] = 1.0 / w[0];
+        w[1] *= w[0];
+        w[3] -= w[1] * w[2];
+        w[3] = 1.0 / w[3];
+        x[0] = b[0];
+        x[1] = b[1] - w[1] * x[0];
+        x[1] *= w[3];
+        x[0] -= w[2] * x[1];
+        x[0] *= w[0];
+        break;
+    default:
+        for (k = 0; k < n; k++) {
+            w[k + k * n] = 1.0 / w[k + k * n];
+            for (i = k + 1; i < n; i++) {
+                t = w[i + k * n] * w[k + k * n];
+                for (j = k + 1; j < n; j++) w[i + j * n] -= t * w[k + j * n];
+                w[i + k * n] = t;
+            }
+        }
+        for (i = 0; i < n; i++) {
+            x[i] = b[i];
+            for (j = 0; j < i; j++) x[i] -= w[i + j * n] * x[j];
+        }
+        for (i = n - 1; i >= 0; i--) {
+            for (j = i + 1; j < n; j++) x[i] -= w[i + j * n] * x[j];
+            x[i] *= w[i + i * n];
+        }
+        break;
+    }
+}
+
+// IDR(s) (solver-idrs.cxx:86-283).  The shadow space P is srand(0); rand() /
+// RAND_MAX over the GLOBAL vector, k-major (:139-144) -- drawn here from a
+// private glibc random_r state seeded the same way (so the caller's rand()
+// stream is left alone), each rank keeping its own rows -- then orthonormalised
+// with idrs_orth (:4-21).  The inline update loops
+//   dX[o][i] = om*av[i] - sum_j dX[j][i]*c[j]   (:198-205, :219-226)
+//   dR[o][i] = -om*t[i] - sum_j dR[j][i]*c[j]   (:207-214)
+// become one y = x*a pass and s axpby passes (y*1 + x*(-c) is y - x*c
+// bitwise) into a spare vector that then takes the place of dX[o] / dR[o].
+int idrs(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
+{
+    L1K K(R);
+    double tol_rel, tol_abs, tol_rb = P.tol_rb < 0 ? DEF_TOL : P.tol_rb, tol = 0;
+    int maxiter, iter, i, j, k, oldest;
+    defaults(P, tol_rel, tol_abs, maxiter);
+    const int s = P.idrs <= 0 ? 4 : P.idrs;  // :100-101; LSSP_IDRS = 4 (lssp.cxx:8)
+    double *r = K.vec(), *t = K.vec(), *v = K.vec(), *av = K.vec(), *spare = K.vec();
+    std::vector<double *> dX(s), dR(s), Pv(s);
+    for (i = 0; i < s; i++) {
+        dX[i] = K.vec();
+        dR[i] = K.vec();
+        Pv[i] = K.vec();
+    }
+    std::vector<double> m(s), c(s), M(s * s), MM(s * s);
+    double om = 0, h, nrm2, ires;
+    iter = 0;
+    K.resid(x, b, r);
+    nrm2 = ires = K.norm(r);
+    if (!K.ok() || nrm2 <= tol_abs) L1_DONE();
+    tol = nrm2 * tol_rel;
+    h = K.norm(b) * tol_rb;
+    if (tol < tol_abs) tol = tol_abs;
+    if (tol < h) tol = h;
+    if (!K.ok()) return K.st;
+    {
+        const long n = R.n, ng = R.A->n_global > 0 ? R.A->n_global : R.n, r0 = R.A->row0;
+        std::vector<double> hp(n);
+        struct random_data rd;
+        char state[128];
+        memset(&rd, 0, sizeof(rd));
+        memset(state, 0, sizeof(state));
+        initstate_r(0, state, sizeof(state), &rd);  // == srand(0) on glibc's default TYPE_3 state
+        for (k = 0; k < s; k++) {
+            for (long q = 0; q < ng; q++) {
+                int32_t v32;
+                random_r(&rd, &v32);
+                if (q >= r0 && q < r0 + n) hp[q - r0] = (v32 * 1.) / (1. * RAND_MAX);
+            }
+            K.chk(hipMemcpyAsync(Pv[k], hp.data(), sizeof(double) * n, hipMemcpyHostToDevice, R.c->stream) ==
+                          hipSuccess ? LSSP_AMD_OK : LSSP_AMD_EHIP);
+            K.chk(hipStreamSynchronize(R.c->stream) == hipSuccess ? LSSP_AMD_OK : LSSP_AMD_EHIP);
+        }
+    }
+    for (j = 0; j < s; j++) {  // idrs_orth (:4-21)
+        double rr = K.norm(Pv[j]);
+        rr = 1.0 / rr;
+        K.scale(Pv[j], rr);
+        for (i = j + 1; i < s; i++) {
+            const double d = K.dot(Pv[j], Pv[i]);
+            K.axpby(-d, Pv[j], 1, Pv[i]);
+        }
+    }
+    for (k = 0; k < s; k++) {
+        K.pc(dX[k], r);
+        K.mxy(dX[k], dR[k]);
+        h = K.dot(dR[k], dR[k]);
+        om = K.dot(dR[k], r);
+        om = om / h;
+        K.scale(dX[k], om);
+        K.scale(dR[k], -om);
+        K.axpby(1, dX[k], 1, x);
+        K.axpby(1, dR[k], 1, r);
+        nrm2 = K.norm(r);
+        if (!K.ok()) return K.st;
+        if (tol >= nrm2) {
+            iter = k + 1;
+            L1_DONE();
+        }
+        for (i = 0; i < s; i++) M[k * s + i] = K.dot(Pv[i], dR[k]);
+    }
+    iter = s;
+    oldest = 0;
+    for (i = 0; i < s; i++) m[i] = K.dot(Pv[i], r);
+    // dst = a*src - sum_j V[j]*c[j], written to the spare vector, which then replaces V[oldest]
+    auto combine = [&](double a, const double *src, std::vector<double *> &V) {
+        K.ew(K_AXY, a, 0, src, nullptr, spare);
+        for (int q = 0; q < s; q++) K.axpby(-c[q], V[q], 1, spare);
+        std::swap(spare, V[oldest]);
+    };
+    while (iter <= maxiter) {
+        if (!K.ok()) return K.st;
+        idrs_array_solve(s, M.data(), m.data(), c.data(), MM.data());
+        K.copy(v, r);
+        for (j = 0; j < s; j++) K.axpby(-c[j], dR[j], 1, v);
+        if ((iter % (s + 1)) == s) {
+            K.pc(av, v);
+            K.mxy(av, t);
+            h = K.dot(t, t);
+            om = K.dot(t, v);
+            om = om / h;
+            combine(om, av, dX);
+            combine(-om, t, dR);
+        } else {
+            K.pc(av, v);
+            combine(om, av, dX);
+            K.mxy(dX[oldest], dR[oldest]);
+            K.scale(dR[oldest], -1.);
+        }
+        K.axpby(1, dR[oldest], 1, r);
+        K.axpby(1, dX[oldest], 1, x);
+        iter++;
+        nrm2 = K.norm(r);
+        if (!K.ok()) return K.st;
+        if (P.verb >= 1 && R.rank == 0)
+            printf("idrs: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+        if (tol >= nrm2) L1_DONE();
+        for (i = 0; i < s; i++) {
+            h = K.dot(Pv[i], dR[oldest]);
+            m[i] += h;
+            M[oldest * s + i] = h;
+        }
+        oldest++;
+        if (oldest == s) oldest = 0;
+    }
+    L1_DONE();
+}
+
 }  // namespace
 }  // namespace lssp_amd
 
@@ -1661,6 +1949,8 @@ extern "C" int lssp_amd_solve(lssp_amd_ctx *c, const lssp_amd_mat *A, const lssp
     case LSSP_AMD_QMRCGSTAB: st = qmrcgstab(R, *prm, x, b, &it, &res); break;
     case LSSP_AMD_TFQMR: st = tfqmr(R, *prm, x, b, &it, &res); break;
     case LSSP_AMD_ORTHOMIN: st = orthomin(R, *prm, x, b, &it, &res); break;
+    case LSSP_AMD_BICGSTABL: st = bicgstabl(R, *prm, x, b, &it, &res); break;
+    case LSSP_AMD_IDRS: st = idrs(R, *prm, x, b, &it, &res); break;
     default: st = LSSP_AMD_EUNSUPPORTED;
     }
     c->d_trace = saved_trace;

@@ -17,6 +17,7 @@ from . import _lib
 GMRES, LGMRES, RGMRES, BICGSTAB, CG = 0, 1, 2, 4, 7
 BICGSAFE, CGS, GPBICG, CR, CRS, BICRSTAB, BICRSAFE, GPBICR, QMRCGSTAB, TFQMR, ORTHOMIN = (
     6, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17)  # LSSP_SOLVER_TYPE (type-defs.h:157-178)
+BICGSTABL, IDRS = 5, 18
 ILUK, ILUT = 1, 2                  # LSSP_PC_TYPE (type-defs.h:63-101)
 SERIAL, TREE = 0, 1                # reduction order
 
@@ -267,8 +268,9 @@ class Result:
 
 
 def solve(dev: Device, A: DMat, M: DILU | None, x: DVec, b: DVec, solver=BICGSTAB, tol_rel=1e-7,
-          tol_abs=1e-7, tol_rb=1e-7, maxit=1000, restart=30, verb=0, trace_cap=0, aug_k=3) -> Result:
-    prm = _lib.SolveParams(solver, tol_rel, tol_abs, tol_rb, maxit, restart, verb, aug_k)
+          tol_abs=1e-7, tol_rb=1e-7, maxit=1000, restart=30, verb=0, trace_cap=0, aug_k=3, bgsl=4,
+          idrs=4) -> Result:
+    prm = _lib.SolveParams(solver, tol_rel, tol_abs, tol_rb, maxit, restart, verb, aug_k, bgsl, idrs)
     it, res, tl = ctypes.c_int(), ctypes.c_double(), ctypes.c_int()
     tr = np.zeros(max(trace_cap, 1))
     _ck(dev.L.lssp_amd_solve(dev.h, A.h, M.h if M is not None else None, ctypes.byref(prm), x.ptr, b.ptr,

@@ -31,6 +31,7 @@ REF_SO = os.path.join(HERE, "_ref", "libref.so")
 GMRES, LGMRES, RGMRES, BICGSTAB, CG = 0, 1, 2, 4, 7
 BICGSAFE, CGS, GPBICG, CR, CRS, BICRSTAB, BICRSAFE, GPBICR, QMRCGSTAB, TFQMR, ORTHOMIN = (
     6, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17)
+BICGSTABL, IDRS = 5, 18  # l of BiCGSTAB(l) / s of IDR(s) are passed as `restart` (<= 0: 4)
 PC_NON, PC_ILUK, PC_ILUT = 0, 1, 2
 SERIAL, TREE = 0, 1
 

@@ -1332,7 +1332,7 @@ done:
 
 enum { SOLVER_BICGSAFE = 6, SOLVER_CGS = 8, SOLVER_GPBICG = 9, SOLVER_CR = 10, SOLVER_CRS = 11,
        SOLVER_BICRSTAB = 12, SOLVER_BICRSAFE = 13, SOLVER_GPBICR = 14, SOLVER_QMRCGSTAB = 15,
-       SOLVER_TFQMR = 16, SOLVER_ORTHOMIN = 17 };
+       SOLVER_TFQMR = 16, SOLVER_ORTHOMIN = 17, SOLVER_BICGSTABL = 5, SOLVER_IDRS = 18 };
 
 typedef struct {
     ctx_t *c;
@@ -1933,6 +1933,276 @@ end:
     return itr_out;
 }
 
+/* solver-bicgstabl.cxx:4-217: BiCGSTAB(l).  x carries the right-preconditioned
+ * iterate and is mapped back as x = M^-1 x + x0 on the converged / breakdown
+ * exits only (:84-86, :105-107, :131-133, :190-192). */
+static void l1_bgsl_back(l1_t *S, double *x, double *t, const double *xp)
+{
+    int n = S->n;
+    PC(t, x);
+    v_copy(n, x, t);
+    AXPBY(1, xp, 1, x);
+}
+
+static int l1_bicgstabl(l1_t *S, int l, double *x, const double *b, double *res)
+{
+    int n = S->n, iter, i, j, zd = l + 1;
+    NV(rtld); NV(xp); NV(bp); NV(t);
+    double **r = (double **)malloc(sizeof(double *) * (size_t)zd);
+    double **u = (double **)malloc(sizeof(double *) * (size_t)zd);
+    for (i = 0; i <= l; i++) { r[i] = v_new(n); u[i] = v_new(n); }
+    double *tau = (double *)calloc((size_t)(zd * (4 + zd)), sizeof(double));
+    double *gamma = tau + zd * zd, *gamma1 = gamma + zd, *gamma2 = gamma1 + zd, *sigma = gamma2 + zd;
+    double alpha, beta, omega, rho0, rho1, nu, nrm2, ires, tol;
+    RESID(x, b, r[0]);
+    v_copy(n, rtld, r[0]);
+    v_copy(n, bp, r[0]);
+    v_copy(n, xp, x);
+    v_set(n, u[0], 0.);
+    iter = 0;
+    nrm2 = ires = NORM(r[0]);
+    (void)ires;
+    if (nrm2 <= S->tol_abs) goto end;
+    tol = nrm2 * S->tol_rel;
+    alpha = NORM(b) * S->tol_rb;
+    if (tol < S->tol_abs) tol = S->tol_abs;
+    if (tol < alpha) tol = alpha;
+    alpha = 0.0;
+    omega = 1.0;
+    rho0 = 1.0;
+    while (iter <= S->maxit) {
+        rho0 = -omega * rho0;
+        for (j = 0; j < l; j++) {
+            iter++;
+            rho1 = DOT(rtld, r[j]);
+            if (rho1 == 0.0) { l1_bgsl_back(S, x, t, xp); goto end; }
+            beta = alpha * (rho1 / rho0);
+            rho0 = rho1;
+            for (i = 0; i <= j; i++) AXPBY(1, r[i], -beta, u[i]);
+            PC(t, u[j]);
+            MXY(t, u[j + 1]);
+            nu = DOT(rtld, u[j + 1]);
+            if (fabs(nu) == 0.0) { l1_bgsl_back(S, x, t, xp); goto end; }
+            alpha = rho1 / nu;
+            AXPBY(alpha, u[0], 1, x);
+            for (i = 0; i <= j; i++) AXPBY(-alpha, u[i + 1], 1, r[i]);
+            nrm2 = NORM(r[0]);
+            if (nrm2 <= tol) { l1_bgsl_back(S, x, t, xp); goto end; }
+            PC(t, r[j]);
+            MXY(t, r[j + 1]);
+        }
+        for (j = 1; j <= l; j++) { /* MR part :143-154 */
+            for (i = 1; i <= j - 1; i++) {
+                nu = DOT(r[j], r[i]);
+                nu = nu / sigma[i];
+                tau[i * zd + j] = nu;
+                AXPBY(-nu, r[i], 1, r[j]);
+            }
+            sigma[j] = DOT(r[j], r[j]);
+            nu = DOT(r[0], r[j]);
+            gamma1[j] = nu / sigma[j];
+        }
+        gamma[l] = gamma1[l];
+        omega = gamma[l];
+        for (j = l - 1; j >= 1; j--) {
+            nu = 0.0;
+            for (i = j + 1; i <= l; i++) nu += tau[j * zd + i] * gamma[i];
+            gamma[j] = gamma1[j] - nu;
+        }
+        for (j = 1; j <= l - 1; j++) {
+            nu = 0.0;
+            for (i = j + 1; i <= l - 1; i++) nu += tau[j * zd + i] * gamma[i + 1];
+            gamma2[j] = gamma[j + 1] + nu;
+        }
+        AXPBY(gamma[1], r[0], 1, x); /* UPDATE :174-182 */
+        AXPBY(-gamma1[l], r[l], 1, r[0]);
+        AXPBY(-gamma[l], u[l], 1, u[0]);
+        for (j = 1; j <= l - 1; j++) {
+            AXPBY(-gamma[j], u[j], 1, u[0]);
+            AXPBY(gamma2[j], r[j], 1, x);
+            AXPBY(-gamma1[j], r[j], 1, r[0]);
+        }
+        nrm2 = NORM(r[0]);
+        if (nrm2 < tol) { l1_bgsl_back(S, x, t, xp); goto end; }
+    }
+end:
+    for (i = 0; i <= l; i++) { free(r[i]); free(u[i]); }
+    free(r); free(u); free(tau); free(rtld); free(xp); free(bp); free(t);
+    *res = nrm2;
+    return iter;
+}
+
+/* glibc rand() after srand(0) (solver-idrs.cxx:139-144): the additive
+ * feedback generator of glibc's default TYPE_3 random(): r[0] = 1 (seed 0 is
+ * taken as 1), r[i] = 16807 r[i-1] mod (2^31 - 1) for i < 31, r[i] = r[i-31]
+ * for i = 31..33, then r[i] = r[i-31] + r[i-3] (mod 2^32); output k is
+ * r[k + 344] >> 1. */
+typedef struct { uint32_t r[34]; int k; } glibc_rand_t;
+
+static void glibc_srand0(glibc_rand_t *g)
+{
+    int64_t w = 1;
+    uint32_t seq[344 + 34];
+    seq[0] = 1;
+    for (int i = 1; i < 31; i++) {
+        w = (16807 * w) % 2147483647;
+        seq[i] = (uint32_t)w;
+    }
+    for (int i = 31; i < 34; i++) seq[i] = seq[i - 31];
+    for (int i = 34; i < 344; i++) seq[i] = seq[i - 31] + seq[i - 3];
+    for (int i = 0; i < 31; i++) g->r[i] = seq[344 - 31 + i]; /* the last 31 values: a ring */
+    g->k = 0;
+}
+
+static int glibc_rand(glibc_rand_t *g)
+{
+    /* ring of the last 31 values, oldest at k: new = oldest + (value 3 back) */
+    uint32_t v = g->r[g->k] + g->r[(g->k + 28) % 31];
+    g->r[g->k] = v;
+    g->k = (g->k + 1) % 31;
+    return (int)(v >> 1);
+}
+
+/* solver-idrs.cxx:23-84 */
+static void idrs_array_solve(int n, const double *a, const double *b, double *x, double *w)
+{
+    int i, j, k;
+    double t;
+    for (i = 0; i < n * n; i++) w[i] = a[i];
+    if (n == 1) {
+        x[0] = b[0] / w[0];
+    } else if (n == 2) {
+        w[0] = 1.0 / w[0];
+        w[1] *= w[0];
+        w[3] -= w[1] * w[2];
+        w[3] = 1.0 / w[3];
+        x[0] = b[0];
+        x[1] = b[1] - w[1] * x[0];
+        x[1] *= w[3];
+        x[0] -= w[2] * x[1];
+        x[0] *= w[0];
+    } else {
+        for (k = 0; k < n; k++) {
+            w[k + k * n] = 1.0 / w[k + k * n];
+            for (i = k + 1; i < n; i++) {
+                t = w[i + k * n] * w[k + k * n];
+                for (j = k + 1; j < n; j++) w[i + j * n] -= t * w[k + j * n];
+                w[i + k * n] = t;
+            }
+        }
+        for (i = 0; i < n; i++) {
+            x[i] = b[i];
+            for (j = 0; j < i; j++) x[i] -= w[i + j * n] * x[j];
+        }
+        for (i = n - 1; i >= 0; i--) {
+            for (j = i + 1; j < n; j++) x[i] -= w[i + j * n] * x[j];
+            x[i] *= w[i + i * n];
+        }
+    }
+}
+
+/* solver-idrs.cxx:86-283: IDR(s) */
+static int l1_idrs(l1_t *S, int s, double *x, const double *b, double *res)
+{
+    int n = S->n, iter, i, j, k, oldest;
+    NV(r); NV(t); NV(v); NV(av);
+    double **dX = (double **)malloc(sizeof(double *) * (size_t)s);
+    double **dR = (double **)malloc(sizeof(double *) * (size_t)s);
+    double **P = (double **)malloc(sizeof(double *) * (size_t)s);
+    for (i = 0; i < s; i++) { dX[i] = v_new(n); dR[i] = v_new(n); P[i] = v_new(n); }
+    double *m = (double *)calloc((size_t)s, sizeof(double)), *cc = (double *)calloc((size_t)s, sizeof(double));
+    double *M = (double *)calloc((size_t)(s * s), sizeof(double)), *MM = (double *)calloc((size_t)(s * s), sizeof(double));
+    double om = 0, h, nrm2, ires, tol;
+    glibc_rand_t g;
+    iter = 0;
+    RESID(x, b, r);
+    nrm2 = ires = NORM(r);
+    (void)ires;
+    if (nrm2 <= S->tol_abs) goto end;
+    tol = nrm2 * S->tol_rel;
+    h = NORM(b) * S->tol_rb;
+    if (tol < S->tol_abs) tol = S->tol_abs;
+    if (tol < h) tol = h;
+    glibc_srand0(&g);
+    for (k = 0; k < s; k++)
+        for (i = 0; i < n; i++) P[k][i] = (glibc_rand(&g) * 1.) / (1. * 2147483647);
+    for (j = 0; j < s; j++) { /* idrs_orth :4-21 */
+        double rr = NORM(P[j]);
+        rr = 1.0 / rr;
+        v_scale(n, P[j], rr);
+        for (i = j + 1; i < s; i++) {
+            double d = DOT(P[j], P[i]);
+            AXPBY(-d, P[j], 1, P[i]);
+        }
+    }
+    for (k = 0; k < s; k++) {
+        PC(dX[k], r);
+        MXY(dX[k], dR[k]);
+        h = DOT(dR[k], dR[k]);
+        om = DOT(dR[k], r);
+        om = om / h;
+        v_scale(n, dX[k], om);
+        v_scale(n, dR[k], -om);
+        AXPBY(1, dX[k], 1, x);
+        AXPBY(1, dR[k], 1, r);
+        nrm2 = NORM(r);
+        if (tol >= nrm2) { iter = k + 1; goto end; }
+        for (i = 0; i < s; i++) M[k * s + i] = DOT(P[i], dR[k]);
+    }
+    iter = s;
+    oldest = 0;
+    for (i = 0; i < s; i++) m[i] = DOT(P[i], r);
+    while (iter <= S->maxit) {
+        idrs_array_solve(s, M, m, cc, MM);
+        v_copy(n, v, r);
+        for (j = 0; j < s; j++) AXPBY(-cc[j], dR[j], 1, v);
+        if ((iter % (s + 1)) == s) {
+            PC(av, v);
+            MXY(av, t);
+            h = DOT(t, t);
+            om = DOT(t, v);
+            om = om / h;
+            for (i = 0; i < n; i++) {
+                h = om * av[i];
+                for (j = 0; j < s; j++) h -= dX[j][i] * cc[j];
+                dX[oldest][i] = h;
+            }
+            for (i = 0; i < n; i++) {
+                h = -om * t[i];
+                for (j = 0; j < s; j++) h -= dR[j][i] * cc[j];
+                dR[oldest][i] = h;
+            }
+        } else {
+            PC(av, v);
+            for (i = 0; i < n; i++) {
+                h = om * av[i];
+                for (j = 0; j < s; j++) h -= dX[j][i] * cc[j];
+                dX[oldest][i] = h;
+            }
+            MXY(dX[oldest], dR[oldest]);
+            v_scale(n, dR[oldest], -1.);
+        }
+        AXPBY(1, dR[oldest], 1, r);
+        AXPBY(1, dX[oldest], 1, x);
+        iter++;
+        nrm2 = NORM(r);
+        if (tol >= nrm2) goto end;
+        for (i = 0; i < s; i++) {
+            h = DOT(P[i], dR[oldest]);
+            m[i] += h;
+            M[oldest * s + i] = h;
+        }
+        oldest++;
+        if (oldest == s) oldest = 0;
+    }
+end:
+    for (i = 0; i < s; i++) { free(dX[i]); free(dR[i]); free(P[i]); }
+    free(dX); free(dR); free(P); free(m); free(cc); free(M); free(MM);
+    free(r); free(t); free(v); free(av);
+    *res = nrm2;
+    return iter;
+}
+
 static int l1_solve(ctx_t *c, int solver, double *x, const double *b, double tol_rel, double tol_abs,
                     double tol_rb, int maxit, int restart, double *res)
 {
@@ -1950,6 +2220,9 @@ static int l1_solve(ctx_t *c, int solver, double *x, const double *b, double tol
     case SOLVER_GPBICR: return l1_gpbi(&S, x, b, res, 1);
     case SOLVER_QMRCGSTAB: return l1_qmrcgstab(&S, x, b, res);
     case SOLVER_TFQMR: return l1_tfqmr(&S, x, b, res);
+    /* l of BiCGSTAB(l) / s of IDR(s) ride in `restart` (<= 0: 4, lssp.cxx:7-8) */
+    case SOLVER_BICGSTABL: return l1_bicgstabl(&S, restart <= 0 ? 4 : restart, x, b, res);
+    case SOLVER_IDRS: return l1_idrs(&S, restart <= 0 ? 4 : restart, x, b, res);
     default: return -1;
     }
 }

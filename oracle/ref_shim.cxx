@@ -182,6 +182,9 @@ int ref_solve(int solver, int pc_type, int level, double ilut_tol, int ilut_p, i
     lssp_solver_set_rbtol(s, rbtol);
     lssp_solver_set_maxit(s, maxit);
     if (restart > 0) lssp_solver_set_restart(s, restart);
+    // BiCGSTAB(l) / IDR(s): l / s ride in `restart` (lssp_solver_set_bgsl / _idrs, lssp.cxx:495-513)
+    if (restart > 0 && solver == LSSP_SOLVER_BICGSTABL) lssp_solver_set_bgsl(s, restart);
+    if (restart > 0 && solver == LSSP_SOLVER_IDRS) lssp_solver_set_idrs(s, restart);
     double t0 = lssp_get_time();
     lssp_solver_assemble(s, A, vview(n, x), vview(n, b), pc);
     double t1 = lssp_get_time();
@@ -312,6 +315,9 @@ extern "C" int ref_solve_bj(void *hp, int solver, int n, const int *Ap, const in
     lssp_solver_set_rbtol(s, rbtol);
     lssp_solver_set_maxit(s, maxit);
     if (restart > 0) lssp_solver_set_restart(s, restart);
+    // BiCGSTAB(l) / IDR(s): l / s ride in `restart` (lssp_solver_set_bgsl / _idrs, lssp.cxx:495-513)
+    if (restart > 0 && solver == LSSP_SOLVER_BICGSTABL) lssp_solver_set_bgsl(s, restart);
+    if (restart > 0 && solver == LSSP_SOLVER_IDRS) lssp_solver_set_idrs(s, restart);
     lssp_solver_assemble(s, A, vview(n, x), vview(n, b), pc);
     g_trace.clear();
     g_trace_on = true;

@@ -179,6 +179,20 @@ def main():
     # ORTHOMIN(k) with k = restart small enough to cycle its direction ring (solver-orthomin.cxx:102, :120)
     solves += [(O.ORTHOMIN, {"kind": "iluk", "level": 0}, P7(16), "ones", None, {"restart": 3}),
                (O.ORTHOMIN, {"kind": "ilut", "tol": 1e-3, "p": 5}, RND2, 0x5EED, 0xB0B, {"restart": 2})]
+    # BiCGSTAB(l) (solver-bicgstabl.cxx:4-217) and IDR(s) (solver-idrs.cxx:86-283); l / s ride in
+    # `restart`: the default 4, the special small cases (IDR(1) / IDR(2) have their own unrolled
+    # array_solve, solver-idrs.cxx:32-50) and 3 (the general LU)
+    for sv in (O.BICGSTABL, O.IDRS):
+        solves += [
+            (sv, {"kind": "iluk", "level": 0}, P7(16), "ones", None, {"restart": 4}),
+            (sv, {"kind": "none"}, P5(48), "ones", None, {"restart": 2}),
+            (sv, {"kind": "ilut", "tol": 1e-3, "p": 5}, RND2, 0x5EED, 0xB0B, {"restart": 4}),
+            (sv, {"kind": "iluk", "level": 1}, P7(12), "ones", None, {"maxit": 4, "restart": 4}),
+            (sv, {"kind": "iluk", "level": 0}, P7(12), "zeros", None, {"restart": 4}),
+            (sv, {"kind": "bj", "nblk": 4}, P7(16), "ones", None, {"restart": 4}),
+            (sv, {"kind": "iluk", "level": 0}, P7(16), "ones", None, {"restart": 1}),
+            (sv, {"kind": "ilut", "tol": 1e-4, "p": 20}, P7(16), "ones", None, {"restart": 3}),
+        ]
     pcmap = {"none": O.PC_NON, "iluk": O.PC_ILUK, "ilut": O.PC_ILUT}
     for solver, pc, mat, bspec, x0spec, kw in solves:
         A = build_matrix(mat)

@@ -58,7 +58,8 @@ def _worker(rank, world, port, N, maxit, seed, out, solver="bicgstab"):
         # b = 1, x0 = 0, tree reductions; block-Jacobi ILU(0) except for CG (PC_NON)
         x = dev.vec(A.nx, np.zeros(A.nx))
         b = dev.vec(A.nx, np.ones(A.nx))
-        sol = {"bicgstab": lssp_amd.BICGSTAB, "gmres": lssp_amd.GMRES, "cg": lssp_amd.CG}[solver]
+        sol = {"bicgstab": lssp_amd.BICGSTAB, "gmres": lssp_amd.GMRES, "cg": lssp_amd.CG,
+               "idrs": lssp_amd.IDRS, "bicgstabl": lssp_amd.BICGSTABL}[solver]
         r = lssp_amd.solve(dev, A, None if solver == "cg" else M, x, b, solver=sol, maxit=maxit, restart=30,
                            trace_cap=100000)
         xl = x.download(nl)
@@ -74,7 +75,9 @@ def _worker(rank, world, port, N, maxit, seed, out, solver="bicgstab"):
 
 
 @pytest.mark.parametrize("world,N,solver", [(2, 12, "bicgstab"), (3, 10, "bicgstab"), (4, 16, "bicgstab"),
-                                             (2, 12, "gmres"), (3, 11, "gmres"), (2, 12, "cg"), (4, 13, "cg")])
+                                             (2, 12, "gmres"), (3, 11, "gmres"), (2, 12, "cg"), (4, 13, "cg"),
+                                             # IDR(4): each rank keeps its rows of the global rand() shadow space
+                                             (2, 12, "idrs"), (3, 10, "bicgstabl")])
 def test_multirank_on_one_gpu_equals_oracle_prank_mode(world, N, solver):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
@@ -95,8 +98,9 @@ def test_multirank_on_one_gpu_equals_oracle_prank_mode(world, N, solver):
     L = U = None
     if solver != "cg":
         L, U = O.ilu(A, "iluk", level=0, blk=(A.n + world - 1) // world)
-    sol = {"bicgstab": O.BICGSTAB, "gmres": O.GMRES, "cg": O.CG}[solver]
-    o = O.solve(sol, A, np.ones(A.n), L=L, U=U, mode=O.TREE, nranks=world, maxit=500, restart=30)
+    sol = {"bicgstab": O.BICGSTAB, "gmres": O.GMRES, "cg": O.CG, "idrs": O.IDRS, "bicgstabl": O.BICGSTABL}[solver]
+    o = O.solve(sol, A, np.ones(A.n), L=L, U=U, mode=O.TREE, nranks=world, maxit=500,
+                restart=4 if solver in ("idrs", "bicgstabl") else 30)  # l / s = 4, the library default
     assert nits == o.nits
     assert res == o.residual
     assert np.array_equal(trace, o.trace)

@@ -48,3 +48,37 @@ def test_exam_drop_in_tree_reduction_converges_alike():
     res = lambda lines: float(next(ln for ln in lines if ln.startswith("verification")).split()[-1])
     assert abs(nits(amd) - nits(ref)) <= 1
     assert res(amd) <= 1e-7 * 100  # ||b|| = 100: the rbn criterion of the run
+
+
+# ---- every driver through the binding ---------------------------------------
+# oracle/drive_solvers.cxx: an exam.cxx-style caller of the reference API
+# (lssp_solver_create / set_* / assemble / solve) parameterised by solver, PC
+# and grid, linked against the reference alone (drive_ref) and through
+# integration/amd_backend.cxx (drive_amd).  In SERIAL reduction mode the two
+# print the same nits, residual and x digests, digit for digit.
+DRV_REF = os.path.join(ROOT, "oracle", "_ref", "drive_ref")
+DRV_AMD = os.path.join(ROOT, "oracle", "_ref", "drive_amd")
+ALL_SOLVERS = {"gmres": 0, "lgmres": 1, "gmres_r": 2, "bicgstab": 4, "bicgstabl": 5, "bicgsafe": 6, "cg": 7,
+               "cgs": 8, "gpbicg": 9, "cr": 10, "crs": 11, "bicrstab": 12, "bicrsafe": 13, "gpbicr": 14,
+               "qmrcgstab": 15, "tfqmr": 16, "orthomin": 17, "idrs": 18}
+# (PC, level, N, maxit, param): ILU(0) on 12^3; no PC on 10^3 with a small restart / l / s
+DRV_CONFIGS = {"iluk0": ("1", "0", "12", "300", "0"), "none": ("0", "0", "10", "300", "3")}
+
+
+def _drive(path, args, **env):
+    out = subprocess.run([path, *args], capture_output=True, text=True, timeout=120,
+                         env=dict(os.environ, **env), cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("nits ")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    return lines[0]
+
+
+@pytest.mark.parametrize("cfg", sorted(DRV_CONFIGS))
+@pytest.mark.parametrize("solver", sorted(ALL_SOLVERS))
+def test_every_driver_drop_in_serial_reduction_bitwise(solver, cfg):
+    assert os.path.exists(DRV_REF) and os.path.exists(DRV_AMD), "run __graft_entry__.build() where /root/reference exists"
+    args = [str(ALL_SOLVERS[solver]), *DRV_CONFIGS[cfg]]
+    ref = _drive(DRV_REF, args)
+    amd = _drive(DRV_AMD, args, LSSP_AMD_REDUCE="serial")
+    assert amd == ref

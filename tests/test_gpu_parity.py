@@ -96,7 +96,8 @@ def test_solver_serial_mode_trace_bitwise_vs_reference(dev, c):
     try:
         A, D, M, x, b = _solve_inputs(dev, c)
         r = lssp_amd.solve(dev, D, M, x, b, solver=c["solver"], tol_rel=fx(c["rtol"]), tol_abs=fx(c["atol"]),
-                           tol_rb=fx(c["rbtol"]), maxit=c["maxit"], restart=c["restart"], trace_cap=100000)
+                           tol_rb=fx(c["rbtol"]), maxit=c["maxit"], restart=c["restart"],
+                           bgsl=c["restart"], idrs=c["restart"], trace_cap=100000)
     finally:
         dev.set_reduction(lssp_amd.TREE)
     assert r.nits == c["nits"]
@@ -116,7 +117,8 @@ def test_solver_tree_mode_bitwise_vs_oracle(dev, c):
     import lssp_amd
     A, D, M, x, b = _solve_inputs(dev, c)
     r = lssp_amd.solve(dev, D, M, x, b, solver=c["solver"], tol_rel=fx(c["rtol"]), tol_abs=fx(c["atol"]),
-                       tol_rb=fx(c["rbtol"]), maxit=c["maxit"], restart=c["restart"], trace_cap=100000)
+                       tol_rb=fx(c["rbtol"]), maxit=c["maxit"], restart=c["restart"],
+                           bgsl=c["restart"], idrs=c["restart"], trace_cap=100000)
     L = U = None
     if M is not None:
         (Lp, Lj, Lx), (Up, Uj, Ux) = M.factors()
