@@ -124,6 +124,7 @@ struct TriSched {
     // bandwidth rows in sweep order, each walked level by level by one workgroup
     int bp_B = 0, bp_nb = 0, bp_nsteps = 0;
     int *bp_perm = nullptr;  // schedule position -> row
+    int *bp_pos = nullptr;   // row -> schedule position (the inverse of bp_perm)
     // packets v1 (tri_mode 4): each block's steps cut into packets of <=
     // PK_ROWS rows / PK_BYTES bytes, laid out contiguously
     int pk_n = 0;

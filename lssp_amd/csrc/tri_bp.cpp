@@ -144,6 +144,7 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
         return LSSP_AMD_OK;
     };
     LSSP_TRY(up(t.bp_perm, perm));  // position -> row: the apply's permutation kernels
+    LSSP_TRY(up(t.bp_pos, pos));    // row -> position: x back to natural order as a gather
     return LSSP_AMD_OK;
 }
 

@@ -908,7 +908,14 @@ int launch_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const do
         if (nat && M->upper.pk6_ep == 4)
             return launch_pk6<true>(c, M->upper, M->d_sh[e], M->d_sh[2 + e], M->d_sh[2 + (e ^ 1)], x);
         LSSP_TRY(launch_pk6<false>(c, M->upper, M->d_sh[e], M->d_sh[2 + e], M->d_sh[2 + (e ^ 1)], nullptr));
-        k_perm<false><<<pg, 256, 0, c->stream>>>(x, M->d_sh[2 + e], M->upper.bp_perm, n);
+        // x back to natural order as a gather through the inverse permutation
+        // (coalesced stores, scattered loads: faster than scattering the stores);
+        // LSSP_AMD_TRI_XOUT=scatter keeps the scatter (timing experiments)
+        static const bool xscatter = getenv("LSSP_AMD_TRI_XOUT") && !strcmp(getenv("LSSP_AMD_TRI_XOUT"), "scatter");
+        if (xscatter || !M->upper.bp_pos)
+            k_perm<false><<<pg, 256, 0, c->stream>>>(x, M->d_sh[2 + e], M->upper.bp_perm, n);
+        else
+            k_perm<true><<<pg, 256, 0, c->stream>>>(x, M->d_sh[2 + e], M->upper.bp_pos, n);
         LSSP_HIP(hipGetLastError());
         return LSSP_AMD_OK;
     }
