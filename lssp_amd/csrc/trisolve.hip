@@ -826,7 +826,8 @@ static int launch_pk6(lssp_amd_ctx *c, const TriSched &t, const double *rhs, dou
     // EP 4 or 8 -- the variants whose inline-asm loader tools/check_vmcnt.py
     // (tests/test_isa_vmcnt.py) verifies hazard-free
     if (t.pk6_rows != 256) return LSSP_AMD_EUNSUPPORTED;
-    // pipeline depths (LSSP_AMD_TRI_PIPE): 0 = (KE 2, IA 4, D 3), 1 = (2, 3, 3), 2 = (2, 3, 2)
+    // pipeline depths (LSSP_AMD_TRI_PIPE): 0 = (KE 2, IA 4, D 3), 1 = (2, 3, 3), 2 = (2, 3, 2),
+    // (measured at 216^3 per apply: KE 1 (IA 2 or 3) 1.83 ms, KE 3 (IA 4, D 3 or 2) 1.63 ms, vs 1.57)
     const int pd = c->tri_pipe;
     if constexpr (NAT) {
         if (t.pk6_ep != 4) return LSSP_AMD_EUNSUPPORTED;
