@@ -882,6 +882,29 @@ __global__ __launch_bounds__(256) void k_perm(double *dst, const double *src, co
     }
 }
 
+// the gather as above with four positions per lane: the four indices come in
+// one 16-byte load and the four (scattered) operand loads are in flight
+// together -- more memory-level parallelism per lane than one dependent
+// index -> operand chain at a time
+__global__ __launch_bounds__(256) void k_gather4(double *dst, const double *src, const int *perm, int n)
+{
+    typedef double v2d __attribute__((ext_vector_type(2)));
+    const int nx = 8, per = gridDim.x / nx;
+    const int xcd = blockIdx.x % nx, k = blockIdx.x / nx;
+    const long n4 = (long)n / 4, chunk = (n4 + nx - 1) / nx;
+    const long lo = xcd * chunk, hi = min(n4, lo + chunk);
+    const int4 *p4 = reinterpret_cast<const int4 *>(perm);
+    v2d *d2 = reinterpret_cast<v2d *>(dst);
+    for (long q = lo + (long)k * 256 + threadIdx.x; q < hi; q += (long)per * 256) {
+        const int4 ix = p4[q];
+        const double a0 = src[ix.x], a1 = src[ix.y], a2 = src[ix.z], a3 = src[ix.w];
+        d2[2 * q] = v2d{a0, a1};
+        d2[2 * q + 1] = v2d{a2, a3};
+    }
+    if (blockIdx.x == 0)
+        for (long p = 4 * n4 + threadIdx.x; p < n; p += 256) dst[p] = src[perm[p]];
+}
+
 // tri_mode 9 apply.  The scattered halves of the work -- reading the rhs in L
 // order and writing x in natural order -- run as fully parallel permutation
 // kernels around the two sweeps, so the pipelined sweeps only touch
@@ -901,8 +924,12 @@ int launch_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const do
         const int e = M->epoch & 1;
         M->epoch++;
         const int pg = 8 * std::max(1, std::min((n + 2047) / 2048, c->num_cus));  // multiple of 8
+        static const bool perm4 = !(getenv("LSSP_AMD_PERM1") && atoi(getenv("LSSP_AMD_PERM1")));
         if (!M->lower.rhs_nat) {
-            k_perm<true><<<pg, 256, 0, c->stream>>>(M->d_rperm, rhs, M->lower.bp_perm, n);
+            if (((uintptr_t)rhs & 15) == 0 && perm4)
+                k_gather4<<<pg, 256, 0, c->stream>>>(M->d_rperm, rhs, M->lower.bp_perm, n);
+            else
+                k_perm<true><<<pg, 256, 0, c->stream>>>(M->d_rperm, rhs, M->lower.bp_perm, n);
             LSSP_HIP(hipGetLastError());
         }
         LSSP_TRY(launch_pk6<false>(c, M->lower, M->lower.rhs_nat ? rhs : M->d_rperm, M->d_sh[e], M->d_sh[e ^ 1],
@@ -917,6 +944,8 @@ int launch_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const do
         static const bool xscatter = getenv("LSSP_AMD_TRI_XOUT") && !strcmp(getenv("LSSP_AMD_TRI_XOUT"), "scatter");
         if (xscatter || !M->upper.bp_pos)
             k_perm<false><<<pg, 256, 0, c->stream>>>(x, M->d_sh[2 + e], M->upper.bp_perm, n);
+        else if (((uintptr_t)x & 15) == 0 && perm4)
+            k_gather4<<<pg, 256, 0, c->stream>>>(x, M->d_sh[2 + e], M->upper.bp_pos, n);
         else
             k_perm<true><<<pg, 256, 0, c->stream>>>(x, M->d_sh[2 + e], M->upper.bp_pos, n);
         LSSP_HIP(hipGetLastError());
