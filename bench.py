@@ -247,7 +247,8 @@ def main():
                      "ms_per_call": round(spmv_ms, 5)},
             "roofline": {"bound": "hbm", "achieved": round(apply_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(apply_gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("ilu_apply"),
-                         "kernel": "ILU(0) apply = k_perm<gather> + k_tri_pk6 (L) + k_tri_pk6 (U) + k_perm<scatter>; "
+                         "kernel": "ILU(0) apply = k_gather4 (rhs to L order) + k_tri_pk6 (L) + k_tri_pk6 (U) + "
+                                   "k_gather4 (x to natural order); "
                                    "latency-bound: 2 x 646 dependent levels",
                          "bytes_per_launch": apply_b, "ms_per_launch": round(apply_ms, 5)},
             "roofline_spmv": {"bound": "hbm", "achieved": round(spmv_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

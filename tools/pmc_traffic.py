@@ -7,7 +7,8 @@ gfx950 correction (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE counts the
 fabric read requests at half their bytes -- checked on this code's 8-byte
 per-lane copy kernel (k_ew, 80.6 MB read: FETCH_SIZE 40.3 MB) -- so it is
 doubled; WRITE_SIZE is exact.  Units: KB.  The ILU apply entry sums the
-median per-launch bytes of its four kernels (2 permutations, 2 sweeps)."""
+median per-launch bytes of its four kernels (2 permutations, 2 sweeps).
+(The permutations are k_gather4 since round 1's later builds; k_perm before.)"""
 import collections
 import csv
 import glob
@@ -35,8 +36,10 @@ def main(fetch_dir, write_dir, out):
         res["k_spmv3"] = int(2 * fe[k] + wr.get(k, 0))
     tri = find("k_tri_pk6")
     perm = find("k_perm")
-    if tri and perm:
-        res["ilu_apply"] = int(sum(2 * fe[k] + wr.get(k, 0) for k in perm) + 2 * sum(2 * fe[k] + wr.get(k, 0) for k in tri) / max(1, len(tri)))
+    g4 = find("k_gather4")  # both permutations of an apply, one kernel: twice its median
+    perm_b = 2 * sum(2 * fe[k] + wr.get(k, 0) for k in g4) if g4 else sum(2 * fe[k] + wr.get(k, 0) for k in perm)
+    if tri and (perm or g4):
+        res["ilu_apply"] = int(perm_b + 2 * sum(2 * fe[k] + wr.get(k, 0) for k in tri) / max(1, len(tri)))
     res["_note"] = "HBM bytes per launch: 2 x FETCH_SIZE + WRITE_SIZE (rocprofv3 --pmc, medians over launches)"
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
