@@ -277,8 +277,9 @@ int lssp_amd_mv_amxpbyz(lssp_amd_ctx *c, double alpha, const lssp_amd_mat *A, co
 {
     if (!c || !A || !x || !y || !z) return LSSP_AMD_EINVAL;
     LSSP_TRY(halo_exchange(A, const_cast<double *>(x)));
-    if (beta == 0.0 && alpha > 0.0)  // y*0 + alpha*sum == alpha*sum for finite y
-        return launch_spmv(c, A, EPI_AMX, alpha, x, beta, nullptr, z, 0, nullptr, nullptr);
+    // y is read even when beta == 0, as the reference does (mvops.cxx:61): a NaN / Inf
+    // in y propagates into z (tests/test_gpu_edge.py); only the drivers use the
+    // y-free epilogue
     return launch_spmv(c, A, EPI_AXPBY, alpha, x, beta, y, z, 0, nullptr, nullptr);
 }
 
