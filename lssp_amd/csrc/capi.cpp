@@ -93,6 +93,9 @@ int lssp_amd_ctx_create(int device, lssp_amd_ctx **out)
     c->num_cus = prop.multiProcessorCount;
     LSSP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     LSSP_HIP(hipMalloc(&c->d_sums, sizeof(double) * MAX_SLOTS));
+    LSSP_HIP(hipMalloc(&c->d_wsum, sizeof(double) * MAX_SLOTS * 16));
+    LSSP_HIP(hipMalloc(&c->d_rcnt, sizeof(unsigned)));
+    LSSP_HIP(hipMemset(c->d_rcnt, 0, sizeof(unsigned)));
     LSSP_HIP(hipMalloc(&c->d_scal, sizeof(double) * NSCAL));
     LSSP_HIP(hipMemset(c->d_scal, 0, sizeof(double) * NSCAL));
     LSSP_HIP(hipHostMalloc(&c->h_scal, sizeof(double) * NSCAL, hipHostMallocDefault));
@@ -122,6 +125,8 @@ int lssp_amd_ctx_destroy(lssp_amd_ctx *c)
     if (c->d_trace) (void)hipFree(c->d_trace);
     (void)hipFree(c->d_sums);
     (void)hipFree(c->d_scal);
+    if (c->d_wsum) (void)hipFree(c->d_wsum);
+    if (c->d_rcnt) (void)hipFree(c->d_rcnt);
     (void)hipHostFree(c->h_scal);
     (void)hipFree(c->d_err);
     (void)hipStreamDestroy(c->stream);

@@ -63,6 +63,8 @@ struct lssp_amd_ctx {
     double *d_part = nullptr;  // [MAX_SLOTS][part_cap] level-1 partials
     long part_cap = 0;
     double *d_sums = nullptr;  // [MAX_SLOTS] rank-local sums
+    double *d_wsum = nullptr;  // [MAX_SLOTS][16] level-2 wave sums (k_reduce2m)
+    unsigned *d_rcnt = nullptr;  // level-2 arrival counter (k_reduce2m), 0 between launches
     double *d_scal = nullptr;  // [NSCAL] scalar slots
     double *h_scal = nullptr;  // pinned mirror
     double *d_trace = nullptr; // device trace buffer

@@ -169,6 +169,69 @@ __global__ __launch_bounds__(1024) void k_reduce2(const double *__restrict__ par
     }
 }
 
+// The same level 2 spread over L2_LANES / 64 one-wave workgroups on as many
+// CUs: workgroup q runs wave q of the 1024-lane level 2 above (lanes 64q ..
+// 64q+63, each adding its partials in order), so the partials are pulled by
+// 16 CUs instead of one (a single CU took ~12 us for the 2 x 315 KB of a
+// 10M-row pair of dots).  Each wave sum is published write-through (sc1) and
+// drained before an arrival ticket; the last arriver combines the 16 wave
+// sums with the same halving tree and runs the finalize program.  Bitwise
+// identical to k_reduce2.
+__device__ __forceinline__ void st_sc1(double *p, double v)
+{
+    __hip_atomic_store(reinterpret_cast<uint64_t *>(p), (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double *p)
+{
+    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const uint64_t *>(p),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__global__ __launch_bounds__(64) void k_reduce2m(const double *__restrict__ part, long pcap, long C, int nslot,
+                                                double *sums, double *scal, double *trace, Fin f, int do_fin,
+                                                double *wsum, unsigned *cnt)
+{
+    const int q = blockIdx.x, t = q * 64 + threadIdx.x;  // lane t of the 1024-lane level 2
+    for (int s = 0; s < nslot; s++) {
+        const double *p = part + s * pcap;
+        double a = 0.0;
+        for (long k0 = t; k0 < C; k0 += 32L * L2_LANES) {
+            double v[32];
+#pragma unroll
+            for (int u = 0; u < 32; u++) {
+                const long k = k0 + (long)u * L2_LANES;
+                v[u] = k < C ? p[k] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 32; u++)
+                if (k0 + (long)u * L2_LANES < C) a += v[u];
+        }
+        a = wave_sum(a);
+        if (threadIdx.x == 0) st_sc1(wsum + s * 16 + q, a);
+    }
+    unsigned last = 0;
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave sums are in memory before the ticket
+        last = atomicAdd(cnt, 1u) == gridDim.x - 1;
+    }
+    last = __shfl(last, 0, 64);
+    if (!last) return;
+    if (threadIdx.x == 0) {
+        double r[MAX_SLOTS] = {0, 0, 0, 0};
+        for (int s = 0; s < nslot; s++) {
+            double u[16];
+            for (int w = 0; w < 16; w++) u[w] = ld_sc1(wsum + s * 16 + w);
+            for (int off = 8; off >= 1; off >>= 1)
+                for (int l = 0; l < off; l++) u[l] = u[l] + u[l + off];
+            r[s] = u[0];
+            sums[s] = r[s];
+        }
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (do_fin) finalize(f, r, scal, trace);
+    }
+}
+
 // serial order: one lane, sum += a[i]*b[i] from 0 (vector.cxx:123-133)
 struct SerialArgs {
     const double *a[MAX_SLOTS];
@@ -811,8 +874,14 @@ int launch_ew(lssp_amd_ctx *c, const Ew &e)
 int launch_reduce_tree(lssp_amd_ctx *c, long C, int nslot, const Fin &f)
 {
     int do_fin = c->nranks > 1 ? 0 : 1;
-    k_reduce2<<<1, L2_LANES, 0, c->stream>>>(c->d_part, c->part_cap, C, nslot, c->d_sums, c->d_scal,
-                                              c->d_trace, f, do_fin);
+    static const bool one_cu = getenv("LSSP_AMD_REDUCE2_ONE_CU") && atoi(getenv("LSSP_AMD_REDUCE2_ONE_CU"));
+    static_assert(L2_LANES == 16 * 64, "k_reduce2m runs the 16 waves of the level-2 workgroup");
+    if (one_cu)
+        k_reduce2<<<1, L2_LANES, 0, c->stream>>>(c->d_part, c->part_cap, C, nslot, c->d_sums, c->d_scal,
+                                                  c->d_trace, f, do_fin);
+    else
+        k_reduce2m<<<L2_LANES / 64, 64, 0, c->stream>>>(c->d_part, c->part_cap, C, nslot, c->d_sums, c->d_scal,
+                                                         c->d_trace, f, do_fin, c->d_wsum, c->d_rcnt);
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;
 }
