@@ -488,6 +488,14 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
     const int cnt = a.Ap[rend] - base;
     const int rr = min(r, a.nrows - 1);
     const int rb = a.Ap[rr], re = a.Ap[rr + 1];
+    // the fused dots' second operands, loaded up front with the row bounds (the
+    // compiler may not move them above the z store: w0 / w1 may alias z, and
+    // then they are read as the value just stored, zv, below)
+    double w0p = 0.0, w1p = 0.0;
+    if (NRED > 0) {
+        if (a.w0 != a.z) w0p = a.w0[rr];
+        if (NRED > 1 && a.w1 && a.w1 != a.z) w1p = a.w1[rr];
+    }
     double sum = 0;
     if (cnt <= SPMV_CAP) {
         typedef double dbl2_t __attribute__((ext_vector_type(2)));
@@ -547,8 +555,8 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
     if (NRED > 0) {
         double v[NRED > 0 ? NRED : 1];
         if (r < a.nrows) {
-            v[0] = zv * a.w0[r];
-            if (NRED > 1) v[NRED > 1 ? 1 : 0] = zv * (a.w1 ? a.w1[r] : zv);
+            v[0] = zv * (a.w0 == a.z ? zv : w0p);
+            if (NRED > 1) v[NRED > 1 ? 1 : 0] = zv * (a.w1 && a.w1 != a.z ? w1p : zv);
         } else {
 #pragma unroll
             for (int q = 0; q < NRED; q++) v[q] = 0.0;
