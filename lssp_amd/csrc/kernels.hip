@@ -789,41 +789,55 @@ __global__ __launch_bounds__(256) void k_ew(EwArgs g)
     for (long c = blockIdx.x; c < g.nchunks; c += gridDim.x) {
         const long i = c * 256 + threadIdx.x;
         const bool in = i < g.n;
+        // the reduction operands: an output of this pass is read as the value just
+        // computed (o0 / o1); any other operand is loaded up front, with the inputs
+        // (the compiler may not move a load above the output stores it might alias)
+        bool w0 = false, w1 = false;  // this element's out0 / out1 written by the kind below
+        double o0 = 0.0, o1 = 0.0, p0a = 0.0, p0b = 0.0, p1a = 0.0, p1b = 0.0;
+        auto pre = [&](const double *q) { return (in && q != g.out0 && q != g.out1) ? q[i] : 0.0; };
+        if (NRED > 0) {
+            p0a = pre(g.r0a);
+            p0b = pre(g.r0b);
+            if (NRED > 1) {
+                p1a = pre(g.r1a);
+                p1b = pre(g.r1b);
+            }
+        }
         if (in) {
             switch (g.kind) {
-            case EW_FILL: g.out0[i] = g.a; break;
-            case EW_COPY: g.out0[i] = g.x[i]; break;
-            case EW_AXY: g.out0[i] = g.x[i] * g.a; break;
-            case EW_AXPBY: g.out0[i] = g.out0[i] * g.b + g.x[i] * g.a; break;
-            case EW_AXPBYZ: g.out0[i] = g.y[i] * g.b + g.x[i] * g.a; break;
-            case EW_SCALE: g.out0[i] = g.out0[i] * g.a; break;
-            case EW_DIVS: g.out0[i] = g.out0[i] / g.scal[g.sidx]; break;
+            case EW_FILL: w0 = true, g.out0[i] = o0 = g.a; break;
+            case EW_COPY: w0 = true, g.out0[i] = o0 = g.x[i]; break;
+            case EW_AXY: w0 = true, g.out0[i] = o0 = g.x[i] * g.a; break;
+            case EW_AXPBY: w0 = true, g.out0[i] = o0 = g.out0[i] * g.b + g.x[i] * g.a; break;
+            case EW_AXPBYZ: w0 = true, g.out0[i] = o0 = g.y[i] * g.b + g.x[i] * g.a; break;
+            case EW_SCALE: w0 = true, g.out0[i] = o0 = g.out0[i] * g.a; break;
+            case EW_DIVS: w0 = true, g.out0[i] = o0 = g.out0[i] / g.scal[g.sidx]; break;
             case EW_DOT: break;
             case EW_BICG_P: {
                 const double beta = g.scal[S_BETA], omega = g.scal[S_OMEGA];
-                g.out0[i] = g.x[i] + beta * (g.out0[i] - omega * g.y[i]);
+                w0 = true, g.out0[i] = o0 = g.x[i] + beta * (g.out0[i] - omega * g.y[i]);
                 break;
             }
-            case EW_BICG_S: g.out0[i] = g.x[i] - g.scal[S_ALPHA] * g.y[i]; break;
+            case EW_BICG_S: w0 = true, g.out0[i] = o0 = g.x[i] - g.scal[S_ALPHA] * g.y[i]; break;
             case EW_BICG_XR: {
                 const double alpha = g.scal[S_ALPHA];
                 if (g.scal[S_BREAK] != 0.0) {
-                    g.out0[i] = g.out0[i] + alpha * g.x[i];
+                    w0 = true, g.out0[i] = o0 = g.out0[i] + alpha * g.x[i];
                 } else {
                     const double omega = g.scal[S_OMEGA];
-                    g.out0[i] = g.out0[i] + alpha * g.x[i] + omega * g.y[i];
-                    g.out1[i] = g.u[i] - omega * g.v[i];
+                    w0 = true, g.out0[i] = o0 = g.out0[i] + alpha * g.x[i] + omega * g.y[i];
+                    w1 = true, g.out1[i] = o1 = g.u[i] - omega * g.v[i];
                 }
                 break;
             }
-            case EW_CG_P: g.out0[i] = g.x[i] + g.scal[S_BETA] * g.out0[i]; break;
+            case EW_CG_P: w0 = true, g.out0[i] = o0 = g.x[i] + g.scal[S_BETA] * g.out0[i]; break;
             case EW_CG_XR: {
                 const double alpha = g.scal[S_ALPHA];
-                g.out0[i] = g.out0[i] + alpha * g.x[i];
-                g.out1[i] = g.out1[i] - alpha * g.y[i];
+                w0 = true, g.out0[i] = o0 = g.out0[i] + alpha * g.x[i];
+                w1 = true, g.out1[i] = o1 = g.out1[i] - alpha * g.y[i];
                 break;
             }
-            case EW_GM_MGS: g.out0[i] = g.out0[i] * 1 + g.x[i] * (-g.scal[g.sidx]); break;
+            case EW_GM_MGS: w0 = true, g.out0[i] = o0 = g.out0[i] * 1 + g.x[i] * (-g.scal[g.sidx]); break;
             case EW_GM_X: {  // b carries the basis stride (vectors hold owned + halo entries)
                 const long ld = (long)g.b;
                 double acc = 0;
@@ -842,22 +856,30 @@ __global__ __launch_bounds__(256) void k_ew(EwArgs g)
                     for (int q = 0; q < nz; q++) t += g.v[(long)q * ld + i] * g.u[q + mk];
                 }
                 g.out0[i] += t;
-                g.out1[i] = t;
+                w1 = true, g.out1[i] = o1 = t;
                 break;
             }
             case EW_GMR_Z: {
                 const long ld = (long)g.b;
                 double z = g.vbase[(long)(g.k - 1) * ld + i] * g.u[g.k - 1];
                 for (int q = g.k - 2; q >= 0; q--) z = z * 1 + g.vbase[(long)q * ld + i] * g.u[q];
-                g.out0[i] = z;
+                w0 = true, g.out0[i] = o0 = z;
                 break;
             }
             }
         }
         if (NRED > 0) {
             double v[NRED > 0 ? NRED : 1];
-            v[0] = in ? g.r0a[i] * g.r0b[i] : 0.0;
-            if (NRED > 1) v[NRED > 1 ? 1 : 0] = in ? g.r1a[i] * g.r1b[i] : 0.0;
+            auto val = [&](const double *q, double pv) {
+                if (q == g.out0 || q == g.out1) {  // an output: the value written, else memory
+                    if (q == g.out1 && w1) return o1;
+                    if (q == g.out0 && w0) return o0;
+                    return q[i];
+                }
+                return pv;
+            };
+            v[0] = in ? val(g.r0a, p0a) * val(g.r0b, p0b) : 0.0;
+            if (NRED > 1) v[NRED > 1 ? 1 : 0] = in ? val(g.r1a, p1a) * val(g.r1b, p1b) : 0.0;
             chunk_reduce<NRED>(v, g.part, g.pcap, c, lds);
         }
     }
