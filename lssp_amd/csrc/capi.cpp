@@ -31,7 +31,13 @@ int ensure_part(lssp_amd_ctx *c, long C)
 int finish_reduce(lssp_amd_ctx *c, long n, int nslot, const double *const *a,
                   const double *const *b, const Fin &f)
 {
-    if (c->reduce_mode == LSSP_AMD_REDUCE_SERIAL) {
+    if (c->reduce_mode == LSSP_AMD_REDUCE_SERIAL && c->nranks > 1) {
+        // the reference's one sequential sum (vector.cxx:129) across P ranks: each
+        // rank continues the running sums of the ranks before it, in rank order
+        LSSP_TRY(comm_carry_in(c));
+        LSSP_TRY(launch_reduce_serial(c, n, nslot, a, b, f, c->d_carry));
+        LSSP_TRY(comm_carry_out(c));
+    } else if (c->reduce_mode == LSSP_AMD_REDUCE_SERIAL) {
         LSSP_TRY(launch_reduce_serial(c, n, nslot, a, b, f));
     } else {
         LSSP_TRY(launch_reduce_tree(c, n > 0 ? num_chunks(n) : 0, nslot, f));

@@ -105,6 +105,22 @@ int comm_allgather_sums(lssp_amd_ctx *c, int nslot)
     return xfer_allgather(c, c->d_sums, c->d_gather, (long)sizeof(double) * MAX_SLOTS);
 }
 
+int comm_carry_in(lssp_amd_ctx *c)
+{
+    const long bytes = (long)sizeof(double) * MAX_SLOTS;
+    if (c->rank == 0) {
+        LSSP_HIP(hipMemsetAsync(c->d_carry, 0, bytes, c->stream));  // +0.0: the reference's sum = 0
+        return LSSP_AMD_OK;
+    }
+    return xfer_group(c, {}, {{c->rank - 1, c->d_carry, bytes}});
+}
+
+int comm_carry_out(lssp_amd_ctx *c)
+{
+    if (c->rank == c->nranks - 1) return LSSP_AMD_OK;
+    return xfer_group(c, {{c->rank + 1, c->d_sums, (long)sizeof(double) * MAX_SLOTS}}, {});
+}
+
 int halo_exchange(const lssp_amd_mat *A, double *x)
 {
     if (!A || A->ctx == nullptr || A->ctx->nranks <= 1) return LSSP_AMD_OK;
@@ -128,6 +144,10 @@ int comm_destroy(lssp_amd_ctx *c)
     if (c->d_gather) {
         (void)hipFree(c->d_gather);
         c->d_gather = nullptr;
+    }
+    if (c->d_carry) {
+        (void)hipFree(c->d_carry);
+        c->d_carry = nullptr;
     }
     c->host = lssp_amd_host_transport{};
     c->nranks = 1;
@@ -166,6 +186,7 @@ int lssp_amd_comm_init(lssp_amd_ctx *c, int nranks, int rank, const void *idp)
     c->nranks = nranks;
     c->rank = rank;
     LSSP_HIP(hipMalloc(&c->d_gather, sizeof(double) * MAX_SLOTS * nranks));
+    LSSP_HIP(hipMalloc(&c->d_carry, sizeof(double) * MAX_SLOTS));
     return LSSP_AMD_OK;
 }
 
@@ -180,6 +201,7 @@ int lssp_amd_comm_init_host(lssp_amd_ctx *c, int nranks, int rank, const lssp_am
     c->nranks = nranks;
     c->rank = rank;
     LSSP_HIP(hipMalloc(&c->d_gather, sizeof(double) * MAX_SLOTS * nranks));
+    LSSP_HIP(hipMalloc(&c->d_carry, sizeof(double) * MAX_SLOTS));
     return LSSP_AMD_OK;
 }
 

@@ -75,6 +75,7 @@ struct lssp_amd_ctx {
     void *comm = nullptr;      // ncclComm_t
     lssp_amd_host_transport host{};  // host-staged transport (comm == nullptr, nranks > 1)
     double *d_gather = nullptr;  // [nranks][MAX_SLOTS]
+    double *d_carry = nullptr;   // [MAX_SLOTS] serial mode: running sums of the ranks before this one
     int tri_blocks_per_cu = 1;
     // 0 sync-free + back-off, 1 one launch per level, 2 sync-free without
     // back-off, 4 packet pipeline (v1 packets), 9 role-split packet sweeps
@@ -212,7 +213,7 @@ int launch_ew(lssp_amd_ctx *c, const Ew &e);
 int launch_reduce_tree(lssp_amd_ctx *c, long C, int nslot, const Fin &f);
 // serial: sums of products a_k[i]*b_k[i] in index order (== vector.cxx:123-133)
 int launch_reduce_serial(lssp_amd_ctx *c, long n, int nslot, const double *const *a,
-                         const double *const *b, const Fin &f);
+                         const double *const *b, const Fin &f, const double *carry = nullptr);
 int launch_finalize(lssp_amd_ctx *c, const double *sums, int nslot, const Fin &f);
 int launch_fill(lssp_amd_ctx *c, double *x, long n, uint64_t bits);
 int launch_trisolve(lssp_amd_ctx *c, const TriSched &t, const double *rhs, double *x,
@@ -265,6 +266,10 @@ int reduce_dots(lssp_amd_ctx *c, long n, int nslot, const double *const *a,
                 const double *const *b, const Fin &f);
 // multi-rank: all-gather rank sums and sum in rank order, then the finalize
 int comm_allgather_sums(lssp_amd_ctx *c, int nslot);
+// serial mode, P ranks: receive the running sums of rank-1 (zeros on rank 0)
+// into c->d_carry / pass this rank's on to rank+1
+int comm_carry_in(lssp_amd_ctx *c);
+int comm_carry_out(lssp_amd_ctx *c);
 int halo_exchange(const lssp_amd_mat *A, double *x);
 int comm_destroy(lssp_amd_ctx *c);
 

@@ -244,8 +244,10 @@ struct SerialArgs {
 // as the reference rounds it) of the next 2048-element chunk into the other
 // LDS buffer meanwhile, so the chain never waits on HBM latency.
 constexpr int SER_C = 2048;
+// carry (multi-rank): the running sums of the ranks before this one, so the
+// chain continues theirs and the P ranks add in global index order.
 __global__ __launch_bounds__(1024) void k_dot_serial(SerialArgs g, long n, int nslot, double *sums, double *scal,
-                                                     double *trace, Fin f, int do_fin)
+                                                     double *trace, Fin f, int do_fin, const double *carry)
 {
     __shared__ double buf[2][MAX_SLOTS][SER_C];
     const int tid = threadIdx.x;
@@ -261,6 +263,8 @@ __global__ __launch_bounds__(1024) void k_dot_serial(SerialArgs g, long n, int n
         }
     };
     double acc[MAX_SLOTS] = {0, 0, 0, 0};
+    if (carry)
+        for (int s = 0; s < MAX_SLOTS; s++) acc[s] = carry[s];
     if (nch > 0) fill(0, 0);
     __syncthreads();
     for (long k = 0; k < nch; k++) {
@@ -292,14 +296,15 @@ __global__ void k_finalize(const double *sums, double *scal, double *trace, Fin 
     finalize(f, r, scal, trace);
 }
 
-// multi-rank: gathered [P][MAX_SLOTS] rank sums, summed in rank order
+// multi-rank: gathered [P][MAX_SLOTS] rank sums, summed in rank order (tree
+// mode), or the last rank's running sums, which are the global sums (serial)
 __global__ void k_sum_ranks(const double *gath, int P, int nslot, double *sums, double *scal,
-                            double *trace, Fin f)
+                            double *trace, Fin f, int serial)
 {
     double r[MAX_SLOTS] = {0, 0, 0, 0};
     for (int s = 0; s < nslot; s++) {
-        double t = gath[s];
-        for (int q = 1; q < P; q++) t = t + gath[q * MAX_SLOTS + s];
+        double t = serial ? gath[(P - 1) * MAX_SLOTS + s] : gath[s];
+        for (int q = 1; q < P && !serial; q++) t = t + gath[q * MAX_SLOTS + s];
         r[s] = t;
         sums[s] = t;
     }
@@ -917,7 +922,7 @@ int launch_reduce_tree(lssp_amd_ctx *c, long C, int nslot, const Fin &f)
 }
 
 int launch_reduce_serial(lssp_amd_ctx *c, long n, int nslot, const double *const *a,
-                         const double *const *b, const Fin &f)
+                         const double *const *b, const Fin &f, const double *carry)
 {
     SerialArgs g{};
     for (int s = 0; s < nslot; s++) {
@@ -925,7 +930,7 @@ int launch_reduce_serial(lssp_amd_ctx *c, long n, int nslot, const double *const
         g.b[s] = b[s];
     }
     int do_fin = c->nranks > 1 ? 0 : 1;
-    k_dot_serial<<<1, 1024, 0, c->stream>>>(g, n, nslot, c->d_sums, c->d_scal, c->d_trace, f, do_fin);
+    k_dot_serial<<<1, 1024, 0, c->stream>>>(g, n, nslot, c->d_sums, c->d_scal, c->d_trace, f, do_fin, carry);
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;
 }
@@ -941,7 +946,7 @@ int launch_finalize(lssp_amd_ctx *c, const double *sums, int nslot, const Fin &f
 int launch_sum_ranks(lssp_amd_ctx *c, int nslot, const Fin &f)
 {
     k_sum_ranks<<<1, 1, 0, c->stream>>>(c->d_gather, c->nranks, nslot, c->d_sums, c->d_scal,
-                                         c->d_trace, f);
+                                         c->d_trace, f, c->reduce_mode == LSSP_AMD_REDUCE_SERIAL);
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;
 }

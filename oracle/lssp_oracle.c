@@ -142,8 +142,12 @@ typedef struct {
     int nranks;
 } red_t;
 
+/* SERIAL: the reference's one sequential sum over the whole vector for any P
+ * (the library's ranks continue each other's running sums, comm.cpp);
+ * TREE: each rank's block in the canonical tree order, rank sums in rank order. */
 static double dot_red(const red_t *R, const double *x, const double *y, long n)
 {
+    if (R->mode != RED_TREE) return dot_serial(x, y, n);
     int P = R->nranks > 1 ? R->nranks : 1;
     long blk = (n + P - 1) / P;
     double total = 0.0;
@@ -151,8 +155,7 @@ static double dot_red(const red_t *R, const double *x, const double *y, long n)
         long s = (long)r * blk, e = s + blk;
         if (s > n) s = n;
         if (e > n) e = n;
-        double part = R->mode == RED_TREE ? dot_tree(x + s, y + s, e - s)
-                                          : dot_serial(x + s, y + s, e - s);
+        double part = dot_tree(x + s, y + s, e - s);
         total = r == 0 ? part : total + part;
     }
     return total;

@@ -29,7 +29,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, N, maxit, seed, out, solver="bicgstab"):
+def _worker(rank, world, port, N, maxit, seed, out, solver="bicgstab", mode=1):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -39,7 +39,7 @@ def _worker(rank, world, port, N, maxit, seed, out, solver="bicgstab"):
         from bench import local_block
         from inputs import uniform
         from lssp_amd.dist import GlooTransport
-        dev = lssp_amd.Device(0)
+        dev = lssp_amd.Device(0, reduction=mode)
         dev.comm_init_host(world, rank, GlooTransport())
         n = N ** 3
         blk = (n + world - 1) // world
@@ -74,24 +74,58 @@ def _worker(rank, world, port, N, maxit, seed, out, solver="bicgstab"):
         dist.destroy_process_group()
 
 
+def _run(world, N, solver, mode, maxit=500):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, maxit, 0x5EED, q, solver, mode))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = q.get(timeout=150)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+    assert all(p.exitcode == 0 for p in procs)
+    return res
+
+
+@pytest.mark.parametrize("mode", [O.TREE, O.SERIAL], ids=["tree", "serial"])
+def test_config4_partition_8_ranks(mode):
+    """Config 4's decomposition (8 row blocks = 8 z-slabs, block-Jacobi ILU(0)
+    per rank, halo planes, rank-combined dots) with 8 ranks on one GPU at 64^3.
+    TREE: bitwise the oracle's 8-rank mode.  SERIAL: the ranks continue each
+    other's running sums, so every dot is the reference's sequential sum and
+    the run is bitwise the REFERENCE's own block-Jacobi (nblk = 8) solve
+    (tests/golden/large.json, from oracle/_ref/libref.so)."""
+    import json
+    world, N = 8, 64
+    nits, res, trace, y, x = _run(world, N, "bicgstab", mode, maxit=5000)
+    A = O.poisson(3, N)
+    L, U = O.ilu(A, "iluk", level=0, blk=(A.n + world - 1) // world)
+    o = O.solve(O.BICGSTAB, A, np.ones(A.n), L=L, U=U, mode=mode, nranks=world, maxit=5000)
+    assert nits == o.nits
+    assert res == o.residual
+    assert np.array_equal(trace, o.trace)
+    assert np.array_equal(x, o.x)
+    if mode == O.SERIAL:
+        from inputs import digest
+        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "large.json")) as f:
+            g = [c for c in json.load(f)["cases"] if c["pc"] == {"kind": "bj", "nblk": 8} and c["N"] == N][0]
+        assert nits == g["nits"]
+        assert res.hex() == g["residual"]
+        assert [v.hex() for v in trace] == g["trace"]
+        assert digest(x) == g["x_sha256"]
+
+
 @pytest.mark.parametrize("world,N,solver", [(2, 12, "bicgstab"), (3, 10, "bicgstab"), (4, 16, "bicgstab"),
                                              (2, 12, "gmres"), (3, 11, "gmres"), (2, 12, "cg"), (4, 13, "cg"),
                                              # IDR(4): each rank keeps its rows of the global rand() shadow space
                                              (2, 12, "idrs"), (3, 10, "bicgstabl")])
 def test_multirank_on_one_gpu_equals_oracle_prank_mode(world, N, solver):
-    import torch.multiprocessing as mp
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, N, 500, 0x5EED, q, solver)) for r in range(world)]
-    for p in procs:
-        p.start()
-    try:
-        nits, res, trace, y, x = q.get(timeout=100)
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-    assert all(p.exitcode == 0 for p in procs)
+    nits, res, trace, y, x = _run(world, N, solver, O.TREE)
     from inputs import uniform
     A = O.poisson(3, N)
     assert np.array_equal(y, O.spmv(0, A, uniform(0x5EED, A.n)))

@@ -100,3 +100,38 @@ def test_tree_reduction_definition():
             u = u[:off] + u[off:2 * off]
         assert O.dot(x, y, O.TREE) == u[0]
         assert O.dot(x, y, O.SERIAL) == pytest.approx(u[0], rel=1e-12)
+
+
+def _large():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "large.json")) as f:
+        return json.load(f)["cases"]
+
+
+def test_oracle_prank_serial_is_the_reference_sequential_sum():
+    """SERIAL mode with P ranks is the reference's one sequential sum (the GPU
+    ranks continue each other's running sums): the oracle's 8-rank block-Jacobi
+    run equals the reference's own nblk = 8 solve at 64^3 (config 4's split)."""
+    from inputs import digest
+    g = [c for c in _large() if c["pc"]["kind"] == "bj"][0]
+    A = O.poisson(3, g["N"])
+    nb = g["pc"]["nblk"]
+    L, U = O.ilu(A, "iluk", level=0, blk=(A.n + nb - 1) // nb)
+    r = O.solve(O.BICGSTAB, A, np.ones(A.n), L=L, U=U, mode=O.SERIAL, nranks=nb, maxit=g["maxit"])
+    assert r.nits == g["nits"] and r.residual.hex() == g["residual"]
+    assert [v.hex() for v in r.trace] == g["trace"]
+    assert digest(r.x) == g["x_sha256"]
+
+
+def test_oracle_matches_reference_at_bench_size():
+    """216^3 (n = 10,077,696): the first five BiCGSTAB + ILU(0) iterations, every
+    scalar and x, equal to the reference's (tests/golden/large.json)."""
+    from inputs import digest
+    g = [c for c in _large() if c["pc"]["kind"] == "iluk" and c["N"] == 216][0]
+    A = O.poisson(3, g["N"])
+    L, U = O.ilu(A, "iluk", level=0)
+    r = O.solve(O.BICGSTAB, A, np.ones(A.n), L=L, U=U, mode=O.SERIAL, maxit=g["maxit"])
+    assert r.nits == g["nits"] and r.residual.hex() == g["residual"]
+    assert [v.hex() for v in r.trace] == g["trace"]
+    assert digest(r.x) == g["x_sha256"]
