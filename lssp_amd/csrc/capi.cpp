@@ -385,8 +385,13 @@ int lssp_amd_vec_norm(lssp_amd_ctx *c, const double *x, long n, double *result)
 // ---- ILU -------------------------------------------------------------------------
 static int ilu_upload(lssp_amd_ctx *c, lssp_amd_ilu *M)
 {
-    LSSP_TRY(build_trisched(c, M->n, M->Lp, M->Lj, M->Lx, false, M->lower));
-    LSSP_TRY(build_trisched(c, M->n, M->Up, M->Uj, M->Ux, true, M->upper, &M->lower));
+    // structured ILU(0) of a 5-/7-point grid: line sweeps (linesweep.hip); the
+    // packet schedules of the general sweeps are then not needed
+    const int ls = build_line_sweep(c, M->n, M->Lp, M->Lj, M->Lx, M->Up, M->Uj, M->Ux, M->line);
+    if (ls != LSSP_AMD_OK && ls != LSSP_AMD_EUNSUPPORTED) return ls;
+    const bool packets = ls != LSSP_AMD_OK;
+    LSSP_TRY(build_trisched(c, M->n, M->Lp, M->Lj, M->Lx, false, M->lower, nullptr, packets));
+    LSSP_TRY(build_trisched(c, M->n, M->Up, M->Uj, M->Ux, true, M->upper, packets ? &M->lower : nullptr, packets));
     M->lower.h_pos.clear();
     M->lower.h_pos.shrink_to_fit();
     LSSP_HIP(hipMalloc(&M->d_cache, sizeof(double) * std::max(M->n, 1)));
@@ -467,6 +472,7 @@ int lssp_amd_ilu_destroy(lssp_amd_ilu *M)
     if (M->ctx) (void)hipStreamSynchronize(M->ctx->stream);
     free_trisched(M->lower);
     free_trisched(M->upper);
+    free_line_sweep(M->line);
     if (M->d_cache) (void)hipFree(M->d_cache);
     for (double *p : M->d_sh)
         if (p) (void)hipFree(p);
@@ -475,13 +481,18 @@ int lssp_amd_ilu_destroy(lssp_amd_ilu *M)
     return LSSP_AMD_OK;
 }
 
-static int check_err(lssp_amd_ctx *c)
+static int check_err(lssp_amd_ctx *c, const lssp_amd_ilu *M = nullptr)
 {
     int e = 0;
     LSSP_HIP(hipMemcpyAsync(&e, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     LSSP_HIP(hipStreamSynchronize(c->stream));
     if (e) {
         LSSP_HIP(hipMemset(c->d_err, 0, sizeof(int)));
+        // a sweep that gave up mid-way leaves hand-off entries written: re-arm
+        if (M && M->line.ntiles) {
+            LSSP_TRY(line_rearm(c, const_cast<lssp_amd_ilu *>(M)->line));
+            LSSP_HIP(hipStreamSynchronize(c->stream));
+        }
         return LSSP_AMD_ETIMEOUT;
     }
     return LSSP_AMD_OK;
@@ -493,12 +504,16 @@ int lssp_amd_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const 
 {
     if (!c || !M || !x || !rhs) return LSSP_AMD_EINVAL;
     LSSP_TRY(launch_ilu_apply(c, M, x, rhs));
-    return check_err(c);
+    return check_err(c, M);
 }
 
 int lssp_amd_ilu_trisolve(lssp_amd_ctx *c, const lssp_amd_ilu *M, int which, double *x, const double *rhs)
 {
     if (!c || !M || !x || !rhs || x == rhs) return LSSP_AMD_EINVAL;
+    if (M->line.ntiles) {
+        LSSP_TRY(launch_line_sweep(c, M->line, which ? 1 : 0, x, rhs));
+        return check_err(c, M);
+    }
     LSSP_TRY(launch_fill(c, x, M->n, TRI_SENTINEL));
     LSSP_TRY(launch_trisolve(c, which ? M->upper : M->lower, rhs, x, nullptr));
     return check_err(c);

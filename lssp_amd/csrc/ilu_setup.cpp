@@ -461,7 +461,7 @@ void ilu_factor(lssp_amd_ctx *c, int kind, const HostCSR &A0, int level, double 
 //          storage order (solver-tri.cxx:35-41) -- stored reversed here so the
 //          kernel always walks forward.
 int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std::vector<int> &Tj,
-                   const std::vector<double> &Tx, bool upper, TriSched &t, const TriSched *prod)
+                   const std::vector<double> &Tx, bool upper, TriSched &t, const TriSched *prod, bool packets)
 {
     t.n = n;
     std::vector<int> lev(n, 0);
@@ -499,7 +499,7 @@ int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std
     int nlev = 0;
     for (int i = 0; i < n; i++) nlev = std::max(nlev, lev[i] + 1);
     t.nlevels = n ? nlev : 0;
-    LSSP_TRY(build_bp_schedule(c, n, Tp, Tj, Tx, upper, lev, t, prod));
+    if (packets) LSSP_TRY(build_bp_schedule(c, n, Tp, Tj, Tx, upper, lev, t, prod));
     // counting sort by level; rows of a level stay in row order (lower) or in
     // descending row order (upper, mirroring the backward sweep)
     std::vector<int> start(nlev + 1, 0), perm(n);

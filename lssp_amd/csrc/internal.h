@@ -152,6 +152,42 @@ constexpr int PK3_EXT = 2;       // v6: HBM x operands per packet row (on averag
 constexpr int PK3_CAP = 4096;    // v6: packets per block (descriptors staged in LDS)
 constexpr int PK4_PAD = -1 - 4096;  // v6 padding code: the value-ring slot past the end (holds +0.0)
 
+// ---- line sweeps of structured ILU(0) factors (linesweep.hip) ----------------
+constexpr int LINE_P = 4;  // planes per tile
+enum { LT_KIN = 1, LT_JIN = 2, LT_KOUT = 4, LT_JOUT = 8 };
+struct LineGeom {
+    int nx = 0, ny = 0, nz = 0;
+    std::vector<char> kin;  // plane k has its (k-1) neighbour
+    bool unitL = true;
+};
+struct LineTile {  // one workgroup's unit of work, in its sweep's coordinates
+    int j0, nj, k0, np;
+    int flags;        // LT_*
+    int T;            // steps
+    int roff;         // (unused)
+    int tk, tj;       // producer tiles of the k / j inputs (-1: none)
+    int ut;           // L sweep: the mirror U tile (its rhs stream)
+    long long cbase;  // first row of the tile in its sweep's streams
+    long long ubase;  // L sweep: cbase of the mirror U tile
+};
+struct LineSweep {
+    int nx = 0, ny = 0, nz = 0, ntiles = 0, tmax = 0, NA = 3;
+    long rows_total = 0;
+    LineTile *d_tiles = nullptr;
+    double *d_coef = nullptr;
+    unsigned long long *d_claim = nullptr;
+    mutable unsigned long long base = 0;
+    std::vector<LineTile> h_tiles;
+};
+struct LineILU {
+    LineGeom g;
+    int W = 0, S = 0, tmax = 0, ntiles = 0;
+    LineSweep L, U;
+    double *d_ustream = nullptr;  // the U sweep's rhs, written by the L sweep
+    double *d_hk = nullptr, *d_hj = nullptr;  // hand-off buffers (armed with TRI_SENTINEL)
+    long hk_stride = 0, hj_stride = 0, hk_n = 0, hj_n = 0;
+};
+
 }  // namespace lssp_amd
 
 struct lssp_amd_ilu {
@@ -166,6 +202,7 @@ struct lssp_amd_ilu {
     mutable double *d_sh[4] = {nullptr, nullptr, nullptr, nullptr};
     mutable double *d_rperm = nullptr;  // the apply's rhs in L order
     mutable unsigned epoch = 0;
+    lssp_amd::LineILU line;  // structured factors: line sweeps (ntiles > 0)
     double setup_seconds = 0;
 };
 
@@ -256,7 +293,17 @@ void ilu_factor(lssp_amd_ctx *c, int kind, const HostCSR &A, int level, double t
 int ilu0_factor_gpu(lssp_amd_ctx *c, int n, int blk, const std::vector<int> &Ap, const std::vector<int> &Aj,
                     std::vector<double> &Ax);
 int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std::vector<int> &Tj,
-                   const std::vector<double> &Tx, bool upper, TriSched &t, const TriSched *prod = nullptr);
+                   const std::vector<double> &Tx, bool upper, TriSched &t, const TriSched *prod = nullptr,
+                   bool packets = true);
+// line sweeps (linesweep.hip): LSSP_AMD_EUNSUPPORTED when the factors are not
+// the structured ILU(0) of a 5-/7-point grid
+int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std::vector<int> &Lj,
+                     const std::vector<double> &Lx, const std::vector<int> &Up, const std::vector<int> &Uj,
+                     const std::vector<double> &Ux, LineILU &li);
+int line_rearm(lssp_amd_ctx *c, LineILU &li);
+void free_line_sweep(LineILU &li);
+int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs);
+int launch_line_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs);
 void free_trisched(TriSched &t);
 
 // reductions with the context's mode; result left in d_sums / scal per Fin

@@ -1,0 +1,798 @@
+// linesweep.hip -- ILU(0) triangular sweeps of a structured (5-/7-point grid)
+// factor, lines in lanes (solver-tri.cxx:4-46, the same arithmetic bit for bit).
+//
+// When a factor's strict rows are exactly the grid neighbours -- L row r holds
+// {r-nx*ny, r-nx, r-1} (those that exist, ascending, unit diagonal last), U row
+// r holds {r, r+1, r+nx, r+nx*ny} -- the sweep is a 3-D wavefront: row
+// (i, j, k) needs (i-1, j, k), (i, j-1, k) and (i, j, k-1).  The U sweep is the
+// same recurrence in mirrored coordinates (i' = nx-1-i, ...), and its
+// descending summation order (solver-tri.cxx:38) is then again k'-1, j'-1, i'-1.
+//
+// Decomposition.  A TILE is nj <= 64 consecutive lines (j) of np <= P
+// consecutive planes (k); one workgroup runs it.  Lane l owns line j0+l; at
+// step s it computes, for each plane p, row i = s - l - p.  Then
+//   * (i-1, j, k):   the lane's own value of the previous step (a register);
+//   * (i, j-1, k):   lane l-1's value of the previous step (DPP wave_shr:1);
+//   * (i, j, k-1):   the lane's own value of plane p-1 at the previous step;
+// so a step is P rows per lane of pure register arithmetic.  Across tiles the
+// two boundary streams (plane np-1 -> the next tile in k, lane nj-1 -> the next
+// tile in j) go through HBM hand-off buffers with the value as the flag
+// (TRI_SENTINEL), indexed by the consumer's step so both sides access them
+// coalesced.  A path through the grid crosses W + S tiles instead of nz planes.
+//
+// Roles (one barrier per step, LDS only):
+//   wave 0          compute: reads the step's slot, writes results to LDS;
+//   waves 1..NL     loaders: LDS-DMA (global_load_lds) of the step's
+//                   coefficient block (and rhs) D steps ahead, steps q = w mod NL;
+//   wave NL+1       poller: LDS-DMA sc1 reads of the hand-off inputs DH steps
+//                   ahead; checks them, re-polls what is not yet written;
+//   wave NL+2       storer: results -> HBM (natural-order x, the U sweep's rhs
+//                   stream, hand-off outputs with sc1 stores), and re-arms the
+//                   consumed hand-off inputs with the sentinel.
+// Only the compute wave is on the critical path; every VMEM queue (vmcnt is
+// in order per wave) belongs to one role with one lead, so no wait ever covers
+// another role's slow operations.
+//
+// Layouts (host, build_line_sweep): per tile, per step, per plane, the rows
+// valid at that step (a contiguous lane range [lo, hi]), each row's NA
+// coefficients {c_k, c_j, c_i(, diag)} together; steps padded to an even row
+// count (16-byte blocks).  The L sweep writes its output into the U
+// sweep's rhs stream of the same compact layout (tile, step, plane and lane
+// mirrored), so the U sweep reads its rhs as one more coalesced block.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "internal.h"
+
+namespace lssp_amd {
+
+constexpr uint32_t SENT_LO = (uint32_t)(TRI_SENTINEL & 0xffffffffu);
+constexpr uint32_t SENT_HI = (uint32_t)(TRI_SENTINEL >> 32);
+
+// ---------------------------------------------------------------------------
+// host: detection of the grid structure
+// ---------------------------------------------------------------------------
+// kin[k] = plane k has its (k-1) neighbour (false at k = 0 and at block-Jacobi cuts)
+static bool detect_grid(int n, const std::vector<int> &Lp, const std::vector<int> &Lj, const std::vector<double> &Lx,
+                        const std::vector<int> &Up, const std::vector<int> &Uj, LineGeom &g)
+{
+    long offs[3];
+    int no = 0;
+    for (int r = 0; r < n; r++) {
+        const int a = Lp[r], b = Lp[r + 1];
+        if (b - a < 1 || b - a > 4 || Lj[b - 1] != r) return false;
+        for (int k = a; k < b - 1; k++) {
+            const long d = (long)r - Lj[k];
+            if (d <= 0) return false;
+            bool seen = false;
+            for (int q = 0; q < no; q++) seen |= offs[q] == d;
+            if (!seen) {
+                if (no == 3) return false;
+                offs[no++] = d;
+            }
+        }
+    }
+    std::sort(offs, offs + no);
+    if (no < 2 || offs[0] != 1) return false;
+    long nx = offs[1], plane = no == 3 ? offs[2] : n;
+    if (plane % nx || n % plane) return false;
+    g.nx = (int)nx;
+    g.ny = (int)(plane / nx);
+    g.nz = (int)(n / plane);
+    if (g.nx < 2 || g.ny < 8) return false;
+    g.kin.assign(g.nz, 0);
+    for (int k = 1; k < g.nz; k++) {
+        const long r = (long)k * plane;  // row (0, 0, k): its only candidate neighbour is k-1
+        g.kin[k] = (Lp[r + 1] - Lp[r] == 2) ? 1 : 0;
+    }
+    g.unitL = true;
+    for (int k = 0; k < g.nz; k++)
+        for (int j = 0; j < g.ny; j++)
+            for (int i = 0; i < g.nx; i++) {
+                const long r = ((long)k * g.ny + j) * g.nx + i;
+                long want[3];
+                int m = 0;
+                if (k > 0 && g.kin[k]) want[m++] = r - plane;
+                if (j > 0) want[m++] = r - nx;
+                if (i > 0) want[m++] = r - 1;
+                const int a = Lp[r], b = Lp[r + 1];
+                if (b - a - 1 != m) return false;
+                for (int q = 0; q < m; q++)
+                    if (Lj[a + q] != want[q]) return false;
+                g.unitL &= Lx[b - 1] == 1.0;
+                m = 0;
+                if (i < g.nx - 1) want[m++] = r + 1;
+                if (j < g.ny - 1) want[m++] = r + nx;
+                if (k < g.nz - 1 && g.kin[k + 1]) want[m++] = r + plane;
+                const int c = Up[r], e = Up[r + 1];
+                if (e - c - 1 != m || Uj[c] != r) return false;
+                for (int q = 0; q < m; q++)
+                    if (Uj[c + 1 + q] != want[q]) return false;
+            }
+    return true;
+}
+
+// rows of a tile (nj lines, np planes) valid at step s, plane p: lanes [lo, hi]
+static inline void step_range(int nx, int nj, int np, int s, int p, int &lo, int &hi)
+{
+    if (p >= np) {
+        lo = 0;
+        hi = -1;
+        return;
+    }
+    lo = std::max(0, s - p - nx + 1);
+    hi = std::min(nj - 1, s - p);
+}
+
+// coefficient of row (i, j, k) of one sweep in that sweep's coordinates:
+// component a = 0 (k-1), 1 (j-1), 2 (i-1), 3 (diagonal)
+struct CoefSrc {
+    const std::vector<int> *Tp, *Tj;
+    const std::vector<double> *Tx;
+    bool upper;
+    long n, nx, plane;
+    double get(long r_sweep, int a) const
+    {
+        const long r = upper ? n - 1 - r_sweep : r_sweep;
+        const int b = (*Tp)[r], e = (*Tp)[r + 1];
+        if (a == 3) return upper ? (*Tx)[b] : (*Tx)[e - 1];
+        const long off = a == 0 ? plane : a == 1 ? nx : 1;
+        const long want = upper ? r + off : r - off;
+        const int s0 = upper ? b + 1 : b, s1 = upper ? e : e - 1;
+        for (int q = s0; q < s1; q++)
+            if ((*Tj)[q] == want) return (*Tx)[q];
+        return 0.0;  // missing neighbour: +0.0 coefficient, the operand is +0.0 too
+    }
+};
+
+static int build_tiles(const LineGeom &g, int P, int W, std::vector<LineTile> &tiles, int &S)
+{
+    // plane segments between cuts, cut into tiles of <= P planes
+    std::vector<std::pair<int, int>> kt;  // (k0, np)
+    for (int k = 0; k < g.nz;) {
+        int e = k + 1;
+        while (e < g.nz && g.kin[e]) e++;
+        for (int k0 = k; k0 < e; k0 += P) kt.push_back({k0, std::min(P, e - k0)});
+        k = e;
+    }
+    S = (int)kt.size();
+    tiles.assign((size_t)S * W, LineTile{});
+    const int base = g.ny / W, extra = g.ny % W;
+    for (int K = 0; K < S; K++) {
+        int j0 = 0;
+        for (int J = 0; J < W; J++) {
+            LineTile &t = tiles[(size_t)K * W + J];
+            t.j0 = j0;
+            t.nj = base + (J < extra ? 1 : 0);
+            j0 += t.nj;
+            t.k0 = kt[K].first;
+            t.np = kt[K].second;
+            const bool kin = t.k0 > 0 && g.kin[t.k0];
+            t.flags = (kin ? LT_KIN : 0) | (J > 0 ? LT_JIN : 0) | (J < W - 1 ? LT_JOUT : 0);
+            t.T = g.nx + t.nj + t.np - 2;
+            t.tk = kin ? (K - 1) * W + J : -1;
+            t.tj = J > 0 ? K * W + J - 1 : -1;
+        }
+    }
+    for (int K = 0; K + 1 < S; K++)
+        for (int J = 0; J < W; J++)
+            if (tiles[(size_t)(K + 1) * W + J].flags & LT_KIN) tiles[(size_t)K * W + J].flags |= LT_KOUT;
+    return LSSP_AMD_OK;
+}
+
+// Stream layout of one sweep: per tile, per step s, a block of P planes x nj
+// rows (row (p, l) at p*nj + l; rows not valid at that step are +0.0), each
+// row's NA coefficients {c_k, c_j, c_i(, diag)} together.  Fixed strides keep
+// every role's addressing to a per-lane base plus immediate offsets.
+static int upload_sweep(lssp_amd_ctx *c, const LineGeom &g, const std::vector<LineTile> &tiles, const CoefSrc &src,
+                        int NA, LineSweep &ls)
+{
+    const int nx = g.nx, P = LINE_P;
+    std::vector<LineTile> tt = tiles;
+    long rows_total = 0;
+    int tmax = 0;
+    for (LineTile &t : tt) {
+        t.roff = 0;
+        t.cbase = rows_total;
+        rows_total += (long)t.T * P * t.nj;
+        tmax = std::max(tmax, t.T);
+    }
+    // + slack for the loaders' whole 1 KB pieces past the last block
+    const long slack = 16 * 1024 / 8;
+    std::vector<double> coef((size_t)rows_total * NA + slack, 0.0);
+    for (const LineTile &t : tt)
+        for (int s = 0; s < t.T; s++) {
+            double *blk = coef.data() + (size_t)(t.cbase + (long)s * P * t.nj) * NA;
+            for (int p = 0; p < t.np; p++) {
+                int lo, hi;
+                step_range(nx, t.nj, t.np, s, p, lo, hi);
+                for (int l = lo; l <= hi; l++) {
+                    const long i = s - l - p;
+                    const long r = ((long)(t.k0 + p) * g.ny + (t.j0 + l)) * nx + i;
+                    for (int a = 0; a < NA; a++) blk[(size_t)(p * t.nj + l) * NA + a] = src.get(r, a);
+                }
+            }
+        }
+    ls.nx = g.nx;
+    ls.ny = g.ny;
+    ls.nz = g.nz;
+    ls.ntiles = (int)tt.size();
+    ls.tmax = tmax;
+    ls.rows_total = rows_total;
+    ls.NA = NA;
+    LSSP_HIP(hipMalloc(&ls.d_tiles, sizeof(LineTile) * tt.size()));
+    LSSP_HIP(hipMemcpy(ls.d_tiles, tt.data(), sizeof(LineTile) * tt.size(), hipMemcpyHostToDevice));
+    LSSP_HIP(hipMalloc(&ls.d_coef, sizeof(double) * coef.size()));
+    LSSP_HIP(hipMemcpy(ls.d_coef, coef.data(), sizeof(double) * coef.size(), hipMemcpyHostToDevice));
+    LSSP_HIP(hipMalloc(&ls.d_claim, sizeof(unsigned long long)));
+    LSSP_HIP(hipMemset(ls.d_claim, 0, sizeof(unsigned long long)));
+    ls.h_tiles = std::move(tt);
+    return LSSP_AMD_OK;
+}
+
+int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std::vector<int> &Lj,
+                     const std::vector<double> &Lx, const std::vector<int> &Up, const std::vector<int> &Uj,
+                     const std::vector<double> &Ux, LineILU &li)
+{
+    const char *env = getenv("LSSP_AMD_LINE");
+    if (env && !atoi(env)) return LSSP_AMD_EUNSUPPORTED;
+    LineGeom g;
+    if (!detect_grid(n, Lp, Lj, Lx, Up, Uj, g)) return LSSP_AMD_EUNSUPPORTED;
+    const int P = LINE_P;
+    const int W = (g.ny + 63) / 64;
+    std::vector<LineTile> Lt;
+    int S = 0;
+    LSSP_TRY(build_tiles(g, P, W, Lt, S));
+    // U tiles: exact mirrors of the L tiles (U tile (W-1-J, S-1-K) <-> L tile (J, K))
+    std::vector<LineTile> Ut(Lt.size());
+    for (int K = 0; K < S; K++)
+        for (int J = 0; J < W; J++) {
+            const LineTile &l = Lt[(size_t)K * W + J];
+            const int Kp = S - 1 - K, Jp = W - 1 - J;
+            LineTile &u = Ut[(size_t)Kp * W + Jp];
+            u = l;
+            u.j0 = g.ny - l.j0 - l.nj;
+            u.k0 = g.nz - l.k0 - l.np;
+            // U tile Kp takes its k-input from U tile Kp-1 = L tile K+1's k-output side
+            const bool kin = K + 1 < S && (Lt[(size_t)(K + 1) * W + J].flags & LT_KIN);
+            const bool kout = (l.flags & LT_KIN) != 0;
+            u.flags = (kin ? LT_KIN : 0) | (kout ? LT_KOUT : 0) | (Jp > 0 ? LT_JIN : 0) | (Jp < W - 1 ? LT_JOUT : 0);
+            u.tk = kin ? (Kp - 1) * W + Jp : -1;
+            u.tj = Jp > 0 ? Kp * W + Jp - 1 : -1;
+        }
+    const long plane = (long)g.nx * g.ny;
+    CoefSrc cl{&Lp, &Lj, &Lx, false, n, g.nx, plane};
+    CoefSrc cu{&Up, &Uj, &Ux, true, n, g.nx, plane};
+    li.g = g;
+    li.W = W;
+    li.S = S;
+    LSSP_TRY(upload_sweep(c, g, Lt, cl, g.unitL ? 3 : 4, li.L));
+    LineGeom gu = g;
+    for (int k = 0; k < g.nz; k++) gu.kin[k] = k > 0 ? g.kin[g.nz - k] : 0;
+    LSSP_TRY(upload_sweep(c, gu, Ut, cu, 4, li.U));
+    // the L sweep writes its output into the U sweep's rhs stream: per L tile
+    // the base row of its mirror U tile
+    for (int K = 0; K < S; K++)
+        for (int J = 0; J < W; J++) {
+            LineTile &l = li.L.h_tiles[(size_t)K * W + J];
+            l.ut = (S - 1 - K) * W + (W - 1 - J);
+            l.ubase = li.U.h_tiles[l.ut].cbase;
+        }
+    LSSP_HIP(hipMemcpy(li.L.d_tiles, li.L.h_tiles.data(), sizeof(LineTile) * li.L.h_tiles.size(),
+                       hipMemcpyHostToDevice));
+    // U rhs stream (written by the L sweep) and the hand-off buffers, shared by
+    // both sweeps (they never run at once) and armed with the sentinel
+    LSSP_HIP(hipMalloc(&li.d_ustream, sizeof(double) * (li.U.rows_total + 16 * 1024 / 8)));
+    LSSP_HIP(hipMemset(li.d_ustream, 0, sizeof(double) * (li.U.rows_total + 16 * 1024 / 8)));  // invalid rows stay +0.0
+    li.tmax = std::max(li.L.tmax, li.U.tmax);
+    li.hk_stride = (long)li.tmax * 64;
+    li.hj_stride = (long)li.tmax * LINE_P;
+    li.ntiles = (int)Lt.size();
+    li.hk_n = li.hk_stride * li.ntiles;
+    li.hj_n = li.hj_stride * li.ntiles;
+    LSSP_HIP(hipMalloc(&li.d_hk, sizeof(double) * li.hk_n));
+    LSSP_HIP(hipMalloc(&li.d_hj, sizeof(double) * li.hj_n));
+    LSSP_TRY(line_rearm(c, li));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    return LSSP_AMD_OK;
+}
+
+int line_rearm(lssp_amd_ctx *c, LineILU &li)
+{
+    LSSP_TRY(launch_fill(c, li.d_hk, li.hk_n, TRI_SENTINEL));
+    return launch_fill(c, li.d_hj, li.hj_n, TRI_SENTINEL);
+}
+
+void free_line_sweep(LineILU &li)
+{
+    for (LineSweep *s : {&li.L, &li.U}) {
+        if (s->d_tiles) (void)hipFree(s->d_tiles);
+        if (s->d_coef) (void)hipFree(s->d_coef);
+        if (s->d_claim) (void)hipFree(s->d_claim);
+        *s = LineSweep{};
+    }
+    if (li.d_ustream) (void)hipFree(li.d_ustream);
+    if (li.d_hk) (void)hipFree(li.d_hk);
+    if (li.d_hj) (void)hipFree(li.d_hj);
+    li.d_ustream = li.d_hk = li.d_hj = nullptr;
+    li.ntiles = 0;
+}
+
+// ---------------------------------------------------------------------------
+// device
+// ---------------------------------------------------------------------------
+struct LineArgs {
+    int nx, ny, ntiles;
+    long n;
+    const LineTile *tiles;
+    const double *coef;
+    const double *rhs;      // natural order (RHS_NAT) or the U rhs stream
+    double *out;            // OUT 1: natural-order output; OUT 2: the U rhs stream
+    double *hk, *hj;
+    long hk_stride, hj_stride;
+    unsigned long long *claim;
+    unsigned long long base;
+    int mirror;             // U sweep: natural row = n-1 - sweep row
+    int *err;
+    // diagnostics (LSSP_AMD_LINE_TRACE): per tile {claim, step 0, end, re-polls,
+    // xcc}; per step of tile ttile {compute start, compute end, poller busy,
+    // loader wait, loader issue, storer busy}
+    unsigned long long *trace;
+    int ttile;
+};
+
+__device__ __forceinline__ void dma16(const void *g, unsigned lds)
+{
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
+}
+__device__ __forceinline__ void dma4(const void *g, unsigned lds)
+{
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
+}
+__device__ __forceinline__ void line_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ uint64_t line_ld_agent(const double *p)
+{
+    return __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void line_st_agent(double *p, double v)
+{
+    uint64_t b = (uint64_t)__double_as_longlong(v);
+    if (b == TRI_SENTINEL) b = 0x7FF8000000000000ull;  // never publish the flag pattern as a value
+    __hip_atomic_store(reinterpret_cast<uint64_t *>(p), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ double dpp_shr1(double v, double old)
+{
+    const long long b = __double_as_longlong(v), o = __double_as_longlong(old);
+    const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), 0x138, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// slot layout (bytes): the step's coefficient block, its rhs, the hand-off inputs
+template <int P, int NA, bool RHS_NAT>
+struct LineSlot {
+    static constexpr int NPC = (P * 64 * NA * 8 + 1023) / 1024;  // 1 KB DMA pieces of the coefficient block
+    static constexpr int NRP = (P * 64 * 8 + 1023) / 1024;       // ... of a U rhs-stream block
+    static constexpr int NRD = RHS_NAT ? 2 * P : NRP;            // rhs DMA instructions per step
+    static constexpr int COEF = 0;
+    static constexpr int RHS = NPC * 1024;
+    static constexpr int KFIN = RHS + (RHS_NAT ? 2 * P * 256 : NRP * 1024);  // double[64]
+    static constexpr int JFIN = KFIN + 512;                                  // double[P]
+    static constexpr int BYTES = (JFIN + 8 * P + 15) & ~15;
+};
+
+// P planes per tile, NA coefficient components (3: unit L, 4: with diagonal),
+// RHS_NAT: the rhs is read in natural order (else from the U rhs stream), CW
+// compute waves (P/CW planes each), NL loader waves, D loader lead (steps),
+// DH poller lead (steps), SW storer waves; OUT 1: natural-order output, 2: the
+// U rhs stream (the L sweep of an apply); TRACE: diagnostics.
+template <int P, int NA, bool RHS_NAT, int OUT, int CW, int NL, int D, int DH, int SW, bool TRACE>
+__global__ __launch_bounds__(64 * (CW + NL + 1 + SW)) void k_line(LineArgs a)
+{
+    // landing lead: the loaders and the poller complete step s+LA's slot during
+    // step s; the compute reads it at step s+LA-1 (into registers, one step ahead)
+    constexpr int LA = 2;
+    static_assert(DH >= 3 && DH < D && P % CW == 0 && (OUT == 1 || OUT == 2), "lead");
+    constexpr int PC = P / CW;
+    constexpr int R = D + 1;
+    constexpr int S0 = -((D + 11) / 12) * 12;  // first step of every role (a multiple of 2, 3 and 4)
+    using SL = LineSlot<P, NA, RHS_NAT>;
+    constexpr int NITEM = SL::NPC + SL::NRD;          // DMA instructions per step, shared by the loaders
+    constexpr int KPER = (NITEM + NL - 1) / NL;
+    static_assert((D - LA) * KPER <= 63 && 2 * (DH - 1) <= 63, "vmcnt range");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char *ring = smem;
+    double *res = reinterpret_cast<double *>(smem + R * SL::BYTES);  // [2][P][64]
+    int *s_tile = reinterpret_cast<int *>(res + 2 * P * 64);
+    const unsigned lds0 = (unsigned)(uintptr_t)smem;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int nx = a.nx;
+
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) *s_tile = (int)(atomicAdd(a.claim, 1ull) - a.base);
+        __syncthreads();
+        const int t = __builtin_amdgcn_readfirstlane(*s_tile);
+        if (t >= a.ntiles) break;
+        if (TRACE && threadIdx.x == 0) a.trace[8 * t] = __builtin_amdgcn_s_memrealtime();
+        const LineTile d = a.tiles[t];
+        const int T = d.T, nj = d.nj, np = d.np;
+        const long SB = (long)P * nj;  // rows per step block
+        const bool kin = d.flags & LT_KIN, jin = d.flags & LT_JIN, kout = d.flags & LT_KOUT,
+                   jout = d.flags & LT_JOUT;
+        const int lc = min(lane, nj - 1);
+        // natural row of (i, line lane, plane p) = nb(p) + i (mirror: nb(p) - i)
+        auto nb = [&](int p, int l) {
+            const long r = ((long)(d.k0 + p) * a.ny + (d.j0 + l)) * nx;
+            return a.mirror ? a.n - 1 - r : r;
+        };
+        unsigned long long *ts = TRACE ? a.trace + 8 * (long)a.ntiles : nullptr;
+        const bool trs = TRACE && t == a.ttile && lane == 0;
+
+        if (wave < CW) {
+            // ---------------- compute: planes p0 .. p0+PC-1 ----------------
+            // Coefficients and rhs of step s+1 are read from LDS at the start of
+            // step s (their slot was completed before the barrier that ended step
+            // s-1), so that latency overlaps step s's arithmetic.  The k-input
+            // of the first plane (the poller's, or the previous compute wave's
+            // result) is read at the step start; planes run in descending order,
+            // so it is needed last.
+            const int p0 = wave * PC;
+            struct In {
+                double ck[PC], cj[PC], ci[PC], dg[PC], rh[PC], jv[PC];
+            };
+            auto load = [&](int s, In &in) {
+                const char *slot = ring + (s % R) * SL::BYTES;
+#pragma unroll
+                for (int u = 0; u < PC; u++) {
+                    const int p = p0 + u;
+                    const double *b = reinterpret_cast<const double *>(slot + SL::COEF) + (p * nj + lc) * NA;
+                    in.ck[u] = b[0];
+                    in.cj[u] = b[1];
+                    in.ci[u] = b[2];
+                    if constexpr (NA == 4) in.dg[u] = b[3];
+                    if constexpr (RHS_NAT) {
+                        const uint32_t *r32 = reinterpret_cast<const uint32_t *>(slot + SL::RHS);
+                        const uint64_t lo32 = r32[p * 64 + lane], hi32 = r32[(P + p) * 64 + lane];
+                        in.rh[u] = __longlong_as_double((long long)((hi32 << 32) | lo32));
+                    } else {
+                        in.rh[u] = reinterpret_cast<const double *>(slot + SL::RHS)[p * nj + lc];
+                    }
+                    in.jv[u] = reinterpret_cast<const double *>(slot + SL::JFIN)[p];
+                }
+            };
+            double xc[PC];
+#pragma unroll
+            for (int u = 0; u < PC; u++) xc[u] = 0.0;
+            // hand-off outputs, stored here (sc1) as soon as computed: this wave
+            // never waits on its VMEM queue, so the stores cost it nothing
+            double *hko = a.hk + (long)t * a.hk_stride + (long)(1 - np) * 64 + lane;  // + q*64
+            double *hjo = a.hj + (long)t * a.hj_stride + (long)(1 - nj) * P;          // + q*P + p
+            auto body = [&](int s, In &cur, In &nxt) {
+                if (TRACE && lane == 0 && wave == 0 && s == 0) a.trace[8 * t + 1] = __builtin_amdgcn_s_memrealtime();
+                if (trs && s >= 0 && s < T) ts[8 * s] = __builtin_amdgcn_s_memtime();
+                if (s == -1) load(0, nxt);
+                if (s >= 0 && s < T) {
+                    const char *slot = ring + (s % R) * SL::BYTES;
+                    const double kx = wave == 0 ? reinterpret_cast<const double *>(slot + SL::KFIN)[lane]
+                                                : res[((s - 1) & 1) * P * 64 + (p0 - 1) * 64 + lane];
+                    if (s + 1 < T) load(s + 1, nxt);
+#pragma unroll
+                    for (int u = PC - 1; u >= 0; u--) {
+                        const int p = p0 + u;
+                        const int i = s - p - lane;
+                        const bool valid = p < np && lane < nj && i >= 0 && i < nx;
+                        const double xk = u > 0 ? xc[u - 1] : kx;
+                        const double xj = dpp_shr1(xc[u], cur.jv[u]);
+                        double v = cur.rh[u] - cur.ck[u] * xk;
+                        v = v - cur.cj[u] * xj;
+                        v = v - cur.ci[u] * xc[u];
+                        if constexpr (NA == 4) v = v / cur.dg[u];
+                        xc[u] = valid ? v : xc[u];
+                        if (kout && p == np - 1 && valid) line_st_agent(hko + (long)s * 64, xc[u]);
+                        if (jout && p < np && lane == nj - 1 && valid) line_st_agent(hjo + (long)s * P + p, xc[u]);
+                    }
+#pragma unroll
+                    for (int u = 0; u < PC; u++) res[((s & 1) * P + p0 + u) * 64 + lane] = xc[u];
+                }
+                if (trs && s >= 0 && s < T) ts[8 * s + 1] = __builtin_amdgcn_s_memtime();
+                line_barrier();
+            };
+            In A, B;  // step s uses the set loaded at step s-1: even steps A, odd steps B
+            for (int s = S0; s <= T; s += 2) {
+                body(s, A, B);
+                if (s + 1 <= T) body(s + 1, B, A);
+            }
+            if (TRACE && lane == 0 && wave == 0) {
+                a.trace[8 * t + 2] = __builtin_amdgcn_s_memrealtime();
+                unsigned xcc;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                a.trace[8 * t + 4] = xcc;
+            }
+        } else if (wave < CW + NL) {
+            // ---------------- loaders: every step's DMAs spread over the NL waves ----------------
+            const int w = wave - CW;
+            long nbr[P];
+#pragma unroll
+            for (int p = 0; p < P; p++) nbr[p] = nb(min(p, np - 1), lc);
+            auto issue = [&](int q) {
+                const int qc = min(max(q, 0), T - 1);
+                const unsigned sl = lds0 + (unsigned)(((q % R + R) % R) * SL::BYTES);
+                const char *cb = reinterpret_cast<const char *>(a.coef) + (d.cbase + qc * SB) * (8L * NA);
+#pragma unroll
+                for (int k = 0; k < KPER; k++) {
+                    const int m = w + k * NL;
+                    if (m < SL::NPC) {
+                        dma16(cb + m * 1024 + lane * 16, sl + SL::COEF + m * 1024);
+                    } else if (m < NITEM) {
+                        const int r = m - SL::NPC;
+                        if constexpr (RHS_NAT) {
+                            const int p = r >> 1, pp = min(p, np - 1);
+                            const long i = min(max((long)qc - lc - pp, 0L), (long)nx - 1);
+                            const char *rp = reinterpret_cast<const char *>(a.rhs + (a.mirror ? nbr[p] - i : nbr[p] + i));
+                            dma4(rp + 4 * (r & 1), sl + SL::RHS + ((r & 1) * P + p) * 256);
+                        } else {
+                            const char *ub = reinterpret_cast<const char *>(a.rhs) + (d.cbase + qc * SB) * 8L;
+                            dma16(ub + r * 1024 + lane * 16, sl + SL::RHS + r * 1024);
+                        }
+                    } else {
+                        dma16(cb + lane * 16, sl + SL::COEF);  // keeps the per-wave count fixed
+                    }
+                }
+            };
+            for (int s = S0; s <= T; s++) {
+                const unsigned long long i0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
+                issue(s + D);  // dummies past T keep the wait counts exact
+                const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
+                // steps s+LA+1 .. s+D were issued after step s+LA's
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - LA) * KPER) : "memory");
+                if (trs && w == 0 && s >= 0 && s < T) {
+                    ts[8 * s + 4] = w0 - i0;
+                    ts[8 * s + 3] = __builtin_amdgcn_s_memtime() - w0;
+                }
+                line_barrier();
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (wave == CW + NL) {
+            // ---------------- poller ----------------
+            // 8-byte sc1 loads into a ring of DH register sets (set = step mod
+            // DH), issued from inline asm with exact vmcnt waits (the compiler
+            // does not see these loads; tests/test_isa_vmcnt.py checks that no
+            // instruction touches a register still in flight).  At step s the
+            // loads for the k-input of step s+DH and the j-input of step s+DH+1
+            // are issued; those of the k-input of step s+1 and the j-input of
+            // step s+2 land (the compute reads k at its step start, j one step
+            // earlier with the coefficients).
+            const double *hk = a.hk + (long)max(d.tk, 0) * a.hk_stride;
+            const double *hj = a.hj + (long)max(d.tj, 0) * a.hj_stride;
+            auto kval = [&](int q) { return kin && q >= 0 && q < T && lane < nj && q - lane >= 0 && q - lane < nx; };
+            auto jval = [&](int q) { return jin && q >= 0 && q < T && lane < np && q - lane >= 0 && q - lane < nx; };
+            auto kaddr = [&](int q) { return hk + (long)min(max(q, 0), a.hk_stride / 64 - 1) * 64 + lane; };
+            auto jaddr = [&](int q) { return hj + (long)min(max(q, 0), a.hk_stride / 64 - 1) * P + min(lane, P - 1); };
+            uint64_t kb[DH], jb[DH];
+#pragma unroll
+            for (int u = 0; u < DH; u++) kb[u] = jb[u] = 0;
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            unsigned polls = 0;
+            auto pstep = [&](int s, auto U) {
+                constexpr int ui = decltype(U)::value;  // s = ui (mod DH): set issued at step s
+                constexpr int ul = (ui + 1) % DH;       // set issued at step s+1-DH: k(s+1), j(s+2)
+                // every pstep issues and waits (past T too), so the load queue has
+                // one shape on every path; only the slot work and the barrier stop at T
+                const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
+                asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(kb[ui]) : "v"(kaddr(s + DH)) : "memory");
+                asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(jb[ui]) : "v"(jaddr(s + DH + 1)) : "memory");
+                // the sets of steps s+2-DH .. s (DH-1 steps, 2 loads each) are younger
+                asm volatile("s_waitcnt vmcnt(%2)" : "+v"(kb[ul]), "+v"(jb[ul]) : "n"(2 * (DH - 1)) : "memory");
+                if (s > T) return;
+                const int qk = s + 1, qj = s + 2;
+                const bool vk = kval(qk), vj = jval(qj);
+                uint64_t kv = vk ? kb[ul] : 0, jv = vj ? jb[ul] : 0;
+                const bool bad = (vk && kv == TRI_SENTINEL) || (vj && jv == TRI_SENTINEL);
+                if (__any(bad)) {
+                    // resync episode: the producer was not done when these polls were
+                    // issued, so probably neither for the polls still in flight.
+                    // Drain them, wait for these values and for the furthest step in
+                    // flight (so the consumer settles that much further behind and
+                    // its early polls find their values from then on), re-issue.
+                    polls++;
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    auto spin = [&](const double *src) {
+                        for (;;) {
+                            const uint64_t b = line_ld_agent(src);
+                            if (b != TRI_SENTINEL) return b;
+                            if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s
+                                atomicOr(a.err, 8);
+                                return (uint64_t)0x7FF8000000000000ull;
+                            }
+                            __builtin_amdgcn_s_sleep(1);
+                        }
+                    };
+                    if (vk && kv == TRI_SENTINEL) kv = spin(hk + (long)qk * 64 + lane);
+                    if (vj && jv == TRI_SENTINEL) jv = spin(hj + (long)qj * P + lane);
+                    if (kval(s + DH)) (void)spin(hk + (long)(s + DH) * 64 + lane);
+                    if (jval(s + DH + 1)) (void)spin(hj + (long)(s + DH + 1) * P + lane);
+#pragma unroll
+                    for (int k = 2; k <= DH; k++) {  // the sets issued at steps s+k-DH
+                        asm volatile("global_load_dwordx2 %0, %1, off sc1"
+                                     : "=v"(kb[(ui + k) % DH])
+                                     : "v"(kaddr(s + k))
+                                     : "memory");
+                        asm volatile("global_load_dwordx2 %0, %1, off sc1"
+                                     : "=v"(jb[(ui + k) % DH])
+                                     : "v"(jaddr(s + k + 1))
+                                     : "memory");
+                    }
+                }
+                if (qk < T) reinterpret_cast<double *>(ring + (qk % R) * SL::BYTES + SL::KFIN)[lane] =
+                    __longlong_as_double((long long)kv);
+                if (lane < P && qj < T)
+                    reinterpret_cast<double *>(ring + (qj % R) * SL::BYTES + SL::JFIN)[lane] =
+                        __longlong_as_double((long long)jv);
+                if (trs && s >= 0 && s < T) ts[8 * s + 2] = __builtin_amdgcn_s_memtime() - w0;
+                line_barrier();
+            };
+            static_assert(DH == 3 || DH == 4, "the poller's register ring is unrolled by DH");
+            for (int s = S0; s <= T; s += DH) {
+                pstep(s, std::integral_constant<int, 0>());
+                pstep(s + 1, std::integral_constant<int, 1>());
+                pstep(s + 2, std::integral_constant<int, 2>());
+                if constexpr (DH == 4) pstep(s + 3, std::integral_constant<int, 3 % DH>());
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (TRACE) {
+                for (int o = 32; o >= 1; o >>= 1) polls += __shfl_xor(polls, o);
+                if (lane == 0) a.trace[8 * t + 3] = polls;
+            }
+        } else {
+            // ---------------- storers: bulk results of step s-1, re-arms ----------------
+            // storer w writes planes w, w+SW, ...; storer 0 re-arms the consumed
+            // j-inputs, storer SW-1 the k-inputs.  Pointers advance by a constant
+            // per step.
+            const int w = wave - (CW + NL + 1);
+            constexpr int PS = (P + SW - 1) / SW;
+            double *po[PS];
+            int vlo[PS];
+#pragma unroll
+            for (int u = 0; u < PS; u++) {
+                const int p = w + u * SW, pp = min(p, np - 1);
+                vlo[u] = p < np && lane < nj ? lane + p : 1 << 30;  // valid iff 0 <= q - vlo < nx
+                if constexpr (OUT == 1) {
+                    // natural row of (i = q - lane - p) at q = 0, moving by +-1 per step
+                    po[u] = a.out + (a.mirror ? nb(pp, lc) + lane + pp : nb(pp, lc) - lane - pp);
+                } else {
+                    // the mirror U tile's row of (step T-1-q, plane np-1-p, lane nj-1-lane) at q = 0
+                    po[u] = a.out + d.ubase + (long)(T - 1) * SB + (long)(np - 1 - pp) * nj + (nj - 1 - lc);
+                }
+            }
+            const long dq = OUT == 1 ? (a.mirror ? -1 : 1) : -SB;  // pointer step per q
+            uint64_t *hki = reinterpret_cast<uint64_t *>(a.hk + (long)max(d.tk, 0) * a.hk_stride) + lane;
+            uint64_t *hji = reinterpret_cast<uint64_t *>(a.hj + (long)max(d.tj, 0) * a.hj_stride) + min(lane, P - 1);
+            const bool rk = w == SW - 1 && kin && lane < nj, rj = w == 0 && jin && lane < np;
+            for (int s = S0; s <= T; s++) {
+                const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
+                const int q = s - 1;
+                if (q >= 0 && q < T) {
+                    const double *rs = res + (q & 1) * P * 64;
+#pragma unroll
+                    for (int u = 0; u < PS; u++) {
+                        const double v = rs[min(w + u * SW, P - 1) * 64 + lane];
+                        if ((unsigned)(q - vlo[u]) < (unsigned)nx) po[u][dq * q] = v;
+                    }
+                    // re-arm the consumed hand-off inputs of step q
+                    if (rk && (unsigned)(q - lane) < (unsigned)nx) hki[(long)q * 64] = TRI_SENTINEL;
+                    if (rj && (unsigned)(q - lane) < (unsigned)nx) hji[(long)q * P] = TRI_SENTINEL;
+                }
+                if (trs && w == 0 && s >= 0 && s < T) ts[8 * s + 5] = __builtin_amdgcn_s_memtime() - w0;
+                line_barrier();
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launch
+// ---------------------------------------------------------------------------
+constexpr int LINE_CW = 2, LINE_NL = 4, LINE_D = 10, LINE_DH = 3, LINE_SW = 2;
+
+template <int NA, bool RHS_NAT, int OUT, bool TRACE>
+static int launch_line_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)
+{
+    auto kern = k_line<LINE_P, NA, RHS_NAT, OUT, LINE_CW, LINE_NL, LINE_D, LINE_DH, LINE_SW, TRACE>;
+    static int attr = 0;
+    if (lds > attr) {
+        LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        attr = lds;
+    }
+    const int grid = std::min(ls.ntiles, c->num_cus);
+    kern<<<grid, 64 * (LINE_CW + LINE_NL + 1 + LINE_SW), lds, c->stream>>>(g);
+    ls.base += (unsigned long long)ls.ntiles + grid;
+    LSSP_HIP(hipGetLastError());
+    return LSSP_AMD_OK;
+}
+
+template <int NA, bool RHS_NAT, int OUT>
+static int launch_line_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a)
+{
+    using SL = LineSlot<LINE_P, NA, RHS_NAT>;
+    const int lds = (LINE_D + 1) * SL::BYTES + 2 * LINE_P * 64 * 8 + 16;
+    if (lds > 160 * 1024) return LSSP_AMD_EUNSUPPORTED;
+    // diagnostics only: LSSP_AMD_LINE_TRACE=path[:tile] appends one JSON line per sweep
+    static const char *trp = getenv("LSSP_AMD_LINE_TRACE");
+    if (!trp) return launch_line_k<NA, RHS_NAT, OUT, false>(c, ls, a, lds);
+    LineArgs g = a;
+    const size_t tn = 8 * (size_t)ls.ntiles + 8 * (size_t)ls.tmax + 64;
+    const char *colon = strrchr(trp, ':');
+    g.ttile = colon ? atoi(colon + 1) : ls.ntiles / 2;
+    LSSP_HIP(hipMalloc(&g.trace, sizeof(unsigned long long) * tn));
+    LSSP_HIP(hipMemsetAsync(g.trace, 0, sizeof(unsigned long long) * tn, c->stream));
+    const int grid = std::min(ls.ntiles, c->num_cus);
+    LSSP_TRY((launch_line_k<NA, RHS_NAT, OUT, true>(c, ls, g, lds)));
+    std::vector<unsigned long long> h(tn);
+    LSSP_HIP(hipMemcpyAsync(h.data(), g.trace, sizeof(unsigned long long) * tn, hipMemcpyDeviceToHost, c->stream));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    (void)hipFree(g.trace);
+    std::string path(trp, colon ? colon - trp : strlen(trp));
+    FILE *f = fopen(path.c_str(), "a");
+    if (f) {
+        fprintf(f, "{\"mirror\": %d, \"ntiles\": %d, \"W\": %d, \"ttile\": %d, \"T\": %d, \"grid\": %d, \"data\": [",
+                a.mirror, ls.ntiles, (ls.ny + 63) / 64, g.ttile, ls.h_tiles[g.ttile].T, grid);
+        for (size_t i = 0; i < tn; i++) fprintf(f, "%s%llu", i ? ", " : "", h[i]);
+        fprintf(f, "]}\n");
+        fclose(f);
+    }
+    return LSSP_AMD_OK;
+}
+
+// which: 0 = L sweep, 1 = U sweep.  The rhs is natural order unless u_in (the
+// U rhs stream); the output goes to out (natural order) or, when out_u, to the
+// U rhs stream (the L sweep of an apply)
+static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const double *rhs, bool u_in, double *out,
+                       bool out_u)
+{
+    const LineSweep &ls = which ? li.U : li.L;
+    LineArgs a{};
+    a.nx = ls.nx;
+    a.ny = ls.ny;
+    a.ntiles = ls.ntiles;
+    a.n = (long)ls.nx * ls.ny * ls.nz;
+    a.tiles = ls.d_tiles;
+    a.coef = ls.d_coef;
+    a.rhs = u_in ? li.d_ustream : rhs;
+    a.out = out_u ? li.d_ustream : out;
+    a.hk = li.d_hk;
+    a.hj = li.d_hj;
+    a.hk_stride = li.hk_stride;
+    a.hj_stride = li.hj_stride;
+    a.claim = ls.d_claim;
+    a.base = ls.base;
+    a.mirror = which;
+    a.err = c->d_err;
+    if (u_in) return launch_line_t<4, false, 1>(c, ls, a);
+    if (out_u) return ls.NA == 3 ? launch_line_t<3, true, 2>(c, ls, a) : launch_line_t<4, true, 2>(c, ls, a);
+    return ls.NA == 3 ? launch_line_t<3, true, 1>(c, ls, a) : launch_line_t<4, true, 1>(c, ls, a);
+}
+
+int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs)
+{
+    LSSP_TRY(launch_line(c, li, 0, rhs, false, nullptr, true));
+    return launch_line(c, li, 1, nullptr, true, x, false);
+}
+
+int launch_line_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs)
+{
+    return launch_line(c, li, which, rhs, false, x, false);
+}
+
+}  // namespace lssp_amd

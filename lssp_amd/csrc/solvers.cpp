@@ -104,6 +104,9 @@ struct Run {
         LSSP_HIP(hipStreamSynchronize(c->stream));
         if (e) {
             LSSP_HIP(hipMemset(c->d_err, 0, sizeof(int)));
+            // a line sweep that gave up mid-way leaves hand-off entries written
+            if (M && M->line.ntiles) LSSP_TRY(line_rearm(c, const_cast<lssp_amd_ilu *>(M)->line));
+            LSSP_HIP(hipStreamSynchronize(c->stream));
             return LSSP_AMD_ETIMEOUT;
         }
         return LSSP_AMD_OK;

@@ -912,6 +912,7 @@ __global__ __launch_bounds__(256) void k_gather4(double *dst, const double *src,
 // sweep's store wave (timing experiments).
 int launch_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const double *rhs)
 {
+    if (M->line.ntiles) return launch_line_apply(c, M->line, x, rhs);
     if (c->tri_mode == 9 && M->lower.pk6_n > 0 && M->upper.pk6_n > 0) {
         const int n = M->n;
         if (!M->d_sh[0]) {

@@ -1,5 +1,6 @@
-"""The packet sweep's loader issues its loads from inline asm with explicit
-vmcnt waits (trisolve.hip k_tri_pk6).  Compile the device code for gfx950 and
+"""The packet sweep's loader (trisolve.hip k_tri_pk6) and the line sweep's
+poller (linesweep.hip k_line) issue loads from inline asm with explicit
+vmcnt waits.  Compile the device code for gfx950 and
 check, on the generated assembly, that no instruction touches a VGPR that is
 still the destination of an outstanding load, and that no instantiation spills
 (a spill of an in-flight register would store garbage).  CPU-only: hipcc
@@ -18,16 +19,25 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 
-@pytest.fixture(scope="module")
-def device_asm(tmp_path_factory):
+def _compile(tmp_path_factory, src):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
-    out = tmp_path_factory.mktemp("isa") / "kernels.s"
+    out = tmp_path_factory.mktemp("isa") / (src + ".s")
     cmd = [HIPCC, "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950",
            "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-S", "-x", "hip",
-           os.path.join(ROOT, "lssp_amd", "csrc", "trisolve.hip"), "-o", str(out)]
+           os.path.join(ROOT, "lssp_amd", "csrc", src), "-o", str(out)]
     subprocess.run(cmd, check=True, capture_output=True)
     return str(out)
+
+
+@pytest.fixture(scope="module")
+def device_asm(tmp_path_factory):
+    return _compile(tmp_path_factory, "trisolve.hip")
+
+
+@pytest.fixture(scope="module")
+def line_asm(tmp_path_factory):
+    return _compile(tmp_path_factory, "linesweep.hip")
 
 
 def _pk6_kernels(path):
@@ -52,3 +62,18 @@ def test_pk6_no_scratch(device_asm):
         assert m, name
         priv = int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", m.group(1)).group(1))
         assert priv == 0, (name, priv)
+
+
+def _line_kernels(path):
+    return sorted(set(re.findall(r"^(_ZN8lssp_amd6k_line\w+):", open(path).read(), re.M)))
+
+
+def test_line_instantiations_hazard_free_and_no_scratch(line_asm):
+    import check_vmcnt
+    names = _line_kernels(line_asm)
+    assert len(names) >= 3, names
+    text = open(line_asm).read()
+    for name in names:
+        assert check_vmcnt.check_loader(line_asm, name) == 0, name
+        m = re.search(r"\.amdhsa_kernel " + name + r"\n(.*?)\.end_amdhsa_kernel", text, re.S)
+        assert int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", m.group(1)).group(1)) == 0, name
