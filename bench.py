@@ -15,9 +15,8 @@ send/recv and dots with an RCCL all-gather; the preconditioner becomes
 block-Jacobi ILU(0) per slab (the reference's blk_size path).
 
 The roofline object describes the dominant operator, the ILU(0) apply
-(pc.solve: a permutation kernel, the two pipelined triangular sweeps
-k_tri_pk6, a permutation kernel -- rocprof attributes ~60% of a step to the
-sweeps); roofline_spmv describes the metric's SpMV kernel, y = A x
+(pc.solve: the two line sweeps k_line, L then U -- rocprof attributes ~75% of
+a step to them); roofline_spmv describes the metric's SpMV kernel, y = A x
 (lssp_mv_mxy).  Both are timed live with HIP events on the library's stream.
 traffic: HBM bytes per launch from rocprofv3 PMC counters (FETCH_SIZE x 2 on
 gfx950, + WRITE_SIZE), read from profiles/pmc_traffic.json when present.
@@ -46,10 +45,11 @@ def spmv_bytes(nnz: int, n: int) -> int:
 
 
 def ilu_apply_bytes(nnzL: int, nnzU: int, n: int) -> int:
-    """algorithmic bytes of one ILU apply: both factors in CSR (8 + 4 per entry,
-    4 per row pointer), rhs read, the L sweep's output written and read back by
-    the U sweep, x written"""
-    return 12 * (nnzL + nnzU) + 8 * (n + 1) + 8 * n * 4
+    """SURVEY 8(d) B_ilu = 12 (nnzL_strict + nnzU) + 40 n: the strict L entries
+    and all of U (8 + 4 per entry; L's unit diagonal is not stored), row
+    pointers, rhs read, the L sweep's output written and read back by the U
+    sweep, x written.  nnzL counts L's unit diagonal (one per row)."""
+    return 12 * (nnzL - n + nnzU) + 40 * n
 
 
 def pmc_traffic(kernel: str):
@@ -247,8 +247,8 @@ def main():
                      "ms_per_call": round(spmv_ms, 5)},
             "roofline": {"bound": "hbm", "achieved": round(apply_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(apply_gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("ilu_apply"),
-                         "kernel": "ILU(0) apply = k_gather4 (rhs to L order) + k_tri_pk6 (L) + k_tri_pk6 (U) + "
-                                   "k_gather4 (x to natural order); "
+                         "kernel": "ILU(0) apply = k_line (L sweep, rhs in natural order -> the U sweep's "
+                                   "rhs stream) + k_line (U sweep -> x in natural order); "
                                    "latency-bound: 2 x 646 dependent levels",
                          "bytes_per_launch": apply_b, "ms_per_launch": round(apply_ms, 5)},
             "roofline_spmv": {"bound": "hbm", "achieved": round(spmv_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

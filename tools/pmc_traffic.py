@@ -34,11 +34,14 @@ def main(fetch_dir, write_dir, out):
     res = {}
     for k in find("k_spmv3<0, 0>"):
         res["k_spmv3"] = int(2 * fe[k] + wr.get(k, 0))
+    line = find("k_line<")  # line sweeps: the apply is one L and one U launch
+    if line:
+        res["ilu_apply"] = int(sum(2 * fe[k] + wr.get(k, 0) for k in line))
     tri = find("k_tri_pk6")
     perm = find("k_perm")
     g4 = find("k_gather4")  # both permutations of an apply, one kernel: twice its median
     perm_b = 2 * sum(2 * fe[k] + wr.get(k, 0) for k in g4) if g4 else sum(2 * fe[k] + wr.get(k, 0) for k in perm)
-    if tri and (perm or g4):
+    if tri and (perm or g4) and not line:
         res["ilu_apply"] = int(perm_b + 2 * sum(2 * fe[k] + wr.get(k, 0) for k in tri) / max(1, len(tri)))
     res["_note"] = "HBM bytes per launch: 2 x FETCH_SIZE + WRITE_SIZE (rocprofv3 --pmc, medians over launches)"
     json.dump(res, open(out, "w"), indent=1)
