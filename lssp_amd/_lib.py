@@ -9,7 +9,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "liblssp_amd.so")
+# LSSP_AMD_LIB: another build of the same library (tuning experiments, tools/build_variant.sh)
+LIB_PATH = os.environ.get("LSSP_AMD_LIB") or os.path.join(HERE, "lib", "liblssp_amd.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "lssp_amd.h")
 
 _vp, _ci, _cd, _cl = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_long

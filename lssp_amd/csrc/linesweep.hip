@@ -347,17 +347,32 @@ struct LineArgs {
     // loader wait, loader issue, storer busy}
     unsigned long long *trace;
     int ttile;
+    int diag;  // LSSP_AMD_LINE_DIAG timing experiments (wrong results when != 0)
 };
 
 __device__ __forceinline__ void dma16(const void *g, unsigned lds)
 {
     asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
 }
+__device__ __forceinline__ void dma16_sc1(const void *g, unsigned lds)
+{
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off sc1" ::"v"(g), "s"(lds) : "memory", "m0");
+}
 __device__ __forceinline__ void dma4(const void *g, unsigned lds)
 {
     asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
 }
-__device__ __forceinline__ void line_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// LDS drained, then the workgroup barrier.  The wait is the builtin (not asm),
+// so the compiler's wait-count tracking knows every LDS load is complete after
+// it and does not re-wait for loads issued before the barrier; the empty asm
+// statements keep memory operations from moving across.
+__device__ __forceinline__ void line_barrier()
+{
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // gfx9: lgkmcnt(0), vmcnt/expcnt unconstrained
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
 
 __device__ __forceinline__ uint64_t line_ld_agent(const double *p)
 {
@@ -370,12 +385,46 @@ __device__ __forceinline__ void line_st_agent(double *p, double v)
     __hip_atomic_store(reinterpret_cast<uint64_t *>(p), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// per lane: bit lane of m ? t : f, as two v_cndmask (the compiler cannot turn an
+// asm select into a branch around the division that produced t)
+__device__ __forceinline__ double sel_lanes(uint64_t m, double t, double f)
+{
+    const long long tb = __double_as_longlong(t), fb = __double_as_longlong(f);
+    int lo, hi;
+    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(lo) : "v"((int)fb), "v"((int)tb), "s"(m));
+    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(hi) : "v"((int)(fb >> 32)), "v"((int)(tb >> 32)), "s"(m));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// a published value never carries the flag pattern
+__device__ __forceinline__ uint64_t canon_bits(double v)
+{
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    return b == TRI_SENTINEL ? 0x7FF8000000000000ull : b;
+}
+typedef unsigned int line_v2u __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ line_v2u split64(uint64_t b)
+{
+    line_v2u d;
+    d.x = (unsigned)b;
+    d.y = (unsigned)(b >> 32);
+    return d;
+}
+
 __device__ __forceinline__ double dpp_shr1(double v, double old)
 {
     const long long b = __double_as_longlong(v), o = __double_as_longlong(old);
     const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, 0x138, 0xf, 0xf, false);
     const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), 0x138, 0xf, 0xf, false);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F &&f)
+{
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>());
+        static_for<I + 1, N>(f);
+    }
 }
 
 // slot layout (bytes): the step's coefficient block, its rhs, the hand-off inputs
@@ -390,6 +439,15 @@ struct LineSlot {
     static constexpr int JFIN = KFIN + 512;                                  // double[P]
     static constexpr int BYTES = (JFIN + 8 * P + 15) & ~15;
 };
+
+// LDS after the slot ring: the compute results of the last RS steps
+// ([RS][P][64] doubles: the next compute wave's k-input, and the storers'
+// source -- natural-order output is written in 8-step runs per line, so it
+// keeps two 8-step blocks), the claimed tile, the poller's DMA sink
+template <int OUT>
+constexpr int line_rs() { return OUT == 1 ? 16 : 2; }
+template <int P, int NA, bool RHS_NAT, int OUT, int D>
+constexpr int line_lds_bytes() { return (D + 1) * LineSlot<P, NA, RHS_NAT>::BYTES + line_rs<OUT>() * P * 64 * 8 + 16 + 512; }
 
 // P planes per tile, NA coefficient components (3: unit L, 4: with diagonal),
 // RHS_NAT: the rhs is read in natural order (else from the U rhs stream), CW
@@ -412,8 +470,9 @@ __global__ __launch_bounds__(64 * (CW + NL + 1 + SW)) void k_line(LineArgs a)
     static_assert((D - LA) * KPER <= 63 && 2 * (DH - 1) <= 63, "vmcnt range");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char *ring = smem;
-    double *res = reinterpret_cast<double *>(smem + R * SL::BYTES);  // [2][P][64]
-    int *s_tile = reinterpret_cast<int *>(res + 2 * P * 64);
+    constexpr int RS = line_rs<OUT>();
+    double *res = reinterpret_cast<double *>(smem + R * SL::BYTES);  // [RS][P][64]
+    int *s_tile = reinterpret_cast<int *>(res + RS * P * 64);
     const unsigned lds0 = (unsigned)(uintptr_t)smem;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -476,18 +535,26 @@ __global__ __launch_bounds__(64 * (CW + NL + 1 + SW)) void k_line(LineArgs a)
 #pragma unroll
             for (int u = 0; u < PC; u++) xc[u] = 0.0;
             // hand-off outputs, stored here (sc1) as soon as computed: this wave
-            // never waits on its VMEM queue, so the stores cost it nothing
-            double *hko = a.hk + (long)t * a.hk_stride + (long)(1 - np) * 64 + lane;  // + q*64
-            double *hjo = a.hj + (long)t * a.hj_stride + (long)(1 - nj) * P;          // + q*P + p
+            // never waits on its VMEM queue, so the stores cost it nothing.  Buffer
+            // stores: a lane with nothing to store gets an out-of-range offset and
+            // its store is dropped, so the step has no branch.
+            const __amdgpu_buffer_rsrc_t hko =
+                __builtin_amdgcn_make_buffer_rsrc(a.hk + (long)t * a.hk_stride, 0, (int)(a.hk_stride * 8), 0x00020000);
+            const __amdgpu_buffer_rsrc_t hjo =
+                __builtin_amdgcn_make_buffer_rsrc(a.hj + (long)t * a.hj_stride, 0, (int)(a.hj_stride * 8), 0x00020000);
+            constexpr int OOB = 0x7ffffff0;
             auto body = [&](int s, In &cur, In &nxt) {
                 if (TRACE && lane == 0 && wave == 0 && s == 0) a.trace[8 * t + 1] = __builtin_amdgcn_s_memrealtime();
-                if (trs && s >= 0 && s < T) ts[8 * s] = __builtin_amdgcn_s_memtime();
+                if (trs && wave == 0 && s >= 0 && s < T) ts[8 * s] = __builtin_amdgcn_s_memtime();
                 if (s == -1) load(0, nxt);
                 if (s >= 0 && s < T) {
                     const char *slot = ring + (s % R) * SL::BYTES;
                     const double kx = wave == 0 ? reinterpret_cast<const double *>(slot + SL::KFIN)[lane]
-                                                : res[((s - 1) & 1) * P * 64 + (p0 - 1) * 64 + lane];
+                                                : res[((s - 1) & (RS - 1)) * P * 64 + (p0 - 1) * 64 + lane];
                     if (s + 1 < T) load(s + 1, nxt);
+                    // every lane computes every plane; rows that do not exist at this
+                    // step keep their old value (a lane-mask select, not a branch)
+                    double xn[PC];
 #pragma unroll
                     for (int u = PC - 1; u >= 0; u--) {
                         const int p = p0 + u;
@@ -499,14 +566,21 @@ __global__ __launch_bounds__(64 * (CW + NL + 1 + SW)) void k_line(LineArgs a)
                         v = v - cur.cj[u] * xj;
                         v = v - cur.ci[u] * xc[u];
                         if constexpr (NA == 4) v = v / cur.dg[u];
-                        xc[u] = valid ? v : xc[u];
-                        if (kout && p == np - 1 && valid) line_st_agent(hko + (long)s * 64, xc[u]);
-                        if (jout && p < np && lane == nj - 1 && valid) line_st_agent(hjo + (long)s * P + p, xc[u]);
+                        xn[u] = sel_lanes(__builtin_amdgcn_ballot_w64(valid), v, xc[u]);
+                        const uint64_t b = canon_bits(xn[u]);
+                        const int ko = kout && p == np - 1 && valid ? ((s + 1 - np) * 64 + lane) * 8 : OOB;
+                        const int jo = jout && p < np && lane == nj - 1 && valid ? ((s + 1 - nj) * P + p) * 8 : OOB;
+                        __builtin_amdgcn_raw_buffer_store_b64(split64(b), hko, ko, 0, 16);  // sc1
+                        __builtin_amdgcn_raw_buffer_store_b64(split64(b), hjo, jo, 0, 16);
                     }
+                    if (trs && wave == 0 && s >= 0 && s < T) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
 #pragma unroll
-                    for (int u = 0; u < PC; u++) res[((s & 1) * P + p0 + u) * 64 + lane] = xc[u];
+                    for (int u = 0; u < PC; u++) {
+                        xc[u] = xn[u];
+                        res[((s & (RS - 1)) * P + p0 + u) * 64 + lane] = xc[u];
+                    }
                 }
-                if (trs && s >= 0 && s < T) ts[8 * s + 1] = __builtin_amdgcn_s_memtime();
+                if (trs && s >= 0 && s < T) ts[8 * s + (wave == 0 ? 1 : 7)] = __builtin_amdgcn_s_memtime();
                 line_barrier();
             };
             In A, B;  // step s uses the set loaded at step s-1: even steps A, odd steps B
@@ -553,7 +627,7 @@ __global__ __launch_bounds__(64 * (CW + NL + 1 + SW)) void k_line(LineArgs a)
             };
             for (int s = S0; s <= T; s++) {
                 const unsigned long long i0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
-                issue(s + D);  // dummies past T keep the wait counts exact
+                if (!(a.diag & 2)) issue(s + D);  // dummies past T keep the wait counts exact
                 const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
                 // steps s+LA+1 .. s+D were issued after step s+LA's
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - LA) * KPER) : "memory");
@@ -566,41 +640,53 @@ __global__ __launch_bounds__(64 * (CW + NL + 1 + SW)) void k_line(LineArgs a)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else if (wave == CW + NL) {
             // ---------------- poller ----------------
-            // 8-byte sc1 loads into a ring of DH register sets (set = step mod
-            // DH), issued from inline asm with exact vmcnt waits (the compiler
-            // does not see these loads; tests/test_isa_vmcnt.py checks that no
-            // instruction touches a register still in flight).  At step s the
-            // loads for the k-input of step s+DH and the j-input of step s+DH+1
-            // are issued; those of the k-input of step s+1 and the j-input of
-            // step s+2 land (the compute reads k at its step start, j one step
-            // earlier with the coefficients).
+            // LDS-DMA sc1 reads of the hand-off inputs straight into their ring
+            // slots, DH steps ahead: at step s the k-input of step s+DH (32 lanes x
+            // 16 B) and the j-input of step s+DH+1 (P/2 lanes x 16 B) are issued,
+            // and those of steps s+1 (k) and s+2 (j) -- issued DH-1 steps ago -- are
+            // waited for and checked (the compute reads k at its step start, j one
+            // step earlier with the coefficients).  DMA loads have no register
+            // destination, so the ring depth is bounded only by the slot ring.
+            // A tile without a k (j) input gets +0.0 there: its coefficient is
+            // +0.0 and +0.0 * +0.0 leaves the row's sum bit for bit unchanged.
             const double *hk = a.hk + (long)max(d.tk, 0) * a.hk_stride;
             const double *hj = a.hj + (long)max(d.tj, 0) * a.hj_stride;
-            auto kval = [&](int q) { return kin && q >= 0 && q < T && lane < nj && q - lane >= 0 && q - lane < nx; };
-            auto jval = [&](int q) { return jin && q >= 0 && q < T && lane < np && q - lane >= 0 && q - lane < nx; };
-            auto kaddr = [&](int q) { return hk + (long)min(max(q, 0), a.hk_stride / 64 - 1) * 64 + lane; };
-            auto jaddr = [&](int q) { return hj + (long)min(max(q, 0), a.hk_stride / 64 - 1) * P + min(lane, P - 1); };
-            uint64_t kb[DH], jb[DH];
-#pragma unroll
-            for (int u = 0; u < DH; u++) kb[u] = jb[u] = 0;
+            const int qmax = (int)(a.hk_stride / 64) - 1;
+            auto kval = [&](int q) { return q >= 0 && q < T && lane < nj && q - lane >= 0 && q - lane < nx; };
+            auto jval = [&](int q) { return q >= 0 && q < T && lane < np && q - lane >= 0 && q - lane < nx; };
+            const unsigned sink = lds0 + (unsigned)(R * SL::BYTES + RS * P * 64 * 8 + 16);
+            auto issue = [&](int q) {
+                // k-input of step q (lanes 0..31), j-input of step q+1 (lanes 0..P/2-1)
+                const char *kp = reinterpret_cast<const char *>(hk + (long)min(max(q, 0), qmax) * 64) + lane * 16;
+                const char *jp = reinterpret_cast<const char *>(hj + (long)min(max(q + 1, 0), qmax) * P) + lane * 16;
+                const unsigned ks = kin ? lds0 + (unsigned)((((q % R) + R) % R) * SL::BYTES + SL::KFIN) : sink;
+                const unsigned js = jin ? lds0 + (unsigned)(((((q + 1) % R) + R) % R) * SL::BYTES + SL::JFIN) : sink;
+                if (lane < 32) dma16_sc1(kp, ks);
+                if (lane < P / 2) dma16_sc1(jp, js);
+            };
+            if (!kin || !jin) {
+                for (int q = 0; q < R; q++) {
+                    if (!kin) reinterpret_cast<double *>(ring + q * SL::BYTES + SL::KFIN)[lane] = 0.0;
+                    if (!jin && lane < P) reinterpret_cast<double *>(ring + q * SL::BYTES + SL::JFIN)[lane] = 0.0;
+                }
+            }
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             unsigned polls = 0;
-            auto pstep = [&](int s, auto U) {
-                constexpr int ui = decltype(U)::value;  // s = ui (mod DH): set issued at step s
-                constexpr int ul = (ui + 1) % DH;       // set issued at step s+1-DH: k(s+1), j(s+2)
-                // every pstep issues and waits (past T too), so the load queue has
+            for (int s = S0; s <= T; s++) {
+                // every step issues and waits (past T too), so the load queue has
                 // one shape on every path; only the slot work and the barrier stop at T
                 const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
-                asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(kb[ui]) : "v"(kaddr(s + DH)) : "memory");
-                asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(jb[ui]) : "v"(jaddr(s + DH + 1)) : "memory");
-                // the sets of steps s+2-DH .. s (DH-1 steps, 2 loads each) are younger
-                asm volatile("s_waitcnt vmcnt(%2)" : "+v"(kb[ul]), "+v"(jb[ul]) : "n"(2 * (DH - 1)) : "memory");
-                if (s > T) return;
+                issue(s + DH);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (DH - 1)) : "memory");
+                if (s > T) break;
                 const int qk = s + 1, qj = s + 2;
-                const bool vk = kval(qk), vj = jval(qj);
-                uint64_t kv = vk ? kb[ul] : 0, jv = vj ? jb[ul] : 0;
-                const bool bad = (vk && kv == TRI_SENTINEL) || (vj && jv == TRI_SENTINEL);
-                if (__any(bad)) {
+                double *kslot = reinterpret_cast<double *>(ring + (qk % R) * SL::BYTES + SL::KFIN) + lane;
+                double *jslot = reinterpret_cast<double *>(ring + (qj % R) * SL::BYTES + SL::JFIN) + min(lane, P - 1);
+                const bool vk = kin && kval(qk), vj = jin && jval(qj);
+                const uint64_t kv = vk ? (uint64_t)__double_as_longlong(*kslot) : 0;
+                const uint64_t jv = vj ? (uint64_t)__double_as_longlong(*jslot) : 0;
+                const bool bk = vk && kv == TRI_SENTINEL, bj = vj && jv == TRI_SENTINEL;
+                if (__any(!(a.diag & 8) && (bk || bj))) {
                     // resync episode: the producer was not done when these polls were
                     // issued, so probably neither for the polls still in flight.
                     // Drain them, wait for these values and for the furthest step in
@@ -619,36 +705,14 @@ __global__ __launch_bounds__(64 * (CW + NL + 1 + SW)) void k_line(LineArgs a)
                             __builtin_amdgcn_s_sleep(1);
                         }
                     };
-                    if (vk && kv == TRI_SENTINEL) kv = spin(hk + (long)qk * 64 + lane);
-                    if (vj && jv == TRI_SENTINEL) jv = spin(hj + (long)qj * P + lane);
-                    if (kval(s + DH)) (void)spin(hk + (long)(s + DH) * 64 + lane);
-                    if (jval(s + DH + 1)) (void)spin(hj + (long)(s + DH + 1) * P + lane);
-#pragma unroll
-                    for (int k = 2; k <= DH; k++) {  // the sets issued at steps s+k-DH
-                        asm volatile("global_load_dwordx2 %0, %1, off sc1"
-                                     : "=v"(kb[(ui + k) % DH])
-                                     : "v"(kaddr(s + k))
-                                     : "memory");
-                        asm volatile("global_load_dwordx2 %0, %1, off sc1"
-                                     : "=v"(jb[(ui + k) % DH])
-                                     : "v"(jaddr(s + k + 1))
-                                     : "memory");
-                    }
+                    if (bk) *kslot = __longlong_as_double((long long)spin(hk + (long)qk * 64 + lane));
+                    if (bj) *jslot = __longlong_as_double((long long)spin(hj + (long)qj * P + lane));
+                    if (kin && kval(s + DH)) (void)spin(hk + (long)(s + DH) * 64 + lane);
+                    if (jin && jval(s + DH + 1)) (void)spin(hj + (long)(s + DH + 1) * P + lane);
+                    for (int k = 2; k <= DH; k++) issue(s + k);  // the polls issued at steps s+k-DH
                 }
-                if (qk < T) reinterpret_cast<double *>(ring + (qk % R) * SL::BYTES + SL::KFIN)[lane] =
-                    __longlong_as_double((long long)kv);
-                if (lane < P && qj < T)
-                    reinterpret_cast<double *>(ring + (qj % R) * SL::BYTES + SL::JFIN)[lane] =
-                        __longlong_as_double((long long)jv);
                 if (trs && s >= 0 && s < T) ts[8 * s + 2] = __builtin_amdgcn_s_memtime() - w0;
                 line_barrier();
-            };
-            static_assert(DH == 3 || DH == 4, "the poller's register ring is unrolled by DH");
-            for (int s = S0; s <= T; s += DH) {
-                pstep(s, std::integral_constant<int, 0>());
-                pstep(s + 1, std::integral_constant<int, 1>());
-                pstep(s + 2, std::integral_constant<int, 2>());
-                if constexpr (DH == 4) pstep(s + 3, std::integral_constant<int, 3 % DH>());
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (TRACE) {
@@ -656,46 +720,76 @@ __global__ __launch_bounds__(64 * (CW + NL + 1 + SW)) void k_line(LineArgs a)
                 if (lane == 0) a.trace[8 * t + 3] = polls;
             }
         } else {
-            // ---------------- storers: bulk results of step s-1, re-arms ----------------
-            // storer w writes planes w, w+SW, ...; storer 0 re-arms the consumed
-            // j-inputs, storer SW-1 the k-inputs.  Pointers advance by a constant
-            // per step.
+            // ---------------- storers: results, re-arms ----------------
+            // OUT 2 (the U sweep's rhs stream, contiguous per plane and step):
+            // storer w writes planes w, w+SW, ... of step s-1.  OUT 1 (natural
+            // order): the results of an 8-step block are written during the next
+            // 8 steps as runs -- 8 consecutive rows of one line (one lane, one
+            // plane) go to 8 consecutive lanes, so a store touches 8 runs instead
+            // of 64 lines.  Storer 0 re-arms the consumed j-inputs, storer SW-1
+            // the k-inputs.
             const int w = wave - (CW + NL + 1);
-            constexpr int PS = (P + SW - 1) / SW;
-            double *po[PS];
-            int vlo[PS];
-#pragma unroll
-            for (int u = 0; u < PS; u++) {
-                const int p = w + u * SW, pp = min(p, np - 1);
-                vlo[u] = p < np && lane < nj ? lane + p : 1 << 30;  // valid iff 0 <= q - vlo < nx
-                if constexpr (OUT == 1) {
-                    // natural row of (i = q - lane - p) at q = 0, moving by +-1 per step
-                    po[u] = a.out + (a.mirror ? nb(pp, lc) + lane + pp : nb(pp, lc) - lane - pp);
-                } else {
-                    // the mirror U tile's row of (step T-1-q, plane np-1-p, lane nj-1-lane) at q = 0
-                    po[u] = a.out + d.ubase + (long)(T - 1) * SB + (long)(np - 1 - pp) * nj + (nj - 1 - lc);
-                }
-            }
-            const long dq = OUT == 1 ? (a.mirror ? -1 : 1) : -SB;  // pointer step per q
             uint64_t *hki = reinterpret_cast<uint64_t *>(a.hk + (long)max(d.tk, 0) * a.hk_stride) + lane;
             uint64_t *hji = reinterpret_cast<uint64_t *>(a.hj + (long)max(d.tj, 0) * a.hj_stride) + min(lane, P - 1);
             const bool rk = w == SW - 1 && kin && lane < nj, rj = w == 0 && jin && lane < np;
-            for (int s = S0; s <= T; s++) {
-                const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
-                const int q = s - 1;
-                if (q >= 0 && q < T) {
-                    const double *rs = res + (q & 1) * P * 64;
+            auto rearm = [&](int q) {
+                if (rk && (unsigned)(q - lane) < (unsigned)nx) hki[(long)q * 64] = TRI_SENTINEL;
+                if (rj && (unsigned)(q - lane) < (unsigned)nx) hji[(long)q * P] = TRI_SENTINEL;
+            };
+            if constexpr (OUT == 1) {
+                // block B (steps 8B .. 8B+7) is written during steps 8B+8 .. 8B+15,
+                // slice k = s - 8B - 8 at step s: values k*NV + w*NV/SW + it*64 + lane
+                constexpr int NV = P * 64;  // values per slice (a block holds 8 * NV)
+                static_assert(NV % (64 * SW) == 0 && RS == 16, "slices");
+                auto slice = [&](int s) {
+                    const int B = (s >> 3) - 1, k = s & 7;
+                    if (B < 0) return;
 #pragma unroll
-                    for (int u = 0; u < PS; u++) {
-                        const double v = rs[min(w + u * SW, P - 1) * 64 + lane];
-                        if ((unsigned)(q - vlo[u]) < (unsigned)nx) po[u][dq * q] = v;
+                    for (int it = 0; it < NV / (64 * SW); it++) {
+                        const int v = k * NV + w * (NV / SW) + it * 64 + lane;
+                        const int r = v >> 3, m = v & 7;  // run r = (plane, line), step 8B+m
+                        const int p = r >> 6, l = r & 63, q = 8 * B + m;
+                        const int i = q - l - p;
+                        const double x = res[((q & (RS - 1)) * P + p) * 64 + l];
+                        if (!(a.diag & 1) && p < np && l < nj && (unsigned)i < (unsigned)nx)
+                            a.out[a.mirror ? nb(p, l) - i : nb(p, l) + i] = x;
                     }
-                    // re-arm the consumed hand-off inputs of step q
-                    if (rk && (unsigned)(q - lane) < (unsigned)nx) hki[(long)q * 64] = TRI_SENTINEL;
-                    if (rj && (unsigned)(q - lane) < (unsigned)nx) hji[(long)q * P] = TRI_SENTINEL;
+                };
+                for (int s = S0; s <= T; s++) {
+                    const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
+                    if (s >= 0) slice(s);
+                    if (s >= 1 && s <= T) rearm(s - 1);
+                    if (trs && w == 0 && s >= 0 && s < T) ts[8 * s + 5] = __builtin_amdgcn_s_memtime() - w0;
+                    line_barrier();
                 }
-                if (trs && w == 0 && s >= 0 && s < T) ts[8 * s + 5] = __builtin_amdgcn_s_memtime() - w0;
-                line_barrier();
+                // the last blocks' remaining slices (every compute result is in LDS)
+                for (int s = T + 1; s < 8 * ((T >> 3) + 2); s++) slice(s);
+            } else {
+                constexpr int PS = (P + SW - 1) / SW;
+                double *po[PS];
+                int vlo[PS];
+#pragma unroll
+                for (int u = 0; u < PS; u++) {
+                    const int p = w + u * SW, pp = min(p, np - 1);
+                    vlo[u] = p < np && lane < nj ? lane + p : 1 << 30;  // valid iff 0 <= q - vlo < nx
+                    // the mirror U tile's row of (step T-1-q, plane np-1-p, lane nj-1-lane) at q = 0
+                    po[u] = a.out + d.ubase + (long)(T - 1) * SB + (long)(np - 1 - pp) * nj + (nj - 1 - lc);
+                }
+                for (int s = S0; s <= T; s++) {
+                    const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
+                    const int q = s - 1;
+                    if (q >= 0 && q < T) {
+                        const double *rs = res + (q & (RS - 1)) * P * 64;
+#pragma unroll
+                        for (int u = 0; u < PS; u++) {
+                            const double v = rs[min(w + u * SW, P - 1) * 64 + lane];
+                            if (!(a.diag & 1) && (unsigned)(q - vlo[u]) < (unsigned)nx) po[u][-SB * q] = v;
+                        }
+                        rearm(q);
+                    }
+                    if (trs && w == 0 && s >= 0 && s < T) ts[8 * s + 5] = __builtin_amdgcn_s_memtime() - w0;
+                    line_barrier();
+                }
             }
         }
     }
@@ -704,7 +798,12 @@ __global__ __launch_bounds__(64 * (CW + NL + 1 + SW)) void k_line(LineArgs a)
 // ---------------------------------------------------------------------------
 // launch
 // ---------------------------------------------------------------------------
-constexpr int LINE_CW = 2, LINE_NL = 4, LINE_D = 10, LINE_DH = 3, LINE_SW = 2;
+#ifndef LINE_DH_OVERRIDE
+constexpr int LINE_DH = 3;
+#else
+constexpr int LINE_DH = LINE_DH_OVERRIDE;
+#endif
+constexpr int LINE_CW = 2, LINE_NL = 4, LINE_D = 10, LINE_SW = 2;
 
 template <int NA, bool RHS_NAT, int OUT, bool TRACE>
 static int launch_line_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)
@@ -726,7 +825,7 @@ template <int NA, bool RHS_NAT, int OUT>
 static int launch_line_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a)
 {
     using SL = LineSlot<LINE_P, NA, RHS_NAT>;
-    const int lds = (LINE_D + 1) * SL::BYTES + 2 * LINE_P * 64 * 8 + 16;
+    const int lds = line_lds_bytes<LINE_P, NA, RHS_NAT, OUT, LINE_D>();
     if (lds > 160 * 1024) return LSSP_AMD_EUNSUPPORTED;
     // diagnostics only: LSSP_AMD_LINE_TRACE=path[:tile] appends one JSON line per sweep
     static const char *trp = getenv("LSSP_AMD_LINE_TRACE");
@@ -779,6 +878,10 @@ static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const doub
     a.base = ls.base;
     a.mirror = which;
     a.err = c->d_err;
+    {
+        const char *dg = getenv("LSSP_AMD_LINE_DIAG");
+        a.diag = dg ? atoi(dg) : 0;
+    }
     if (u_in) return launch_line_t<4, false, 1>(c, ls, a);
     if (out_u) return ls.NA == 3 ? launch_line_t<3, true, 2>(c, ls, a) : launch_line_t<4, true, 2>(c, ls, a);
     return ls.NA == 3 ? launch_line_t<3, true, 1>(c, ls, a) : launch_line_t<4, true, 1>(c, ls, a);

@@ -54,6 +54,10 @@ def summarise(rec):
     print(f"  tile {rec['ttile']}: step period median {np.median(per):.0f} clk (mean {per.mean():.0f}), "
           f"busy (median clk): compute {np.median(comp):.0f}, poller {med(2):.0f}, loader wait {med(3):.0f}, "
           f"loader issue {med(4):.0f}, storer {med(5):.0f}")
+    ar = steps[:, 6] - steps[:, 0]
+    w1 = steps[:, 7] - steps[:, 0]
+    print(f"  compute wave 0: arithmetic done at {np.median(ar):.0f} clk after the step start; "
+          f"wave 1 reaches the barrier at {np.median(w1):.0f} clk")
     lim = np.percentile(per, [10, 50, 90, 99])
     print(f"  step period p10/50/90/99: {lim.astype(int).tolist()}")
 
