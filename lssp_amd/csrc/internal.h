@@ -154,6 +154,7 @@ constexpr int PK4_PAD = -1 - 4096;  // v6 padding code: the value-ring slot past
 
 // ---- line sweeps of structured ILU(0) factors (linesweep.hip) ----------------
 constexpr int LINE_P = 4;  // planes per tile
+constexpr int LINE_M = 2;  // levels per barrier step (k_line2)
 enum { LT_KIN = 1, LT_JIN = 2, LT_KOUT = 4, LT_JOUT = 8 };
 struct LineGeom {
     int nx = 0, ny = 0, nz = 0;
@@ -171,7 +172,7 @@ struct LineTile {  // one workgroup's unit of work, in its sweep's coordinates
     long long ubase;  // L sweep: cbase of the mirror U tile
 };
 struct LineSweep {
-    int nx = 0, ny = 0, nz = 0, ntiles = 0, tmax = 0, NA = 3;
+    int nx = 0, ny = 0, nz = 0, ntiles = 0, tmax = 0, NA = 3, M = 1;
     long rows_total = 0;
     LineTile *d_tiles = nullptr;
     double *d_coef = nullptr;
