@@ -109,14 +109,6 @@ int lssp_amd_ctx_create(int device, lssp_amd_ctx **out)
     LSSP_HIP(hipMemset(c->d_err, 0, sizeof(int)));
     const char *m = getenv("LSSP_AMD_REDUCE");
     if (m && !strcmp(m, "serial")) c->reduce_mode = LSSP_AMD_REDUCE_SERIAL;
-    const char *tb = getenv("LSSP_AMD_TRI_BLOCKS_PER_CU");
-    if (tb) c->tri_blocks_per_cu = std::max(1, atoi(tb));
-    const char *tm = getenv("LSSP_AMD_TRI_MODE");
-    if (tm) c->tri_mode = atoi(tm);
-    const char *td = getenv("LSSP_AMD_TRI_DIAG");
-    if (td) c->tri_diag = atoi(td);
-    const char *tpp = getenv("LSSP_AMD_TRI_PIPE");
-    if (tpp) c->tri_pipe = atoi(tpp);
     *out = c;
     return LSSP_AMD_OK;
 }
@@ -230,7 +222,6 @@ int lssp_amd_mat_upload(lssp_amd_ctx *c, int nrows, int ncols, int nnz, const in
     M->nnz = nnz;
     M->n_global = nrows;
     int st = upload_csr(M, Ap, Aj, Ax);
-    if (st == LSSP_AMD_OK) st = plan_spmv_xt(M, Ap, Aj);
     if (st != LSSP_AMD_OK) {
         lssp_amd_mat_destroy(M);
         return st;
@@ -248,8 +239,6 @@ int lssp_amd_mat_destroy(lssp_amd_mat *M)
     if (M->Ax) (void)hipFree(M->Ax);
     if (M->d_send_idx) (void)hipFree(M->d_send_idx);
     if (M->d_send_buf) (void)hipFree(M->d_send_buf);
-    if (M->d_xt_lo) (void)hipFree(M->d_xt_lo);
-    if (M->d_xt_span) (void)hipFree(M->d_xt_span);
     delete M;
     return LSSP_AMD_OK;
 }

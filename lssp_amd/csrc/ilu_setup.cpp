@@ -562,8 +562,7 @@ void free_trisched(TriSched &t)
     if (t.cols) (void)hipFree(t.cols);
     if (t.vals) (void)hipFree(t.vals);
     if (t.diag) (void)hipFree(t.diag);
-    for (void *p : {(void *)t.bp_perm, (void *)t.bp_pos, (void *)t.pk_blk, (void *)t.pk_off, t.pk_data, (void *)t.pk_claim,
-                    (void *)t.pk6_blk, (void *)t.pk6_desc, (void *)t.pk6_idx, (void *)t.pk6_rec,
+    for (void *p : {(void *)t.bp_perm, (void *)t.bp_pos, (void *)t.pk6_blk, (void *)t.pk6_desc, (void *)t.pk6_idx, (void *)t.pk6_rec,
                     (void *)t.pk6_claim})
         if (p) (void)hipFree(p);
     t = TriSched();

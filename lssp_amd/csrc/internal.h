@@ -76,13 +76,7 @@ struct lssp_amd_ctx {
     lssp_amd_host_transport host{};  // host-staged transport (comm == nullptr, nranks > 1)
     double *d_gather = nullptr;  // [nranks][MAX_SLOTS]
     double *d_carry = nullptr;   // [MAX_SLOTS] serial mode: running sums of the ranks before this one
-    int tri_blocks_per_cu = 1;
-    // 0 sync-free + back-off, 1 one launch per level, 2 sync-free without
-    // back-off, 4 packet pipeline (v1 packets), 9 role-split packet sweeps
-    // through schedule-ordered shadows (default): trisolve.hip
-    int tri_mode = 9;
-    int tri_diag = 0;  // LSSP_AMD_TRI_DIAG timing experiments (wrong results when != 0)
-    int tri_pipe = 0;  // LSSP_AMD_TRI_PIPE: tri_mode 9 prefetch depths (trisolve.hip launch_pk6)
+    int tri_blocks_per_cu = 1;  // the sync-free sweep's grid (k_trisolve)
     // Krylov work vectors, kept across solves (no hipMalloc on the solve path)
     struct WsBuf {
         double *p;
@@ -105,11 +99,6 @@ struct lssp_amd_mat {
     int *d_send_idx = nullptr;
     double *d_send_buf = nullptr;
     int nsend = 0;
-    // x-tile SpMV plan (kernels.hip k_spmv_xt): per XT_ROWS-row block the first
-    // column and the column span; set only when the gathers are scattered and
-    // every block's span fits the LDS tile
-    int *d_xt_lo = nullptr, *d_xt_span = nullptr;
-    bool xt = false;
 };
 
 namespace lssp_amd {
@@ -128,25 +117,14 @@ struct TriSched {
     int bp_B = 0, bp_nb = 0, bp_nsteps = 0;
     int *bp_perm = nullptr;  // schedule position -> row
     int *bp_pos = nullptr;   // row -> schedule position (the inverse of bp_perm)
-    // packets v1 (tri_mode 4): each block's steps cut into packets of <=
-    // PK_ROWS rows / PK_BYTES bytes, laid out contiguously
-    int pk_n = 0;
-    int *pk_blk = nullptr;        // [nb+1] first packet of each block
-    int *pk_off = nullptr;        // [npk+1] packet offsets in 16-byte units
-    void *pk_data = nullptr;
-    mutable unsigned long long pk_base = 0;
-    unsigned long long *pk_claim = nullptr;
-    // packets v6 (tri_mode 9: schedule-ordered shadow vectors between sweeps)
+    // packets v6 (k_tri_pk6: schedule-ordered shadow vectors between sweeps)
     int pk6_n = 0, pk6_ep = 4, pk6_rows = 256;
     int *pk6_blk = nullptr, *pk6_desc = nullptr, *pk6_idx = nullptr;
     uint32_t *pk6_rec = nullptr;
     mutable unsigned long long pk6_base = 0;
     unsigned long long *pk6_claim = nullptr;
     std::vector<int> h_pos;  // L factor: row -> schedule position (for the U factor's build)
-    bool rhs_nat = false;    // L factor, v6: the loader gathers the rhs in natural order
 };
-constexpr int PK_ROWS = 256;
-constexpr int PK_BYTES = 12288;
 constexpr int PK3_ROWS = 256;    // v6: rows per packet = compute lanes = loader lanes
 constexpr int PK3_EXT = 2;       // v6: HBM x operands per packet row (on average)
 constexpr int PK3_CAP = 4096;    // v6: packets per block (descriptors staged in LDS)
@@ -154,7 +132,6 @@ constexpr int PK4_PAD = -1 - 4096;  // v6 padding code: the value-ring slot past
 
 // ---- line sweeps of structured ILU(0) factors (linesweep.hip) ----------------
 constexpr int LINE_P = 4;  // planes per tile
-constexpr int LINE_M = 2;  // levels per barrier step (k_line2)
 enum { LT_KIN = 1, LT_JIN = 2, LT_KOUT = 4, LT_JOUT = 8 };
 struct LineGeom {
     int nx = 0, ny = 0, nz = 0;
@@ -172,7 +149,7 @@ struct LineTile {  // one workgroup's unit of work, in its sweep's coordinates
     long long ubase;  // L sweep: cbase of the mirror U tile
 };
 struct LineSweep {
-    int nx = 0, ny = 0, nz = 0, ntiles = 0, tmax = 0, NA = 3, M = 1;
+    int nx = 0, ny = 0, nz = 0, ntiles = 0, tmax = 0, NA = 3;
     long rows_total = 0;
     LineTile *d_tiles = nullptr;
     double *d_coef = nullptr;
@@ -198,7 +175,7 @@ struct lssp_amd_ilu {
     std::vector<double> Lx, Ux;
     lssp_amd::TriSched lower, upper;
     double *d_cache = nullptr;  // L sweep output, kept all-sentinel between applies
-    // tri_mode 9: schedule-ordered shadows {L out, L out', U out, U out'} and the
+    // packet sweeps: schedule-ordered shadows {L out, L out', U out, U out'} and the
     // apply counter selecting the buffer pair (trisolve.hip launch_ilu_apply)
     mutable double *d_sh[4] = {nullptr, nullptr, nullptr, nullptr};
     mutable double *d_rperm = nullptr;  // the apply's rhs in L order
@@ -260,10 +237,6 @@ constexpr int BP_RING = 4096;  // LDS ring of recently computed values (32 KB)
 int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std::vector<int> &Tj,
                       const std::vector<double> &Tx, bool upper, const std::vector<int> &lev,
                       TriSched &t, const TriSched *prod = nullptr);
-int build_packets(int n, const std::vector<int> &perm, const std::vector<int> &rp,
-                  const std::vector<int> &cols, const std::vector<double> &vals,
-                  const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
-                  const std::vector<int> &blk_step, int nb, long B, TriSched &t);
 int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &pos, const std::vector<int> &rp,
                    const std::vector<int> &cols, const std::vector<double> &vals,
                    const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
@@ -271,8 +244,6 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
                    TriSched &t);
 int launch_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const double *rhs);
 int launch_pack(lssp_amd_ctx *c, const int *idx, const double *x, double *buf, int n);
-// x-tile SpMV plan for a host CSR (capi.cpp upload): decides and uploads
-int plan_spmv_xt(lssp_amd_mat *M, const int *Ap, const int *Aj);
 int launch_sum_ranks(lssp_amd_ctx *c, int nslot, const Fin &f);
 
 long num_chunks(long n);

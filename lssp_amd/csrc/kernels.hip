@@ -127,56 +127,15 @@ __device__ void finalize(const Fin &f, const double *s, double *scal, double *tr
     }
 }
 
-// level 2 (tree) + finalize
-__global__ __launch_bounds__(1024) void k_reduce2(const double *__restrict__ part, long pcap, long C,
-                                                  int nslot, double *sums, double *scal, double *trace,
-                                                  Fin f, int do_fin)
-{
-    __shared__ double wsum[MAX_SLOTS][16];
-    const int t = threadIdx.x;
-    for (int s = 0; s < nslot; s++) {
-        const double *p = part + s * pcap;
-        // lane t adds partials t, t + L2_LANES, ... in order onto 0.0; the
-        // loads of 32 of them are issued together before the in-order adds
-        // (one memory round trip per 32 partials instead of one per 8)
-        double a = 0.0;
-        for (long k0 = t; k0 < C; k0 += 32L * L2_LANES) {
-            double v[32];
-#pragma unroll
-            for (int u = 0; u < 32; u++) {
-                const long k = k0 + (long)u * L2_LANES;
-                v[u] = k < C ? p[k] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < 32; u++)
-                if (k0 + (long)u * L2_LANES < C) a += v[u];
-        }
-        a = wave_sum(a);
-        if ((t & 63) == 0) wsum[s][t >> 6] = a;
-    }
-    __syncthreads();
-    if (t == 0) {
-        double r[MAX_SLOTS] = {0, 0, 0, 0};
-        for (int s = 0; s < nslot; s++) {
-            double u[16];
-            for (int q = 0; q < 16; q++) u[q] = wsum[s][q];
-            for (int off = 8; off >= 1; off >>= 1)
-                for (int l = 0; l < off; l++) u[l] = u[l] + u[l + off];
-            r[s] = u[0];
-            sums[s] = r[s];
-        }
-        if (do_fin) finalize(f, r, scal, trace);
-    }
-}
-
-// The same level 2 spread over L2_LANES / 64 one-wave workgroups on as many
-// CUs: workgroup q runs wave q of the 1024-lane level 2 above (lanes 64q ..
-// 64q+63, each adding its partials in order), so the partials are pulled by
-// 16 CUs instead of one (a single CU took ~12 us for the 2 x 315 KB of a
-// 10M-row pair of dots).  Each wave sum is published write-through (sc1) and
-// drained before an arrival ticket; the last arriver combines the 16 wave
-// sums with the same halving tree and runs the finalize program.  Bitwise
-// identical to k_reduce2.
+// Level 2 of the canonical reduction, spread over L2_LANES / 64
+// one-wave workgroups on as many CUs: workgroup q is wave q of the 1024-lane
+// level 2 (lanes 64q .. 64q+63, lane t adding partials t, t+1024, ... in order
+// onto 0.0, then the wave's halving tree), so the partials are pulled by 16
+// CUs instead of one (a single 1024-lane workgroup took ~12 us for the 2 x
+// 315 KB of a 10M-row pair of dots, this 7.7 us).  Each wave sum is published
+// write-through (sc1) and drained before an arrival ticket; the last arriver
+// combines the 16 wave sums with the same halving tree and runs the finalize
+// program.
 __device__ __forceinline__ void st_sc1(double *p, double v)
 {
     __hip_atomic_store(reinterpret_cast<uint64_t *>(p), (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED,
@@ -330,147 +289,12 @@ struct SpmvArgs {
     long pcap;
 };
 
-// XCD != 0: the 256-row blocks are dealt so that each of the 8 XCDs owns one
-// contiguous eighth of the rows (dispatch round-robins workgroups over XCDs,
-// workgroup w runs on XCD w % 8); the x entries a block gathers are then
-// re-used by the neighbouring blocks of the same XCD out of its L2 (7-pt:
-// x is fetched once instead of ~1.3 times, rocprofv3 FETCH_SIZE).
-template <int EPI, int NRED, int XCD>
-__global__ __launch_bounds__(256) void k_spmv(SpmvArgs a, long nblk)
-{
-    __shared__ int sj[SPMV_CAP];
-    __shared__ double sx[SPMV_CAP];
-    __shared__ double lds[MAX_SLOTS][4];
-    long blk = blockIdx.x;
-    if (XCD) {
-        const long per = gridDim.x / 8;
-        blk = (blockIdx.x % 8) * per + blockIdx.x / 8;
-        if (blk >= nblk) return;
-    }
-    const int r0 = (int)(blk * 256);
-    const int tid = threadIdx.x;
-    const int r = r0 + tid;
-    const int rend = min(r0 + 256, a.nrows);
-    const int base = a.Ap[r0];
-    const int cnt = a.Ap[rend] - base;
-    double sum = 0;
-    if (cnt <= SPMV_CAP) {
-        for (int k = tid; k < cnt; k += 256) {
-            sj[k] = __builtin_nontemporal_load(a.Aj + base + k);
-            sx[k] = __builtin_nontemporal_load(a.Ax + base + k);
-        }
-        __syncthreads();
-        if (r < a.nrows) {
-            const int b = a.Ap[r] - base, e = a.Ap[r + 1] - base;
-            for (int k = b; k < e; k++) sum += a.x[sj[k]] * sx[k];
-        }
-    } else if (r < a.nrows) {
-        const int b = a.Ap[r], e = a.Ap[r + 1];
-        for (int k = b; k < e; k++) sum += a.x[a.Aj[k]] * a.Ax[k];
-    }
-    double zv = 0;
-    if (r < a.nrows) {
-        if (EPI == EPI_MXY) zv = sum;                          // mvops.cxx:134
-        else if (EPI == EPI_AMXY) zv = sum * a.alpha;          // :99
-        else if (EPI == EPI_AXPBY) zv = a.y[r] * a.beta + a.alpha * sum;  // :23, :61
-        else zv = a.alpha * sum;  // :61 with beta == 0 and alpha > 0
-        a.z[r] = zv;
-    }
-    if (NRED > 0) {
-        double v[NRED > 0 ? NRED : 1];
-        if (r < a.nrows) {
-            v[0] = zv * a.w0[r];
-            if (NRED > 1) v[NRED > 1 ? 1 : 0] = zv * (a.w1 ? a.w1[r] : zv);
-        } else {
-#pragma unroll
-            for (int q = 0; q < NRED; q++) v[q] = 0.0;
-        }
-        chunk_reduce<NRED>(v, a.part, a.pcap, blk, lds);
-    }
-}
-
-// Variant 2: the block's Ax / Aj ranges are staged with 16-byte loads (the
-// range is widened to 16-byte boundaries; the extra head/tail entries are
-// dropped when landing in LDS), all loads of a thread are issued before any
-// LDS store, and with XCD != 0 the 256-row blocks are dealt so that each of
-// the 8 XCDs owns one contiguous eighth of the rows (dispatch round-robins
-// blocks over XCDs: block b runs on XCD b % 8), keeping the x gathers of
-// neighbouring blocks in one L2.  Same per-row arithmetic as k_spmv.
-constexpr int SPMV2_CAP = 2048;
-template <int EPI, int NRED, int XCD>
-__global__ __launch_bounds__(256) void k_spmv2(SpmvArgs a, long nblk)
-{
-    __shared__ __attribute__((aligned(16))) double sx[SPMV2_CAP + 2];
-    __shared__ __attribute__((aligned(16))) int sj[SPMV2_CAP + 4];
-    __shared__ double lds[MAX_SLOTS][4];
-    long blk = blockIdx.x;
-    if (XCD) {
-        const long per = gridDim.x / 8;
-        blk = (blockIdx.x % 8) * per + blockIdx.x / 8;
-        if (blk >= nblk) return;
-    }
-    const int r0 = (int)(blk * 256);
-    const int tid = threadIdx.x;
-    const int r = r0 + tid;
-    const int rend = min(r0 + 256, a.nrows);
-    const int base = a.Ap[r0];
-    const int cnt = a.Ap[rend] - base;
-    double sum = 0;
-    if (cnt <= SPMV2_CAP) {
-        const int xb = base & ~1, xn = (base + cnt - xb + 1) >> 1;  // double2 count
-        const int jb = base & ~3, jn = (base + cnt - jb + 3) >> 2;  // int4 count
-        typedef double dbl2_t __attribute__((ext_vector_type(2)));
-        typedef int int4_t __attribute__((ext_vector_type(4)));
-        const dbl2_t *X2 = reinterpret_cast<const dbl2_t *>(a.Ax + xb);
-        const int4_t *J4 = reinterpret_cast<const int4_t *>(a.Aj + jb);
-        dbl2_t vx[(SPMV2_CAP / 2 + 1 + 255) / 256];
-        int4_t vj[(SPMV2_CAP / 4 + 1 + 255) / 256];
-#pragma unroll
-        for (int u = 0; u < (int)(sizeof(vx) / sizeof(vx[0])); u++)
-            if (tid + 256 * u < xn) vx[u] = __builtin_nontemporal_load(X2 + tid + 256 * u);
-#pragma unroll
-        for (int u = 0; u < (int)(sizeof(vj) / sizeof(vj[0])); u++)
-            if (tid + 256 * u < jn) vj[u] = __builtin_nontemporal_load(J4 + tid + 256 * u);
-        const int ox = base - xb, oj = base - jb;  // LDS entry e lives at e + o
-#pragma unroll
-        for (int u = 0; u < (int)(sizeof(vx) / sizeof(vx[0])); u++)
-            if (tid + 256 * u < xn) reinterpret_cast<dbl2_t *>(sx)[tid + 256 * u] = vx[u];
-#pragma unroll
-        for (int u = 0; u < (int)(sizeof(vj) / sizeof(vj[0])); u++)
-            if (tid + 256 * u < jn) reinterpret_cast<int4_t *>(sj)[tid + 256 * u] = vj[u];
-        __syncthreads();
-        if (r < a.nrows) {
-            const int b = a.Ap[r] - base, e = a.Ap[r + 1] - base;
-            for (int k = b; k < e; k++) sum += a.x[sj[k + oj]] * sx[k + ox];
-        }
-    } else if (r < a.nrows) {
-        const int b = a.Ap[r], e = a.Ap[r + 1];
-        for (int k = b; k < e; k++) sum += a.x[a.Aj[k]] * a.Ax[k];
-    }
-    double zv = 0;
-    if (r < a.nrows) {
-        if (EPI == EPI_MXY) zv = sum;
-        else if (EPI == EPI_AMXY) zv = sum * a.alpha;
-        else if (EPI == EPI_AXPBY) zv = a.y[r] * a.beta + a.alpha * sum;
-        else zv = a.alpha * sum;
-        a.z[r] = zv;
-    }
-    if (NRED > 0) {
-        double v[NRED > 0 ? NRED : 1];
-        if (r < a.nrows) {
-            v[0] = zv * a.w0[r];
-            if (NRED > 1) v[NRED > 1 ? 1 : 0] = zv * (a.w1 ? a.w1[r] : zv);
-        } else {
-#pragma unroll
-            for (int q = 0; q < NRED; q++) v[q] = 0.0;
-        }
-        chunk_reduce<NRED>(v, a.part, a.pcap, blk, lds);
-    }
-}
-
-// Variant 3 of the staged SpMV: as k_spmv (XCD-ordered blocks), but every
-// global access a lane makes before the barrier is issued up front and
-// branch-free -- the block's Aj / Ax range as 16-byte loads (widened to 16-byte
+// The 256-row blocks are dealt so that each of the 8 XCDs owns one contiguous
+// eighth of the rows (dispatch round-robins workgroups over XCDs, workgroup w
+// runs on XCD w % 8); the x entries a block gathers are then re-used by the
+// neighbouring blocks of the same XCD out of its L2 (7-pt: x is fetched once
+// instead of ~1.3 times, rocprofv3 FETCH_SIZE).  Every global access a lane
+// makes before the barrier is issued up front and branch-free -- the block's Aj / Ax range as 16-byte loads (widened to 16-byte
 // boundaries, clamped to the padded arrays; entries outside the block are
 // dropped when landing in LDS) and the lane's own Ap[r], Ap[r+1] -- so one
 // memory round trip covers the staging and the row bounds.
@@ -570,141 +394,13 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
     }
 }
 
-// x-tile SpMV for matrices whose x gathers are scattered (unstructured rows,
-// e.g. config 5): a gather instruction whose 64 lanes hit 64 different cache
-// lines costs ~64 L1/TA cycles, so instead each 1024-row block first copies
-// the x range its rows touch, [lo, lo + span), into LDS with coalesced loads,
-// and its rows then gather from LDS.  One row per thread, entries in CSR
-// order from 0.0 (mvops.cxx:55-58) -- bitwise the same sums as k_spmv3.  A
-// block's four 256-row quarters are the canonical reduction chunks.
-constexpr int XT_ROWS = 1024;
-constexpr int XT_CAP = 16384;  // doubles in the LDS tile (128 KB)
-template <int EPI, int NRED>
-__global__ __launch_bounds__(XT_ROWS) void k_spmv_xt(SpmvArgs a, const int *xt_lo, const int *xt_span, long nblk)
-{
-    __shared__ double tile[XT_CAP];
-    __shared__ double lds[4][MAX_SLOTS][4];
-    const long per = gridDim.x / 8;
-    const long blk = (blockIdx.x % 8) * per + blockIdx.x / 8;  // XCD-contiguous, as k_spmv3
-    if (blk >= nblk) return;
-    const int tid = threadIdx.x;
-    const int r = (int)(blk * XT_ROWS) + tid;
-    const int lo = xt_lo[blk], span = xt_span[blk];
-    for (int i = tid; i < span; i += XT_ROWS) tile[i] = a.x[lo + i];
-    __syncthreads();
-    double sum = 0;
-    if (r < a.nrows) {
-        const int rb = a.Ap[r], re = a.Ap[r + 1], len = re - rb;
-        if (len > 0 && len <= 12) {
-            double pr[12];
-#pragma unroll
-            for (int u = 0; u < 12; u++) {
-                const int k = min(rb + u, re - 1);
-                pr[u] = tile[a.Aj[k] - lo] * a.Ax[k];
-            }
-#pragma unroll
-            for (int u = 0; u < 12; u++)
-                if (u < len) sum += pr[u];
-        } else {
-            for (int k = rb; k < re; k++) sum += tile[a.Aj[k] - lo] * a.Ax[k];
-        }
-    }
-    double zv = 0;
-    if (r < a.nrows) {
-        if (EPI == EPI_MXY) zv = sum;
-        else if (EPI == EPI_AMXY) zv = sum * a.alpha;
-        else if (EPI == EPI_AXPBY) zv = a.y[r] * a.beta + a.alpha * sum;
-        else zv = a.alpha * sum;
-        a.z[r] = zv;
-    }
-    if (NRED > 0) {
-        double v[NRED > 0 ? NRED : 1];
-        if (r < a.nrows) {
-            v[0] = zv * a.w0[r];
-            if (NRED > 1) v[NRED > 1 ? 1 : 0] = zv * (a.w1 ? a.w1[r] : zv);
-        } else {
-#pragma unroll
-            for (int q = 0; q < NRED; q++) v[q] = 0.0;
-        }
-        const int lane = tid & 63, wave = (tid >> 6) & 3, quarter = tid >> 8;
-#pragma unroll
-        for (int q = 0; q < NRED; q++) {
-            const double w = wave_sum(v[q]);
-            if (lane == 0) lds[quarter][q][wave] = w;
-        }
-        __syncthreads();
-        if ((tid & 255) == 0 && blk * 4 + quarter < (a.nrows + CHUNK - 1) / CHUNK) {
-#pragma unroll
-            for (int q = 0; q < NRED; q++)
-                a.part[q * a.pcap + blk * 4 + quarter] =
-                    (lds[quarter][q][0] + lds[quarter][q][1]) + (lds[quarter][q][2] + lds[quarter][q][3]);
-        }
-    }
-}
-
-// Decide and upload the x-tile plan: every 1024-row block's column span
-// must fit the LDS tile.
-int plan_spmv_xt(lssp_amd_mat *M, const int *Ap, const int *Aj)
-{
-    const int n = M->nrows;
-    // opt-in (LSSP_AMD_SPMV_XT=1): measured no faster than k_spmv3 on the
-    // thermal-like matrix of config 5 (40.9 vs 40.2 us per call)
-    const char *e = getenv("LSSP_AMD_SPMV_XT");
-    if (!e || atoi(e) == 0 || n <= 0 || M->nnz <= 0) return LSSP_AMD_OK;
-    const long nb = (n + XT_ROWS - 1) / XT_ROWS;
-    std::vector<int> lo(nb), span(nb);
-    for (long b = 0; b < nb; b++) {
-        const int r0 = (int)(b * XT_ROWS), r1 = std::min<int>(n, r0 + XT_ROWS);
-        int mn = INT_MAX, mx = -1;
-        for (int k = Ap[r0]; k < Ap[r1]; k++) {
-            mn = std::min(mn, Aj[k]);
-            mx = std::max(mx, Aj[k]);
-        }
-        if (mx < 0) mn = mx = 0;
-        lo[b] = mn;
-        span[b] = mx - mn + 1;
-        if (span[b] > XT_CAP) return LSSP_AMD_OK;  // some block does not fit: k_spmv3
-    }
-    LSSP_HIP(hipMalloc(&M->d_xt_lo, sizeof(int) * nb));
-    LSSP_HIP(hipMalloc(&M->d_xt_span, sizeof(int) * nb));
-    LSSP_HIP(hipMemcpy(M->d_xt_lo, lo.data(), sizeof(int) * nb, hipMemcpyHostToDevice));
-    LSSP_HIP(hipMemcpy(M->d_xt_span, span.data(), sizeof(int) * nb, hipMemcpyHostToDevice));
-    M->xt = true;
-    return LSSP_AMD_OK;
-}
-
-static int g_spmv_variant = -1;  // LSSP_AMD_SPMV: 4 k_spmv3 (default), 3 k_spmv + XCD order,
-                                 // 0 k_spmv, 1 k_spmv2, 2 k_spmv2 + XCD order
-
 template <int EPI>
 static void spmv_dispatch(const SpmvArgs &a, int nred, long nblocks, hipStream_t s, long nnz_pad)
 {
-    if (g_spmv_variant < 0) {
-        const char *e = getenv("LSSP_AMD_SPMV");
-        g_spmv_variant = e ? atoi(e) : 4;
-    }
-    const long g = (nblocks + 7) / 8 * 8;
-    if (g_spmv_variant == 0) {
-        if (nred == 0) k_spmv<EPI, 0, 0><<<nblocks, 256, 0, s>>>(a, nblocks);
-        else if (nred == 1) k_spmv<EPI, 1, 0><<<nblocks, 256, 0, s>>>(a, nblocks);
-        else k_spmv<EPI, 2, 0><<<nblocks, 256, 0, s>>>(a, nblocks);
-    } else if (g_spmv_variant == 1) {
-        if (nred == 0) k_spmv2<EPI, 0, 0><<<nblocks, 256, 0, s>>>(a, nblocks);
-        else if (nred == 1) k_spmv2<EPI, 1, 0><<<nblocks, 256, 0, s>>>(a, nblocks);
-        else k_spmv2<EPI, 2, 0><<<nblocks, 256, 0, s>>>(a, nblocks);
-    } else if (g_spmv_variant == 2) {
-        if (nred == 0) k_spmv2<EPI, 0, 1><<<g, 256, 0, s>>>(a, nblocks);
-        else if (nred == 1) k_spmv2<EPI, 1, 1><<<g, 256, 0, s>>>(a, nblocks);
-        else k_spmv2<EPI, 2, 1><<<g, 256, 0, s>>>(a, nblocks);
-    } else if (g_spmv_variant == 4) {
-        if (nred == 0) k_spmv3<EPI, 0><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
-        else if (nred == 1) k_spmv3<EPI, 1><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
-        else k_spmv3<EPI, 2><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
-    } else {
-        if (nred == 0) k_spmv<EPI, 0, 1><<<g, 256, 0, s>>>(a, nblocks);
-        else if (nred == 1) k_spmv<EPI, 1, 1><<<g, 256, 0, s>>>(a, nblocks);
-        else k_spmv<EPI, 2, 1><<<g, 256, 0, s>>>(a, nblocks);
-    }
+    const long g = (nblocks + 7) / 8 * 8;  // a multiple of 8: whole XCD shares
+    if (nred == 0) k_spmv3<EPI, 0><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
+    else if (nred == 1) k_spmv3<EPI, 1><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
+    else k_spmv3<EPI, 2><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
 }
 
 int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, const double *x,
@@ -715,24 +411,6 @@ int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, c
     long nb = num_chunks(A->nrows);
     LSSP_TRY(ensure_part(c, nb));
     SpmvArgs a{A->nrows, A->Ap, A->Aj, A->Ax, x, y, z, alpha, beta, w0, w1, c->d_part, c->part_cap};
-    if (A->xt) {
-        const long nxb = (A->nrows + XT_ROWS - 1) / XT_ROWS, g = (nxb + 7) / 8 * 8;
-#define LSSP_XT(E)                                                                                            \
-    do {                                                                                                      \
-        if (nred == 0) k_spmv_xt<E, 0><<<g, XT_ROWS, 0, c->stream>>>(a, A->d_xt_lo, A->d_xt_span, nxb);      \
-        else if (nred == 1) k_spmv_xt<E, 1><<<g, XT_ROWS, 0, c->stream>>>(a, A->d_xt_lo, A->d_xt_span, nxb); \
-        else k_spmv_xt<E, 2><<<g, XT_ROWS, 0, c->stream>>>(a, A->d_xt_lo, A->d_xt_span, nxb);               \
-    } while (0)
-        switch (epi) {
-        case EPI_MXY: LSSP_XT(EPI_MXY); break;
-        case EPI_AMXY: LSSP_XT(EPI_AMXY); break;
-        case EPI_AXPBY: LSSP_XT(EPI_AXPBY); break;
-        default: LSSP_XT(EPI_AMX); break;
-        }
-#undef LSSP_XT
-        LSSP_HIP(hipGetLastError());
-        return LSSP_AMD_OK;
-    }
     switch (epi) {
     case EPI_MXY: spmv_dispatch<EPI_MXY>(a, nred, nb, c->stream, A->nnz + 4L); break;
     case EPI_AMXY: spmv_dispatch<EPI_AMXY>(a, nred, nb, c->stream, A->nnz + 4L); break;
@@ -909,13 +587,8 @@ int launch_ew(lssp_amd_ctx *c, const Ew &e)
 int launch_reduce_tree(lssp_amd_ctx *c, long C, int nslot, const Fin &f)
 {
     int do_fin = c->nranks > 1 ? 0 : 1;
-    static const bool one_cu = getenv("LSSP_AMD_REDUCE2_ONE_CU") && atoi(getenv("LSSP_AMD_REDUCE2_ONE_CU"));
     static_assert(L2_LANES == 16 * 64, "k_reduce2m runs the 16 waves of the level-2 workgroup");
-    if (one_cu)
-        k_reduce2<<<1, L2_LANES, 0, c->stream>>>(c->d_part, c->part_cap, C, nslot, c->d_sums, c->d_scal,
-                                                  c->d_trace, f, do_fin);
-    else
-        k_reduce2m<<<L2_LANES / 64, 64, 0, c->stream>>>(c->d_part, c->part_cap, C, nslot, c->d_sums, c->d_scal,
+    k_reduce2m<<<L2_LANES / 64, 64, 0, c->stream>>>(c->d_part, c->part_cap, C, nslot, c->d_sums, c->d_scal,
                                                          c->d_trace, f, do_fin, c->d_wsum, c->d_rcnt);
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;

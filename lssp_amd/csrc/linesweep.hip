@@ -54,8 +54,6 @@
 
 namespace lssp_amd {
 
-constexpr uint32_t SENT_LO = (uint32_t)(TRI_SENTINEL & 0xffffffffu);
-constexpr uint32_t SENT_HI = (uint32_t)(TRI_SENTINEL >> 32);
 
 // ---------------------------------------------------------------------------
 // host: detection of the grid structure
@@ -192,10 +190,8 @@ static int build_tiles(const LineGeom &g, int P, int W, std::vector<LineTile> &t
 // rows (row (p, l) at p*nj + l; rows not valid at that step are +0.0), each
 // row's NA coefficients {c_k, c_j, c_i(, diag)} together.  Fixed strides keep
 // every role's addressing to a per-lane base plus immediate offsets.
-// With M levels per step (k_line2) the per-level blocks are the same; a tile's
-// stream is padded to whole steps (levels T .. M*ceil(T/M)-1 hold +0.0).
 static int upload_sweep(lssp_amd_ctx *c, const LineGeom &g, const std::vector<LineTile> &tiles, const CoefSrc &src,
-                        int NA, int M, LineSweep &ls)
+                        int NA, LineSweep &ls)
 {
     const int nx = g.nx, P = LINE_P;
     std::vector<LineTile> tt = tiles;
@@ -204,7 +200,7 @@ static int upload_sweep(lssp_amd_ctx *c, const LineGeom &g, const std::vector<Li
     for (LineTile &t : tt) {
         t.roff = 0;
         t.cbase = rows_total;
-        rows_total += (long)((t.T + M - 1) / M * M) * P * t.nj;
+        rows_total += (long)t.T * P * t.nj;
         tmax = std::max(tmax, t.T);
     }
     // + slack for the loaders' whole 1 KB pieces past the last block
@@ -230,7 +226,6 @@ static int upload_sweep(lssp_amd_ctx *c, const LineGeom &g, const std::vector<Li
     ls.tmax = tmax;
     ls.rows_total = rows_total;
     ls.NA = NA;
-    ls.M = M;
     LSSP_HIP(hipMalloc(&ls.d_tiles, sizeof(LineTile) * tt.size()));
     LSSP_HIP(hipMemcpy(ls.d_tiles, tt.data(), sizeof(LineTile) * tt.size(), hipMemcpyHostToDevice));
     LSSP_HIP(hipMalloc(&ls.d_coef, sizeof(double) * coef.size()));
@@ -277,13 +272,10 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
     li.g = g;
     li.W = W;
     li.S = S;
-    // levels per barrier step: LSSP_AMD_LINE_M (1: k_line, one level per step)
-    const char *me = getenv("LSSP_AMD_LINE_M");
-    const int M = me && atoi(me) == LINE_M ? LINE_M : 1;
-    LSSP_TRY(upload_sweep(c, g, Lt, cl, g.unitL ? 3 : 4, M, li.L));
+    LSSP_TRY(upload_sweep(c, g, Lt, cl, g.unitL ? 3 : 4, li.L));
     LineGeom gu = g;
     for (int k = 0; k < g.nz; k++) gu.kin[k] = k > 0 ? g.kin[g.nz - k] : 0;
-    LSSP_TRY(upload_sweep(c, gu, Ut, cu, 4, M, li.U));
+    LSSP_TRY(upload_sweep(c, gu, Ut, cu, 4, li.U));
     // the L sweep writes its output into the U sweep's rhs stream: per L tile
     // the base row of its mirror U tile
     for (int K = 0; K < S; K++)
@@ -298,8 +290,7 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
     // both sweeps (they never run at once) and armed with the sentinel
     LSSP_HIP(hipMalloc(&li.d_ustream, sizeof(double) * (li.U.rows_total + 16 * 1024 / 8)));
     LSSP_HIP(hipMemset(li.d_ustream, 0, sizeof(double) * (li.U.rows_total + 16 * 1024 / 8)));  // invalid rows stay +0.0
-    // hand-off buffers indexed by level, padded to whole steps plus one
-    li.tmax = (std::max(li.L.tmax, li.U.tmax) + M - 1) / M * M + M;
+    li.tmax = std::max(li.L.tmax, li.U.tmax);
     li.hk_stride = (long)li.tmax * 64;
     li.hj_stride = (long)li.tmax * LINE_P;
     li.ntiles = (int)Lt.size();
@@ -365,10 +356,6 @@ __device__ __forceinline__ void dma16_sc1(const void *g, unsigned lds)
 {
     asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off sc1" ::"v"(g), "s"(__builtin_amdgcn_readfirstlane(lds))
                  : "memory", "m0");
-}
-__device__ __forceinline__ void dma4(const void *g, unsigned lds)
-{
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
 }
 // LDS drained, then the workgroup barrier.  The wait is the builtin (not asm),
 // so the compiler's wait-count tracking knows every LDS load is complete after
@@ -535,12 +522,6 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                 double ck[PC], cj[PC], ci[PC], dg[PC], rh[PC], jv[PC];
             };
             auto load = [&](int s, In &in) {
-#ifdef LINE_EXP
-                if (LINE_EXP & 2) {
-                    for (int u = 0; u < PC; u++) in.ck[u] = in.cj[u] = in.ci[u] = in.dg[u] = in.rh[u] = in.jv[u] = 0.25 + s * 1e-9;
-                    return;
-                }
-#endif
                 const char *slot = ring + (s % R) * SL::BYTES;
 #pragma unroll
                 for (int u = 0; u < PC; u++) {
@@ -578,12 +559,8 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                 // next step's operands in flight
                 const int sc = min(max(s, 0), T - 1);
                 const char *slot = ring + (sc % R) * SL::BYTES;
-#if defined(LINE_EXP) && (LINE_EXP & 8)
-                const double kx = 0.5;
-#else
                 const double kx = wave == 0 ? reinterpret_cast<const double *>(slot + SL::KFIN)[lane]
                                             : res[((sc - 1) & (RS - 1)) * P * 64 + (p0 - 1) * 64 + lane];
-#endif
                 asm volatile("" ::: "memory");  // kx's read is issued first (LDS returns in order)
                 load(min(max(s + 1, 0), T - 1), nxt);
                 if (s >= 0 && s < T) {
@@ -600,30 +577,14 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                         double v = cur.rh[u] - cur.ck[u] * xk;
                         v = v - cur.cj[u] * xj;
                         v = v - cur.ci[u] * xc[u];
-#if defined(LINE_EXP) && (LINE_EXP & 16)
-                        if constexpr (NA == 4) v = v * cur.dg[u];
-#else
                         if constexpr (NA == 4) v = v / cur.dg[u];
-#endif
-#if defined(LINE_EXP) && (LINE_EXP & 4)
-                        xn[u] = v;
-#else
                         xn[u] = sel_lanes(__builtin_amdgcn_ballot_w64(valid), v, xc[u]);
-#endif
-#if defined(LINE_EXP) && (LINE_EXP & 1)
-                        if (false) {
-#else
-                        if (kout && p == np - 1) {
-#endif  // uniform: the tile's last plane feeds the next k-tile
+                        if (kout && p == np - 1) {  // uniform: the tile's last plane feeds the next k-tile
                             const int ko = valid ? ((s + 1 - np) * 64 + lane) * 8 : OOB;
                             __builtin_amdgcn_raw_buffer_store_b64(split64(canon_bits(xn[u])), hko, ko, 0, 16);  // sc1
                         }
                     }
-#if defined(LINE_EXP) && (LINE_EXP & 1)
-                    if (false) {
-#else
                     if (jout) {
-#endif
                         // lane nj-1 feeds the next j-tile: this wave's PC planes in one store
                         // (entries of planes whose row does not exist are never polled)
                         const int jo = lane == nj - 1 ? ((s + 1 - nj) * P + p0) * 8 : OOB;
@@ -645,9 +606,7 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
 #pragma unroll
                     for (int u = 0; u < PC; u++) {
                         xc[u] = xn[u];
-#if !(defined(LINE_EXP) && (LINE_EXP & 8))
                         res[((s & (RS - 1)) * P + p0 + u) * 64 + lane] = xc[u];
-#endif
                     }
                 }
                 if (trs && s >= 0 && s < T) ts[8 * s + (wave == 0 ? 1 : 7)] = __builtin_amdgcn_s_memtime();
@@ -909,431 +868,6 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
 }
 
 // ---------------------------------------------------------------------------
-// k_line2: M levels per barrier step, one compute wave owning all P planes
-// ---------------------------------------------------------------------------
-// The step of k_line costs ~1300-1500 clk whatever it computes (a barrier over
-// nine waves each with a memory role): measured with the compute gutted, the
-// loaders / poller / stores switched off one by one (tools/line_diag.py,
-// LSSP_AMD_LINE_DIAG).  k_line2 amortises it over M levels: at barrier step
-// sigma the compute wave does levels M*sigma .. M*sigma+M-1, each level all P
-// planes (independent within a level: P-way ILP), so no value crosses waves
-// inside a step.  Lane l, plane p at level t owns row i = t - l - p, so a
-// lane's M rows of a step are M consecutive rows of its line.
-//
-// Slot of step q (LDS ring of R = D+1): coefficient block [M][P][nj][NA], the
-// U rhs stream block [M][P][nj] (from the stream; a natural-order rhs lives in
-// rhs blocks filled by the rhs wave), the k-input [M][64] and j-input [M][P].
-// Loaders complete slot q during step q-2, the poller the k-input of q during
-// q-1 and the j-input of q during q-2.  The compute wave reads the operands of
-// level m+1 while computing level m (the first level of step sigma+1 during
-// the last level of sigma), and each level's k-input at its start (needed by
-// plane 0, computed last).
-template <int P, int M, int NA, bool RHS_NAT>
-struct LineSlot2 {
-    static constexpr int NPC = (M * P * 64 * NA * 8 + 1023) / 1024;         // coefficient DMA pieces (1 KB)
-    static constexpr int NRP = RHS_NAT ? 0 : (M * P * 64 * 8 + 1023) / 1024;  // rhs-stream DMA pieces
-    static constexpr int COEF = 0;
-    static constexpr int RHS = NPC * 1024;
-    static constexpr int KIN = RHS + NRP * 1024;  // double[M][64]
-    static constexpr int JIN = KIN + M * 512;     // double[M][P]
-    static constexpr int BYTES = (JIN + M * P * 8 + 15) & ~15;
-};
-// result ring (levels): natural-order output is written in 8-level runs while
-// the compute wave fills the next levels -> 2M + 14 levels at least
-template <int M, int OUT>
-constexpr int line2_rsl() { return OUT == 1 ? (2 * M + 14 + 7) / 8 * 8 : 2 * M; }
-constexpr int LINE2_RW = 3;  // rhs wave: loads land LINE2_RW steps after issue
-template <int P, int M, int NA, bool RHS_NAT, int OUT, int D>
-constexpr int line2_lds_bytes()
-{
-    return (D + 1) * LineSlot2<P, M, NA, RHS_NAT>::BYTES + line2_rsl<M, OUT>() * P * 64 * 8 + 16 + 1024 +
-           (RHS_NAT ? 3 * line_rhs_blk<P>() * 8 : 0);
-}
-template <int NL, int SW, bool RHS_NAT>
-constexpr int line2_waves() { return 1 + NL + 1 + SW + (RHS_NAT ? 1 : 0); }
-
-// waves: 0 compute, 1..NL loaders, NL+1 poller, then SW storers, then (natural
-// rhs) the rhs wave -- with NL = 3 the compute wave shares its SIMD only with
-// the poller
-template <int P, int M, int NA, bool RHS_NAT, int OUT, int NL, int D, int DH, int SW, bool TRACE>
-__global__ __launch_bounds__((64 * line2_waves<NL, SW, RHS_NAT>())) void k_line2(LineArgs a)
-{
-    constexpr int LA = 2;
-    static_assert(DH >= 2 && DH < D && (OUT == 1 || OUT == 2) && 8 % M == 0 && M % 2 == 0, "config");
-    constexpr int R = D + 1;
-    using SL = LineSlot2<P, M, NA, RHS_NAT>;
-    constexpr int RSL = line2_rsl<M, OUT>();
-    constexpr int NKD = (M * 512 + 1023) / 1024;  // k-input DMAs per step (64 lanes x 16 B each)
-    constexpr int NPOLL = NKD + 1;
-    constexpr int NITEM = SL::NPC + SL::NRP;
-    constexpr int KPER = (NITEM + NL - 1) / NL;
-    static_assert((D - LA) * KPER <= 63 && NPOLL * (DH - 1) <= 63, "vmcnt range");
-    constexpr int QB = 8 / M;  // rhs wave: steps per 8-level block
-    constexpr int LEAD = D > 1 + QB + LINE2_RW ? D : 1 + QB + LINE2_RW;
-    constexpr int S0 = -((LEAD + 11) / 12) * 12;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    char *ring = smem;
-    double *res = reinterpret_cast<double *>(smem + R * SL::BYTES);  // [RSL][P][64]
-    int *s_tile = reinterpret_cast<int *>(res + RSL * P * 64);
-    const unsigned sink = (unsigned)(uintptr_t)(smem + R * SL::BYTES + RSL * P * 64 * 8 + 16);
-    double *rhsblk = reinterpret_cast<double *>(smem + R * SL::BYTES + RSL * P * 64 * 8 + 16 + 1024);  // [3][8][P*64+1]
-    const unsigned lds0 = (unsigned)(uintptr_t)smem;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int nx = a.nx;
-
-    for (;;) {
-        __syncthreads();
-        if (threadIdx.x == 0) *s_tile = (int)(atomicAdd(a.claim, 1ull) - a.base);
-        __syncthreads();
-        const int t = __builtin_amdgcn_readfirstlane(*s_tile);
-        if (t >= a.ntiles) break;
-        if (TRACE && threadIdx.x == 0) a.trace[8 * t] = __builtin_amdgcn_s_memrealtime();
-        const LineTile d = a.tiles[t];
-        const int T = d.T, nj = d.nj, np = d.np;
-        const int St = (T + M - 1) / M;  // steps
-        const long SB = (long)P * nj;    // rows per level block
-        const bool kin = d.flags & LT_KIN, jin = d.flags & LT_JIN, kout = d.flags & LT_KOUT,
-                   jout = d.flags & LT_JOUT;
-        const int lc = min(lane, nj - 1);
-        auto nb = [&](int p, int l) {
-            const long r = ((long)(d.k0 + p) * a.ny + (d.j0 + l)) * nx;
-            return a.mirror ? a.n - 1 - r : r;
-        };
-        unsigned long long *ts = TRACE ? a.trace + 8 * (long)a.ntiles : nullptr;
-        const bool trs = TRACE && t == a.ttile && lane == 0;
-
-        if (wave == 0) {
-            // ---------------- compute ----------------
-            struct Lv {
-                double ck[P], cj[P], ci[P], dg[P], rh[P], jv[P];
-            };
-            auto load = [&](int v, Lv &in) {  // level v's operands (its step's slot must be complete)
-                const int q = v / M, m = v - q * M;
-                const char *slot = ring + (q % R) * SL::BYTES;
-#pragma unroll
-                for (int p = 0; p < P; p++) {
-                    const double *b = reinterpret_cast<const double *>(slot + SL::COEF) + ((m * P + p) * nj + lc) * NA;
-                    in.ck[p] = b[0];
-                    in.cj[p] = b[1];
-                    in.ci[p] = b[2];
-                    if constexpr (NA == 4) in.dg[p] = b[3];
-                    if constexpr (RHS_NAT)
-                        in.rh[p] = rhsblk[((v >> 3) % 3) * line_rhs_blk<P>() + (v & 7) * (P * 64 + 1) + p * 64 + lane];
-                    else
-                        in.rh[p] = reinterpret_cast<const double *>(slot + SL::RHS)[(m * P + p) * nj + lc];
-                    in.jv[p] = reinterpret_cast<const double *>(slot + SL::JIN)[m * P + p];
-                }
-            };
-            double xc[P];
-            int lp[P], nxp[P];  // plane p's row at level v exists iff (unsigned)(v - lp) < nxp
-#pragma unroll
-            for (int p = 0; p < P; p++) {
-                xc[p] = 0.0;
-                lp[p] = lane + p;
-                nxp[p] = lane < nj && p < np ? nx : 0;
-            }
-            const __amdgpu_buffer_rsrc_t hko =
-                __builtin_amdgcn_make_buffer_rsrc(a.hk + (long)t * a.hk_stride, 0, (int)(a.hk_stride * 8), 0x00020000);
-            constexpr int OOB = 0x7ffffff0;
-            Lv A, B;  // even levels A, odd levels B (M is even)
-            auto level = [&](int sg, int m, Lv &cur, Lv &nxt) {
-                const int v = M * sg + m;  // level
-                // every step issues the same LDS reads (clamped), so the wait for kx
-                // leaves the next level's operands in flight
-                const int vc = min(max(v, 0), M * St - 1);
-                const double kx = reinterpret_cast<const double *>(ring + ((vc / M) % R) * SL::BYTES + SL::KIN)[m * 64 + lane];
-                asm volatile("" ::: "memory");  // kx first (LDS returns in order)
-                load(min(max(v + 1, 0), M * St - 1), nxt);
-                if (sg < 0 || sg >= St) return;
-                // the P planes are independent within a level: every operation is
-                // issued for all planes before the next one (each f64 op's latency is
-                // covered by the other planes'), plane 0 last in each group (kx)
-                double xn[P], r[P], m1[P], m2[P], m3[P];
-#pragma unroll
-                for (int p = P - 1; p >= 0; p--) {
-                    m2[p] = cur.cj[p] * dpp_shr1(xc[p], cur.jv[p]);
-                    m3[p] = cur.ci[p] * xc[p];
-                    m1[p] = cur.ck[p] * (p > 0 ? xc[p - 1] : kx);
-                }
-#pragma unroll
-                for (int p = P - 1; p >= 0; p--) r[p] = cur.rh[p] - m1[p];
-#pragma unroll
-                for (int p = P - 1; p >= 0; p--) r[p] = r[p] - m2[p];
-#pragma unroll
-                for (int p = P - 1; p >= 0; p--) r[p] = r[p] - m3[p];
-#pragma unroll
-                for (int p = P - 1; p >= 0; p--) {
-                    if constexpr (NA == 4) r[p] = r[p] / cur.dg[p];
-                    xn[p] = sel_lanes(__builtin_amdgcn_ballot_w64((unsigned)(v - lp[p]) < (unsigned)nxp[p]), r[p], xc[p]);
-                }
-                if (kout) {  // plane np-1 feeds the next k-tile (sc1 buffer store, OOB lanes dropped)
-                    const int pl = np - 1;
-                    double xo = xn[0];
-#pragma unroll
-                    for (int p = 1; p < P; p++) xo = pl == p ? xn[p] : xo;
-                    const int ko = (unsigned)(v - lane - pl) < (unsigned)nxp[pl] ? ((v + 1 - np) * 64 + lane) * 8 : OOB;
-                    __builtin_amdgcn_raw_buffer_store_b64(split64(canon_bits(xo)), hko, ko, 0, 16);
-                }
-#pragma unroll
-                for (int p = 0; p < P; p++) {
-                    xc[p] = xn[p];
-                    res[((v % RSL) * P + p) * 64 + lane] = xn[p];
-                }
-            };
-            for (int sg = S0; sg <= St; sg++) {
-                if (trs && sg >= 0 && sg < St) ts[8 * sg] = __builtin_amdgcn_s_memtime();
-                static_for<0, M>([&](auto U) {
-                    constexpr int m = decltype(U)::value;
-                    if constexpr (m % 2 == 0)
-                        level(sg, m, A, B);
-                    else
-                        level(sg, m, B, A);
-                });
-                if (trs && sg >= 0 && sg < St) ts[8 * sg + 1] = __builtin_amdgcn_s_memtime();
-                line_barrier();
-            }
-            if (TRACE && lane == 0) {
-                a.trace[8 * t + 2] = __builtin_amdgcn_s_memrealtime();
-                unsigned xcc;
-                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-                a.trace[8 * t + 4] = xcc;
-            }
-        } else if (wave <= NL) {
-            // ---------------- loaders ----------------
-            const int w = wave - 1;
-            auto issue = [&](int q) {
-                const int qc = min(max(q, 0), St - 1);
-                const unsigned sl = lds0 + (unsigned)(((q % R + R) % R) * SL::BYTES);
-                const char *cb = reinterpret_cast<const char *>(a.coef) + (d.cbase + (long)qc * M * SB) * (8L * NA);
-                const char *ub = reinterpret_cast<const char *>(a.rhs) + (d.cbase + (long)qc * M * SB) * 8L;
-#pragma unroll
-                for (int k = 0; k < KPER; k++) {
-                    const int m = w + k * NL;
-                    if (m < SL::NPC)
-                        dma16(cb + m * 1024 + lane * 16, sl + SL::COEF + m * 1024);
-                    else if (m < NITEM)
-                        dma16(ub + (m - SL::NPC) * 1024 + lane * 16, sl + SL::RHS + (m - SL::NPC) * 1024);
-                    else
-                        dma16(cb + lane * 16, sl + SL::COEF);  // keeps the per-wave count fixed
-                }
-            };
-            for (int sg = S0; sg <= St; sg++) {
-                if (!(a.diag & 2)) issue(sg + D);
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - LA) * KPER) : "memory");
-                line_barrier();
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else if (wave == NL + 1) {
-            // ---------------- poller ----------------
-            // LDS-DMA sc1 reads of the hand-off inputs into their slots, DH steps
-            // ahead: at step sg the k-input of step sg+DH and the j-input of step
-            // sg+DH+1; those of steps sg+1 (k) and sg+2 (j) are waited for and checked.
-            const double *hk = a.hk + (long)max(d.tk, 0) * a.hk_stride;
-            const double *hj = a.hj + (long)max(d.tj, 0) * a.hj_stride;
-            const int vmax = (int)(a.hk_stride / 64) - M;
-            auto kval = [&](int v, int l) { return v >= 0 && v < T && l < nj && v - l >= 0 && v - l < nx; };
-            auto jval = [&](int v, int p) { return v >= 0 && v < T && p < np && v - p >= 0 && v - p < nx; };
-            auto issue = [&](int q) {
-                const int vk = min(max(M * q, 0), vmax), vj = min(max(M * (q + 1), 0), vmax);
-                const unsigned ks = lds0 + (unsigned)((((q % R) + R) % R) * SL::BYTES + SL::KIN);
-                const unsigned js = lds0 + (unsigned)(((((q + 1) % R) + R) % R) * SL::BYTES + SL::JIN);
-#pragma unroll
-                for (int k = 0; k < NKD; k++) {
-                    const char *kp = reinterpret_cast<const char *>(hk + (long)vk * 64) + k * 1024 + lane * 16;
-                    if (k * 64 + lane < M * 32) dma16_sc1(kp, kin ? ks + k * 1024 : sink);
-                }
-                const char *jp = reinterpret_cast<const char *>(hj + (long)vj * P) + lane * 16;
-                if (lane < M * P / 2) dma16_sc1(jp, jin ? js : sink);
-            };
-            if (!kin || !jin) {
-                for (int q = 0; q < R; q++) {
-#pragma unroll
-                    for (int m = 0; m < M; m++)
-                        if (!kin) reinterpret_cast<double *>(ring + q * SL::BYTES + SL::KIN)[m * 64 + lane] = 0.0;
-                    if (!jin && lane < M * P) reinterpret_cast<double *>(ring + q * SL::BYTES + SL::JIN)[lane] = 0.0;
-                }
-            }
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            unsigned polls = 0;
-            for (int sg = S0; sg <= St; sg++) {
-                const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
-                issue(sg + DH);
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPOLL * (DH - 1)) : "memory");
-                const int qk = sg + 1, qj = sg + 2;
-                double *kslot = reinterpret_cast<double *>(ring + (((qk % R) + R) % R) * SL::BYTES + SL::KIN);
-                double *jslot = reinterpret_cast<double *>(ring + (((qj % R) + R) % R) * SL::BYTES + SL::JIN);
-                bool bad = false;
-                uint64_t kv[M];
-#pragma unroll
-                for (int m = 0; m < M; m++) {
-                    kv[m] = kin && kval(M * qk + m, lane) ? (uint64_t)__double_as_longlong(kslot[m * 64 + lane]) : 0;
-                    bad |= kin && kval(M * qk + m, lane) && kv[m] == TRI_SENTINEL;
-                }
-                const int jm = min(lane, M * P - 1) / P, jp = min(lane, M * P - 1) % P;
-                const bool jv_ok = jin && lane < M * P && jval(M * qj + jm, jp);
-                const uint64_t jv = jv_ok ? (uint64_t)__double_as_longlong(jslot[lane]) : 0;
-                bad |= jv_ok && jv == TRI_SENTINEL;
-                if (__any(!(a.diag & 8) && bad)) {
-                    // resync episode (as in k_line): drain, wait for these values and the
-                    // furthest step in flight, re-issue
-                    polls++;
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    auto spin = [&](const double *src) {
-                        for (;;) {
-                            const uint64_t b = line_ld_agent(src);
-                            if (b != TRI_SENTINEL) return b;
-                            if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s
-                                atomicOr(a.err, 8);
-                                return (uint64_t)0x7FF8000000000000ull;
-                            }
-                            __builtin_amdgcn_s_sleep(1);
-                        }
-                    };
-#pragma unroll
-                    for (int m = 0; m < M; m++)
-                        if (kin && kval(M * qk + m, lane) && kv[m] == TRI_SENTINEL)
-                            kslot[m * 64 + lane] = __longlong_as_double((long long)spin(hk + (long)(M * qk + m) * 64 + lane));
-                    if (jv_ok && jv == TRI_SENTINEL)
-                        jslot[lane] = __longlong_as_double((long long)spin(hj + (long)(M * qj) * P + lane));
-                    if (kin && kval(M * (sg + DH), lane)) (void)spin(hk + (long)M * (sg + DH) * 64 + lane);
-                    if (jin && lane < P && jval(M * (sg + DH + 1), lane)) (void)spin(hj + (long)M * (sg + DH + 1) * P + lane);
-                    for (int k = 2; k <= DH; k++) issue(sg + k);
-                }
-                if (trs && sg >= 0 && sg < St) ts[8 * sg + 2] = __builtin_amdgcn_s_memtime() - w0;
-                line_barrier();
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (TRACE) {
-                for (int o = 32; o >= 1; o >>= 1) polls += __shfl_xor(polls, o);
-                if (lane == 0) a.trace[8 * t + 3] = polls;
-            }
-        } else if (wave < NL + 2 + SW) {
-            // ---------------- storers ----------------
-            // storer 0: the j-output (lane nj-1's values of the previous step, all
-            // planes) and the re-arm of the consumed j-inputs; storer SW-1: the
-            // re-arm of the consumed k-inputs; all: the results.
-            const int w = wave - (NL + 2);
-            uint64_t *hki = reinterpret_cast<uint64_t *>(a.hk + (long)max(d.tk, 0) * a.hk_stride);
-            uint64_t *hji = reinterpret_cast<uint64_t *>(a.hj + (long)max(d.tj, 0) * a.hj_stride);
-            double *hjo = a.hj + (long)t * a.hj_stride;
-            auto after = [&](int sg) {  // the previous step's levels are complete
-                const int v0 = M * (sg - 1);
-                if (sg < 1 || sg > St) return;
-                if (w == SW - 1 && kin) {
-#pragma unroll
-                    for (int m = 0; m < M; m++) {
-                        const int v = v0 + m;
-                        if (v < T && lane < nj && (unsigned)(v - lane) < (unsigned)nx) hki[(long)v * 64 + lane] = TRI_SENTINEL;
-                    }
-                }
-                if (w == 0 && lane < M * P) {
-                    const int m = lane / P, p = lane % P, v = v0 + m;
-                    const bool ok = v < T && p < np && (unsigned)(v - p) < (unsigned)nx;
-                    if (jin && ok) hji[(long)v * P + p] = TRI_SENTINEL;
-                    // j-output: row (v - (nj-1) - p) of lane nj-1 -> consumer level v+1-nj
-                    const int i = v - (nj - 1) - p;
-                    if (jout && p < np && v < T && (unsigned)i < (unsigned)nx)
-                        line_st_agent(hjo + (long)(v + 1 - nj) * P + p, res[((v % RSL) * P + p) * 64 + nj - 1]);
-                }
-            };
-            if constexpr (OUT == 1) {
-                // 8-level blocks written as runs (8 consecutive rows of a line on 8
-                // consecutive lanes): virtual step u = M*sg - M + 1 + k, k < M, writes
-                // slice u & 7 of block (u >> 3) - 1
-                constexpr int NV = P * 64;
-                static_assert(NV % (64 * SW) == 0, "slices");
-                auto slice = [&](int u) {
-                    const int Bk = (u >> 3) - 1, k = u & 7;
-                    if (Bk < 0) return;
-#pragma unroll
-                    for (int it = 0; it < NV / (64 * SW); it++) {
-                        const int vv = k * NV + w * (NV / SW) + it * 64 + lane;
-                        const int r = vv >> 3, m = vv & 7;
-                        const int p = r >> 6, l = r & 63, v = 8 * Bk + m;
-                        const int i = v - l - p;
-                        const double x = res[((v % RSL) * P + p) * 64 + l];
-                        if (!(a.diag & 1) && p < np && l < nj && (unsigned)i < (unsigned)nx)
-                            a.out[a.mirror ? nb(p, l) - i : nb(p, l) + i] = x;
-                    }
-                };
-                for (int sg = S0; sg <= St; sg++) {
-                    if (sg >= 1)
-#pragma unroll
-                        for (int k = 0; k < M; k++) slice(M * sg - M + 1 + k);
-                    after(sg);
-                    line_barrier();
-                }
-                for (int u = M * St + 1; u < 8 * ((M * St) / 8 + 2); u++) slice(u);  // the last blocks
-            } else {
-                // the U sweep's rhs stream: level v, plane p, lane l -> the mirror tile's
-                // level T-1-v, plane np-1-p, lane nj-1-l
-                for (int sg = S0; sg <= St; sg++) {
-                    if (sg >= 1 && sg <= St) {
-#pragma unroll
-                        for (int k = 0; k < M * P / SW; k++) {
-                            const int mp = w + k * SW, m = mp / P, p = mp % P, v = M * (sg - 1) + m;
-                            if (!(a.diag & 1) && p < np && lane < nj && v < T && (unsigned)(v - lane - p) < (unsigned)nx)
-                                a.out[d.ubase + (long)(T - 1 - v) * SB + (long)(np - 1 - p) * nj + (nj - 1 - lane)] =
-                                    res[((v % RSL) * P + p) * 64 + lane];
-                        }
-                    }
-                    after(sg);
-                    line_barrier();
-                }
-            }
-        } else {
-            // ---------------- rhs wave (natural-order rhs) ----------------
-            // Block b (levels 8b .. 8b+7) in buffer b % 3, as runs of 8 rows of a line
-            // (8 lanes per run), written in QB quarters at steps 8b/M - 1 - QB + k (the
-            // compute reads its first level during step 8b/M - 1), each from loads
-            // issued LINE2_RW steps earlier (a register ring the compiler tracks).
-            constexpr int NI = P * 64 * 8 / QB / 64;  // loads per lane per quarter
-            double ringv[LINE2_RW][NI];
-            auto where = [&](int sg, int &b, int &k) {  // block and quarter written at step sg
-                const int u = sg + 1 + QB;
-                b = u >= 0 ? u / QB : -((-u + QB - 1) / QB);
-                k = u - b * QB;
-            };
-            auto issue = [&](int sg, double (&dst)[NI]) {
-                int b, k;
-                where(sg, b, k);
-#pragma unroll
-                for (int it = 0; it < NI; it++) {
-                    const int vv = (k * NI + it) * 64 + lane;
-                    const int r = vv >> 3, m = vv & 7;
-                    const int p = r >> 6, l = r & 63;
-                    const int i = 8 * b + m - l - p;
-                    const bool ok = b >= 0 && p < np && l < nj && (unsigned)i < (unsigned)nx;
-                    dst[it] = ok ? a.rhs[a.mirror ? nb(p, l) - i : nb(p, l) + i] : 0.0;
-                }
-            };
-            auto write = [&](int sg, const double (&src)[NI]) {
-                int b, k;
-                where(sg, b, k);
-                if (b < 0) return;
-                double *blk = rhsblk + (b % 3) * line_rhs_blk<P>();
-#pragma unroll
-                for (int it = 0; it < NI; it++) {
-                    const int vv = (k * NI + it) * 64 + lane;
-                    blk[(vv & 7) * (P * 64 + 1) + (vv >> 3)] = src[it];
-                }
-            };
-            static_for<0, LINE2_RW>([&](auto U) { issue(S0 + decltype(U)::value, ringv[decltype(U)::value]); });
-            auto rstep = [&](int sg, auto U) {
-                constexpr int u = decltype(U)::value;
-                if (sg > St) return;
-                write(sg, ringv[u]);
-                issue(sg + LINE2_RW, ringv[u]);
-                line_barrier();
-            };
-            for (int sg = S0; sg <= St; sg += LINE2_RW)
-                static_for<0, LINE2_RW>([&](auto U) { rstep(sg + decltype(U)::value, U); });
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // launch
 // ---------------------------------------------------------------------------
 #ifndef LINE_DH_OVERRIDE
@@ -1362,7 +896,6 @@ static int launch_line_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g
 template <int NA, bool RHS_NAT, int OUT>
 static int launch_line_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a)
 {
-    using SL = LineSlot<LINE_P, NA, RHS_NAT>;
     const int lds = line_lds_bytes<LINE_P, NA, RHS_NAT, OUT, LINE_D>();
     if (lds > 160 * 1024) return LSSP_AMD_EUNSUPPORTED;
     // diagnostics only: LSSP_AMD_LINE_TRACE=path[:tile] appends one JSON line per sweep
@@ -1385,61 +918,6 @@ static int launch_line_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a
     if (f) {
         fprintf(f, "{\"mirror\": %d, \"ntiles\": %d, \"W\": %d, \"ttile\": %d, \"T\": %d, \"grid\": %d, \"data\": [",
                 a.mirror, ls.ntiles, (ls.ny + 63) / 64, g.ttile, ls.h_tiles[g.ttile].T, grid);
-        for (size_t i = 0; i < tn; i++) fprintf(f, "%s%llu", i ? ", " : "", h[i]);
-        fprintf(f, "]}\n");
-        fclose(f);
-    }
-    return LSSP_AMD_OK;
-}
-
-#ifndef LINE2_DH_OVERRIDE
-constexpr int LINE2_DH = 3;
-#else
-constexpr int LINE2_DH = LINE2_DH_OVERRIDE;
-#endif
-constexpr int LINE2_NL = 3, LINE2_D = 4, LINE2_SW = 2;
-
-template <int NA, bool RHS_NAT, int OUT, bool TRACE>
-static int launch_line2_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)
-{
-    auto kern = k_line2<LINE_P, LINE_M, NA, RHS_NAT, OUT, LINE2_NL, LINE2_D, LINE2_DH, LINE2_SW, TRACE>;
-    static int attr = 0;
-    if (lds > attr) {
-        LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        attr = lds;
-    }
-    const int grid = std::min(ls.ntiles, c->num_cus);
-    kern<<<grid, 64 * line2_waves<LINE2_NL, LINE2_SW, RHS_NAT>(), lds, c->stream>>>(g);
-    ls.base += (unsigned long long)ls.ntiles + grid;
-    LSSP_HIP(hipGetLastError());
-    return LSSP_AMD_OK;
-}
-
-template <int NA, bool RHS_NAT, int OUT>
-static int launch_line2_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a)
-{
-    constexpr int lds = line2_lds_bytes<LINE_P, LINE_M, NA, RHS_NAT, OUT, LINE2_D>();
-    static_assert(lds <= 160 * 1024, "LDS");
-    static const char *trp = getenv("LSSP_AMD_LINE_TRACE");
-    if (!trp) return launch_line2_k<NA, RHS_NAT, OUT, false>(c, ls, a, lds);
-    LineArgs g = a;
-    const size_t tn = 8 * (size_t)ls.ntiles + 8 * (size_t)ls.tmax + 64;
-    const char *colon = strrchr(trp, ':');
-    g.ttile = colon ? atoi(colon + 1) : ls.ntiles / 2;
-    LSSP_HIP(hipMalloc(&g.trace, sizeof(unsigned long long) * tn));
-    LSSP_HIP(hipMemsetAsync(g.trace, 0, sizeof(unsigned long long) * tn, c->stream));
-    const int grid = std::min(ls.ntiles, c->num_cus);
-    LSSP_TRY((launch_line2_k<NA, RHS_NAT, OUT, true>(c, ls, g, lds)));
-    std::vector<unsigned long long> h(tn);
-    LSSP_HIP(hipMemcpyAsync(h.data(), g.trace, sizeof(unsigned long long) * tn, hipMemcpyDeviceToHost, c->stream));
-    LSSP_HIP(hipStreamSynchronize(c->stream));
-    (void)hipFree(g.trace);
-    std::string path(trp, colon ? colon - trp : strlen(trp));
-    FILE *f = fopen(path.c_str(), "a");
-    if (f) {
-        const int T = ls.h_tiles[g.ttile].T;
-        fprintf(f, "{\"mirror\": %d, \"ntiles\": %d, \"W\": %d, \"ttile\": %d, \"T\": %d, \"M\": %d, \"grid\": %d, \"data\": [",
-                a.mirror, ls.ntiles, (ls.ny + 63) / 64, g.ttile, (T + LINE_M - 1) / LINE_M, LINE_M, grid);
         for (size_t i = 0; i < tn; i++) fprintf(f, "%s%llu", i ? ", " : "", h[i]);
         fprintf(f, "]}\n");
         fclose(f);
@@ -1474,12 +952,6 @@ static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const doub
     {
         const char *dg = getenv("LSSP_AMD_LINE_DIAG");
         a.diag = dg ? atoi(dg) : 0;
-    }
-    // an apply (L into the U rhs stream, U from it) runs k_line2 when the streams
-    // are laid out in M-level steps; single sweeps (natural in and out) run k_line
-    if (ls.M == LINE_M && LINE_M > 1) {
-        if (u_in) return launch_line2_t<4, false, 1>(c, ls, a);
-        if (out_u) return ls.NA == 3 ? launch_line2_t<3, true, 2>(c, ls, a) : launch_line2_t<4, true, 2>(c, ls, a);
     }
     if (u_in) return launch_line_t<4, false, 1>(c, ls, a);
     if (out_u) return ls.NA == 3 ? launch_line_t<3, true, 2>(c, ls, a) : launch_line_t<4, true, 2>(c, ls, a);

@@ -1,5 +1,5 @@
 // tri_bp.cpp -- host setup of the block-pipelined triangular sweeps
-// (tri_mode 9, k_tri_pk6; tri_mode 4, k_tri_pk: trisolve.hip).
+// (k_tri_pk6, trisolve.hip).
 //
 // The factor's rows, in sweep order (q = r for L, q = n-1-r for U), are cut
 // into contiguous blocks of B rows with B >= the factor's bandwidth, so every
@@ -35,12 +35,7 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
         unit &= (upper ? Tx[Tp[i]] : Tx[Tp[i + 1] - 1]) == 1.0;
         for (int k = strict_begin(i); k < strict_end(i); k++) bw = std::max(bw, std::abs(i - Tj[k]));
     }
-    const char *em = getenv("LSSP_AMD_TRI_BP_MULT");
-    long mult = em ? atol(em) : 0;
-    const long nbw = (n + (long)bw - 1) / bw;
-    if (mult <= 0) mult = 1;  // measured best on 7-pt 216^3 (tools/bench_trisolve.py)
-    (void)nbw;
-    long B = std::max(64L, mult * (long)bw);
+    long B = std::max(64L, (long)bw);  // one bandwidth per block: measured best
     if (B > n) B = n;
     const int nb = (int)((n + B - 1) / B);
 
@@ -109,29 +104,16 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
         rp[p + 1] = (int)cols.size();
     }
     {
-        // v6 packets (tri_mode 9); the rhs of the U sweep is the L sweep's
-        // output, read in L's schedule order
-        // LSSP_AMD_TRI_RNAT=1: the L sweep's loader gathers the rhs straight
-        // from the caller's natural-order vector (rhs_nat) instead of the
-        // permutation kernel into L order -- measured slower
-        const char *en = getenv("LSSP_AMD_TRI_RNAT");
-        const bool rnat = !upper && !prod && en && atoi(en) != 0;
+        // v6 packets; the rhs of the U sweep is the L sweep's output, read in
+        // L's schedule order (the L sweep's rhs is permuted into L order first)
         std::vector<int> rhs_index(n);
-        for (int r = 0; r < n; r++)
-            rhs_index[r] = prod && !prod->h_pos.empty() ? prod->h_pos[r] : rnat ? r : pos[r];
+        for (int r = 0; r < n; r++) rhs_index[r] = prod && !prod->h_pos.empty() ? prod->h_pos[r] : pos[r];
         const int st6 = build_packets6(n, perm, pos, rp, cols, vals, diag, unit, step_pos, blk_step, nb, B,
                                        rhs_index, t);
-        if (st6 == LSSP_AMD_EUNSUPPORTED) t.pk6_n = -1;  // mode 9 falls back to mode 4
+        // a row longer than the longest record: the sync-free sweep serves the factor
+        if (st6 == LSSP_AMD_EUNSUPPORTED) t.pk6_n = -1;
         else if (st6 != LSSP_AMD_OK) return st6;
-        t.rhs_nat = rnat && t.pk6_n > 0;
         if (!upper) t.h_pos = pos;
-        // v1 packets (tri_mode 4): when selected, or as mode 9's fallback
-        t.pk_n = -1;
-        if (c->tri_mode == 4 || t.pk6_n < 0) {
-            const int st = build_packets(n, perm, rp, cols, vals, diag, unit, step_pos, blk_step, nb, B, t);
-            if (st == LSSP_AMD_EUNSUPPORTED) t.pk_n = -1;  // a row too long for a packet: mode 0 serves it
-            else if (st != LSSP_AMD_OK) return st;
-        }
     }
     t.bp_B = (int)B;
     t.upper = upper;
@@ -148,74 +130,7 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
     return LSSP_AMD_OK;
 }
 
-// Packet layout (4-byte words, every packet 16-byte aligned):
-//   [0] nrows  [1] nent  [2] block-local position of the first row  [3] 0
-//   rows[nrows]  rp[nrows+1] (packet-local)  codes[nent]  (pad to 8 bytes)
-//   vals[nent] (double)  diag[nrows] (double, only when the diagonal is not 1)
-// A packet holds rows of ONE step (level) of one block, in schedule order.
-int build_packets(int n, const std::vector<int> &perm, const std::vector<int> &rp,
-                  const std::vector<int> &cols, const std::vector<double> &vals,
-                  const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
-                  const std::vector<int> &blk_step, int nb, long B, TriSched &t)
-{
-    auto words = [&](int nr, int ne) {
-        long w = 5 + 2L * nr + ne;
-        w = (w + 1) & ~1L;
-        w += 2L * ne + (unit ? 0 : 2L * nr);
-        return (w + 3) & ~3L;
-    };
-    std::vector<int> blk(nb + 1, 0), off(1, 0);
-    std::vector<uint32_t> data;
-    for (int b = 0; b < nb; b++) {
-        blk[b] = (int)off.size() - 1;
-        for (int s = blk_step[b]; s < blk_step[b + 1]; s++) {
-            int p = step_pos[s];
-            while (p < step_pos[s + 1]) {
-                int nr = 0, ne = 0;
-                while (p + nr < step_pos[s + 1] && nr < PK_ROWS) {
-                    const int e = rp[p + nr + 1] - rp[p + nr];
-                    if (words(nr + 1, ne + e) * 4 > PK_BYTES) break;
-                    nr++;
-                    ne += e;
-                }
-                if (nr == 0) return LSSP_AMD_EUNSUPPORTED;  // one row does not fit a packet
-                const size_t o = data.size();
-                data.resize(o + words(nr, ne), 0u);
-                uint32_t *w = data.data() + o;
-                w[0] = nr;
-                w[1] = ne;
-                w[2] = (uint32_t)(p - (long)b * B);
-                for (int r = 0; r < nr; r++) w[4 + r] = (uint32_t)perm[p + r];
-                for (int r = 0; r <= nr; r++) w[4 + nr + r] = (uint32_t)(rp[p + r] - rp[p]);
-                for (int e = 0; e < ne; e++) w[5 + 2 * nr + e] = (uint32_t)cols[rp[p] + e];
-                long vo = (5 + 2L * nr + ne + 1) & ~1L;
-                memcpy(w + vo, vals.data() + rp[p], sizeof(double) * ne);
-                if (!unit) memcpy(w + vo + 2L * ne, diag.data() + p, sizeof(double) * nr);
-                off.push_back((int)(data.size() / 4));
-                p += nr;
-            }
-        }
-    }
-    blk[nb] = (int)off.size() - 1;
-    t.pk_n = (int)off.size() - 1;
-    LSSP_HIP(hipMalloc(&t.pk_blk, sizeof(int) * (nb + 1)));
-    LSSP_HIP(hipMemcpy(t.pk_blk, blk.data(), sizeof(int) * (nb + 1), hipMemcpyHostToDevice));
-    LSSP_HIP(hipMalloc(&t.pk_off, sizeof(int) * off.size()));
-    LSSP_HIP(hipMemcpy(t.pk_off, off.data(), sizeof(int) * off.size(), hipMemcpyHostToDevice));
-    LSSP_HIP(hipMalloc(&t.pk_data, sizeof(uint32_t) * std::max<size_t>(data.size(), 4)));
-    if (!data.empty())
-        LSSP_HIP(hipMemcpy(t.pk_data, data.data(), sizeof(uint32_t) * data.size(), hipMemcpyHostToDevice));
-    LSSP_HIP(hipMalloc(&t.pk_claim, sizeof(unsigned long long)));
-    LSSP_HIP(hipMemset(t.pk_claim, 0, sizeof(unsigned long long)));
-    t.pk_base = 0;
-    (void)n;
-    return LSSP_AMD_OK;
-}
-
-
-
-
-// Packets v6 (tri_mode 9, trisolve.hip k_tri_pk6).  The sweeps exchange values
+// Packets v6 (trisolve.hip k_tri_pk6).  The sweeps exchange values
 // through "shadow" vectors kept in schedule order (position p holds the value
 // of row perm[p]), so the cross-block operands of a packet and its output are
 // contiguous runs instead of one cache line per row.  Per packet:

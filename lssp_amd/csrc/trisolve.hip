@@ -1,11 +1,12 @@
 // trisolve.hip -- the ILU triangular sweeps (solver-tri.cxx:4-60) on gfx950.
 //
-// tri_mode 9 (default): role-split packet pipeline through schedule-ordered
-// shadow vectors (k_tri_pk6, packets from tri_bp.cpp build_packets6); tri_mode
-// 4: the first packet pipeline (k_tri_pk, build_packets), used when a factor
-// has rows longer than the v6 record holds; tri_mode 0 / 2: the sync-free
-// level-ordered sweep (also the single-sweep API's path); tri_mode 1: one
-// launch per level.  DESIGN.md 5 has the measurements behind the choice.
+// Structured ILU(0) factors of 5-/7-point grids run the line sweeps
+// (linesweep.hip).  Every other factor (ILUK(k>0), ILUT, block-Jacobi, general
+// patterns): the role-split packet pipeline through schedule-ordered shadow
+// vectors (k_tri_pk6, packets from tri_bp.cpp build_packets6), or -- when a
+// factor has rows longer than the longest packet record, and for the
+// single-sweep API -- the sync-free level-ordered sweep (k_trisolve).
+// DESIGN.md 3.4 has the measurements behind the choice.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -55,17 +56,20 @@ __device__ __forceinline__ uint64_t ld_agent(const double *p)
                              __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// a published value never carries the flag pattern: a computed NaN with the
+// sentinel's payload (e.g. propagated from such an rhs entry) becomes the
+// default quiet NaN, so no reader waits for it
 __device__ __forceinline__ void st_agent(double *p, double v)
 {
-    __hip_atomic_store(reinterpret_cast<uint64_t *>(p), (uint64_t)__double_as_longlong(v),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t b = (uint64_t)__double_as_longlong(v);
+    if (b == TRI_SENTINEL) b = 0x7FF8000000000000ull;
+    __hip_atomic_store(reinterpret_cast<uint64_t *>(p), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Sync-free sweep.  First pass over a row's entries loads them in batches of
 // four; once a dependency is found missing, the lane re-polls only that one
 // entry (one load per lane per poll) with an exponential back-off, so waves
 // far ahead of the wavefront do not flood the memory system with polls.
-template <int BACKOFF>
 __global__ __launch_bounds__(256) void k_trisolve(TriArgs a)
 {
     const int lane = threadIdx.x & 63;
@@ -121,48 +125,10 @@ __global__ __launch_bounds__(256) void k_trisolve(TriArgs a)
                 break;
             }
             for (int q = 0; q < nap; q++) __builtin_amdgcn_s_sleep(2);
-            if (BACKOFF && nap < 32) nap <<= 1;
+            if (nap < 32) nap <<= 1;
         }
     }
 }
-
-// Level-synchronous alternative: one launch per level, every dependency lies in
-// an earlier launch, so plain loads suffice and nothing waits.
-__global__ __launch_bounds__(256) void k_trisolve_level(TriArgs a, int lo, int hi)
-{
-    const int p = lo + blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= hi) return;
-    const int row = a.perm[p];
-    double acc = a.rhs[row];
-    if (a.reset) a.reset[row] = __longlong_as_double((long long)TRI_SENTINEL);
-    for (int k = a.rp[p]; k < a.rp[p + 1]; k++) acc = acc - a.vals[k] * a.x[a.cols[k]];
-    a.x[row] = a.unit ? acc : acc / a.diag[p];
-}
-
-// Packet-streamed block pipeline (tri_mode 4, packets from tri_bp.cpp).
-// Blocks are claimed in sweep order as in k_tri_bp.  Inside a block the
-// workgroup streams its packets (one level's rows each) through a 3-slot LDS
-// ring: while it computes packet q it loads packet q+2 with 16-byte loads and
-// gathers the right-hand side of packet q+1, so only the x dependencies are
-// on the critical path.  Same-block values of the last BP_RING positions come
-// from the LDS value ring; all other x values are read with agent-scope loads
-// and, because x is armed with TRI_SENTINEL before the sweep, a value that is
-// not yet visible is simply re-read (value-as-flag): no store drains, no
-// progress words.  A block only ever waits on the block before it, which was
-// claimed earlier by a running workgroup, so the sweep always drains.
-struct PkArgs {
-    int nb;
-    const int *blk, *off;
-    const int4 *data;
-    int unit;
-    const double *rhs;
-    double *x;
-    double *reset;
-    unsigned long long *claim;
-    unsigned long long base;
-    int *err;
-    int diag;  // diagnostics only (LSSP_AMD_TRI_DIAG): 1 = no waiting, 2 = no cross-block loads
-};
 
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() is a
 // workgroup-scope fence + s_barrier, which on gfx950 also waits vmcnt(0): every
@@ -172,115 +138,6 @@ struct PkArgs {
 __device__ __forceinline__ void lds_barrier()
 {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-__device__ __forceinline__ double ld_ready(const double *p, int *err)
-{
-    uint64_t bits = ld_agent(p);
-    if (bits == TRI_SENTINEL) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        do {
-            __builtin_amdgcn_s_sleep(1);
-            bits = ld_agent(p);
-            if (bits != TRI_SENTINEL) break;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s
-                atomicOr(err, 4);
-                return __longlong_as_double(0x7FF8000000000000ll);
-            }
-        } while (true);
-    }
-    return __longlong_as_double((long long)bits);
-}
-
-constexpr int PK_VEC = PK_BYTES / 16;         // int4 per packet slot
-constexpr int PK_LD = (PK_VEC + 255) / 256;   // int4 loads per thread to stage one packet
-
-__global__ __launch_bounds__(256) void k_tri_pk(PkArgs a)
-{
-    __shared__ double ring[BP_RING];
-    __shared__ int4 pbuf[3][PK_VEC];
-    __shared__ double rbuf[3][PK_ROWS];
-    __shared__ int s_blk;
-    const int tid = threadIdx.x;
-    for (;;) {
-        __syncthreads();
-        if (tid == 0) s_blk = (int)(atomicAdd(a.claim, 1ull) - a.base);
-        __syncthreads();
-        const int b = s_blk;
-        if (b >= a.nb) break;
-        const int q0 = a.blk[b], q1 = a.blk[b + 1];
-        // prologue: packets q0, q0+1 into slots 0, 1; rhs of q0 into rbuf[0]
-        for (int j = 0; j < 2 && q0 + j < q1; j++) {
-            const int o = a.off[q0 + j], len = a.off[q0 + j + 1] - o;
-            for (int i = tid; i < len; i += 256) pbuf[j][i] = a.data[o + i];
-        }
-        __syncthreads();
-        {
-            const int *w = reinterpret_cast<const int *>(pbuf[0]);
-            if (tid < w[0]) rbuf[0][tid] = a.rhs[w[4 + tid]];
-        }
-        __syncthreads();
-        for (int q = q0; q < q1; q++) {
-            const int cur = (q - q0) % 3, nxt = (cur + 1) % 3, nn = (cur + 2) % 3;
-            // (1) stage packet q+2
-            int4 st[PK_LD];
-            int o2 = 0, len2 = 0;
-            if (q + 2 < q1) {
-                o2 = a.off[q + 2];
-                len2 = a.off[q + 3] - o2;
-#pragma unroll
-                for (int u = 0; u < PK_LD; u++) {
-                    const int i = tid + 256 * u;
-                    if (i < len2) st[u] = a.data[o2 + i];
-                }
-            }
-            // (2) gather the right-hand side of packet q+1
-            double rh = 0;
-            bool have_rh = false;
-            if (q + 1 < q1) {
-                const int *w = reinterpret_cast<const int *>(pbuf[nxt]);
-                if (tid < w[0]) {
-                    rh = a.rhs[w[4 + tid]];
-                    have_rh = true;
-                }
-            }
-            // (3) packet q
-            {
-                const int *w = reinterpret_cast<const int *>(pbuf[cur]);
-                const int nr = w[0], ne = w[1], pos0 = w[2];
-                if (tid < nr) {
-                    const int *rows = w + 4, *rp = w + 4 + nr, *codes = w + 5 + 2 * nr;
-                    const int vo = (5 + 2 * nr + ne + 1) & ~1;
-                    const double *vals = reinterpret_cast<const double *>(w + vo);
-                    const int row = rows[tid];
-                    double acc = rbuf[cur][tid];
-                    if (a.reset) a.reset[row] = __longlong_as_double((long long)TRI_SENTINEL);
-                    for (int k = rp[tid]; k < rp[tid + 1]; k++) {
-                        const int code = codes[k];
-                        double xv;
-                        if (code < 0) xv = ring[-1 - code];
-                        else if (a.diag == 0) xv = ld_ready(a.x + code, a.err);
-                        else if (a.diag == 1) xv = __longlong_as_double((long long)ld_agent(a.x + code));
-                        else xv = 0.0;
-                        acc = acc - vals[k] * xv;
-                    }
-                    const double xi = a.unit ? acc : acc / reinterpret_cast<const double *>(w + vo + 2 * ne)[tid];
-                    ring[(pos0 + tid) % BP_RING] = xi;
-                    st_agent(a.x + row, xi);
-                }
-            }
-            // (4) land the staged data
-            if (q + 2 < q1) {
-#pragma unroll
-                for (int u = 0; u < PK_LD; u++) {
-                    const int i = tid + 256 * u;
-                    if (i < len2) pbuf[nn][i] = st[u];
-                }
-            }
-            if (have_rh) rbuf[nxt][tid] = rh;
-            lds_barrier();
-        }
-    }
 }
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -321,15 +178,12 @@ struct PkLd {
     int rlen;   // record length in 16-byte units (0: none)
 };
 
-// tri_mode 9: packets v6 (tri_bp.cpp build_packets6) with schedule-ordered
-// shadow vectors.  the loader/compute role split of the earlier packet kernels, plus:
+// Packets v6 (tri_bp.cpp build_packets6) with schedule-ordered shadow vectors:
+// compute and loader roles, and
 //   * the sweep's output goes to a shadow vector in schedule order with
 //     coalesced agent-scope stores (position pos0+t), and the HBM operands of
 //     a packet are read from that shadow by schedule position: for a stencil
 //     both are contiguous runs (one line per 8 rows instead of one per row);
-//   * when the natural-order output is wanted too (the U sweep), a store wave
-//     (wave 8) writes it from the LDS value ring one step later with plain
-//     stores; it never waits on its vmcnt, so neither do the compute waves;
 //   * arming for the next apply: the shadows are double-buffered, and every
 //     block fills its own position range of the other buffer with
 //     TRI_SENTINEL when it is done (coalesced).
@@ -345,16 +199,11 @@ struct Pk6Args {
     const double *rhs;   // rhs entries, indexed by the packet's rhs indices
     double *sh;          // this sweep's shadow (schedule order), armed with TRI_SENTINEL
     double *sh_next;     // the other shadow buffer: armed here for the next apply
-    double *nat;         // natural-order output (nullptr: none)
     int n, B;
     int unit;  // unit diagonal (ILUK / ILUT L): x / 1.0 == x, the division is skipped
     unsigned long long *claim;
     unsigned long long base;
     int *err;
-    int diag;
-    unsigned long long *trace;
-    unsigned long long *trace2;  // diagnostics (LSSP_AMD_TRI_TRACE2): per-step clocks of blocks tb0, tb0+1
-    int tb0;
 };
 
 template <int EP>
@@ -365,7 +214,6 @@ struct Pk6Rec {
     CW c[NCW];
     double v[EP];
     double dg;
-    int row;
     int nr, pos0;
     __device__ __forceinline__ int code(int e) const
     {
@@ -394,8 +242,8 @@ __device__ __forceinline__ T &sel4(T &a, T &b, T &c, T &d)
 // registers; the loader lanes fetch it KE steps ahead with the gathers and land
 // it in an LDS slot at the end of the step before, and the compute lanes read
 // it from there (D unused).
-template <int EP, int KE, int IA, int D, bool NAT, int NR, bool LREC = false>
-__global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args a)
+template <int EP, int KE, int IA, int D, int NR, bool LREC = false>
+__global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
 {
     constexpr int Q = 4;
     static_assert(D + 1 <= Q && IA <= Q && KE >= 1 && IA - KE >= 1 && IA - KE <= 2, "pipeline depths");
@@ -404,44 +252,21 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
     __shared__ double ring[BP_RING + 1];
     __shared__ double rbuf[2][NR];
     __shared__ double xbuf[2][NR * PK3_EXT];
-    __shared__ int rowbuf[2][NR];
     __shared__ int4 sdesc[PK3_CAP];
     __shared__ v4u recbuf[LREC ? 2 : 1][LREC ? PK6_REC16 : 1];
     __shared__ int s_blk;
-    __shared__ unsigned s_polls;
     const int tid = threadIdx.x;
-    const int role = __builtin_amdgcn_readfirstlane(tid) / NR;  // 0 compute, 1 loader, 2 store
-    static_assert(!NAT || NR == 256, "the store wave needs a 256-row packet");
+    const int role = __builtin_amdgcn_readfirstlane(tid) / NR;  // 0 compute, 1 loader
     const int t = tid & (NR - 1);
     if (tid == 0) ring[BP_RING] = 0.0;
-    int prev = -1;
     for (;;) {
         __syncthreads();
-        if (tid == 0) {
-            if (a.trace && prev >= 0) {
-                a.trace[8 * prev + 1] = __builtin_amdgcn_s_memrealtime();
-                a.trace[8 * prev + 2] = s_polls;
-            }
-            s_polls = 0;
-            s_blk = (int)(atomicAdd(a.claim, 1ull) - a.base);
-        }
+        if (tid == 0) s_blk = (int)(atomicAdd(a.claim, 1ull) - a.base);
         __syncthreads();
         const int b = s_blk;
         if (b >= a.nb) break;
-        if (a.trace && tid == 0) {
-            unsigned xcc;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            a.trace[8 * b] = __builtin_amdgcn_s_memrealtime();
-            a.trace[8 * b + 3] = xcc;
-        }
-        prev = b;
         const int q0 = a.blk[b], np = a.blk[b + 1] - q0;
         const int bbase = b * a.B;  // first schedule position of the block
-        const bool tr2 = a.trace2 && (b == a.tb0 || b == a.tb0 + 1);
-        auto mark = [&](int j, int k) {
-            if (tr2 && j >= -8 && j < 1016)
-                a.trace2[((long)(b - a.tb0) * 1024 + (j + 8)) * 4 + k] = __builtin_amdgcn_s_memrealtime();
-        };
         for (int i = tid; i < np; i += blockDim.x) sdesc[i] = a.desc[q0 + i];
         __syncthreads();
         // both roles run steps J0 .. J0+T-1 (T a multiple of Q); out-of-range
@@ -495,22 +320,19 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                     const double xi = a.unit ? acc : acc / dg;
                     const int pos = d.w + t;
                     ring[(pos - bbase) & (BP_RING - 1)] = xi;
-                    if (!(a.diag & 2)) st_agent(a.sh + pos, xi);
+                    st_agent(a.sh + pos, xi);
                 }
                 lds_barrier();
             }
-            if (!(a.diag & 1)) {
-                const long s0 = bbase, s1 = min(s0 + a.B, (long)a.n);
-                uint64_t *rs = reinterpret_cast<uint64_t *>(a.sh_next);
-                for (long i = s0 + t; i < s1; i += NR) rs[i] = TRI_SENTINEL;
-            }
+            const long s0 = bbase, s1 = min(s0 + a.B, (long)a.n);
+            uint64_t *rs = reinterpret_cast<uint64_t *>(a.sh_next);
+            for (long i = s0 + t; i < s1; i += NR) rs[i] = TRI_SENTINEL;
         } else if (role == 0) {
-            uint64_t c0 = 0, c1 = 0, acc_c = 0, acc_b = 0;
             auto issue = [&](const int4 d, Pk6Rec<EP> &Rr) {
                 const int nr = d.z & 0x3ff;
                 const int n1 = nr > 0 ? nr : 1, tt = min(t, n1 - 1);
                 const uint32_t *base = a.rec + 4L * d.x;
-                const int wc = ((EP / 2) * n1 + 3) & ~3, wd = (2 * n1 + 3) & ~3;
+                const int wc = ((EP / 2) * n1 + 3) & ~3;
 #pragma unroll
                 for (int q = 0; q < Pk6Rec<EP>::NCW; q++)
                     Rr.c[q] = reinterpret_cast<const typename Pk6Rec<EP>::CW *>(base)[Pk6Rec<EP>::NCW * tt + q];
@@ -525,13 +347,11 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                 // unit diagonal (ILUK / ILUT L): the stored 1.0 is never read -- 8 bytes
                 // per row less on the sweep's record stream
                 Rr.dg = a.unit ? 1.0 : reinterpret_cast<const double *>(vb + (EP / 2) * n1)[tt];
-                if (NAT) Rr.row = reinterpret_cast<const int *>(base + wc + 2 * EP * n1 + wd)[tt];
                 Rr.nr = nr;
                 Rr.pos0 = d.w;
             };
             int4 dn = descc(J0 + D);  // descriptor of packet j+D, read one step ahead
             auto step = [&](int j, Pk6Rec<EP> &Rc, Pk6Rec<EP> &Rn) {
-                if (a.trace) c0 = __builtin_amdgcn_s_memtime();
                 issue(dn, Rn);
                 dn = descc(j + D + 1);
                 // the current record must be complete here, at one fixed point
@@ -540,7 +360,6 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
 #pragma unroll
                 for (int e = 0; e < EP; e++) asm volatile("" ::"v"(Rc.v[e]));
                 asm volatile("" ::"v"(Rc.dg));
-                if (NAT) asm volatile("" ::"v"(Rc.row));
                 if (t < Rc.nr) {  // nr == 0 outside the block's packets
                     const double *xb = xbuf[j & 1];
                     double acc = rbuf[j & 1][t];
@@ -556,17 +375,9 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                     const double xi = a.unit ? acc : acc / Rc.dg;
                     const int pos = Rc.pos0 + t;
                     ring[(pos - bbase) & (BP_RING - 1)] = xi;
-                    if (NAT) rowbuf[j & 1][t] = Rc.row;
-                    if (!(a.diag & 2)) st_agent(a.sh + pos, xi);
+                    st_agent(a.sh + pos, xi);
                 }
-                if (a.trace) c1 = __builtin_amdgcn_s_memtime();
-                if (tid == 0) mark(j, 0);
                 lds_barrier();
-                if (a.trace) {
-                    const uint64_t c2 = __builtin_amdgcn_s_memtime();
-                    acc_c += c1 - c0;
-                    acc_b += c2 - c1;
-                }
             };
             Pk6Rec<EP> R0, R1, R2, R3;
             R0.nr = R1.nr = R2.nr = R3.nr = 0;
@@ -577,16 +388,10 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                 step(j0 + 3, sel4<3>(R0, R1, R2, R3), sel4<(3 + D) % Q>(R0, R1, R2, R3));
             }
             // arm the block's positions of the other shadow for the next apply
-            if (!(a.diag & 1)) {
-                const long s0 = bbase, s1 = min(s0 + a.B, (long)a.n);
-                uint64_t *rs = reinterpret_cast<uint64_t *>(a.sh_next);
-                for (long i = s0 + t; i < s1; i += NR) rs[i] = TRI_SENTINEL;
-            }
-            if (a.trace && tid == 0) {
-                a.trace[8 * b + 4] = acc_c;
-                a.trace[8 * b + 5] = acc_b;
-            }
-        } else if (role == 1) {
+            const long s0 = bbase, s1 = min(s0 + a.B, (long)a.n);
+            uint64_t *rs = reinterpret_cast<uint64_t *>(a.sh_next);
+            for (long i = s0 + t; i < s1; i += NR) rs[i] = TRI_SENTINEL;
+        } else {
             // The loader's loads are issued from inline asm with explicit
             // vmcnt waits: its register sets rotate across the loop back-edge,
             // where the compiler's own wait counting turns conservative and
@@ -616,7 +421,6 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                     L.rlen = nr > 0 ? len : 0;
                 }
             };
-            uint64_t acc_w = 0, acc_lb = 0, acc_is = 0, acc_ld = 0, m0 = 0;
             auto issue_idx = [&](const int4 d, PkLd &L) {
                 const int nr = d.z & 0x3ff, nx = (d.z >> 10) & 0x7ff;
                 const int *base = a.idx + d.y;
@@ -631,29 +435,19 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
             };
             auto gather = [&](PkLd &L) {
                 asm volatile("s_waitcnt vmcnt(%3)" : "+v"(L.row), "+v"(L.xi[0]), "+v"(L.xi[1]) : "n"(WAIT_IDX) : "memory");
-                const double *pr = a.rhs + ((a.diag & 4) ? t : L.row);
-                const double *px0 = a.sh + ((a.diag & 8) ? 0 : L.xi[0]);
-                const double *px1 = a.sh + ((a.diag & 8) ? 0 : L.xi[1]);
+                const double *pr = a.rhs + L.row;
+                const double *px0 = a.sh + L.xi[0];
+                const double *px1 = a.sh + L.xi[1];
                 asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(L.rh) : "v"(pr) : "memory");
                 asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(L.ev[0]) : "v"(px0) : "memory");
                 asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(L.ev[1]) : "v"(px1) : "memory");
             };
             int4 dl = descc(J0 + IA);  // descriptor of packet j+IA, read one step ahead
             auto step = [&](int j, PkLd &Li, PkLd &Lg, PkLd &Ll) {
-                if (a.diag & 16) {  // timing experiment: loader idle
-                    lds_barrier();
-                    return;
-                }
-                if (a.trace) m0 = __builtin_amdgcn_s_memtime();
                 issue_rec(descc(j + KE), Lg);
                 issue_idx(dl, Li);
                 gather(Lg);
                 dl = descc(j + IA + 1);
-                uint64_t l0 = 0;
-                if (a.trace) {
-                    l0 = __builtin_amdgcn_s_memtime();
-                    acc_is += l0 - m0;
-                }
                 // gathers of packet j+1 were issued at step j+1-KE
                 if constexpr (LREC)
                     asm volatile("s_waitcnt vmcnt(%7)"
@@ -663,12 +457,6 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                                  : "memory");
                 else
                     asm volatile("s_waitcnt vmcnt(%3)" : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]) : "n"(WAIT_G) : "memory");
-                uint64_t l2 = 0;
-                if (a.trace) {
-                    l2 = __builtin_amdgcn_s_memtime();
-                    acc_w += l2 - l0;
-                }
-                if (tid == NR) mark(j, 2);
                 // land packet j+1 (nr = nx = 0 outside the block's packets)
                 if (t < Ll.nr) rbuf[(j + 1) & 1][t] = Ll.rh;
                 if constexpr (LREC) {
@@ -681,24 +469,11 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
                     const int k = t + NR * e;
                     if (k < Ll.nx) {
                         uint64_t bits = Ll.ev[e];
-                        if (bits == TRI_SENTINEL && !(a.diag & 8)) {
-                            bits = poll_ready(a.sh + Ll.xi[e], a.err);
-                            if (a.trace) atomicAdd(&s_polls, 1u);
-                        }
+                        if (bits == TRI_SENTINEL) bits = poll_ready(a.sh + Ll.xi[e], a.err);
                         xbuf[(j + 1) & 1][k] = __longlong_as_double((long long)bits);
                     }
                 }
-                uint64_t l1 = 0;
-                if (a.trace) {
-                    l1 = __builtin_amdgcn_s_memtime();
-                    acc_ld += l1 - l2;
-                }
-                if (tid == NR) {
-                    mark(j, 1);
-                    if (tr2 && j >= -8 && j < 1016) a.trace2[((long)(b - a.tb0) * 1024 + (j + 8)) * 4 + 3] = s_polls;
-                }
                 lds_barrier();
-                if (a.trace) acc_lb += __builtin_amdgcn_s_memtime() - l1;
             };
             PkLd L0, L1, L2, L3;
             L0.nr = L1.nr = L2.nr = L3.nr = 0;
@@ -719,54 +494,8 @@ __global__ __launch_bounds__(NAT ? 2 * NR + 64 : 2 * NR) void k_tri_pk6(Pk6Args 
             }
 #undef LSSP_PK6_LSTEP
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            (void)acc_lb;
-            if (a.trace && tid == NR) {  // compute's barrier share is dropped here
-                a.trace[8 * b + 5] = acc_w;
-                a.trace[8 * b + 6] = acc_is;
-                a.trace[8 * b + 7] = acc_ld;
-            }
-        } else {
-            // store wave: at step j write packet j-1's values in natural order
-            // (the last step's packet after the loop)
-            const int lane = tid & 63;
-            auto store = [&](int p) {
-                if (NAT && p >= 0 && p < np) {
-                    const int4 d = desc(p);
-                    const int nr = d.z & 0x3ff;
-                    for (int k = lane; k < nr; k += 64)
-                        a.nat[rowbuf[p & 1][k]] = ring[(d.w + k - bbase) % BP_RING];
-                }
-            };
-            for (int j = J0; j < J0 + T; j++) {
-                store(j - 1);
-                lds_barrier();
-            }
-            store(J0 + T - 1);
         }
     }
-}
-
-// diagnostics only (LSSP_AMD_TRI_TRACE): synchronous dump of the per-block
-// trace of one packet sweep, one JSON line (tools/tri_trace.py)
-static int dump_trace(lssp_amd_ctx *c, unsigned long long *d_trace, int nb, int n, int npk, int grid,
-                      const char *path, int width = 8)
-{
-    std::vector<unsigned long long> h(width * (size_t)nb);
-    LSSP_HIP(hipMemcpyAsync(h.data(), d_trace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost,
-                            c->stream));
-    LSSP_HIP(hipStreamSynchronize(c->stream));
-    (void)hipFree(d_trace);
-    FILE *f = fopen(path, "a");
-    if (!f) return LSSP_AMD_OK;
-    fprintf(f, "{\"n\": %d, \"nb\": %d, \"npk\": %d, \"grid\": %d, \"blocks\": [", n, nb, npk, grid);
-    for (int b = 0; b < nb; b++) {
-        fprintf(f, "%s[", b ? ", " : "");
-        for (int k = 0; k < width; k++) fprintf(f, "%s%llu", k ? ", " : "", h[(size_t)width * b + k]);
-        fprintf(f, "]");
-    }
-    fprintf(f, "]}\n");
-    fclose(f);
-    return LSSP_AMD_OK;
 }
 
 int launch_trisolve(lssp_amd_ctx *c, const TriSched &t, const double *rhs, double *x, double *reset)
@@ -774,93 +503,31 @@ int launch_trisolve(lssp_amd_ctx *c, const TriSched &t, const double *rhs, doubl
     if (t.n == 0) return LSSP_AMD_OK;
     long nchunks = (t.n + 63) / 64;
     TriArgs a{t.n, nchunks, t.perm, t.rp, t.cols, t.vals, t.diag, t.unit, rhs, x, reset, c->d_err};
-    if (c->tri_mode == 4 && t.pk_n >= 0) {
-        const int grid = std::min(t.bp_nb, c->num_cus);
-        PkArgs g{t.bp_nb, t.pk_blk, t.pk_off, reinterpret_cast<const int4 *>(t.pk_data), t.unit, rhs, x, reset,
-                 t.pk_claim, t.pk_base, c->d_err, c->tri_diag};
-        k_tri_pk<<<grid, 256, 0, c->stream>>>(g);
-        t.pk_base += (unsigned long long)t.bp_nb + grid;
-        LSSP_HIP(hipGetLastError());
-        return LSSP_AMD_OK;
-    }
-    if (c->tri_mode == 1) {
-        for (int l = 0; l < t.nlevels; l++) {
-            const int lo = t.level_ptr[l], hi = t.level_ptr[l + 1];
-            k_trisolve_level<<<(hi - lo + 255) / 256, 256, 0, c->stream>>>(a, lo, hi);
-        }
-    } else {
-        long grid = (long)c->num_cus * c->tri_blocks_per_cu;
-        long need = (nchunks + 3) / 4;
-        if (grid > need) grid = need;
-        if (c->tri_mode == 2) k_trisolve<0><<<grid, 256, 0, c->stream>>>(a);
-        else k_trisolve<1><<<grid, 256, 0, c->stream>>>(a);
-    }
+    long grid = (long)c->num_cus * c->tri_blocks_per_cu;
+    long need = (nchunks + 3) / 4;
+    if (grid > need) grid = need;
+    k_trisolve<<<grid, 256, 0, c->stream>>>(a);
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;
 }
 
-// tri_mode 9 apply: cache = L^-1 rhs, x = U^-1 cache through the shadows
-template <bool NAT>
-static int launch_pk6(lssp_amd_ctx *c, const TriSched &t, const double *rhs, double *sh, double *sh_next,
-                      double *nat)
+// packet sweep of one factor: its output to the shadow sh (schedule order)
+static int launch_pk6(lssp_amd_ctx *c, const TriSched &t, const double *rhs, double *sh, double *sh_next)
 {
     const int grid = std::min(t.bp_nb, c->num_cus);
-    const char *trace_path = getenv("LSSP_AMD_TRI_TRACE");
-    unsigned long long *d_trace = nullptr;
-    if (trace_path) {
-        LSSP_HIP(hipMalloc(&d_trace, sizeof(unsigned long long) * 8 * t.bp_nb));
-        LSSP_HIP(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * 8 * t.bp_nb, c->stream));
-    }
-    const char *t2 = getenv("LSSP_AMD_TRI_TRACE2");  // "path:block"
-    unsigned long long *d_t2 = nullptr;
-    int tb0 = 0;
-    if (t2) {
-        const char *colon = strrchr(t2, ':');
-        tb0 = colon ? atoi(colon + 1) : t.bp_nb / 2;
-        LSSP_HIP(hipMalloc(&d_t2, sizeof(unsigned long long) * 2 * 1024 * 4));
-        LSSP_HIP(hipMemsetAsync(d_t2, 0, sizeof(unsigned long long) * 2 * 1024 * 4, c->stream));
-    }
     Pk6Args g{t.bp_nb, t.pk6_blk, reinterpret_cast<const int4 *>(t.pk6_desc), t.pk6_rec, t.pk6_idx, rhs, sh,
-              sh_next, nat, t.n, t.bp_B, t.unit, t.pk6_claim, t.pk6_base, c->d_err, c->tri_diag, d_trace, d_t2, tb0};
-    // Instantiated: 256-row packets, x operands gathered 2 steps ahead (KE 2),
-    // EP 4 or 8 -- the variants whose inline-asm loader tools/check_vmcnt.py
+              sh_next, t.n, t.bp_B, t.unit, t.pk6_claim, t.pk6_base, c->d_err};
+    // Instantiated: 256-row packets, x operands gathered 2 steps ahead (KE 2);
+    // EP 4 / 8 with register records, EP 16 / 24 with LDS records -- the
+    // variants whose inline-asm loader tools/check_vmcnt.py
     // (tests/test_isa_vmcnt.py) verifies hazard-free
     if (t.pk6_rows != 256) return LSSP_AMD_EUNSUPPORTED;
-    // pipeline depths (LSSP_AMD_TRI_PIPE): 0 = (KE 2, IA 4, D 3), 1 = (2, 3, 3), 2 = (2, 3, 2),
-    // (measured at 216^3 per apply: KE 1 (IA 2 or 3) 1.83 ms, KE 3 (IA 4, D 3 or 2) 1.63 ms, vs 1.57)
-    const int pd = c->tri_pipe;
-    if constexpr (NAT) {
-        if (t.pk6_ep != 4) return LSSP_AMD_EUNSUPPORTED;
-        k_tri_pk6<4, 2, 4, 3, true, 256><<<grid, 2 * 256 + 64, 0, c->stream>>>(g);
-    } else if (t.pk6_ep == 4) {
-        if (pd == 1) k_tri_pk6<4, 2, 3, 3, false, 256><<<grid, 512, 0, c->stream>>>(g);
-        else if (pd == 2) k_tri_pk6<4, 2, 3, 2, false, 256><<<grid, 512, 0, c->stream>>>(g);
-        else k_tri_pk6<4, 2, 4, 3, false, 256><<<grid, 512, 0, c->stream>>>(g);
-    } else if (t.pk6_ep == 8) {
-        k_tri_pk6<8, 2, 4, 3, false, 256><<<grid, 512, 0, c->stream>>>(g);
-    } else if (t.pk6_ep == 16) {
-        k_tri_pk6<16, 3, 4, 1, false, 256, true><<<grid, 512, 0, c->stream>>>(g);
-    } else {
-        k_tri_pk6<24, 3, 4, 1, false, 256, true><<<grid, 512, 0, c->stream>>>(g);
-    }
+    if (t.pk6_ep == 4) k_tri_pk6<4, 2, 4, 3, 256><<<grid, 512, 0, c->stream>>>(g);
+    else if (t.pk6_ep == 8) k_tri_pk6<8, 2, 4, 3, 256><<<grid, 512, 0, c->stream>>>(g);
+    else if (t.pk6_ep == 16) k_tri_pk6<16, 3, 4, 1, 256, true><<<grid, 512, 0, c->stream>>>(g);
+    else k_tri_pk6<24, 3, 4, 1, 256, true><<<grid, 512, 0, c->stream>>>(g);
     t.pk6_base += (unsigned long long)t.bp_nb + grid;
     LSSP_HIP(hipGetLastError());
-    if (trace_path) LSSP_TRY(dump_trace(c, d_trace, t.bp_nb, t.n, t.pk6_n, grid, trace_path));
-    if (t2) {  // diagnostics only: per-step clocks of two consecutive blocks
-        std::vector<unsigned long long> h(2 * 1024 * 4);
-        LSSP_HIP(hipMemcpyAsync(h.data(), d_t2, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost,
-                                c->stream));
-        LSSP_HIP(hipStreamSynchronize(c->stream));
-        (void)hipFree(d_t2);
-        std::string path(t2, strrchr(t2, ':') ? strrchr(t2, ':') - t2 : strlen(t2));
-        FILE *f = fopen(path.c_str(), "a");
-        if (f) {
-            fprintf(f, "{\"tb0\": %d, \"steps\": [", tb0);
-            for (size_t i = 0; i < h.size(); i++) fprintf(f, "%s%llu", i ? ", " : "", h[i]);
-            fprintf(f, "]}\n");
-            fclose(f);
-        }
-    }
     return LSSP_AMD_OK;
 }
 
@@ -905,15 +572,14 @@ __global__ __launch_bounds__(256) void k_gather4(double *dst, const double *src,
         for (long p = 4 * n4 + threadIdx.x; p < n; p += 256) dst[p] = src[perm[p]];
 }
 
-// tri_mode 9 apply.  The scattered halves of the work -- reading the rhs in L
-// order and writing x in natural order -- run as fully parallel permutation
-// kernels around the two sweeps, so the pipelined sweeps only touch
-// contiguous runs of HBM.  LSSP_AMD_TRI_NAT=1 instead writes x from the U
-// sweep's store wave (timing experiments).
+// ILU apply (solver-tri.cxx:57-60).  Packet sweeps: the scattered halves of
+// the work -- reading the rhs in L order and writing x in natural order -- run
+// as fully parallel permutation kernels around the two sweeps, so the
+// pipelined sweeps only touch contiguous runs of HBM.
 int launch_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const double *rhs)
 {
     if (M->line.ntiles) return launch_line_apply(c, M->line, x, rhs);
-    if (c->tri_mode == 9 && M->lower.pk6_n > 0 && M->upper.pk6_n > 0) {
+    if (M->lower.pk6_n > 0 && M->upper.pk6_n > 0) {
         const int n = M->n;
         if (!M->d_sh[0]) {
             for (int k = 0; k < 4; k++) {
@@ -925,27 +591,16 @@ int launch_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const do
         const int e = M->epoch & 1;
         M->epoch++;
         const int pg = 8 * std::max(1, std::min((n + 2047) / 2048, c->num_cus));  // multiple of 8
-        static const bool perm4 = !(getenv("LSSP_AMD_PERM1") && atoi(getenv("LSSP_AMD_PERM1")));
-        if (!M->lower.rhs_nat) {
-            if (((uintptr_t)rhs & 15) == 0 && perm4)
-                k_gather4<<<pg, 256, 0, c->stream>>>(M->d_rperm, rhs, M->lower.bp_perm, n);
-            else
-                k_perm<true><<<pg, 256, 0, c->stream>>>(M->d_rperm, rhs, M->lower.bp_perm, n);
-            LSSP_HIP(hipGetLastError());
-        }
-        LSSP_TRY(launch_pk6<false>(c, M->lower, M->lower.rhs_nat ? rhs : M->d_rperm, M->d_sh[e], M->d_sh[e ^ 1],
-                                   nullptr));
-        static const bool nat = getenv("LSSP_AMD_TRI_NAT") && atoi(getenv("LSSP_AMD_TRI_NAT"));
-        if (nat && M->upper.pk6_ep == 4)
-            return launch_pk6<true>(c, M->upper, M->d_sh[e], M->d_sh[2 + e], M->d_sh[2 + (e ^ 1)], x);
-        LSSP_TRY(launch_pk6<false>(c, M->upper, M->d_sh[e], M->d_sh[2 + e], M->d_sh[2 + (e ^ 1)], nullptr));
+        if (((uintptr_t)rhs & 15) == 0)
+            k_gather4<<<pg, 256, 0, c->stream>>>(M->d_rperm, rhs, M->lower.bp_perm, n);
+        else
+            k_perm<true><<<pg, 256, 0, c->stream>>>(M->d_rperm, rhs, M->lower.bp_perm, n);
+        LSSP_HIP(hipGetLastError());
+        LSSP_TRY(launch_pk6(c, M->lower, M->d_rperm, M->d_sh[e], M->d_sh[e ^ 1]));
+        LSSP_TRY(launch_pk6(c, M->upper, M->d_sh[e], M->d_sh[2 + e], M->d_sh[2 + (e ^ 1)]));
         // x back to natural order as a gather through the inverse permutation
-        // (coalesced stores, scattered loads: faster than scattering the stores);
-        // LSSP_AMD_TRI_XOUT=scatter keeps the scatter (timing experiments)
-        static const bool xscatter = getenv("LSSP_AMD_TRI_XOUT") && !strcmp(getenv("LSSP_AMD_TRI_XOUT"), "scatter");
-        if (xscatter || !M->upper.bp_pos)
-            k_perm<false><<<pg, 256, 0, c->stream>>>(x, M->d_sh[2 + e], M->upper.bp_perm, n);
-        else if (((uintptr_t)x & 15) == 0 && perm4)
+        // (coalesced stores, scattered loads: faster than scattering the stores)
+        if (((uintptr_t)x & 15) == 0)
             k_gather4<<<pg, 256, 0, c->stream>>>(x, M->d_sh[2 + e], M->upper.bp_pos, n);
         else
             k_perm<true><<<pg, 256, 0, c->stream>>>(x, M->d_sh[2 + e], M->upper.bp_pos, n);

@@ -228,18 +228,13 @@ def _scattered(n, seed, maxlen=20, reach=3000):
     return O.CSR(n, Ap.astype(np.int32), Aj.astype(np.int32), Ax)
 
 
-@pytest.mark.parametrize("xt", ["0", "1", None])
 @pytest.mark.parametrize("which", ["thermal", "scattered"])
-def test_spmv_xtile_bitwise_vs_oracle(dev, monkeypatch, xt, which):
-    """k_spmv_xt (x range staged in LDS per 1024-row block) and k_spmv3 give
-    the oracle's sums bit for bit (mvops.cxx:42-78, 118-150) on scattered-
-    column matrices; LSSP_AMD_SPMV_XT=1 selects the x-tile plan, None is the default."""
+def test_spmv_scattered_bitwise_vs_oracle(dev, which):
+    """k_spmv3 gives the oracle's sums bit for bit (mvops.cxx:42-78, 118-150) on
+    scattered-column matrices (the thermal-like matrix of config 5, random
+    rows of up to 11 entries)."""
     import lssp_amd
     from lssp_amd.synthetic import thermal_like
-    if xt is None:
-        monkeypatch.delenv("LSSP_AMD_SPMV_XT", raising=False)
-    else:
-        monkeypatch.setenv("LSSP_AMD_SPMV_XT", xt)
     if which == "thermal":
         Ap, Aj, Ax = thermal_like(m=150, window=512)
         A = O.CSR(Ap.size - 1, Ap, Aj, Ax)

@@ -1,5 +1,5 @@
-"""SpMV micro-benchmark (tuning aid): y = A x on the 7-pt grid, HIP events on the
-library stream; variant chosen by LSSP_AMD_SPMV (read once per process)."""
+"""SpMV micro-benchmark (tuning aid): y = A x (k_spmv3) on the 7-pt grid, HIP
+events on the library stream."""
 import argparse
 import json
 import os
@@ -37,7 +37,7 @@ def main():
     e1.synchronize()
     ms = e0.elapsed_time(e1) / args.reps
     b = 12 * int(Ap[-1]) + 20 * n + 4
-    print(json.dumps({"variant": os.environ.get("LSSP_AMD_SPMV", "0"), "grid": args.grid, "ms": round(ms, 5),
+    print(json.dumps({"grid": args.grid, "ms": round(ms, 5),
                       "GBps": round(b / ms / 1e6, 1), "sum": float(y.download().sum())}))
 
 
