@@ -54,6 +54,14 @@ typedef struct lssp_amd_ilu lssp_amd_ilu; /* device L/U + trisolve schedules (LS
 const char *lssp_amd_strerror(int status);
 int lssp_amd_version(void);
 
+/* Where the drivers' messages go (the lines the reference prints with
+ * lssp_printf, utils.cxx:93-112: parameters at verb >= 2, the per-iteration
+ * line at verb >= 1, "total iteration" / "total time" at verb >= 2).  fn ==
+ * NULL (the default): stdout, flushed after every line.  The reference-side
+ * binding routes them through lssp_printf, so a log file set with
+ * lssp_set_log receives them too.  Process-wide; fn returns < 0 on error. */
+void lssp_amd_set_print(int (*fn)(void *user, const char *msg), void *user);
+
 /* ---- context: replaces the implicit single host thread ------------------ */
 int lssp_amd_ctx_create(int device, lssp_amd_ctx **ctx);
 int lssp_amd_ctx_destroy(lssp_amd_ctx *ctx);
@@ -79,17 +87,22 @@ int lssp_amd_mat_upload(lssp_amd_ctx *ctx, int nrows, int ncols, int nnz, const 
 int lssp_amd_mat_destroy(lssp_amd_mat *A);
 int lssp_amd_mat_info(const lssp_amd_mat *A, int *nrows, int *ncols, int *nnz);
 
-/* ---- SpMV: mvops.h:9-19 (mvops.cxx:5-150), bitwise per row -------------- */
+/* ---- SpMV: mvops.h:9-19 (mvops.cxx:5-150), bitwise per row --------------
+ * x: for a matrix from lssp_amd_mat_upload the first ncols entries are read.
+ * For a distributed matrix (lssp_amd_mat_upload_dist) x MUST hold
+ * nrows + nhalo entries (lssp_amd_mat_local_rows): the rank's own entries,
+ * then room for the halo, which every product OVERWRITES with the peers'
+ * values before computing -- hence x is not const. */
 /* y = y*beta + alpha*A*x            (lssp_mv_amxpby,  mvops.cxx:33-39)  */
-int lssp_amd_mv_amxpby(lssp_amd_ctx *ctx, double alpha, const lssp_amd_mat *A, const double *x,
+int lssp_amd_mv_amxpby(lssp_amd_ctx *ctx, double alpha, const lssp_amd_mat *A, double *x,
                        double beta, double *y);
 /* z = y*beta + alpha*A*x            (lssp_mv_amxpbyz, mvops.cxx:71-78)  */
-int lssp_amd_mv_amxpbyz(lssp_amd_ctx *ctx, double alpha, const lssp_amd_mat *A, const double *x,
+int lssp_amd_mv_amxpbyz(lssp_amd_ctx *ctx, double alpha, const lssp_amd_mat *A, double *x,
                         double beta, const double *y, double *z);
 /* y = a*A*x                         (lssp_mv_amxy,    mvops.cxx:109-115) */
-int lssp_amd_mv_amxy(lssp_amd_ctx *ctx, double a, const lssp_amd_mat *A, const double *x, double *y);
+int lssp_amd_mv_amxy(lssp_amd_ctx *ctx, double a, const lssp_amd_mat *A, double *x, double *y);
 /* y = A*x                           (lssp_mv_mxy,     mvops.cxx:144-150) */
-int lssp_amd_mv_mxy(lssp_amd_ctx *ctx, const lssp_amd_mat *A, const double *x, double *y);
+int lssp_amd_mv_mxy(lssp_amd_ctx *ctx, const lssp_amd_mat *A, double *x, double *y);
 
 /* ---- BLAS-1: vector.h:8-39 (vector.cxx:31-146) -------------------------- */
 int lssp_amd_vec_set_value(lssp_amd_ctx *ctx, double *x, long n, double val);
@@ -150,7 +163,9 @@ typedef struct {
 
 /* x: device, x0 on entry, solution on exit; b: device.  M == NULL is PC_NON
  * (pc.cxx:67-70).  trace (host, optional) receives every dot/norm the driver
- * evaluates, in the reference's call order. */
+ * evaluates, in the reference's call order.  On a distributed matrix x and
+ * every work vector hold nrows + nhalo entries (the halo part of x is
+ * overwritten by the solve's products); b holds nrows. */
 int lssp_amd_solve(lssp_amd_ctx *ctx, const lssp_amd_mat *A, const lssp_amd_ilu *M,
                    const lssp_amd_solve_params *prm, double *x, const double *b, int *nits,
                    double *residual, double *trace, int trace_cap, int *trace_len);
@@ -185,7 +200,10 @@ typedef struct {
 } lssp_amd_host_transport;
 int lssp_amd_comm_init_host(lssp_amd_ctx *ctx, int nranks, int rank, const lssp_amd_host_transport *t);
 
-/* rows [row0, row0 + nlocal) of a global n x n CSR given by its local rows */
+/* rows [row0, row0 + nlocal) of a global n x n CSR given by its local rows.
+ * Collective: every rank calls it; the input checks are agreed on across the
+ * ranks first, so a bad argument on one rank makes EVERY rank return
+ * LSSP_AMD_EINVAL (no rank is left waiting in a collective). */
 int lssp_amd_mat_upload_dist(lssp_amd_ctx *ctx, int n_global, int row0, int nlocal,
                              const int *Ap, const int *Aj, const double *Ax, lssp_amd_mat **A);
 int lssp_amd_mat_local_rows(const lssp_amd_mat *A, int *row0, int *nlocal, int *nhalo);

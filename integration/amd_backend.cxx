@@ -6,24 +6,36 @@
 // This is the translation unit a maintainer adds to huiscliu/lssp (as
 // src/amd-backend.cxx); INTEGRATION.md describes it.  It compiles against the
 // reference's own headers and replaces, at link time, the drivers that
-// lssp_solver_solve dispatches to (lssp.cxx:259-336):
+// lssp_solver_solve dispatches to (lssp.cxx:259-336), and hooks the solver /
+// PC lifecycle (lssp.cxx:142-200, pc.cxx):
 //
 //     -Wl,--wrap=<mangled lssp_solver_*>   (one per AMD_DRIVER line below)
+//     -Wl,--wrap=<mangled lssp_solver_assemble, lssp_solver_destroy, lssp_pc_assemble>
 //
 // so lssp.cxx, the drivers and every caller (example/exam.cxx) stay unchanged.
 // Everything else (assemble, the column sort, the ILU setup of pc-iluk.cxx /
 // pc-ilut.cxx, other solvers and preconditioners) is the reference's own code.
 //
-// Per solve: A (the sorted copy lssp_solver_assemble made, lssp.cxx:166-173)
-// and the factors pc.L / pc.U the reference built are uploaded, x0 and b too;
-// the whole iteration runs in HBM (lssp_amd_solve); x is downloaded into the
-// caller's view s.x.d (lssp.cxx:175-176) and s.residual / s.nits are set as the
-// drivers set them (solver-bicgstab.cxx:156-157, :174).  A non-zero lssp_amd
-// status becomes lssp_error(1, ...) -> exit(1), the reference's fatal path
-// (utils.cxx:114-135).  LSSP_AMD_REDUCE=serial selects the reference's
+// Device state per LSSP_SOLVER, kept across solves: A (the sorted copy
+// lssp_solver_assemble made, lssp.cxx:166-173), the factors pc.L / pc.U the
+// reference built with their sweep schedules, and the x / b work vectors.
+// They are built at the first solve after an assemble and dropped when the
+// solver is re-assembled or destroyed or its PC re-assembled, so a caller that
+// solves repeatedly after one lssp_solver_assemble pays the upload and the
+// schedule build once; each solve uploads only x0 and b.  The whole iteration
+// runs in HBM (lssp_amd_solve); x is downloaded into the caller's view s.x.d
+// (lssp.cxx:175-176) and s.residual / s.nits are set as the drivers set them
+// (solver-bicgstab.cxx:156-157, :174).  The drivers' messages go through
+// lssp_printf (utils.cxx:93-112: stdout and the lssp_set_log file).  A non-zero
+// lssp_amd status becomes lssp_error(1, ...) -> exit(1), the reference's fatal
+// path (utils.cxx:114-135).  LSSP_AMD_REDUCE=serial selects the reference's
 // sequential dot order (bitwise-identical runs).
 #include "lssp.h"
 #include "lssp_amd.h"
+
+#include <map>
+
+static int amd_print(void *, const char *msg) { return lssp_printf("%s", msg); }
 
 static lssp_amd_ctx *amd_ctx()
 {
@@ -32,6 +44,7 @@ static lssp_amd_ctx *amd_ctx()
         const char *d = getenv("LSSP_AMD_DEVICE");
         int st = lssp_amd_ctx_create(d ? atoi(d) : 0, &c);
         if (st != LSSP_AMD_OK) lssp_error(1, "amd: cannot open the device: %s\n", lssp_amd_strerror(st));
+        lssp_amd_set_print(amd_print, NULL);
     }
     return c;
 }
@@ -47,21 +60,70 @@ static bool amd_handles(const LSSP_PC &pc)
     return pc.type == LSSP_PC_NON || pc.type == LSSP_PC_ILUK || pc.type == LSSP_PC_ILUT;
 }
 
+// ---- device state per solver ------------------------------------------------
+struct AmdState {
+    const LSSP_PC *pc = NULL;
+    const double *Ax = NULL;  // identity of the uploaded A (s.A)
+    int n = 0, nnz = 0;
+    lssp_amd_mat *A = NULL;
+    const double *Lx = NULL, *Ux = NULL;  // identity of the uploaded factors (pc.L, pc.U)
+    lssp_amd_ilu *M = NULL;
+    double *x = NULL, *b = NULL;
+};
+static std::map<const LSSP_SOLVER *, AmdState> amd_states;
+
+static void amd_drop_factors(AmdState &d)
+{
+    if (d.M) lssp_amd_ilu_destroy(d.M);
+    d.M = NULL;
+    d.Lx = d.Ux = NULL;
+}
+
+static void amd_drop(const LSSP_SOLVER *s)
+{
+    std::map<const LSSP_SOLVER *, AmdState>::iterator it = amd_states.find(s);
+    if (it == amd_states.end()) return;
+    AmdState &d = it->second;
+    lssp_amd_ctx *c = amd_ctx();
+    amd_drop_factors(d);
+    if (d.A) lssp_amd_mat_destroy(d.A);
+    if (d.x) lssp_amd_vec_free(c, d.x);
+    if (d.b) lssp_amd_vec_free(c, d.b);
+    amd_states.erase(it);
+}
+
 static int amd_solve(LSSP_SOLVER &s, LSSP_PC &pc, int solver)
 {
     lssp_amd_ctx *c = amd_ctx();
     const int n = s.A.num_rows;
-    lssp_amd_mat *A = NULL;
-    lssp_amd_ilu *M = NULL;
-    double *x = NULL, *b = NULL;
-
-    AMD_CK(lssp_amd_mat_upload(c, n, s.A.num_cols, s.A.num_nnzs, s.A.Ap, s.A.Aj, s.A.Ax, &A));
-    if (pc.type != LSSP_PC_NON)
-        AMD_CK(lssp_amd_ilu_from_factors(c, n, pc.L.Ap, pc.L.Aj, pc.L.Ax, pc.U.Ap, pc.U.Aj, pc.U.Ax, &M));
-    AMD_CK(lssp_amd_vec_alloc(c, n, &x));
-    AMD_CK(lssp_amd_vec_alloc(c, n, &b));
-    AMD_CK(lssp_amd_vec_upload(c, x, s.x.d, n));
-    AMD_CK(lssp_amd_vec_upload(c, b, s.rhs.d, n));
+    AmdState &d = amd_states[&s];
+    d.pc = &pc;
+    if (d.A && (d.Ax != s.A.Ax || d.n != n || d.nnz != s.A.num_nnzs)) {  // defensive: a different A
+        lssp_amd_mat_destroy(d.A);
+        d.A = NULL;
+    }
+    if (!d.A) {
+        AMD_CK(lssp_amd_mat_upload(c, n, s.A.num_cols, s.A.num_nnzs, s.A.Ap, s.A.Aj, s.A.Ax, &d.A));
+        d.Ax = s.A.Ax;
+        d.nnz = s.A.num_nnzs;
+    }
+    if (d.n != n) {
+        if (d.x) lssp_amd_vec_free(c, d.x);
+        if (d.b) lssp_amd_vec_free(c, d.b);
+        AMD_CK(lssp_amd_vec_alloc(c, n, &d.x));
+        AMD_CK(lssp_amd_vec_alloc(c, n, &d.b));
+        d.n = n;
+    }
+    if (pc.type == LSSP_PC_NON) {
+        amd_drop_factors(d);
+    } else if (!d.M || d.Lx != pc.L.Ax || d.Ux != pc.U.Ax) {
+        amd_drop_factors(d);
+        AMD_CK(lssp_amd_ilu_from_factors(c, n, pc.L.Ap, pc.L.Aj, pc.L.Ax, pc.U.Ap, pc.U.Aj, pc.U.Ax, &d.M));
+        d.Lx = pc.L.Ax;
+        d.Ux = pc.U.Ax;
+    }
+    AMD_CK(lssp_amd_vec_upload(c, d.x, s.x.d, n));
+    AMD_CK(lssp_amd_vec_upload(c, d.b, s.rhs.d, n));
 
     lssp_amd_solve_params p;
     p.solver = solver;
@@ -76,18 +138,45 @@ static int amd_solve(LSSP_SOLVER &s, LSSP_PC &pc, int solver)
     p.idrs = s.idrs;
     int nits = 0;
     double res = 0.;
-    fflush(stdout);  // the device driver prints with stdio too: keep the line order
-    AMD_CK(lssp_amd_solve(c, A, M, &p, x, b, &nits, &res, NULL, 0, NULL));
-    fflush(stdout);
-    AMD_CK(lssp_amd_vec_download(c, s.x.d, x, n));
+    AMD_CK(lssp_amd_solve(c, d.A, pc.type == LSSP_PC_NON ? NULL : d.M, &p, d.x, d.b, &nits, &res, NULL, 0, NULL));
+    AMD_CK(lssp_amd_vec_download(c, s.x.d, d.x, n));
 
     s.residual = res;
     s.nits = nits;
-    lssp_amd_vec_free(c, x);
-    lssp_amd_vec_free(c, b);
-    if (M) lssp_amd_ilu_destroy(M);
-    lssp_amd_mat_destroy(A);
     return nits;
+}
+
+// ---- lifecycle hooks: the cached device state follows the reference's objects
+#define SYM_SOLVER_ASSEMBLE _Z20lssp_solver_assembleR12LSSP_SOLVER_R13lssp_mat_csr_9lssp_vec_S3_R8LSSP_PC_
+#define SYM_SOLVER_DESTROY _Z19lssp_solver_destroyR12LSSP_SOLVER_R8LSSP_PC_
+#define SYM_PC_ASSEMBLE _Z16lssp_pc_assembleR8LSSP_PC_12LSSP_SOLVER_
+#define AMD_CAT_(a, b) a##b
+#define AMD_CAT(a, b) AMD_CAT_(a, b)
+
+// lssp_solver_assemble (lssp.cxx:142-189): a new copy of A, the PC re-assembled
+extern "C" void AMD_CAT(__real_, SYM_SOLVER_ASSEMBLE)(LSSP_SOLVER &, lssp_mat_csr &, lssp_vec, lssp_vec, LSSP_PC &);
+extern "C" void AMD_CAT(__wrap_, SYM_SOLVER_ASSEMBLE)(LSSP_SOLVER &s, lssp_mat_csr &A, lssp_vec x, lssp_vec b,
+                                                      LSSP_PC &pc)
+{
+    amd_drop(&s);
+    AMD_CAT(__real_, SYM_SOLVER_ASSEMBLE)(s, A, x, b, pc);
+}
+
+// lssp_solver_destroy (lssp.cxx:191-208)
+extern "C" void AMD_CAT(__real_, SYM_SOLVER_DESTROY)(LSSP_SOLVER &, LSSP_PC &);
+extern "C" void AMD_CAT(__wrap_, SYM_SOLVER_DESTROY)(LSSP_SOLVER &s, LSSP_PC &pc)
+{
+    amd_drop(&s);
+    AMD_CAT(__real_, SYM_SOLVER_DESTROY)(s, pc);
+}
+
+// lssp_pc_assemble (pc.cxx): new factors for every solver using this PC
+extern "C" void AMD_CAT(__real_, SYM_PC_ASSEMBLE)(LSSP_PC &, LSSP_SOLVER);
+extern "C" void AMD_CAT(__wrap_, SYM_PC_ASSEMBLE)(LSSP_PC &pc, LSSP_SOLVER s)
+{
+    for (std::map<const LSSP_SOLVER *, AmdState>::iterator it = amd_states.begin(); it != amd_states.end(); ++it)
+        if (it->second.pc == &pc) amd_drop_factors(it->second);
+    AMD_CAT(__real_, SYM_PC_ASSEMBLE)(pc, s);
 }
 
 // One wrapper per driver: the linker's --wrap=SYM sends every call of SYM here

@@ -37,6 +37,7 @@ class SolveParams(ctypes.Structure):
 SIGNATURES = {
     "lssp_amd_strerror": (ctypes.c_char_p, [_ci]),
     "lssp_amd_version": (_ci, []),
+    "lssp_amd_set_print": (None, [_vp, _vp]),
     "lssp_amd_ctx_create": (_ci, [_ci, _pvp]),
     "lssp_amd_ctx_destroy": (_ci, [_vp]),
     "lssp_amd_ctx_set_reduction": (_ci, [_vp, _ci]),

@@ -217,22 +217,62 @@ int lssp_amd_comm_barrier(lssp_amd_ctx *c)
 }
 
 // Local rows [row0, row0+nlocal) of the global matrix, global column indices.
+// Collective.  A rank that finds bad input does not return on its own: the
+// statuses are agreed on (agree_status) before each collective step, so every
+// rank fails together with the same status and none is left waiting in an
+// all-gather or send/recv.  Temporary device buffers and the half-built matrix
+// are released on every path.
+namespace {
+struct DevMem {  // device scratch, freed when the upload returns
+    void *p = nullptr;
+    ~DevMem()
+    {
+        if (p) (void)hipFree(p);
+    }
+};
+struct MatGuard {  // the half-built matrix, destroyed unless released
+    lssp_amd_mat *m;
+    ~MatGuard() { lssp_amd_mat_destroy(m); }
+};
+}  // namespace
+
+// every rank's status -> the first non-zero one (rank order), identical on all ranks
+static int agree_status(lssp_amd_ctx *c, int st)
+{
+    DevMem d_mine, d_all;
+    LSSP_HIP(hipMalloc(&d_mine.p, sizeof(int)));
+    LSSP_HIP(hipMalloc(&d_all.p, sizeof(int) * c->nranks));
+    LSSP_HIP(hipMemcpy(d_mine.p, &st, sizeof(int), hipMemcpyHostToDevice));
+    LSSP_TRY(xfer_allgather(c, d_mine.p, d_all.p, (long)sizeof(int)));
+    std::vector<int> all(c->nranks);
+    LSSP_HIP(hipMemcpyAsync(all.data(), d_all.p, sizeof(int) * c->nranks, hipMemcpyDeviceToHost, c->stream));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    for (int s : all)
+        if (s != LSSP_AMD_OK) return s;
+    return LSSP_AMD_OK;
+}
+
 int lssp_amd_mat_upload_dist(lssp_amd_ctx *c, int n_global, int row0, int nlocal, const int *Ap,
                              const int *Aj, const double *Ax, lssp_amd_mat **out)
 {
-    if (!c || !out || !Ap || n_global <= 0 || nlocal < 0) return LSSP_AMD_EINVAL;
+    if (!c || !out) return LSSP_AMD_EINVAL;  // no context: nothing to agree through
     const int P = c->nranks;
-    const int blk = (n_global + P - 1) / P;
-    const int my0 = std::min(c->rank * blk, n_global);
-    const int myn = std::min(blk, n_global - my0);
-    if (row0 != my0 || nlocal != myn) return LSSP_AMD_EINVAL;  // canonical partition only
-    const int nnz = Ap[nlocal];
-    if (Ap[0] != 0) return LSSP_AMD_EINVAL;
+    // ---- local checks, then agreed on ----
+    int st = LSSP_AMD_OK;
+    const int blk = n_global > 0 ? (n_global + P - 1) / P : 1;
+    const int my0 = std::min(c->rank * blk, std::max(n_global, 0));
+    const int myn = std::max(0, std::min(blk, n_global - my0));
+    if (!Ap || n_global <= 0 || nlocal < 0 || row0 != my0 || nlocal != myn || Ap[0] != 0)
+        st = LSSP_AMD_EINVAL;  // canonical partition only
+    const int nnz = st == LSSP_AMD_OK ? Ap[nlocal] : 0;
+    if (st == LSSP_AMD_OK && (nnz < 0 || (nnz > 0 && (!Aj || !Ax)))) st = LSSP_AMD_EINVAL;
+    for (int k = 0; st == LSSP_AMD_OK && k < nnz; k++)
+        if (Aj[k] < 0 || Aj[k] >= n_global) st = LSSP_AMD_EINVAL;
+    LSSP_TRY(agree_status(c, st));
     // halo columns, grouped by owner then ascending
     std::map<int, int> halo;  // global col -> slot
     for (int k = 0; k < nnz; k++) {
         const int g = Aj[k];
-        if (g < 0 || g >= n_global) return LSSP_AMD_EINVAL;
         if (g < row0 || g >= row0 + nlocal) halo[g] = 0;
     }
     std::vector<int> hcols;
@@ -244,7 +284,8 @@ int lssp_amd_mat_upload_dist(lssp_amd_ctx *c, int n_global, int row0, int nlocal
         const int g = Aj[k];
         lj[k] = (g >= row0 && g < row0 + nlocal) ? g - row0 : nlocal + halo[g];
     }
-    lssp_amd_mat *M = new lssp_amd_mat();
+    MatGuard guard{new lssp_amd_mat()};
+    lssp_amd_mat *M = guard.m;
     M->ctx = c;
     M->nrows = nlocal;
     M->nhalo = (int)hcols.size();
@@ -265,13 +306,16 @@ int lssp_amd_mat_upload_dist(lssp_amd_ctx *c, int n_global, int row0, int nlocal
         off += need[q];
     }
     // tell every owner which of its columns we need: counts then index lists
-    int *d_cnt_mine, *d_cnt_all;
-    LSSP_HIP(hipMalloc(&d_cnt_mine, sizeof(int) * P));
-    LSSP_HIP(hipMalloc(&d_cnt_all, sizeof(int) * P * P));
-    LSSP_HIP(hipMemcpy(d_cnt_mine, need.data(), sizeof(int) * P, hipMemcpyHostToDevice));
-    LSSP_TRY(xfer_allgather(c, d_cnt_mine, d_cnt_all, (long)sizeof(int) * P));
+    DevMem d_cnt_mine, d_cnt_all, d_hcols, d_sendg;
+    st = hipMalloc(&d_cnt_mine.p, sizeof(int) * P) == hipSuccess &&
+                 hipMalloc(&d_cnt_all.p, sizeof(int) * P * P) == hipSuccess &&
+                 hipMemcpy(d_cnt_mine.p, need.data(), sizeof(int) * P, hipMemcpyHostToDevice) == hipSuccess
+             ? LSSP_AMD_OK
+             : LSSP_AMD_ENOMEM;
+    LSSP_TRY(agree_status(c, st));
+    LSSP_TRY(xfer_allgather(c, d_cnt_mine.p, d_cnt_all.p, (long)sizeof(int) * P));
     std::vector<int> all(P * P);
-    LSSP_HIP(hipMemcpyAsync(all.data(), d_cnt_all, sizeof(int) * P * P, hipMemcpyDeviceToHost, c->stream));
+    LSSP_HIP(hipMemcpyAsync(all.data(), d_cnt_all.p, sizeof(int) * P * P, hipMemcpyDeviceToHost, c->stream));
     LSSP_HIP(hipStreamSynchronize(c->stream));
     int nsend = 0;
     for (int q = 0; q < P; q++) {
@@ -284,35 +328,37 @@ int lssp_amd_mat_upload_dist(lssp_amd_ctx *c, int n_global, int row0, int nlocal
         }
     }
     M->nsend = nsend;
-    int *d_hcols = nullptr, *d_sendg = nullptr;
-    LSSP_HIP(hipMalloc(&d_hcols, sizeof(int) * std::max<size_t>(hcols.size(), 1)));
-    LSSP_HIP(hipMalloc(&d_sendg, sizeof(int) * std::max(nsend, 1)));
-    if (!hcols.empty())
-        LSSP_HIP(hipMemcpy(d_hcols, hcols.data(), sizeof(int) * hcols.size(), hipMemcpyHostToDevice));
+    st = hipMalloc(&d_hcols.p, sizeof(int) * std::max<size_t>(hcols.size(), 1)) == hipSuccess &&
+                 hipMalloc(&d_sendg.p, sizeof(int) * std::max(nsend, 1)) == hipSuccess &&
+                 (hcols.empty() || hipMemcpy(d_hcols.p, hcols.data(), sizeof(int) * hcols.size(),
+                                             hipMemcpyHostToDevice) == hipSuccess)
+             ? LSSP_AMD_OK
+             : LSSP_AMD_ENOMEM;
+    LSSP_TRY(agree_status(c, st));
     {
         std::vector<Msg> s, r;  // my halo columns to their owners; the columns peers need from me
+        int *hc = static_cast<int *>(d_hcols.p), *sg = static_cast<int *>(d_sendg.p);
         for (size_t q = 0; q < M->recv_peer.size(); q++)
-            s.push_back({M->recv_peer[q], d_hcols + M->recv_off[q], (long)sizeof(int) * M->recv_cnt[q]});
+            s.push_back({M->recv_peer[q], hc + M->recv_off[q], (long)sizeof(int) * M->recv_cnt[q]});
         for (size_t q = 0; q < M->send_peer.size(); q++)
-            r.push_back({M->send_peer[q], d_sendg + M->send_off[q], (long)sizeof(int) * M->send_cnt[q]});
+            r.push_back({M->send_peer[q], sg + M->send_off[q], (long)sizeof(int) * M->send_cnt[q]});
         LSSP_TRY(xfer_group(c, s, r));
     }
     std::vector<int> sendg(nsend);
     if (nsend)
-        LSSP_HIP(hipMemcpyAsync(sendg.data(), d_sendg, sizeof(int) * nsend, hipMemcpyDeviceToHost, c->stream));
+        LSSP_HIP(hipMemcpyAsync(sendg.data(), d_sendg.p, sizeof(int) * nsend, hipMemcpyDeviceToHost, c->stream));
     LSSP_HIP(hipStreamSynchronize(c->stream));
+    // a peer asking for a column this rank does not own: every rank learns it
+    st = LSSP_AMD_OK;
     for (int &g : sendg) {
-        if (g < row0 || g >= row0 + nlocal) return LSSP_AMD_EINVAL;
+        if (g < row0 || g >= row0 + nlocal) st = LSSP_AMD_EINVAL;
         g -= row0;
     }
+    LSSP_TRY(agree_status(c, st));
     LSSP_HIP(hipMalloc(&M->d_send_idx, sizeof(int) * std::max(nsend, 1)));
     LSSP_HIP(hipMalloc(&M->d_send_buf, sizeof(double) * std::max(nsend, 1)));
     if (nsend)
         LSSP_HIP(hipMemcpy(M->d_send_idx, sendg.data(), sizeof(int) * nsend, hipMemcpyHostToDevice));
-    (void)hipFree(d_cnt_mine);
-    (void)hipFree(d_cnt_all);
-    (void)hipFree(d_hcols);
-    (void)hipFree(d_sendg);
     LSSP_HIP(hipMalloc(&M->Ap, sizeof(int) * (nlocal + 1)));
     LSSP_HIP(hipMalloc(&M->Aj, sizeof(int) * (nnz + 4)));  // +4: see upload_csr (capi.cpp)
     LSSP_HIP(hipMalloc(&M->Ax, sizeof(double) * (nnz + 4)));
@@ -321,6 +367,7 @@ int lssp_amd_mat_upload_dist(lssp_amd_ctx *c, int n_global, int row0, int nlocal
         LSSP_HIP(hipMemcpy(M->Aj, lj.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
         LSSP_HIP(hipMemcpy(M->Ax, Ax, sizeof(double) * nnz, hipMemcpyHostToDevice));
     }
+    guard.m = nullptr;
     *out = M;
     return LSSP_AMD_OK;
 }

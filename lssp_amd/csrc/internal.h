@@ -250,6 +250,11 @@ long num_chunks(long n);
 int ensure_part(lssp_amd_ctx *c, long C);
 
 // ---- host pieces ---------------------------------------------------------------
+// the drivers' messages (the reference's lssp_printf lines): to the hook set
+// with lssp_amd_set_print, else to stdout (flushed, as lssp_printf does)
+int lprint(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+double wall_time();  // seconds, lssp_get_time() (utils.cxx:40-46)
+
 // ILU setup (ilu_setup.cpp), exact restatement of pc-iluk.cxx / pc-ilut.cxx
 struct HostCSR {
     int n = 0, ncols = 0;

@@ -155,14 +155,15 @@ void defaults(const lssp_amd_solve_params &P, double &tol_rel, double &tol_abs, 
 int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits,
              double *res_out)
 {
+    const double t_start = wall_time();  // the reference driver's lssp_get_time() ("total time")
     double tol_rel, tol_abs, tol_rb = P.tol_rb, tol;
     int maxit, it;
     defaults(P, tol_rel, tol_abs, maxit);
     if (P.verb >= 2 && R.rank == 0) {
-        printf("bicgstab: maximal iteration: %d\n", maxit);
-        printf("bicgstab: tolerance abs: %g\n", tol_abs);
-        printf("bicgstab: tolerance rel: %g\n", tol_rel);
-        printf("bicgstab: tolerance rbn: %g\n", tol_rb);
+        lprint("bicgstab: maximal iteration: %d\n", maxit);
+        lprint("bicgstab: tolerance abs: %g\n", tol_abs);
+        lprint("bicgstab: tolerance rel: %g\n", tol_rel);
+        lprint("bicgstab: tolerance rbn: %g\n", tol_rb);
     }
     double *r = R.vec(), *rh = R.vec(), *p = R.vec(), *ph = R.vec();
     double *s = R.vec(), *sh = R.vec(), *t = R.vec(), *v = R.vec();
@@ -200,7 +201,7 @@ int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
     for (it = 0; it < maxit; it++) {
         pending_rho = false;
         if (rho1 == 0) {  // :89-92
-            if (R.rank == 0) printf("bicgstab: method failed.!\n");
+            if (R.rank == 0) lprint("bicgstab: method failed.!\n");
             break;
         }
         Ew e;
@@ -255,7 +256,7 @@ int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
         }
         LSSP_TRY(R.sync(0, 16));
         if (R.h(S_BREAK) != 0.0) {  // :117-128 -- x += alpha*ph already done on the device
-            if (R.rank == 0) printf("bicgstab: ||s|| is too small: %f, terminated.\n", R.h(S_SNORM));
+            if (R.rank == 0) lprint("bicgstab: ||s|| is too small: %f, terminated.\n", R.h(S_SNORM));
             R.tl = pos_s + 1;
             long q = R.tl++;
             R.patches.push_back({q, R.h(S_SNORM)});  // the reference evaluates the norm again (:118)
@@ -268,14 +269,17 @@ int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
         pending_rho = true;
         res = R.h(S_RES);
         if (P.verb >= 1 && R.rank == 0)
-            printf("bicgstab: itr: %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", it, res,
+            lprint("bicgstab: itr: %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", it, res,
                    (err_rel == 0 ? 0 : res / err_rel), (b_norm == 0 ? 0 : res / b_norm));
         if (res <= tol) break;  // :149
         rho1 = R.h(S_RHO1);
     }
     if (pending_rho) R.tl--;  // the fused next-iteration rho1 is not part of the reference's run
     if (it < maxit) it += 1;  // :152
-    if (P.verb >= 2 && R.rank == 0) printf("bicgstab: total iteration: %d\n", it);
+    if (P.verb >= 2 && R.rank == 0) {
+        lprint("bicgstab: total iteration: %d\n", it);
+        lprint("bicgstab: total time: %g\n", wall_time() - t_start);
+    }
     *nits = it;
     *res_out = res;
     return LSSP_AMD_OK;
@@ -286,14 +290,15 @@ int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
 // ---------------------------------------------------------------------------
 int cg(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
 {
+    const double t_start = wall_time();  // the reference driver's lssp_get_time() ("total time")
     double tol_rel, tol_abs, tol_rb = P.tol_rb, tol;
     int maxit, it;
     defaults(P, tol_rel, tol_abs, maxit);
     if (P.verb >= 2 && R.rank == 0) {
-        printf("cg: maximal iteration: %d\n", maxit);
-        printf("cg: tolerance abs: %g\n", tol_abs);
-        printf("cg: tolerance rel: %g\n", tol_rel);
-        printf("cg: tolerance rbn: %g\n", tol_rb);
+        lprint("cg: maximal iteration: %d\n", maxit);
+        lprint("cg: tolerance abs: %g\n", tol_abs);
+        lprint("cg: tolerance rel: %g\n", tol_rel);
+        lprint("cg: tolerance rbn: %g\n", tol_rb);
     }
     double *r = R.vec(), *p = R.vec(), *q = R.vec();
     double *z = R.M ? R.vec() : r;  // PC_NON copies r into z (pc.cxx:67-70): alias instead
@@ -358,13 +363,16 @@ int cg(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *
         LSSP_TRY(R.sync(0, 16));
         res = R.h(S_RES);
         if (P.verb >= 1 && R.rank == 0)
-            printf("cg: itr: %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", it, res,
+            lprint("cg: itr: %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", it, res,
                    (err_rel == 0 ? 0 : res / err_rel), (b_norm == 0 ? 0 : res / b_norm));
         if (res <= tol) break;  // :109
     }
     if (pending_rho) R.tl--;
     if (it < maxit) it += 1;
-    if (P.verb >= 2 && R.rank == 0) printf("cg: total iteration: %d\n", it);
+    if (P.verb >= 2 && R.rank == 0) {
+        lprint("cg: total iteration: %d\n", it);
+        lprint("cg: total time: %g\n", wall_time() - t_start);
+    }
     *nits = it;
     *res_out = res;
     return LSSP_AMD_OK;
@@ -376,6 +384,7 @@ int cg(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *
 // ---------------------------------------------------------------------------
 int gmres(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
 {
+    const double t_start = wall_time();  // the reference driver's lssp_get_time() ("total time")
     lssp_amd_ctx *c = R.c;
     double tol_rel, tol_abs, tol_rb = P.tol_rb;
     int maxit;
@@ -385,11 +394,11 @@ int gmres(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, in
     if (m <= 0) return LSSP_AMD_EINVAL;
     if (S_H + 2 * m + 2 > NSCAL) return LSSP_AMD_EUNSUPPORTED;  // Hessenberg column + ym staging
     if (P.verb >= 2 && R.rank == 0) {
-        printf("gmres: restart parameter m: %d\n", m);
-        printf("gmres: maximal iteration: %d\n", maxit);
-        printf("gmres: tolerance abs: %g\n", tol_abs);
-        printf("gmres: tolerance rel: %g\n", tol_rel);
-        printf("gmres: tolerance rbn: %g\n", tol_rb);
+        lprint("gmres: restart parameter m: %d\n", m);
+        lprint("gmres: maximal iteration: %d\n", maxit);
+        lprint("gmres: tolerance abs: %g\n", tol_abs);
+        lprint("gmres: tolerance rel: %g\n", tol_rel);
+        lprint("gmres: tolerance rbn: %g\n", tol_rb);
     }
     double *wj = R.vec(), *rg = R.vec();
     double *V = R.vec(R.nx * (long)m);
@@ -523,12 +532,15 @@ int gmres(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, in
         LSSP_TRY(R.sync(0, 16));
         beta = R.h(S_RES);
         if (P.verb >= 1 && R.rank == 0)
-            printf("gmres: itr: %4d / %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", inner, inner, beta,
+            lprint("gmres: itr: %4d / %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", inner, inner, beta,
                    (err_rel == 0 ? 0 : beta / err_rel), (b_norm == 0 ? 0 : beta / b_norm));
         if (beta <= tol) break;                                  // :215-217
         gstol = rtol * gs_norm / (beta / err_rel) * 0.5;          // :220
     }
-    if (P.verb >= 2 && R.rank == 0) printf("gmres: total iteration: %d\n", inner);
+    if (P.verb >= 2 && R.rank == 0) {
+        lprint("gmres: total iteration: %d\n", inner);
+        lprint("gmres: total time: %g\n", wall_time() - t_start);
+    }
     *nits = inner;
     *res_out = beta;
     return LSSP_AMD_OK;
@@ -541,6 +553,7 @@ int gmres(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, in
 // ---------------------------------------------------------------------------
 int gmres_r(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
 {
+    const double t_start = wall_time();  // the reference driver's lssp_get_time() ("total time")
     lssp_amd_ctx *c = R.c;
     double tol_rel, tol_abs, tol_rb = P.tol_rb;
     int maxit;
@@ -550,11 +563,11 @@ int gmres_r(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, 
     if (m <= 0) return LSSP_AMD_EINVAL;
     if (S_H + 2 * m + 2 > NSCAL) return LSSP_AMD_EUNSUPPORTED;
     if (P.verb >= 2 && R.rank == 0) {
-        printf("gmres: restart parameter m: %d\n", m);
-        printf("gmres: maximal iteration: %d\n", maxit);
-        printf("gmres: tolerance abs: %g\n", tol_abs);
-        printf("gmres: tolerance rel: %g\n", tol_rel);
-        printf("gmres: tolerance rbn: %g\n", tol_rb);
+        lprint("gmres: restart parameter m: %d\n", m);
+        lprint("gmres: maximal iteration: %d\n", maxit);
+        lprint("gmres: tolerance abs: %g\n", tol_abs);
+        lprint("gmres: tolerance rel: %g\n", tol_rel);
+        lprint("gmres: tolerance rbn: %g\n", tol_rb);
     }
     double *wj = R.vec(), *rg = R.vec();
     double *V = R.vec(R.nx * (long)m);
@@ -648,7 +661,7 @@ int gmres_r(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, 
             HG(i, i) = cs[i] * HG(i, i) + sn[i] * HG(i + 1, i);
             beta = std::fabs(gg[i + 1]);
             if (P.verb >= 1 && R.rank == 0)
-                printf("rgmres: itr: %4d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", inner, beta,
+                lprint("rgmres: itr: %4d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", inner, beta,
                        (err_rel == 0 ? 0 : beta / err_rel), (b_norm == 0 ? 0 : beta / b_norm));
             if (beta <= tol) {  // :409-411 (goto solve: i is not advanced)
                 converged = true;
@@ -685,7 +698,10 @@ int gmres_r(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, 
         if (beta <= tol) break;                          // :433-435
         LSSP_TRY(R.spmv(EPI_AXPBY, -1, x, 1, b, rg));    // :437
     }
-    if (P.verb >= 2 && R.rank == 0) printf("gmres: total iteration: %d\n", inner);
+    if (P.verb >= 2 && R.rank == 0) {
+        lprint("gmres: total iteration: %d\n", inner);
+        lprint("gmres: total time: %g\n", wall_time() - t_start);
+    }
     LSSP_TRY(R.sync(0, 1));  // the last x update is complete when the call returns
     *nits = inner;
     *res_out = beta;
@@ -704,6 +720,7 @@ int gmres_r(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, 
 // ---------------------------------------------------------------------------
 int lgmres(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *nits, double *res_out)
 {
+    const double t_start = wall_time();  // the reference driver's lssp_get_time() ("total time")
     lssp_amd_ctx *c = R.c;
     double tol_rel, tol_abs, tol_rb = P.tol_rb;
     int maxit;
@@ -715,12 +732,12 @@ int lgmres(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, i
     const int mmax = mk + auk;
     if (S_H + 2 * mmax + 2 > NSCAL || mmax > 0x7fff || auk > 0x7fff) return LSSP_AMD_EUNSUPPORTED;
     if (P.verb >= 2 && R.rank == 0) {
-        printf("lgmres: restart parameter m: %d\n", mk);
-        printf("lgmres: aug k: %d\n", auk);
-        printf("lgmres: maximal iteration: %d\n", maxit);
-        printf("lgmres: tolerance abs: %g\n", tol_abs);
-        printf("lgmres: tolerance rel: %g\n", tol_rel);
-        printf("lgmres: tolerance rbn: %g\n", tol_rb);
+        lprint("lgmres: restart parameter m: %d\n", mk);
+        lprint("lgmres: aug k: %d\n", auk);
+        lprint("lgmres: maximal iteration: %d\n", maxit);
+        lprint("lgmres: tolerance abs: %g\n", tol_abs);
+        lprint("lgmres: tolerance rel: %g\n", tol_rel);
+        lprint("lgmres: tolerance rbn: %g\n", tol_rb);
     }
     double *wj = R.vec(), *rg = R.vec();
     double *V = R.vec(R.nx * (long)mmax);
@@ -853,13 +870,16 @@ int lgmres(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, i
         LSSP_TRY(R.sync(0, 16));
         beta = R.h(S_RES);
         if (P.verb >= 1 && R.rank == 0)
-            printf("lgmres: itr: %4d / %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", outer, inner, beta,
+            lprint("lgmres: itr: %4d / %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", outer, inner, beta,
                    (err_rel == 0 ? 0 : beta / err_rel), (b_norm == 0 ? 0 : beta / b_norm));
         if (beta <= tol) break;                                  // :262
         gstol = rtol * gs_norm / (beta / err_rel) * 0.5;          // :265
         outer++;
     }
-    if (P.verb >= 2 && R.rank == 0) printf("lgmres: total iteration: %d\n", inner);
+    if (P.verb >= 2 && R.rank == 0) {
+        lprint("lgmres: total iteration: %d\n", inner);
+        lprint("lgmres: total time: %g\n", wall_time() - t_start);
+    }
     *nits = inner;
     *res_out = beta;
     return LSSP_AMD_OK;
@@ -992,7 +1012,7 @@ int cgs(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int 
         K.axpby(-alpha, qhat, 1, r);
         nrm2 = K.norm(r);
         if (P.verb >= 1 && R.rank == 0)
-            printf("cgs: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+            lprint("cgs: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
         if (!K.ok() || tol >= nrm2) L1_DONE();
         rho_old = rho;
     }
@@ -1027,7 +1047,7 @@ int cr(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *
         K.axpby(-alpha, q, 1, r);
         nrm2 = K.norm(r);
         if (P.verb >= 1 && R.rank == 0)
-            printf("cr: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+            lprint("cr: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
         if (!K.ok() || tol >= nrm2) L1_DONE();
         K.axpby(-alpha, qtld, 1, z);
         K.mxy(z, az);
@@ -1080,7 +1100,7 @@ int crs(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int 
         K.axpby(-alpha, auq, 1, r);
         nrm2 = K.norm(r);
         if (P.verb >= 1 && R.rank == 0)
-            printf("crs: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+            lprint("crs: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
         if (!K.ok() || tol >= nrm2) L1_DONE();
         rho_old = rho;
     }
@@ -1130,7 +1150,7 @@ int bicrstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
         K.axpbyz(-omega, ams, 1, s, r);
         nrm2 = K.norm(r);
         if (P.verb >= 2 && R.rank == 0)
-            printf("bicrstab: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+            lprint("bicrstab: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
         if (!K.ok() || tol >= nrm2) L1_DONE();
         K.pc(z, r);
         rho = K.dot(rtld, z);
@@ -1208,7 +1228,7 @@ int bicgsafe(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
         K.axpby(-1, y, 1.0, r);
         nrm2 = K.norm(r);
         if (P.verb >= 1 && R.rank == 0)
-            printf("bicgsafe: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+            lprint("bicgsafe: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
         if (!K.ok() || tol >= nrm2) L1_DONE();
         rho = K.dot(rtld, r);
         if (!K.ok() || rho == 0.0) L1_DONE();
@@ -1270,7 +1290,7 @@ int bicrsafe(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
         K.axpby(-1, y, 1, r);
         nrm2 = K.norm(r);
         if (P.verb >= 2 && R.rank == 0)
-            printf("bicrsafe: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+            lprint("bicrsafe: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
         if (!K.ok() || tol >= nrm2) L1_DONE();
         K.axpby(-alpha, map, 1, mr);
         K.axpby(-1, my, 1, mr);
@@ -1336,7 +1356,7 @@ int gpbi(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int
         K.axpbyz(-alpha, ap, 1, r, t);
         nrm2 = K.norm(t);
         if (P.verb >= 1 && R.rank == 0)
-            printf("%s: itr: %5d, abs res: %.6e, rel res: %.6e\n", name, iter, nrm2, nrm2 / ires);
+            lprint("%s: itr: %5d, abs res: %.6e, rel res: %.6e\n", name, iter, nrm2, nrm2 / ires);
         if (!K.ok()) L1_DONE();
         if (nrm2 <= tol) {
             K.axpby(alpha, p, 1, x);
@@ -1358,7 +1378,7 @@ int gpbi(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int
         K.axpby(-eta, y, 1, r);
         nrm2 = K.norm(r);
         if (P.verb >= 1 && R.rank == 0)
-            printf("%s: itr: %5d, abs res: %.6e, rel res: %.6e\n", name, iter, nrm2, nrm2 / ires);
+            lprint("%s: itr: %5d, abs res: %.6e, rel res: %.6e\n", name, iter, nrm2, nrm2 / ires);
         if (!K.ok() || tol >= nrm2) L1_DONE();
         K.pc(mr, r);
         rho = K.dot(rtld, cr_ ? mr : r);
@@ -1376,15 +1396,16 @@ int gpbi(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int
 // QMRCGSTAB (solver-qmrcgstab.cxx:10-186)
 int qmrcgstab(Run &R, const lssp_amd_solve_params &P, double *xk, const double *bg, int *nits, double *res_out)
 {
+    const double t_start = wall_time();  // the reference driver's lssp_get_time() ("total time")
     L1K K(R);
     double tol_rel, tol_abs, tol_rb = P.tol_rb;
     int itr_max, itr_out;
     defaults(P, tol_rel, tol_abs, itr_max);
     if (P.verb >= 2 && R.rank == 0) {
-        printf("qmrcgstab: maximal iteration: %d\n", itr_max);
-        printf("qmrcgstab: tolerance abs: %g\n", tol_abs);
-        printf("qmrcgstab: tolerance rel: %g\n", tol_rel);
-        printf("qmrcgstab: tolerance rbn: %g\n", tol_rb);
+        lprint("qmrcgstab: maximal iteration: %d\n", itr_max);
+        lprint("qmrcgstab: tolerance abs: %g\n", tol_abs);
+        lprint("qmrcgstab: tolerance rel: %g\n", tol_rel);
+        lprint("qmrcgstab: tolerance rbn: %g\n", tol_rb);
     }
     double *rk = K.vec(), *r = K.vec(), *br0 = K.vec(), *pk = K.vec(), *vk = K.vec(), *sk = K.vec();
     double *dk = K.vec(), *tk = K.vec(), *bdk = K.vec(), *bxk = K.vec();
@@ -1443,7 +1464,7 @@ int qmrcgstab(Run &R, const lssp_amd_solve_params &P, double *xk, const double *
         K.axpbyz(1, bxk, eta, dk, xk);
         rerror = K.norm(rk) / ires;
         if (!K.ok()) return K.st;
-        if (P.verb >= 1 && R.rank == 0) printf("qmrcgstab: itr: %4d, rel res: %.6e\n", itr_out, rerror);
+        if (P.verb >= 1 && R.rank == 0) lprint("qmrcgstab: itr: %4d, rel res: %.6e\n", itr_out, rerror);
         if (rerror <= tol) {
             K.resid(xk, bg, tk);
             residual = K.norm(tk);
@@ -1452,6 +1473,11 @@ int qmrcgstab(Run &R, const lssp_amd_solve_params &P, double *xk, const double *
     }
     if (!K.ok()) return K.st;
     if (itr_out < itr_max) itr_out += 1;
+    if (P.verb >= 2 && R.rank == 0) {  // solver-qmrcgstab.cxx:178-183
+        lprint("qmrcgstab: total iteration: %d\n", itr_out);
+        lprint("qmrcgstab: total time: %g\n", wall_time() - t_start);
+        lprint("qmrcgstab: absolute error (residual): %g\n", residual);
+    }
     *nits = itr_out;
     *res_out = residual;
     return LSSP_AMD_OK;
@@ -1514,7 +1540,7 @@ int tfqmr(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, in
             K.axpby(eta, t1, 1, x);
             nrm2 = tau * sqrt(1.0 + m);
             if (P.verb >= 1 && R.rank == 0)
-                printf("tfqmr: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+                lprint("tfqmr: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
             if (!K.ok() || tol >= nrm2) L1_DONE();
         }
         rho = K.dot(r, rtld);
@@ -1535,6 +1561,7 @@ int tfqmr(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, in
 // ORTHOMIN(k), k = restart (solver-orthomin.cxx:12-180)
 int orthomin(Run &R, const lssp_amd_solve_params &P, double *x, const double *rhs, int *nits, double *res_out)
 {
+    const double t_start = wall_time();  // the reference driver's lssp_get_time() ("total time")
     L1K K(R);
     double tol_rel, tol_abs, tol_rb = P.tol_rb < 0 ? DEF_TOL : P.tol_rb;
     int itr_max, itr_out, i, j;
@@ -1542,11 +1569,11 @@ int orthomin(Run &R, const lssp_amd_solve_params &P, double *x, const double *rh
     int k = P.restart < 0 ? DEF_RESTART : P.restart;
     if (k == 0) return LSSP_AMD_EINVAL;  // the reference divides by it (:102)
     if (P.verb >= 2 && R.rank == 0) {
-        printf("orthomin: k parameter m: %d\n", k);
-        printf("orthomin: maximal iteration: %d\n", itr_max);
-        printf("orthomin: tolerance abs: %g\n", tol_abs);
-        printf("orthomin: tolerance rel: %g\n", tol_rel);
-        printf("orthomin: tolerance rbn: %g\n", tol_rb);
+        lprint("orthomin: k parameter m: %d\n", k);
+        lprint("orthomin: maximal iteration: %d\n", itr_max);
+        lprint("orthomin: tolerance abs: %g\n", tol_abs);
+        lprint("orthomin: tolerance rel: %g\n", tol_rel);
+        lprint("orthomin: tolerance rbn: %g\n", tol_rb);
     }
     double *z = K.vec(), *r = K.vec(), *s = K.vec(), *sd = K.vec();
     std::vector<double *> p(k), q(k);
@@ -1602,12 +1629,15 @@ int orthomin(Run &R, const lssp_amd_solve_params &P, double *x, const double *rh
         beta = K.norm(z);
         if (!K.ok()) return K.st;
         if (P.verb >= 1 && R.rank == 0)
-            printf("orthomin: itr: %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", itr_out, beta,
+            lprint("orthomin: itr: %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", itr_out, beta,
                    (err_rel == 0 ? 0 : beta / err_rel), (b_norm == 0 ? 0 : beta / b_norm));
         if (beta <= tol) break;
     }
     if (itr_out < itr_max) itr_out += 1;
-    if (P.verb >= 2 && R.rank == 0) printf("orthomin: total iteration: %d\n", itr_out);
+    if (P.verb >= 2 && R.rank == 0) {
+        lprint("orthomin: total iteration: %d\n", itr_out);
+        lprint("orthomin: total time: %g\n", wall_time() - t_start);
+    }
     *nits = itr_out;
     *res_out = beta;
     return LSSP_AMD_OK;
@@ -1678,7 +1708,7 @@ int bicgstabl(Run &R, const lssp_amd_solve_params &P, double *x, const double *b
             nrm2 = K.norm(r[0]);
             if (!K.ok()) return K.st;
             if (P.verb >= 1 && R.rank == 0)
-                printf("bicgstabl: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+                lprint("bicgstabl: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
             if (nrm2 <= tol) {
                 unprecondition();
                 L1_DONE();
@@ -1723,7 +1753,7 @@ int bicgstabl(Run &R, const lssp_amd_solve_params &P, double *x, const double *b
         nrm2 = K.norm(r[0]);
         if (!K.ok()) return K.st;
         if (P.verb >= 1 && R.rank == 0)
-            printf("bicgstabl: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+            lprint("bicgstabl: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
         if (nrm2 < tol) {
             unprecondition();
             L1_DONE();
@@ -1888,7 +1918,7 @@ int idrs(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int
         nrm2 = K.norm(r);
         if (!K.ok()) return K.st;
         if (P.verb >= 1 && R.rank == 0)
-            printf("idrs: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
+            lprint("idrs: itr: %5d, abs res: %.6e, rel res: %.6e\n", iter, nrm2, nrm2 / ires);
         if (tol >= nrm2) L1_DONE();
         for (i = 0; i < s; i++) {
             h = K.dot(Pv[i], dR[oldest]);

@@ -268,7 +268,7 @@ class Result:
 
 
 def solve(dev: Device, A: DMat, M: DILU | None, x: DVec, b: DVec, solver=BICGSTAB, tol_rel=1e-7,
-          tol_abs=1e-7, tol_rb=1e-7, maxit=1000, restart=30, verb=0, trace_cap=0, aug_k=3, bgsl=4,
+          tol_abs=1e-7, tol_rb=1e-7, maxit=1000, restart=-1, verb=0, trace_cap=0, aug_k=3, bgsl=4,
           idrs=4) -> Result:
     prm = _lib.SolveParams(solver, tol_rel, tol_abs, tol_rb, maxit, restart, verb, aug_k, bgsl, idrs)
     it, res, tl = ctypes.c_int(), ctypes.c_double(), ctypes.c_int()

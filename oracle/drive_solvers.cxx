@@ -10,11 +10,13 @@
 // It prints the iteration count, the residual and digests of x in %.17e, so
 // the two binaries' outputs can be compared as strings.
 //
-// usage: drive_solvers SOLVER PC LEVEL N MAXIT PARAM
+// usage: drive_solvers SOLVER PC LEVEL N MAXIT PARAM [REPEAT]
 //   SOLVER  LSSP_SOLVER_TYPE value (type-defs.h:157-178)
 //   PC      0 PC_NON, 1 ILUK (LEVEL), 2 ILUT(1e-4, 20)
 //   N       7-pt Poisson N^3 (6 / -1, natural order, b = 1, x0 = 0)
 //   PARAM   restart m (GMRES family, ORTHOMIN), l (BiCGSTAB(l)) or s (IDR(s)); <= 0: default
+//   REPEAT  1: after the first solve, solve again with b = 2 (same assemble),
+//           then scale A by 1.5, re-assemble and solve with b = 1 -- three lines
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -52,8 +54,8 @@ static lssp_mat_csr poisson7(int N)
 
 int main(int argc, char **argv)
 {
-    if (argc != 7) {
-        fprintf(stderr, "usage: %s SOLVER PC LEVEL N MAXIT PARAM\n", argv[0]);
+    if (argc != 7 && argc != 8) {
+        fprintf(stderr, "usage: %s SOLVER PC LEVEL N MAXIT PARAM [REPEAT]\n", argv[0]);
         return 2;
     }
     const int sv = atoi(argv[1]), pct = atoi(argv[2]), level = atoi(argv[3]), N = atoi(argv[4]);
@@ -84,17 +86,34 @@ int main(int argc, char **argv)
         else if (sv == LSSP_SOLVER_IDRS) lssp_solver_set_idrs(solver, param);
         else lssp_solver_set_restart(solver, param);
     }
+    const bool repeat = argc == 8 && atoi(argv[7]) == 1;
+    auto report = [&]() {
+        double s1 = 0, s2 = 0;
+        for (int i = 0; i < n; i++) {
+            s1 += x.d[i];
+            s2 += x.d[i] * x.d[i];
+        }
+        lssp_mv_amxpbyz(-1, A, x, 1, b, r);
+        printf("nits %d residual %.17e xsum %.17e xsq %.17e x0 %.17e xlast %.17e true_res %.17e\n", solver.nits,
+               solver.residual, s1, s2, x.d[0], x.d[n - 1], lssp_vec_norm(r));
+    };
     lssp_solver_assemble(solver, A, x, b, pc);
     lssp_solver_solve(solver, pc);
-
-    double s1 = 0, s2 = 0;
-    for (int i = 0; i < n; i++) {
-        s1 += x.d[i];
-        s2 += x.d[i] * x.d[i];
+    report();
+    if (repeat) {
+        // the same assembled system, another right-hand side
+        lssp_vec_set_value(x, 0.);
+        lssp_vec_set_value(b, 2.);
+        lssp_solver_solve(solver, pc);
+        report();
+        // a new matrix: re-assemble (new copy of A, new factors), then solve
+        for (int k = 0; k < A.num_nnzs; k++) A.Ax[k] *= 1.5;
+        lssp_vec_set_value(x, 0.);
+        lssp_vec_set_value(b, 1.);
+        lssp_solver_assemble(solver, A, x, b, pc);
+        lssp_solver_solve(solver, pc);
+        report();
     }
-    lssp_mv_amxpbyz(-1, A, x, 1, b, r);
-    printf("nits %d residual %.17e xsum %.17e xsq %.17e x0 %.17e xlast %.17e true_res %.17e\n", solver.nits,
-           solver.residual, s1, s2, x.d[0], x.d[n - 1], lssp_vec_norm(r));
 
     lssp_solver_destroy(solver, pc);
     lssp_mat_destroy(A);

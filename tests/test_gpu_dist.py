@@ -139,3 +139,54 @@ def test_multirank_on_one_gpu_equals_oracle_prank_mode(world, N, solver):
     assert res == o.residual
     assert np.array_equal(trace, o.trace)
     assert np.array_equal(x, o.x)
+
+
+def _bad_worker(rank, world, port, bad_rank, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import lssp_amd
+        from lssp_amd.dist import GlooTransport
+        dev = lssp_amd.Device(0)
+        dev.comm_init_host(world, rank, GlooTransport())
+        N = 8
+        n = N ** 3
+        blk = (n + world - 1) // world
+        r0 = min(rank * blk, n)
+        nl = min(blk, n - r0)
+        Ap, Aj, Ax = lssp_amd.poisson(3, N, r0, nl)
+        if rank == bad_rank:
+            Aj = Aj.copy()
+            Aj[3] = n + 7  # a column outside the global matrix
+        try:
+            lssp_amd.DMat(dev, Ap, Aj, Ax, dist=(n, r0))
+            status = 0
+        except lssp_amd.LsspError as e:
+            status = e.status
+        out.put((rank, status))
+        dev.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bad_rank", [0, 1])
+def test_dist_upload_bad_input_fails_on_every_rank(bad_rank):
+    """lssp_amd_mat_upload_dist agrees on the input checks before any
+    collective: one rank's bad column makes BOTH ranks return EINVAL instead
+    of leaving the good one waiting in the halo-plan exchange."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bad_worker, args=(r, 2, port, bad_rank, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        got = dict(q.get(timeout=120) for _ in range(2))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+    assert got == {0: 1, 1: 1}
+    assert all(p.exitcode == 0 for p in procs)
