@@ -6,6 +6,7 @@
 #include <chrono>
 #include <cstdarg>
 #include <cstring>
+#include <thread>
 
 #include "internal.h"
 
@@ -86,6 +87,34 @@ int lprint(const char *fmt, ...)
     fputs(buf, stdout);
     fflush(stdout);
     return n;
+}
+
+void setup_mark(const char *phase)
+{
+    static const bool on = getenv("LSSP_AMD_SETUP_TIMES") && atoi(getenv("LSSP_AMD_SETUP_TIMES"));
+    static double last = 0;
+    if (!on) return;
+    const double t = wall_time();
+    if (phase) fprintf(stderr, "lssp_amd setup: %-28s %8.3f s\n", phase, last ? t - last : 0.0);
+    last = t;
+}
+
+void parallel_for(long n, const std::function<void(long, long)> &f)
+{
+    static const int nt = [] {
+        int t = (int)std::thread::hardware_concurrency();
+        const char *e = getenv("OMP_NUM_THREADS");
+        if (e && atoi(e) > 0) t = std::min(t, atoi(e));
+        return std::max(1, std::min(t, 16));
+    }();
+    const int k = (int)std::min<long>(nt, std::max<long>(1, n / 4096));
+    if (k <= 1) {
+        f(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int q = 0; q < k; q++) th.emplace_back([&, q] { f(n * q / k, n * (q + 1) / k); });
+    for (std::thread &t : th) t.join();
 }
 
 double wall_time()
@@ -406,15 +435,23 @@ static int ilu_upload(lssp_amd_ctx *c, lssp_amd_ilu *M)
 {
     // structured ILU(0) of a 5-/7-point grid: line sweeps (linesweep.hip); the
     // packet schedules of the general sweeps are then not needed
+    setup_mark(nullptr);
     const int ls = build_line_sweep(c, M->n, M->Lp, M->Lj, M->Lx, M->Up, M->Uj, M->Ux, M->line);
     if (ls != LSSP_AMD_OK && ls != LSSP_AMD_EUNSUPPORTED) return ls;
-    const bool packets = ls != LSSP_AMD_OK;
-    LSSP_TRY(build_trisched(c, M->n, M->Lp, M->Lj, M->Lx, false, M->lower, nullptr, packets));
-    LSSP_TRY(build_trisched(c, M->n, M->Up, M->Uj, M->Ux, true, M->upper, packets ? &M->lower : nullptr, packets));
+    setup_mark("line sweeps");
+    // line sweeps serve every sweep of a structured factor: the packet and
+    // sync-free schedules are then not built (only the level counts)
+    const bool general = ls != LSSP_AMD_OK;
+    LSSP_TRY(build_trisched(c, M->n, M->Lp, M->Lj, M->Lx, false, M->lower, nullptr, general, general));
+    LSSP_TRY(build_trisched(c, M->n, M->Up, M->Uj, M->Ux, true, M->upper, general ? &M->lower : nullptr, general,
+                            general));
+    setup_mark("sweep schedules (L, U)");
     M->lower.h_pos.clear();
     M->lower.h_pos.shrink_to_fit();
-    LSSP_HIP(hipMalloc(&M->d_cache, sizeof(double) * std::max(M->n, 1)));
-    LSSP_TRY(launch_fill(c, M->d_cache, M->n, TRI_SENTINEL));
+    if (general) {  // the sync-free sweeps' intermediate vector
+        LSSP_HIP(hipMalloc(&M->d_cache, sizeof(double) * std::max(M->n, 1)));
+        LSSP_TRY(launch_fill(c, M->d_cache, M->n, TRI_SENTINEL));
+    }
     LSSP_HIP(hipStreamSynchronize(c->stream));
     return LSSP_AMD_OK;
 }
@@ -427,6 +464,7 @@ int lssp_amd_ilu_create(lssp_amd_ctx *c, int kind, int n, const int *Ap, const i
     if (Ap[n] < 1) return LSSP_AMD_EINVAL;
     LSSP_HIP(hipSetDevice(c->device));
     auto t0 = std::chrono::steady_clock::now();
+    setup_mark(nullptr);
     HostCSR A;
     A.n = n;
     A.ncols = n;
@@ -434,10 +472,11 @@ int lssp_amd_ilu_create(lssp_amd_ctx *c, int kind, int n, const int *Ap, const i
     A.Aj.assign(Aj, Aj + Ap[n]);
     A.Ax.assign(Ax, Ax + Ap[n]);
     sort_columns(A);  // lssp.cxx:173
+    setup_mark("copy + column sort");
     if (kind == LSSP_AMD_ILUK && level < 0) level = 1;  // pc-iluk.cxx:583-592
     HostCSR L, U;
     int fst = LSSP_AMD_OK;
-    ilu_factor(c, kind, A, level, tol < 0 ? 1e-3 : tol, p, blk, L, U, &fst);
+    ilu_factor(c, kind, std::move(A), level, tol < 0 ? 1e-3 : tol, p, blk, L, U, &fst);
     if (fst != LSSP_AMD_OK) return fst;
     lssp_amd_ilu *M = new lssp_amd_ilu();
     M->ctx = c;

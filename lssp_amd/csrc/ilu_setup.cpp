@@ -22,9 +22,16 @@ constexpr double ZERO_DIAG_TOL = 1e-10;   // pc.cxx:7
 // matrix-utils.cxx:483-587 -- a row without a diagonal gets (i, tol) at its
 // sorted position.  (The reference leaves num_nnzs stale here, so its ILU(0)
 // and ILUT then read past the copied arrays; we insert the entry as intended.)
-HostCSR adjust_zero_diag(const HostCSR &A, double tol)
+HostCSR adjust_zero_diag(HostCSR &&A, double tol)
 {
     const int n = A.n;
+    bool all = true;  // the common case: every row has its diagonal -- no copy
+    for (int i = 0; i < n && all; i++) {
+        bool has = false;
+        for (int k = A.Ap[i]; k < A.Ap[i + 1] && !has; k++) has = A.Aj[k] == i;
+        all = has;
+    }
+    if (all) return std::move(A);
     HostCSR M;
     M.n = n;
     M.ncols = A.ncols;
@@ -54,10 +61,10 @@ HostCSR adjust_zero_diag(const HostCSR &A, double tol)
 }
 
 // matrix-utils.cxx:589-698
-HostCSR block_diag(const HostCSR &A, int blk)
+HostCSR block_diag(HostCSR &&A, int blk)
 {
     const int n = A.n;
-    if (blk >= n) return A;
+    if (blk >= n) return std::move(A);
     HostCSR M;
     M.n = n;
     M.ncols = A.ncols;
@@ -376,22 +383,24 @@ void sort_columns(HostCSR &A)
 // pc-iluk.cxx:411-581 / pc-ilut.cxx:288-456: adjust_zero_diag, optional
 // symbolic ILU(k), block-diagonal extraction, per-block factorization, split
 // into L (unit diagonal LAST) and U (pivot FIRST).
-void ilu_factor(lssp_amd_ctx *c, int kind, const HostCSR &A0, int level, double tol, int p, int blk, HostCSR &L,
+void ilu_factor(lssp_amd_ctx *c, int kind, HostCSR &&A0, int level, double tol, int p, int blk, HostCSR &L,
                 HostCSR &U, int *status)
 {
     *status = LSSP_AMD_OK;
     const int n = A0.n;
     if (kind == LSSP_AMD_ILUT && p <= 0) p = (A0.Ap[n] + n - 1) / n;  // pc-ilut.cxx:436-438
-    HostCSR Az = adjust_zero_diag(A0, ZERO_DIAG_TOL);
+    HostCSR Az = adjust_zero_diag(std::move(A0), ZERO_DIAG_TOL);
+    setup_mark("adjust_zero_diag");
     if (blk <= 0 || blk > n) blk = n;
     HostCSR M;
     if (kind == LSSP_AMD_ILUK && level > 0) {
         HostCSR S = iluk_symbolic(Az, level);
-        M = block_diag(S, blk);
+        M = block_diag(std::move(S), blk);
     } else {
-        M = block_diag(Az, blk);
+        M = block_diag(std::move(Az), blk);
     }
     Az = HostCSR();
+    setup_mark("symbolic / block_diag");
 
     HostCSR F;
     static const bool host_ilu0 = getenv("LSSP_AMD_ILU_HOST") && atoi(getenv("LSSP_AMD_ILU_HOST"));
@@ -425,33 +434,53 @@ void ilu_factor(lssp_amd_ctx *c, int kind, const HostCSR &A0, int level, double 
     }
     }
     M = HostCSR();
+    setup_mark("numeric factorization");
 
+    // split: row counts first, then every entry written in place
     L.n = U.n = L.ncols = U.ncols = n;
     L.Ap.assign(n + 1, 0);
     U.Ap.assign(n + 1, 0);
-    L.Aj.clear();
-    L.Ax.clear();
-    U.Aj.clear();
-    U.Ax.clear();
+    parallel_for(n, [&](long i0, long i1) {
+        for (int i = (int)i0; i < (int)i1; i++) {
+            int nl = 0, nu = 0;
+            for (int k = F.Ap[i]; k < F.Ap[i + 1]; k++) {
+                const int c = F.Aj[k];
+                nl += c <= i;
+                nu += c >= i;
+            }
+            L.Ap[i + 1] = nl;
+            U.Ap[i + 1] = nu;
+        }
+    });
     for (int i = 0; i < n; i++) {
+        L.Ap[i + 1] += L.Ap[i];
+        U.Ap[i + 1] += U.Ap[i];
+    }
+    L.Aj.resize(L.Ap[n]);
+    L.Ax.resize(L.Ap[n]);
+    U.Aj.resize(U.Ap[n]);
+    U.Ax.resize(U.Ap[n]);
+    parallel_for(n, [&](long i0, long i1) {
+    for (int i = (int)i0; i < (int)i1; i++) {
+        int pl = L.Ap[i], pu = U.Ap[i];
         for (int k = F.Ap[i]; k < F.Ap[i + 1]; k++) {
             const int c = F.Aj[k];
             if (c < i) {
-                L.Aj.push_back(c);
-                L.Ax.push_back(F.Ax[k]);
+                L.Aj[pl] = c;
+                L.Ax[pl++] = F.Ax[k];
             } else if (c == i) {
-                L.Aj.push_back(c);
-                L.Ax.push_back(1);
-                U.Aj.push_back(c);
-                U.Ax.push_back(F.Ax[k]);
+                L.Aj[pl] = c;
+                L.Ax[pl++] = 1;
+                U.Aj[pu] = c;
+                U.Ax[pu++] = F.Ax[k];
             } else {
-                U.Aj.push_back(c);
-                U.Ax.push_back(F.Ax[k]);
+                U.Aj[pu] = c;
+                U.Ax[pu++] = F.Ax[k];
             }
         }
-        L.Ap[i + 1] = (int)L.Aj.size();
-        U.Ap[i + 1] = (int)U.Aj.size();
     }
+    });
+    setup_mark("L/U split");
 }
 
 // Level analysis + upload of one triangular factor.
@@ -461,7 +490,8 @@ void ilu_factor(lssp_amd_ctx *c, int kind, const HostCSR &A0, int level, double 
 //          storage order (solver-tri.cxx:35-41) -- stored reversed here so the
 //          kernel always walks forward.
 int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std::vector<int> &Tj,
-                   const std::vector<double> &Tx, bool upper, TriSched &t, const TriSched *prod, bool packets)
+                   const std::vector<double> &Tx, bool upper, TriSched &t, const TriSched *prod, bool packets,
+                   bool arrays)
 {
     t.n = n;
     std::vector<int> lev(n, 0);
@@ -500,6 +530,7 @@ int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std
     for (int i = 0; i < n; i++) nlev = std::max(nlev, lev[i] + 1);
     t.nlevels = n ? nlev : 0;
     if (packets) LSSP_TRY(build_bp_schedule(c, n, Tp, Tj, Tx, upper, lev, t, prod));
+    if (!arrays) return LSSP_AMD_OK;  // line sweeps: only the level count is reported
     // counting sort by level; rows of a level stay in row order (lower) or in
     // descending row order (upper, mirroring the backward sweep)
     std::vector<int> start(nlev + 1, 0), perm(n);

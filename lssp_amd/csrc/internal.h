@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -254,6 +255,11 @@ int ensure_part(lssp_amd_ctx *c, long C);
 // with lssp_amd_set_print, else to stdout (flushed, as lssp_printf does)
 int lprint(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 double wall_time();  // seconds, lssp_get_time() (utils.cxx:40-46)
+// setup phase timings to stderr when LSSP_AMD_SETUP_TIMES=1 (tuning aid)
+void setup_mark(const char *phase);
+// host setup loops: f(lo, hi) over [0, n) in contiguous chunks on up to 16
+// threads (OMP_NUM_THREADS / the hardware concurrency, whichever is smaller)
+void parallel_for(long n, const std::function<void(long, long)> &f);
 
 // ILU setup (ilu_setup.cpp), exact restatement of pc-iluk.cxx / pc-ilut.cxx
 struct HostCSR {
@@ -265,13 +271,13 @@ void sort_columns(HostCSR &A);
 // c != nullptr: ILUK's numeric ILU(0) runs on c's GPU (ilu_factor.hip), bitwise
 // the host restatement (LSSP_AMD_ILU_HOST=1 selects the host one); ILUT stays
 // on the host (pc-ilut.cxx:51-286 is sequential by row)
-void ilu_factor(lssp_amd_ctx *c, int kind, const HostCSR &A, int level, double tol, int p, int blk, HostCSR &L,
+void ilu_factor(lssp_amd_ctx *c, int kind, HostCSR &&A, int level, double tol, int p, int blk, HostCSR &L,
                 HostCSR &U, int *status);
 int ilu0_factor_gpu(lssp_amd_ctx *c, int n, int blk, const std::vector<int> &Ap, const std::vector<int> &Aj,
                     std::vector<double> &Ax);
 int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std::vector<int> &Tj,
                    const std::vector<double> &Tx, bool upper, TriSched &t, const TriSched *prod = nullptr,
-                   bool packets = true);
+                   bool packets = true, bool arrays = true);
 // line sweeps (linesweep.hip): LSSP_AMD_EUNSUPPORTED when the factors are not
 // the structured ILU(0) of a 5-/7-point grid
 int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std::vector<int> &Lj,

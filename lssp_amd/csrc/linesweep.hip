@@ -130,25 +130,31 @@ static inline void step_range(int nx, int nj, int np, int s, int p, int &lo, int
     hi = std::min(nj - 1, s - p);
 }
 
-// coefficient of row (i, j, k) of one sweep in that sweep's coordinates:
-// component a = 0 (k-1), 1 (j-1), 2 (i-1), 3 (diagonal)
+// coefficients of one sweep in that sweep's row order (row r_sweep = r for L,
+// n-1-r for U), NA per row: component a = 0 (k-1), 1 (j-1), 2 (i-1), 3
+// (diagonal); a missing neighbour gets +0.0 (its operand is +0.0 too)
 struct CoefSrc {
-    const std::vector<int> *Tp, *Tj;
-    const std::vector<double> *Tx;
-    bool upper;
-    long n, nx, plane;
-    double get(long r_sweep, int a) const
+    std::vector<double> c;
+    int NA = 3;
+    void build(const std::vector<int> &Tp, const std::vector<int> &Tj, const std::vector<double> &Tx, bool upper,
+               long n, long nx, long plane, int na)
     {
-        const long r = upper ? n - 1 - r_sweep : r_sweep;
-        const int b = (*Tp)[r], e = (*Tp)[r + 1];
-        if (a == 3) return upper ? (*Tx)[b] : (*Tx)[e - 1];
-        const long off = a == 0 ? plane : a == 1 ? nx : 1;
-        const long want = upper ? r + off : r - off;
-        const int s0 = upper ? b + 1 : b, s1 = upper ? e : e - 1;
-        for (int q = s0; q < s1; q++)
-            if ((*Tj)[q] == want) return (*Tx)[q];
-        return 0.0;  // missing neighbour: +0.0 coefficient, the operand is +0.0 too
+        NA = na;
+        c.assign((size_t)n * NA, 0.0);
+        parallel_for(n, [&](long r0, long r1) {
+        for (long r = r0; r < r1; r++) {
+            double *row = c.data() + (size_t)(upper ? n - 1 - r : r) * NA;
+            const int b = Tp[r], e = Tp[r + 1];
+            if (NA == 4) row[3] = upper ? Tx[b] : Tx[e - 1];
+            for (int q = upper ? b + 1 : b; q < (upper ? e : e - 1); q++) {
+                const long off = upper ? Tj[q] - r : r - Tj[q];
+                const int a = off == plane ? 0 : off == nx ? 1 : 2;  // detect_grid: off is one of 1, nx, plane
+                row[a] = Tx[q];
+            }
+        }
+        });
     }
+    double get(long r_sweep, int a) const { return c[(size_t)r_sweep * NA + a]; }
 };
 
 static int build_tiles(const LineGeom &g, int P, int W, std::vector<LineTile> &tiles, int &S)
@@ -206,7 +212,9 @@ static int upload_sweep(lssp_amd_ctx *c, const LineGeom &g, const std::vector<Li
     // + slack for the loaders' whole 1 KB pieces past the last block
     const long slack = 16 * 1024 / 8;
     std::vector<double> coef((size_t)rows_total * NA + slack, 0.0);
-    for (const LineTile &t : tt)
+    parallel_for((long)tt.size(), [&](long t0, long t1) {
+    for (long ti = t0; ti < t1; ti++) {
+        const LineTile &t = tt[ti];
         for (int s = 0; s < t.T; s++) {
             double *blk = coef.data() + (size_t)(t.cbase + (long)s * P * t.nj) * NA;
             for (int p = 0; p < t.np; p++) {
@@ -219,6 +227,8 @@ static int upload_sweep(lssp_amd_ctx *c, const LineGeom &g, const std::vector<Li
                 }
             }
         }
+    }
+    });
     ls.nx = g.nx;
     ls.ny = g.ny;
     ls.nz = g.nz;
@@ -267,8 +277,9 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
             u.tj = Jp > 0 ? Kp * W + Jp - 1 : -1;
         }
     const long plane = (long)g.nx * g.ny;
-    CoefSrc cl{&Lp, &Lj, &Lx, false, n, g.nx, plane};
-    CoefSrc cu{&Up, &Uj, &Ux, true, n, g.nx, plane};
+    CoefSrc cl, cu;
+    cl.build(Lp, Lj, Lx, false, n, g.nx, plane, g.unitL ? 3 : 4);
+    cu.build(Up, Uj, Ux, true, n, g.nx, plane, 4);
     li.g = g;
     li.W = W;
     li.S = S;
