@@ -208,6 +208,54 @@ int lssp_amd_mat_upload_dist(lssp_amd_ctx *ctx, int n_global, int row0, int nloc
                              const int *Ap, const int *Aj, const double *Ax, lssp_amd_mat **A);
 int lssp_amd_mat_local_rows(const lssp_amd_mat *A, int *row0, int *nlocal, int *nhalo);
 
+/* ---- device index arrays: the int members of lssp_mat_csr / lssp_mat_coo /
+ *      lssp_mat_bcsr (type-defs.h:15-55) in HBM, as lssp_amd_vec_* for doubles */
+int lssp_amd_idx_alloc(lssp_amd_ctx *ctx, long n, int **d);
+int lssp_amd_idx_free(lssp_amd_ctx *ctx, int *d);
+int lssp_amd_idx_upload(lssp_amd_ctx *ctx, int *d, const int *h, long n);
+int lssp_amd_idx_download(lssp_amd_ctx *ctx, int *h, const int *d, long n);
+
+/* ---- format conversions on the device (matrix-utils.h:22-49) --------------
+ * Every array is DEVICE memory (idx_alloc / vec_alloc); outputs are caller
+ * allocated and must not overlap the inputs.  Results are bitwise those of
+ * the reference functions, entry order included.  Input structure is checked
+ * on the device first (row pointers non-decreasing from 0 to nnz, indices
+ * that address memory in range); a violation returns LSSP_AMD_EINVAL where the
+ * reference would assert or read out of bounds.  With nnz == 0 the output row
+ * pointers are all 0 (the reference leaves them unallocated). */
+/* lssp_mat_csr_to_coo (matrix-utils.cxx:281-322): Ci[k] = row of entry k,
+ * Cj/Cx copies.  Cj/Cx may be NULL (the caller keeps using Aj/Ax). */
+int lssp_amd_csr_to_coo(lssp_amd_ctx *ctx, int nrows, int nnz, const int *Ap, const int *Aj,
+                        const double *Ax, int *Ci, int *Cj, double *Cx);
+/* lssp_mat_coo_to_csr (matrix-utils.cxx:324-380): rows bucketed in order,
+ * entries of one row kept in input order (a stable sort by row); Ci must lie
+ * in [0, nrows), column indices are copied unchecked as in the reference.
+ * Ap holds nrows + 1. */
+int lssp_amd_coo_to_csr(lssp_amd_ctx *ctx, int nrows, int nnz, const int *Ci, const int *Cj,
+                        const double *Cx, int *Ap, int *Aj, double *Ax);
+/* lssp_mat_transpose (matrix-utils.cxx:700-765): T (ncols x nrows), row c of
+ * T lists the rows of A holding column c in increasing row order (entry
+ * order within a row of A for duplicates).  Tp holds ncols + 1. */
+int lssp_amd_csr_transpose(lssp_amd_ctx *ctx, int nrows, int ncols, int nnz, const int *Ap,
+                           const int *Aj, const double *Ax, int *Tp, int *Tj, double *Tx);
+/* lssp_mat_csr_to_bcsr (matrix-utils.cxx:62-162): n x n CSR (n % bs == 0,
+ * nnz > 0, else EINVAL as lssp_error/assert there) to (n/bs)^2 blocks of
+ * bs x bs, block columns of a block row ascending, each block COLUMN-major
+ * (entry (r, c) at Bx[blk*bs*bs + (c%bs)*bs + r%bs]), absent entries 0, and a
+ * duplicate (r, c) keeps its last value.  Two calls: with Bj == NULL only
+ * *bnnz (number of blocks) is computed; then Bp (n/bs + 1), Bj (*bnnz) and
+ * Bx (*bnnz * bs * bs) are filled. */
+int lssp_amd_csr_to_bcsr(lssp_amd_ctx *ctx, int n, int nnz, int bs, const int *Ap, const int *Aj,
+                         const double *Ax, int *bnnz, int *Bp, int *Bj, double *Bx);
+/* lssp_mat_bcsr_to_csr (matrix-utils.cxx:164-215): the entries with
+ * fabs(v) > 0 (zeros and NaNs are dropped, as there), each row's columns
+ * sorted (lssp_mat_sort_column, :387-481: a row that was out of order gives
+ * every duplicate column the value of its last occurrence).  Two calls: with
+ * Aj == NULL only *nnz is computed (Ap may be NULL); then Ap (nbrows*bs + 1),
+ * Aj and Ax (*nnz) are filled. */
+int lssp_amd_bcsr_to_csr(lssp_amd_ctx *ctx, int nbrows, int nbcols, int bs, int bnnz, const int *Bp,
+                         const int *Bj, const double *Bx, int *nnz, int *Ap, int *Aj, double *Ax);
+
 /* ---- synthetic inputs (example/exam.cxx:4-59 and its 7-pt analogue) ------ */
 long lssp_amd_poisson_nnz(int dim, int N);
 /* rows [row0, row0+nrows) of the 5-pt (dim 2) or 7-pt (dim 3) Laplacian */

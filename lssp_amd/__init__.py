@@ -2,6 +2,7 @@
 trisolves, BiCGSTAB / GMRES / CG) behind the reference's API.
 
     from lssp_amd.device import ...   # C-ABI handles (include/lssp_amd.h): Device, DMat, DILU, solve
+    from lssp_amd import convert      # CSR / COO / BCSR conversions and transpose on the device
     from lssp_amd.dist import GlooTransport   # host-staged multi-rank transport
     from lssp_amd.synthetic import thermal_like   # config 5's matrix
 
@@ -16,11 +17,11 @@ from . import _lib
 _lib.load()
 
 from .device import (BICGSTAB, CG, GMRES, LGMRES, RGMRES, ILUK, ILUT, SERIAL, TREE, DILU, DMat,  # noqa: E402,F401
-                     Device, DVec, LsspError, comm_unique_id, poisson, solve, sort_columns,
+                     Device, DIdx, DVec, LsspError, comm_unique_id, poisson, solve, sort_columns,
                      BICGSAFE, CGS, GPBICG, CR, CRS, BICRSTAB, BICRSAFE, GPBICR, QMRCGSTAB, TFQMR, ORTHOMIN,
                      BICGSTABL, IDRS)
 
-__all__ = ["Device", "DVec", "DMat", "DILU", "solve", "poisson", "sort_columns", "LsspError",
+__all__ = ["Device", "DIdx", "DVec", "DMat", "DILU", "solve", "poisson", "sort_columns", "LsspError",
            "comm_unique_id", "GMRES", "LGMRES", "RGMRES", "BICGSTAB", "CG", "ILUK", "ILUT", "SERIAL", "TREE",
            "BICGSAFE", "CGS", "GPBICG", "CR", "CRS", "BICRSTAB", "BICRSAFE", "GPBICR", "QMRCGSTAB", "TFQMR", "ORTHOMIN",
            "BICGSTABL", "IDRS"]

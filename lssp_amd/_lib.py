@@ -78,6 +78,15 @@ SIGNATURES = {
     "lssp_amd_comm_init_host": (_ci, [_vp, _ci, _ci, _vp]),
     "lssp_amd_mat_upload_dist": (_ci, [_vp, _ci, _ci, _ci, _vp, _vp, _vp, _pvp]),
     "lssp_amd_mat_local_rows": (_ci, [_vp, _vp, _vp, _vp]),
+    "lssp_amd_idx_alloc": (_ci, [_vp, _cl, _pvp]),
+    "lssp_amd_idx_free": (_ci, [_vp, _vp]),
+    "lssp_amd_idx_upload": (_ci, [_vp, _vp, _vp, _cl]),
+    "lssp_amd_idx_download": (_ci, [_vp, _vp, _vp, _cl]),
+    "lssp_amd_csr_to_coo": (_ci, [_vp, _ci, _ci, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "lssp_amd_coo_to_csr": (_ci, [_vp, _ci, _ci, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "lssp_amd_csr_transpose": (_ci, [_vp, _ci, _ci, _ci, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "lssp_amd_csr_to_bcsr": (_ci, [_vp, _ci, _ci, _ci, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "lssp_amd_bcsr_to_csr": (_ci, [_vp, _ci, _ci, _ci, _ci, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "lssp_amd_poisson_nnz": (_cl, [_ci, _ci]),
     "lssp_amd_poisson_rows": (_ci, [_ci, _ci, _cl, _cl, _vp, _vp, _vp]),
 }

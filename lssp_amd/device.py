@@ -92,6 +92,12 @@ class Device:
             v.upload(data)
         return v
 
+    def idx(self, n: int, data=None) -> "DIdx":
+        v = DIdx(self, n)
+        if data is not None:
+            v.upload(data)
+        return v
+
     # ---- comm ------------------------------------------------------------------
     def comm_init(self, nranks: int, rank: int, uid: bytes):
         buf = ctypes.create_string_buffer(uid, len(uid))
@@ -148,6 +154,35 @@ class DVec:
             self.free()
         except Exception:
             pass
+
+
+class DIdx(DVec):
+    """A device int32 array (the Ap / Aj / Ai members of a matrix in HBM)."""
+
+    def __init__(self, dev: Device, n: int):
+        self.dev, self.n = dev, int(n)
+        p = ctypes.c_void_p()
+        _ck(dev.L.lssp_amd_idx_alloc(dev.h, self.n, ctypes.byref(p)), "idx_alloc")
+        self.ptr = p
+        dev._adopt(self)
+
+    def upload(self, a):
+        a = _i32(a)
+        assert a.size <= self.n
+        _ck(self.dev.L.lssp_amd_idx_upload(self.dev.h, self.ptr, _p(a), a.size), "idx_upload")
+        return self
+
+    def download(self, n: int | None = None) -> np.ndarray:
+        out = np.empty(self.n if n is None else n, np.int32)
+        _ck(self.dev.L.lssp_amd_idx_download(self.dev.h, _p(out), self.ptr, out.size), "idx_download")
+        return out
+
+    def free(self):
+        if self.ptr:
+            self.dev.L.lssp_amd_idx_free(self.dev.h, self.ptr)
+            self.ptr = None
+
+    close = free
 
 
 class DMat:

@@ -269,3 +269,55 @@ def ref_solve_bj(solver, A: CSR, b, nblk: int, x0=None, rtol=1e-7, atol=1e-7, rb
         return SolveResult(it, res.value, x, tr[: min(tl.value, trace_cap)].copy())
     finally:
         R.ref_bj_free(h)
+
+
+# ---- format conversions (matrix-utils.cxx:62-380, :700-765) ------------------
+# src "orc": the C restatement; "ref": the reference itself (libref.so)
+def _conv_lib(src):
+    return lib() if src == "orc" else ref()  # every conversion entry point returns int or void
+
+
+def csr_to_coo(nrows, ncols, Ap, Aj, Ax, src="orc"):
+    L = _conv_lib(src)
+    nnz = int(Ap[nrows])
+    Ci, Cj, Cx = np.zeros(nnz, np.int32), np.zeros(nnz, np.int32), np.zeros(nnz)
+    getattr(L, f"{src}_csr_to_coo")(nrows, ncols, _ptr(Ap), _ptr(Aj), _ptr(Ax), _ptr(Ci), _ptr(Cj), _ptr(Cx))
+    return Ci, Cj, Cx
+
+
+def coo_to_csr(nrows, ncols, Ci, Cj, Cx, src="orc"):
+    L = _conv_lib(src)
+    nnz = len(Ci)
+    Ap = np.zeros(nrows + 1, np.int32)
+    Aj, Ax = np.zeros(max(nnz, 1), np.int32), np.zeros(max(nnz, 1))
+    getattr(L, f"{src}_coo_to_csr")(nrows, ncols, nnz, _ptr(Ci), _ptr(Cj), _ptr(Cx), _ptr(Ap), _ptr(Aj),
+                                    _ptr(Ax))
+    return Ap, Aj[:nnz], Ax[:nnz]
+
+
+def transpose(nrows, ncols, Ap, Aj, Ax, src="orc"):
+    L = _conv_lib(src)
+    nnz = int(Ap[nrows])
+    Tp = np.zeros(ncols + 1, np.int32)
+    Tj, Tx = np.zeros(max(nnz, 1), np.int32), np.zeros(max(nnz, 1))
+    getattr(L, f"{src}_transpose")(nrows, ncols, _ptr(Ap), _ptr(Aj), _ptr(Ax), _ptr(Tp), _ptr(Tj), _ptr(Tx))
+    return Tp, Tj[:nnz], Tx[:nnz]
+
+
+def csr_to_bcsr(n, bs, Ap, Aj, Ax, src="orc"):
+    L = _conv_lib(src)
+    nnz = int(Ap[n])
+    Bp = np.zeros(n // bs + 1, np.int32)
+    Bj, Bx = np.zeros(nnz, np.int32), np.zeros(nnz * bs * bs)
+    m = getattr(L, f"{src}_csr_to_bcsr")(n, bs, _ptr(Ap), _ptr(Aj), _ptr(Ax), _ptr(Bp), _ptr(Bj), _ptr(Bx))
+    return Bp, Bj[:m].copy(), Bx[:m * bs * bs].copy()
+
+
+def bcsr_to_csr(nbrows, nbcols, bs, Bp, Bj, Bx, src="orc"):
+    L = _conv_lib(src)
+    cap = max(int(Bp[nbrows]) * bs * bs, 1)
+    Ap = np.zeros(nbrows * bs + 1, np.int32)
+    Aj, Ax = np.zeros(cap, np.int32), np.zeros(cap)
+    m = getattr(L, f"{src}_bcsr_to_csr")(nbrows, nbcols, bs, _ptr(Bp), _ptr(Bj), _ptr(Bx), _ptr(Ap), _ptr(Aj),
+                                         _ptr(Ax))
+    return Ap, Aj[:m].copy(), Ax[:m].copy()

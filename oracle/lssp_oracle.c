@@ -2314,3 +2314,121 @@ EXPORT void orc_poisson(int dim, int N, int *Ap, int *Aj, double *Ax)
                 Ap[r + 1] = (int)o;
             }
 }
+
+/* ------------------------------------------------------------------------ */
+/* Format conversions (matrix-utils.cxx:62-380, :700-765)                   */
+/* ------------------------------------------------------------------------ */
+
+/* matrix-utils.cxx:281-300: the row of every entry; columns / values copied */
+EXPORT void orc_csr_to_coo(int nrows, int ncols, const int *Ap, const int *Aj, const double *Ax, int *Ci, int *Cj,
+                           double *Cx)
+{
+    for (int i = 0; i < nrows; i++)
+        for (int k = Ap[i]; k < Ap[i + 1]; k++) Ci[k] = i;
+    (void)ncols;
+    memcpy(Cj, Aj, sizeof(int) * (size_t)Ap[nrows]);
+    memcpy(Cx, Ax, sizeof(double) * (size_t)Ap[nrows]);
+}
+
+/* matrix-utils.cxx:324-359: counting sort by row; the sequential scatter
+ * keeps the input order inside a row */
+EXPORT void orc_coo_to_csr(int nrows, int ncols, int nnz, const int *Ci, const int *Cj, const double *Cx, int *Ap,
+                           int *Aj, double *Ax)
+{
+    int *next = (int *)calloc((size_t)nrows + 1, sizeof(int));
+    (void)ncols;
+    for (int k = 0; k < nnz; k++) next[Ci[k] + 1]++;
+    for (int i = 0; i < nrows; i++) next[i + 1] += next[i];
+    memcpy(Ap, next, sizeof(int) * ((size_t)nrows + 1));
+    for (int k = 0; k < nnz; k++) {
+        int d = next[Ci[k]]++;
+        Aj[d] = Cj[k];
+        Ax[d] = Cx[k];
+    }
+    free(next);
+}
+
+/* matrix-utils.cxx:700-739: counting sort by column, rows visited in order */
+EXPORT void orc_transpose(int nrows, int ncols, const int *Ap, const int *Aj, const double *Ax, int *Tp,
+                          int *Tj, double *Tx)
+{
+    int *next = (int *)calloc((size_t)ncols + 1, sizeof(int));
+    for (int k = 0; k < Ap[nrows]; k++) next[Aj[k] + 1]++;
+    for (int c = 0; c < ncols; c++) next[c + 1] += next[c];
+    memcpy(Tp, next, sizeof(int) * ((size_t)ncols + 1));
+    for (int i = 0; i < nrows; i++)
+        for (int k = Ap[i]; k < Ap[i + 1]; k++) {
+            int d = next[Aj[k]]++;
+            Tj[d] = i;
+            Tx[d] = Ax[k];
+        }
+    free(next);
+}
+
+/* matrix-utils.cxx:62-162: block pattern per block row (distinct block
+ * columns, ascending), then the entries written row by row into zeroed
+ * column-major bs x bs blocks (a duplicate keeps its last value).  Bj holds
+ * up to nnz, Bx up to nnz*bs*bs; returns the number of blocks. */
+EXPORT int orc_csr_to_bcsr(int n, int bs, const int *Ap, const int *Aj, const double *Ax, int *Bp, int *Bj,
+                           double *Bx)
+{
+    int nb = n / bs, bs2 = bs * bs;
+    int *slot = (int *)malloc(sizeof(int) * (size_t)nb);
+    for (int b = 0; b < nb; b++) slot[b] = -1;
+    Bp[0] = 0;
+    for (int ib = 0; ib < nb; ib++) {
+        int m = Bp[ib];
+        for (int r = ib * bs; r < (ib + 1) * bs; r++)
+            for (int k = Ap[r]; k < Ap[r + 1]; k++) {
+                int bc = Aj[k] / bs;
+                if (slot[bc] != ib) {
+                    slot[bc] = ib;
+                    Bj[m++] = bc;
+                }
+            }
+        qsort(Bj + Bp[ib], (size_t)(m - Bp[ib]), sizeof(int), cmp_int);
+        Bp[ib + 1] = m;
+    }
+    memset(Bx, 0, sizeof(double) * (size_t)Bp[nb] * (size_t)bs2);
+    for (int b = 0; b < nb; b++) slot[b] = -1;
+    for (int ib = 0; ib < nb; ib++) {
+        for (int t = Bp[ib]; t < Bp[ib + 1]; t++) slot[Bj[t]] = t;
+        for (int r = ib * bs; r < (ib + 1) * bs; r++)
+            for (int k = Ap[r]; k < Ap[r + 1]; k++)
+                Bx[(size_t)slot[Aj[k] / bs] * bs2 + (size_t)(Aj[k] % bs) * bs + r % bs] = Ax[k];
+    }
+    free(slot);
+    return Bp[nb];
+}
+
+/* matrix-utils.cxx:164-215: COO of the entries with fabs(v) > 0 in block
+ * order (column-major inside a block), coo_to_csr, then sort_columns
+ * (:387-481).  Aj/Ax hold up to bnnz*bs*bs; returns nnz. */
+EXPORT int orc_bcsr_to_csr(int nbrows, int nbcols, int bs, const int *Bp, const int *Bj, const double *Bx,
+                           int *Ap, int *Aj, double *Ax)
+{
+    int bs2 = bs * bs;
+    size_t cap = (size_t)Bp[nbrows] * (size_t)bs2;
+    int *Ci = (int *)malloc(sizeof(int) * (cap ? cap : 1));
+    int *Cj = (int *)malloc(sizeof(int) * (cap ? cap : 1));
+    double *Cx = (double *)malloc(sizeof(double) * (cap ? cap : 1));
+    int m = 0;
+    for (int ib = 0; ib < nbrows; ib++)
+        for (int t = Bp[ib]; t < Bp[ib + 1]; t++)
+            for (int k = 0; k < bs2; k++) {
+                double v = Bx[(size_t)t * bs2 + k];
+                if (fabs(v) > 0.) {
+                    Ci[m] = ib * bs + k % bs;
+                    Cj[m] = Bj[t] * bs + k / bs;
+                    Cx[m] = v;
+                    m++;
+                }
+            }
+    orc_coo_to_csr(nbrows * bs, nbcols * bs, m, Ci, Cj, Cx, Ap, Aj, Ax);
+    csr_t A = {nbrows * bs, nbcols * bs, m, Ap, Aj, Ax};
+    sort_columns(&A);
+    free(Ci);
+    free(Cj);
+    free(Cx);
+    return m;
+}

@@ -330,3 +330,87 @@ extern "C" int ref_solve_bj(void *hp, int solver, int n, const int *Ap, const in
     lssp_mat_destroy(s.A);
     return it;
 }
+
+// ---------------------------------------------------------------------------
+// Format conversions through the public API (matrix-utils.h:22-49).  Outputs
+// are copied into caller arrays sized as in oracle/lssp_oracle.c's orc_*.
+static void put_csr(const lssp_mat_csr &B, int *Ap, int *Aj, double *Ax)
+{
+    if (B.Ap) memcpy(Ap, B.Ap, sizeof(int) * (B.num_rows + 1));
+    else memset(Ap, 0, sizeof(int) * (B.num_rows + 1));
+    if (B.num_nnzs > 0) {
+        memcpy(Aj, B.Aj, sizeof(int) * B.num_nnzs);
+        memcpy(Ax, B.Ax, sizeof(double) * B.num_nnzs);
+    }
+}
+
+extern "C" void ref_csr_to_coo(int nrows, int ncols, const int *Ap, const int *Aj, const double *Ax, int *Ci,
+                               int *Cj, double *Cx)
+{
+    lssp_mat_csr A = view(nrows, Ap, Aj, Ax);
+    A.num_cols = ncols;
+    lssp_mat_coo C = lssp_mat_csr_to_coo(A);
+    if (C.num_nnzs > 0) {
+        memcpy(Ci, C.Ai, sizeof(int) * C.num_nnzs);
+        memcpy(Cj, C.Aj, sizeof(int) * C.num_nnzs);
+        memcpy(Cx, C.Ax, sizeof(double) * C.num_nnzs);
+    }
+    lssp_mat_destroy(C);
+}
+
+extern "C" void ref_coo_to_csr(int nrows, int ncols, int nnz, const int *Ci, const int *Cj, const double *Cx,
+                               int *Ap, int *Aj, double *Ax)
+{
+    lssp_mat_coo C;
+    C.num_rows = nrows;
+    C.num_cols = ncols;
+    C.num_nnzs = nnz;
+    C.Ai = const_cast<int *>(Ci);
+    C.Aj = const_cast<int *>(Cj);
+    C.Ax = const_cast<double *>(Cx);
+    lssp_mat_csr B = lssp_mat_coo_to_csr(C);
+    put_csr(B, Ap, Aj, Ax);
+    lssp_mat_destroy(B);
+}
+
+extern "C" void ref_transpose(int nrows, int ncols, const int *Ap, const int *Aj, const double *Ax, int *Tp,
+                              int *Tj, double *Tx)
+{
+    lssp_mat_csr A = view(nrows, Ap, Aj, Ax);
+    A.num_cols = ncols;
+    lssp_mat_csr T = lssp_mat_transpose(A);
+    put_csr(T, Tp, Tj, Tx);
+    lssp_mat_destroy(T);
+}
+
+extern "C" int ref_csr_to_bcsr(int n, int bs, const int *Ap, const int *Aj, const double *Ax, int *Bp, int *Bj,
+                               double *Bx)
+{
+    lssp_mat_csr A = view(n, Ap, Aj, Ax);
+    lssp_mat_bcsr B = lssp_mat_csr_to_bcsr(A, bs);
+    int nb = B.num_rows;
+    memcpy(Bp, B.Ap, sizeof(int) * (nb + 1));
+    memcpy(Bj, B.Aj, sizeof(int) * B.num_nnzs);
+    memcpy(Bx, B.Ax, sizeof(double) * (size_t)B.num_nnzs * bs * bs);
+    int m = B.num_nnzs;
+    lssp_mat_destroy(B);
+    return m;
+}
+
+extern "C" int ref_bcsr_to_csr(int nbrows, int nbcols, int bs, const int *Bp, const int *Bj, const double *Bx,
+                               int *Ap, int *Aj, double *Ax)
+{
+    lssp_mat_bcsr B;
+    B.num_rows = nbrows;
+    B.num_cols = nbcols;
+    B.num_nnzs = Bp[nbrows];
+    B.blk_size = bs;
+    B.Ap = const_cast<int *>(Bp);
+    B.Aj = const_cast<int *>(Bj);
+    B.Ax = const_cast<double *>(Bx);
+    lssp_mat_csr A = lssp_mat_bcsr_to_csr(B);
+    put_csr(A, Ap, Aj, Ax);
+    int m = A.num_nnzs;
+    lssp_mat_destroy(A);
+    return m;
+}

@@ -73,3 +73,46 @@ def digest(*arrays) -> str:
         h.update(str(a.dtype).encode())
         h.update(a.tobytes())
     return h.hexdigest()
+
+
+def conv_rand(nr: int, nc: int, k: int, seed: int, specials=False):
+    """Random CSR for the format conversions (vectorised, any size): each row
+    takes 0..k columns drawn with replacement, so rows are unsorted, may repeat
+    a column and may be empty.  ``specials`` plants explicit 0.0, -0.0, NaN and
+    inf values (bcsr_to_csr keeps only fabs(v) > 0, matrix-utils.cxx:192)."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, k + 1, nr)
+    cols = rng.integers(0, nc, (nr, k)).astype(np.int32)
+    keep = np.arange(k)[None, :] < lens[:, None]
+    Aj = cols[keep]
+    Ax = rng.uniform(-1, 1, Aj.size)
+    if specials and Aj.size >= 8:
+        idx = rng.choice(Aj.size, 4 + Aj.size // 50, replace=False)
+        Ax[idx] = np.resize(np.array([0.0, -0.0, np.nan, np.inf]), idx.size)
+    Ap = np.zeros(nr + 1, np.int32)
+    np.cumsum(lens, out=Ap[1:])
+    return Ap, Aj, Ax
+
+
+def conv_handmade_bcsr():
+    """Block CSR inputs the round trip from CSR never produces: block columns
+    out of order, repeated block columns (sorted and unsorted rows), zero /
+    -0.0 / NaN / inf entries, all-zero blocks, no blocks."""
+    rng = np.random.default_rng(2718)
+
+    def mk(nbr, nbc, bs, Bp, Bj, vals=None):
+        Bp, Bj = np.asarray(Bp, np.int32), np.asarray(Bj, np.int32)
+        Bx = rng.uniform(-1, 1, Bj.size * bs * bs) if vals is None else np.asarray(vals, np.float64)
+        return nbr, nbc, bs, Bp, Bj, Bx
+
+    z = rng.uniform(-1, 1, 2 * 9)
+    z[[0, 4, 7, 9, 13]] = [0.0, -0.0, np.nan, np.inf, 0.0]
+    return {
+        "unsorted_blocks": mk(4, 4, 2, [0, 3, 5, 6, 8], [3, 0, 2, 1, 0, 2, 3, 1]),
+        "dup_blocks_bs2": mk(3, 3, 2, [0, 3, 4, 6], [1, 0, 1, 2, 0, 0]),
+        "dup_blocks_bs1": mk(4, 4, 1, [0, 2, 4, 5, 7], [2, 2, 0, 3, 1, 3, 0]),
+        "specials_bs3": mk(2, 3, 3, [0, 1, 2], [2, 0], z),
+        "all_zero": mk(2, 2, 2, [0, 1, 2], [1, 0], np.zeros(8)),
+        "no_blocks": mk(3, 3, 2, [0, 0, 0, 0], []),
+        "rect_bs2": mk(2, 5, 2, [0, 2, 5], [4, 1, 0, 3, 2]),
+    }
