@@ -1,7 +1,9 @@
 // amd_backend.cxx -- the reference-side binding: route LSSP's Krylov hot path
 // (all 18 internal Krylov drivers: BiCGSTAB, BiCGSTAB(l), GMRES(m), GMRES-R(m),
 // LGMRES(m, k), CG, CGS, CR, CRS, BiCGSafe, BiCRSTAB, BiCRSafe, GPBiCG, GPBiCR,
-// QMRCGSTAB, TFQMR, ORTHOMIN, IDR(s), with PC_NON, ILUK or ILUT) to lssp_amd on MI355X.
+// QMRCGSTAB, TFQMR, ORTHOMIN, IDR(s), with PC_NON, ILUK, ILUT or a user PC whose
+// pc.solve is the ILU apply) and the pc.solve seam itself (lssp_pc_ilu_solve,
+// solver-tri.cxx:57-60) to lssp_amd on MI355X.
 //
 // This is the translation unit a maintainer adds to huiscliu/lssp (as
 // src/amd-backend.cxx); INTEGRATION.md describes it.  It compiles against the
@@ -11,6 +13,7 @@
 //
 //     -Wl,--wrap=<mangled lssp_solver_*>   (one per AMD_DRIVER line below)
 //     -Wl,--wrap=<mangled lssp_solver_assemble, lssp_solver_destroy, lssp_pc_assemble>
+//     -Wl,--wrap=<mangled lssp_pc_ilu_solve>
 //
 // so lssp.cxx, the drivers and every caller (example/exam.cxx) stay unchanged.
 // Everything else (assemble, the column sort, the ILU setup of pc-iluk.cxx /
@@ -37,6 +40,14 @@
 
 static int amd_print(void *, const char *msg) { return lssp_printf("%s", msg); }
 
+// LSSP_AMD_BINDING_STATS=1: at exit, report to stderr how many solves and
+// pc.solve applications ran on the device (which calls the binding took)
+static long amd_n_solves = 0, amd_n_applies = 0;
+static void amd_stats(void)
+{
+    fprintf(stderr, "amd: device solves %ld, device pc applies %ld\n", amd_n_solves, amd_n_applies);
+}
+
 static lssp_amd_ctx *amd_ctx()
 {
     static lssp_amd_ctx *c = NULL;
@@ -45,6 +56,8 @@ static lssp_amd_ctx *amd_ctx()
         int st = lssp_amd_ctx_create(d ? atoi(d) : 0, &c);
         if (st != LSSP_AMD_OK) lssp_error(1, "amd: cannot open the device: %s\n", lssp_amd_strerror(st));
         lssp_amd_set_print(amd_print, NULL);
+        const char *bs = getenv("LSSP_AMD_BINDING_STATS");
+        if (bs && atoi(bs) > 0) atexit(amd_stats);
     }
     return c;
 }
@@ -55,10 +68,22 @@ static lssp_amd_ctx *amd_ctx()
         if (st_ != LSSP_AMD_OK) lssp_error(1, "amd: %s: %s\n", #call, lssp_amd_strerror(st_)); \
     } while (0)
 
-static bool amd_handles(const LSSP_PC &pc)
+// the pc.solve seam (type-defs.h:103-105): lssp_pc_ilu_solve as every object
+// linked with --wrap sees it (pc-iluk.cxx:578, pc-ilut.cxx:453, user code)
+#define SYM_PC_ILU_SOLVE _Z17lssp_pc_ilu_solveP8LSSP_PC_9lssp_vec_S1_
+#define AMD_CAT_(a, b) a##b
+#define AMD_CAT(a, b) AMD_CAT_(a, b)
+extern "C" void AMD_CAT(__wrap_, SYM_PC_ILU_SOLVE)(LSSP_PC *pc, lssp_vec x, lssp_vec rhs);
+
+// a user PC (LSSP_PC_USER, pc.cxx:219-227) whose assemble installed the ILU
+// apply (e.g. by calling lssp_pc_iluk_assemble) is an ILU on pc.L / pc.U too
+static bool amd_is_ilu(const LSSP_PC &pc)
 {
-    return pc.type == LSSP_PC_NON || pc.type == LSSP_PC_ILUK || pc.type == LSSP_PC_ILUT;
+    return pc.type == LSSP_PC_ILUK || pc.type == LSSP_PC_ILUT ||
+           (pc.type == LSSP_PC_USER && pc.solve == AMD_CAT(__wrap_, SYM_PC_ILU_SOLVE));
 }
+
+static bool amd_handles(const LSSP_PC &pc) { return pc.type == LSSP_PC_NON || amd_is_ilu(pc); }
 
 // ---- device state per solver ------------------------------------------------
 struct AmdState {
@@ -140,18 +165,69 @@ static int amd_solve(LSSP_SOLVER &s, LSSP_PC &pc, int solver)
     double res = 0.;
     AMD_CK(lssp_amd_solve(c, d.A, pc.type == LSSP_PC_NON ? NULL : d.M, &p, d.x, d.b, &nits, &res, NULL, 0, NULL));
     AMD_CK(lssp_amd_vec_download(c, s.x.d, d.x, n));
+    amd_n_solves++;
 
     s.residual = res;
     s.nits = nits;
     return nits;
 }
 
+// ---- the pc.solve seam: x = U^-1 L^-1 rhs on the device ------------------------
+// A caller that applies the preconditioner itself (pc.solve(&pc, x, rhs)) or a
+// driver this library does not replace reaches lssp_pc_ilu_solve through the
+// function pointer.  The factors pc->L / pc->U go to the device once per PC
+// (identity-checked, dropped with the PC's lifecycle like AmdState); every
+// call moves rhs and x over PCIe, as the caller's vectors are host memory.
+struct AmdPcState {
+    const double *Lx = NULL, *Ux = NULL;
+    int n = 0;
+    lssp_amd_ilu *M = NULL;
+    double *x = NULL, *r = NULL;
+};
+static std::map<const LSSP_PC *, AmdPcState> amd_pcs;
+
+static void amd_drop_pc(const LSSP_PC *pc)
+{
+    std::map<const LSSP_PC *, AmdPcState>::iterator it = amd_pcs.find(pc);
+    if (it == amd_pcs.end()) return;
+    lssp_amd_ctx *c = amd_ctx();
+    if (it->second.M) lssp_amd_ilu_destroy(it->second.M);
+    if (it->second.x) lssp_amd_vec_free(c, it->second.x);
+    if (it->second.r) lssp_amd_vec_free(c, it->second.r);
+    amd_pcs.erase(it);
+}
+
+extern "C" void AMD_CAT(__wrap_, SYM_PC_ILU_SOLVE)(LSSP_PC *pc, lssp_vec x, lssp_vec rhs)
+{
+    assert(x.d != NULL && rhs.d != NULL);
+    lssp_amd_ctx *c = amd_ctx();
+    const int n = pc->L.num_rows;
+    std::map<const LSSP_PC *, AmdPcState>::iterator it = amd_pcs.find(pc);
+    if (it != amd_pcs.end() && (it->second.Lx != pc->L.Ax || it->second.Ux != pc->U.Ax || it->second.n != n)) {
+        amd_drop_pc(pc);  // defensive: factors replaced without lssp_pc_assemble
+        it = amd_pcs.end();
+    }
+    if (it == amd_pcs.end()) {
+        AmdPcState e;
+        AMD_CK(lssp_amd_ilu_from_factors(c, n, pc->L.Ap, pc->L.Aj, pc->L.Ax, pc->U.Ap, pc->U.Aj, pc->U.Ax, &e.M));
+        AMD_CK(lssp_amd_vec_alloc(c, n, &e.x));
+        AMD_CK(lssp_amd_vec_alloc(c, n, &e.r));
+        e.Lx = pc->L.Ax;
+        e.Ux = pc->U.Ax;
+        e.n = n;
+        it = amd_pcs.insert(std::make_pair(pc, e)).first;
+    }
+    AmdPcState &e = it->second;
+    AMD_CK(lssp_amd_vec_upload(c, e.r, rhs.d, n));
+    AMD_CK(lssp_amd_ilu_apply(c, e.M, e.x, e.r));
+    AMD_CK(lssp_amd_vec_download(c, x.d, e.x, n));
+    amd_n_applies++;
+}
+
 // ---- lifecycle hooks: the cached device state follows the reference's objects
 #define SYM_SOLVER_ASSEMBLE _Z20lssp_solver_assembleR12LSSP_SOLVER_R13lssp_mat_csr_9lssp_vec_S3_R8LSSP_PC_
 #define SYM_SOLVER_DESTROY _Z19lssp_solver_destroyR12LSSP_SOLVER_R8LSSP_PC_
 #define SYM_PC_ASSEMBLE _Z16lssp_pc_assembleR8LSSP_PC_12LSSP_SOLVER_
-#define AMD_CAT_(a, b) a##b
-#define AMD_CAT(a, b) AMD_CAT_(a, b)
 
 // lssp_solver_assemble (lssp.cxx:142-189): a new copy of A, the PC re-assembled
 extern "C" void AMD_CAT(__real_, SYM_SOLVER_ASSEMBLE)(LSSP_SOLVER &, lssp_mat_csr &, lssp_vec, lssp_vec, LSSP_PC &);
@@ -167,6 +243,7 @@ extern "C" void AMD_CAT(__real_, SYM_SOLVER_DESTROY)(LSSP_SOLVER &, LSSP_PC &);
 extern "C" void AMD_CAT(__wrap_, SYM_SOLVER_DESTROY)(LSSP_SOLVER &s, LSSP_PC &pc)
 {
     amd_drop(&s);
+    amd_drop_pc(&pc);
     AMD_CAT(__real_, SYM_SOLVER_DESTROY)(s, pc);
 }
 
@@ -176,12 +253,14 @@ extern "C" void AMD_CAT(__wrap_, SYM_PC_ASSEMBLE)(LSSP_PC &pc, LSSP_SOLVER s)
 {
     for (std::map<const LSSP_SOLVER *, AmdState>::iterator it = amd_states.begin(); it != amd_states.end(); ++it)
         if (it->second.pc == &pc) amd_drop_factors(it->second);
+    amd_drop_pc(&pc);
     AMD_CAT(__real_, SYM_PC_ASSEMBLE)(pc, s);
 }
 
 // One wrapper per driver: the linker's --wrap=SYM sends every call of SYM here
 // and names the original __real_SYM; PCs this library does not hold (BILUK,
-// ITSOL, AMG, user PCs) fall through to the reference's own driver.
+// ITSOL, AMG, user PCs with their own solve) fall through to the reference's
+// own driver.
 #define AMD_DRIVER(SYM, KIND)                                                   \
     extern "C" int __real_##SYM(LSSP_SOLVER &, LSSP_PC &);                      \
     extern "C" int __wrap_##SYM(LSSP_SOLVER &s, LSSP_PC &pc)                    \

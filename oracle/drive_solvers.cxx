@@ -12,11 +12,15 @@
 //
 // usage: drive_solvers SOLVER PC LEVEL N MAXIT PARAM [REPEAT]
 //   SOLVER  LSSP_SOLVER_TYPE value (type-defs.h:157-178)
-//   PC      0 PC_NON, 1 ILUK (LEVEL), 2 ILUT(1e-4, 20)
+//   PC      0 PC_NON, 1 ILUK (LEVEL), 2 ILUT(1e-4, 20), 3 a user PC (LSSP_PC_USER,
+//           pc.cxx:219-227) whose assemble calls lssp_pc_iluk_assemble (LEVEL)
 //   N       7-pt Poisson N^3 (6 / -1, natural order, b = 1, x0 = 0)
 //   PARAM   restart m (GMRES family, ORTHOMIN), l (BiCGSTAB(l)) or s (IDR(s)); <= 0: default
 //   REPEAT  1: after the first solve, solve again with b = 2 (same assemble),
 //           then scale A by 1.5, re-assemble and solve with b = 1 -- three lines
+//           2: after the solve, apply the preconditioner directly through the
+//           function pointer, pc.solve(&pc, r, x) and pc.solve(&pc, r, b)
+//           (type-defs.h:103-105) -- two "pcsolve" lines
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -52,6 +56,16 @@ static lssp_mat_csr poisson7(int N)
     return A;
 }
 
+static int g_user_level = 0;
+
+// LSSP_PC_USER's assemble: the reference's own ILU(k) setup, which installs
+// pc.solve = lssp_pc_ilu_solve (pc-iluk.cxx:566-581)
+static void user_ilu_assemble(LSSP_PC &pc, LSSP_SOLVER s)
+{
+    pc.iluk_level = g_user_level;
+    lssp_pc_iluk_assemble(pc, s);
+}
+
 int main(int argc, char **argv)
 {
     if (argc != 7 && argc != 8) {
@@ -74,8 +88,13 @@ int main(int argc, char **argv)
 
     LSSP_SOLVER solver;
     LSSP_PC pc;
-    lssp_solver_create(solver, (LSSP_SOLVER_TYPE)sv, pc, pct == 0 ? LSSP_PC_NON : pct == 1 ? LSSP_PC_ILUK : LSSP_PC_ILUT);
+    lssp_solver_create(solver, (LSSP_SOLVER_TYPE)sv, pc,
+                       pct == 0 ? LSSP_PC_NON : pct == 1 ? LSSP_PC_ILUK : pct == 2 ? LSSP_PC_ILUT : LSSP_PC_USER);
     if (pct == 1) lssp_pc_iluk_set_level(pc, level);
+    if (pct == 3) {
+        g_user_level = level;
+        pc.assemble = user_ilu_assemble;
+    }
     if (pct == 2) {
         lssp_pc_ilut_set_drop_tol(pc, 1e-4);
         lssp_pc_ilut_set_p(pc, 20);
@@ -86,7 +105,8 @@ int main(int argc, char **argv)
         else if (sv == LSSP_SOLVER_IDRS) lssp_solver_set_idrs(solver, param);
         else lssp_solver_set_restart(solver, param);
     }
-    const bool repeat = argc == 8 && atoi(argv[7]) == 1;
+    const int mode = argc == 8 ? atoi(argv[7]) : 0;
+    const bool repeat = mode == 1;
     auto report = [&]() {
         double s1 = 0, s2 = 0;
         for (int i = 0; i < n; i++) {
@@ -100,6 +120,17 @@ int main(int argc, char **argv)
     lssp_solver_assemble(solver, A, x, b, pc);
     lssp_solver_solve(solver, pc);
     report();
+    if (mode == 2 && pct != 0) {
+        for (int t = 0; t < 2; t++) {
+            pc.solve(&pc, r, t == 0 ? x : b);
+            double s1 = 0, s2 = 0;
+            for (int i = 0; i < n; i++) {
+                s1 += r.d[i];
+                s2 += r.d[i] * r.d[i];
+            }
+            printf("pcsolve %d sum %.17e sq %.17e r0 %.17e rlast %.17e\n", t, s1, s2, r.d[0], r.d[n - 1]);
+        }
+    }
     if (repeat) {
         // the same assembled system, another right-hand side
         lssp_vec_set_value(x, 0.);

@@ -100,3 +100,27 @@ def test_binding_keeps_device_state_across_solves_and_follows_reassemble(solver,
     amd = run(DRV_AMD, LSSP_AMD_REDUCE="serial")
     assert len(ref) == 3 and amd == ref
     assert ref[0] != ref[2]  # the re-assembled system really differs
+
+
+@pytest.mark.parametrize("solver,pc,level", [("bicgstab", "3", "0"), ("gmres", "3", "1"), ("cg", "3", "0"),
+                                             ("tfqmr", "3", "0"), ("bicgstab", "1", "0"), ("gmres", "2", "0")])
+def test_pc_solve_seam_runs_on_the_device(solver, pc, level):
+    """The function-pointer PC seam (type-defs.h:103-105, pc.cxx:219-227):
+    PC 3 is an LSSP_PC_USER whose assemble calls lssp_pc_iluk_assemble, so
+    pc.solve = lssp_pc_ilu_solve -- the binding runs that whole solve on the
+    device; then drive_solvers calls pc.solve(&pc, r, x) and pc.solve(&pc, r, b)
+    itself, which the wrapped lssp_pc_ilu_solve applies on the device.  Every
+    line bitwise the reference's (SERIAL mode); LSSP_AMD_BINDING_STATS shows
+    the calls really took the device."""
+    args = [str(ALL_SOLVERS[solver]), pc, level, "12", "300", "0", "2"]
+
+    def run(path, **env):
+        out = subprocess.run([path, *args], capture_output=True, text=True, timeout=120,
+                             env=dict(os.environ, **env), cwd=ROOT)
+        assert out.returncode == 0, out.stderr[-2000:]
+        return [ln for ln in out.stdout.splitlines() if ln.startswith(("nits ", "pcsolve "))], out.stderr
+
+    ref, _ = run(DRV_REF)
+    amd, err = run(DRV_AMD, LSSP_AMD_REDUCE="serial", LSSP_AMD_BINDING_STATS="1")
+    assert len(ref) == 3 and amd == ref
+    assert "amd: device solves 1, device pc applies 2" in err
