@@ -39,9 +39,11 @@ sys.path.insert(0, HERE)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def spmv_bytes(nnz: int, n: int) -> int:
-    """algorithmic bytes of y = A x: Ax 8 + Aj 4 per nnz, Ap 4 + x 8 + y 8 per row"""
-    return 12 * nnz + 20 * n + 4
+def spmv_bytes(nnz: int, n: int, coded: bool = False) -> int:
+    """algorithmic bytes of y = A x: Ax 8 + Aj 4 per nnz, Ap 4 + x 8 + y 8 per row.
+    coded: the device layout's 1-byte diagonal id replaces Aj's 4 bytes
+    (lssp_amd_mat_layout; 7-pt: 7 offsets), so the kernel moves 9 per nnz"""
+    return (9 if coded else 12) * nnz + 20 * n + 4
 
 
 def ilu_apply_bytes(nnzL: int, nnzU: int, n: int) -> int:
@@ -178,7 +180,10 @@ def main():
     e1.record(stream)
     e1.synchronize()
     spmv_ms = e0.elapsed_time(e1) / args.spmv_reps
-    spmv_gbs = spmv_bytes(nnz_local, nl) / (spmv_ms * 1e-3) / 1e9
+    ndiag = A.ndiag
+    spmv_b = spmv_bytes(nnz_local, nl, coded=ndiag > 0)
+    spmv_gbs = spmv_b / (spmv_ms * 1e-3) / 1e9
+    csr_equiv_gbs = spmv_bytes(nnz_local, nl) / (spmv_ms * 1e-3) / 1e9
 
     # ---- ILU apply roofline leg (the dominant operator) ----
     zs = dev.vec(A.nx)
@@ -244,7 +249,9 @@ def main():
                        "transport": ("host-staged gloo, all ranks on GPU 0 (rehearsal, not a scaling number)"
                                      if args.share_gpu and world > 1 else "rccl" if world > 1 else "none")},
             "spmv": {"gbps": round(spmv_gbs_total, 1), "frac_hbm_peak": round(spmv_gbs / HBM_PEAK_GBS, 4),
-                     "ms_per_call": round(spmv_ms, 5)},
+                     "ms_per_call": round(spmv_ms, 5),
+                     "column_stream": (f"1-byte diagonal ids ({ndiag} offsets)" if ndiag else "int32 columns"),
+                     "csr_int32_equivalent_gbps": round(csr_equiv_gbs, 1)},
             "roofline": {"bound": "hbm", "achieved": round(apply_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(apply_gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("ilu_apply"),
                          "kernel": "ILU(0) apply = k_line (L sweep, rhs in natural order -> the U sweep's "
@@ -253,8 +260,8 @@ def main():
                          "bytes_per_launch": apply_b, "ms_per_launch": round(apply_ms, 5)},
             "roofline_spmv": {"bound": "hbm", "achieved": round(spmv_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(spmv_gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("k_spmv3"),
-                              "kernel": "k_spmv3<EPI_MXY,0> (y = A x)",
-                              "bytes_per_launch": spmv_bytes(nnz_local, nl), "ms_per_launch": round(spmv_ms, 5)},
+                              "kernel": f"k_spmv3<EPI_MXY,0,{'true' if ndiag else 'false'}> (y = A x)",
+                              "bytes_per_launch": spmv_b, "ms_per_launch": round(spmv_ms, 5)},
             "ilu": {"levels_L": M.levelsL, "levels_U": M.levelsU, "setup_s": round(M.setup_seconds, 3)},
             "setup_s": round(t_setup, 2),
         }

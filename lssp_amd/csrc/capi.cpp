@@ -5,7 +5,9 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdarg>
+#include <atomic>
 #include <cstring>
+#include <mutex>
 #include <thread>
 
 #include "internal.h"
@@ -115,6 +117,83 @@ void parallel_for(long n, const std::function<void(long, long)> &f)
     std::vector<std::thread> th;
     for (int q = 0; q < k; q++) th.emplace_back([&, q] { f(n * q / k, n * (q + 1) / k); });
     for (std::thread &t : th) t.join();
+}
+
+// Diagonal-id column coding of a device CSR (the SpMV's index stream): the
+// distinct offsets col - row are collected per thread in small open-addressing
+// sets and merged; with at most 255 of them (5- / 7- / 27-point stencils, the
+// z-slab halo columns of a distributed stencil) every entry becomes the byte
+// index of its offset in the ascending table.  Rows are summed exactly as
+// before (same entries, same order): only the way the column is found changes.
+namespace {
+constexpr int DIAG_MAX = 255, DIAG_HS = 1024;
+
+struct OffSet {
+    int key[DIAG_HS];
+    unsigned char used[DIAG_HS] = {};
+    int count = 0;
+    static unsigned slot(int k) { return ((unsigned)k * 2654435761u) >> 22; }  // 10 bits
+    int find(int k) const
+    {
+        for (unsigned h = slot(k);; h = (h + 1) & (DIAG_HS - 1)) {
+            if (!used[h]) return -1;
+            if (key[h] == k) return (int)h;
+        }
+    }
+    bool add(int k)  // false once more than DIAG_MAX distinct keys were seen
+    {
+        unsigned h = slot(k);
+        for (; used[h]; h = (h + 1) & (DIAG_HS - 1))
+            if (key[h] == k) return true;
+        if (count == DIAG_MAX) return false;
+        used[h] = 1;
+        key[h] = k;
+        count++;
+        return true;
+    }
+};
+}  // namespace
+
+int build_diag_ids(lssp_amd_mat *M, const int *Ap, const int *Aj)
+{
+    M->ndiag = 0;
+    const int n = M->nrows;
+    if (M->nnz == 0 || n == 0) return LSSP_AMD_OK;
+    std::mutex mu;
+    OffSet all;
+    std::atomic<bool> too_many{false};
+    parallel_for(n, [&](long lo, long hi) {
+        OffSet mine;
+        for (long i = lo; i < hi && !too_many.load(std::memory_order_relaxed); i++)
+            for (int k = Ap[i]; k < Ap[i + 1]; k++)
+                if (!mine.add(Aj[k] - (int)i)) {
+                    too_many = true;
+                    return;
+                }
+        std::lock_guard<std::mutex> g(mu);
+        for (int h = 0; h < DIAG_HS && !too_many; h++)
+            if (mine.used[h] && !all.add(mine.key[h])) too_many = true;
+    });
+    if (too_many) return LSSP_AMD_OK;
+    std::vector<int> off;
+    for (int h = 0; h < DIAG_HS; h++)
+        if (all.used[h]) off.push_back(all.key[h]);
+    std::sort(off.begin(), off.end());
+    int id_of[DIAG_HS];
+    for (int t = 0; t < (int)off.size(); t++) id_of[all.find(off[t])] = t;
+    // +32: the SpMV stages the byte stream with 16-byte loads that may touch one
+    // vector past the last entry
+    std::vector<uint8_t> ad((size_t)M->nnz + 32, 0);
+    parallel_for(n, [&](long lo, long hi) {
+        for (long i = lo; i < hi; i++)
+            for (int k = Ap[i]; k < Ap[i + 1]; k++) ad[k] = (uint8_t)id_of[all.find(Aj[k] - (int)i)];
+    });
+    LSSP_HIP(hipMalloc(&M->Ad, ad.size()));
+    LSSP_HIP(hipMalloc(&M->d_off, sizeof(int) * off.size()));
+    LSSP_HIP(hipMemcpy(M->Ad, ad.data(), ad.size(), hipMemcpyHostToDevice));
+    LSSP_HIP(hipMemcpy(M->d_off, off.data(), sizeof(int) * off.size(), hipMemcpyHostToDevice));
+    M->ndiag = (int)off.size();
+    return LSSP_AMD_OK;
 }
 
 double wall_time()
@@ -265,7 +344,7 @@ static int upload_csr(lssp_amd_mat *M, const int *Ap, const int *Aj, const doubl
         LSSP_HIP(hipMemcpy(M->Aj, Aj, sizeof(int) * M->nnz, hipMemcpyHostToDevice));
         LSSP_HIP(hipMemcpy(M->Ax, Ax, sizeof(double) * M->nnz, hipMemcpyHostToDevice));
     }
-    return LSSP_AMD_OK;
+    return build_diag_ids(M, Ap, Aj);
 }
 
 int lssp_amd_mat_upload(lssp_amd_ctx *c, int nrows, int ncols, int nnz, const int *Ap, const int *Aj,
@@ -296,6 +375,8 @@ int lssp_amd_mat_destroy(lssp_amd_mat *M)
     if (M->Ap) (void)hipFree(M->Ap);
     if (M->Aj) (void)hipFree(M->Aj);
     if (M->Ax) (void)hipFree(M->Ax);
+    if (M->Ad) (void)hipFree(M->Ad);
+    if (M->d_off) (void)hipFree(M->d_off);
     if (M->d_send_idx) (void)hipFree(M->d_send_idx);
     if (M->d_send_buf) (void)hipFree(M->d_send_buf);
     delete M;
@@ -308,6 +389,13 @@ int lssp_amd_mat_info(const lssp_amd_mat *A, int *nrows, int *ncols, int *nnz)
     if (nrows) *nrows = A->nrows;
     if (ncols) *ncols = A->ncols;
     if (nnz) *nnz = A->nnz;
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_mat_layout(const lssp_amd_mat *A, int *ndiag)
+{
+    if (!A || !ndiag) return LSSP_AMD_EINVAL;
+    *ndiag = A->ndiag;
     return LSSP_AMD_OK;
 }
 

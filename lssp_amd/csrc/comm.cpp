@@ -367,6 +367,7 @@ int lssp_amd_mat_upload_dist(lssp_amd_ctx *c, int n_global, int row0, int nlocal
         LSSP_HIP(hipMemcpy(M->Aj, lj.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
         LSSP_HIP(hipMemcpy(M->Ax, Ax, sizeof(double) * nnz, hipMemcpyHostToDevice));
     }
+    LSSP_TRY(agree_status(c, build_diag_ids(M, Ap, lj.data())));  // the SpMV's column coding (capi.cpp)
     guard.m = nullptr;
     *out = M;
     return LSSP_AMD_OK;

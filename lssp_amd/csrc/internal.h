@@ -92,6 +92,12 @@ struct lssp_amd_mat {
     int nrows = 0, ncols = 0, nnz = 0;  // local rows; ncols = local column space (owned + halo)
     int *Ap = nullptr, *Aj = nullptr;
     double *Ax = nullptr;
+    // diagonal-id column coding (SpMV): when the rows use at most 255 distinct
+    // offsets col - row (stencil matrices), Ad[k] indexes d_off and the SpMV
+    // reads one byte per entry instead of Aj's four; ndiag == 0: not coded
+    uint8_t *Ad = nullptr;
+    int *d_off = nullptr;
+    int ndiag = 0;
     // distributed layout
     int n_global = 0, row0 = 0, nhalo = 0;
     // halo exchange plan: for each peer, indices (local) to send and the count to receive
@@ -206,6 +212,7 @@ namespace lssp_amd {
 
 // ---- kernel launchers (kernels.hip) ------------------------------------------
 enum Epi { EPI_MXY = 0, EPI_AMXY, EPI_AXPBY, EPI_AMX };  // see spmv kernel
+int build_diag_ids(lssp_amd_mat *M, const int *Ap, const int *Aj);
 int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, const double *x,
                 double beta, const double *y, double *z, int nred, const double *w0,
                 const double *w1);

@@ -287,6 +287,9 @@ struct SpmvArgs {
     const double *w0, *w1;  // fused dot operands: red0 = z*w0, red1 = z*(w1 ? w1 : z)
     double *part;
     long pcap;
+    const uint8_t *Ad;  // diagonal-id column coding (lssp_amd_mat::Ad), CMP kernels
+    const int *off;
+    int ndiag;
 };
 
 // The 256-row blocks are dealt so that each of the 8 XCDs owns one contiguous
@@ -298,13 +301,16 @@ struct SpmvArgs {
 // boundaries, clamped to the padded arrays; entries outside the block are
 // dropped when landing in LDS) and the lane's own Ap[r], Ap[r+1] -- so one
 // memory round trip covers the staging and the row bounds.
-template <int EPI, int NRED>
+// CMP: the columns come from the diagonal-id bytes (col = row + off[Ad[k]]),
+// 1 byte per entry instead of 4 (7-pt: 0.83 of the CSR bytes per product).
+template <int EPI, int NRED, bool CMP>
 __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_pad)
 {
     constexpr int NX2 = (SPMV_CAP / 2 + 1 + 255) / 256;  // double2 loads per lane
-    constexpr int NJ4 = (SPMV_CAP / 4 + 1 + 255) / 256;  // int4 loads per lane
+    constexpr int NJ4 = CMP ? 1 : (SPMV_CAP / 4 + 1 + 255) / 256;  // int4 loads per lane (16 ids when CMP)
     __shared__ __attribute__((aligned(16))) double sx[SPMV_CAP + 2];
-    __shared__ __attribute__((aligned(16))) int sj[SPMV_CAP + 4];
+    __shared__ __attribute__((aligned(16))) int sj[CMP ? SPMV_CAP / 4 + 8 : SPMV_CAP + 4];
+    __shared__ int soff[CMP ? 256 : 1];
     __shared__ double lds[MAX_SLOTS][4];
     const long per = gridDim.x / 8;
     const long blk = (blockIdx.x % 8) * per + blockIdx.x / 8;
@@ -329,21 +335,24 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
     if (cnt <= SPMV_CAP) {
         typedef double dbl2_t __attribute__((ext_vector_type(2)));
         typedef int int4_t __attribute__((ext_vector_type(4)));
-        const long xb = base & ~1L, jb = base & ~3L;
+        // CMP: jb / jmax / jn count 16-byte vectors of ids (16 entries each)
+        constexpr int JS = CMP ? 4 : 2;  // log2 entries per 16-byte vector
+        const long xb = base & ~1L, jb = base & ~((1L << JS) - 1);
         // clamp to the block's last vector: lanes past the range re-read it
         // (no extra lines), and the padded arrays keep it in bounds
         const long last = cnt > 0 ? (long)base + cnt - 1 : (long)base;
         const long xmax = min(last >> 1, (nnz_pad >> 1) - 1);
-        const long jmax = min(last >> 2, (nnz_pad >> 2) - 1);
+        const long jmax = min(last >> JS, (CMP ? (nnz_pad - 4 + 32) >> 4 : nnz_pad >> 2) - 1);
+        if (CMP && tid < a.ndiag) soff[tid] = a.off[tid];
         const dbl2_t *X2 = reinterpret_cast<const dbl2_t *>(a.Ax);
-        const int4_t *J4 = reinterpret_cast<const int4_t *>(a.Aj);
+        const int4_t *J4 = CMP ? reinterpret_cast<const int4_t *>(a.Ad) : reinterpret_cast<const int4_t *>(a.Aj);
         dbl2_t vx[NX2];
         int4_t vj[NJ4];
 #pragma unroll
         for (int u = 0; u < NX2; u++) vx[u] = __builtin_nontemporal_load(X2 + min((xb >> 1) + tid + 256 * u, xmax));
 #pragma unroll
-        for (int u = 0; u < NJ4; u++) vj[u] = __builtin_nontemporal_load(J4 + min((jb >> 2) + tid + 256 * u, jmax));
-        const int xn = (int)(xmax - (xb >> 1)) + 1, jn = (int)(jmax - (jb >> 2)) + 1;  // vectors in range
+        for (int u = 0; u < NJ4; u++) vj[u] = __builtin_nontemporal_load(J4 + min((jb >> JS) + tid + 256 * u, jmax));
+        const int xn = (int)(xmax - (xb >> 1)) + 1, jn = (int)(jmax - (jb >> JS)) + 1;  // vectors in range
 #pragma unroll
         for (int u = 0; u < NX2; u++)
             if (tid + 256 * u < xn) reinterpret_cast<dbl2_t *>(sx)[tid + 256 * u] = vx[u];
@@ -354,6 +363,8 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
         if (r < a.nrows) {
             const int ox = (int)(base - xb) - base, oj = (int)(base - jb) - base;
             const int len = re - rb;
+            const unsigned char *sd = reinterpret_cast<const unsigned char *>(sj);
+            auto col = [&](int k) { return CMP ? r + soff[sd[k + oj]] : sj[k + oj]; };
             if (len > 0 && len <= 8) {
                 // all x gathers of the row in flight at once; the products are
                 // then added in CSR order (clamped extra lanes are not added)
@@ -361,13 +372,13 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
                     const int k = min(rb + u, re - 1);
-                    pr[u] = a.x[sj[k + oj]] * sx[k + ox];
+                    pr[u] = a.x[col(k)] * sx[k + ox];
                 }
 #pragma unroll
                 for (int u = 0; u < 8; u++)
                     if (u < len) sum += pr[u];
             } else {
-                for (int k = rb; k < re; k++) sum += a.x[sj[k + oj]] * sx[k + ox];
+                for (int k = rb; k < re; k++) sum += a.x[col(k)] * sx[k + ox];
             }
         }
     } else if (r < a.nrows) {
@@ -394,13 +405,20 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
     }
 }
 
-template <int EPI>
+template <int EPI, bool CMP>
 static void spmv_dispatch(const SpmvArgs &a, int nred, long nblocks, hipStream_t s, long nnz_pad)
 {
     const long g = (nblocks + 7) / 8 * 8;  // a multiple of 8: whole XCD shares
-    if (nred == 0) k_spmv3<EPI, 0><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
-    else if (nred == 1) k_spmv3<EPI, 1><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
-    else k_spmv3<EPI, 2><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
+    if (nred == 0) k_spmv3<EPI, 0, CMP><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
+    else if (nred == 1) k_spmv3<EPI, 1, CMP><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
+    else k_spmv3<EPI, 2, CMP><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
+}
+
+template <int EPI>
+static void spmv_dispatch(const SpmvArgs &a, int nred, long nblocks, hipStream_t s, long nnz_pad)
+{
+    if (a.ndiag > 0) spmv_dispatch<EPI, true>(a, nred, nblocks, s, nnz_pad);
+    else spmv_dispatch<EPI, false>(a, nred, nblocks, s, nnz_pad);
 }
 
 int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, const double *x,
@@ -410,7 +428,8 @@ int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, c
     if (A->nrows == 0) return LSSP_AMD_OK;
     long nb = num_chunks(A->nrows);
     LSSP_TRY(ensure_part(c, nb));
-    SpmvArgs a{A->nrows, A->Ap, A->Aj, A->Ax, x, y, z, alpha, beta, w0, w1, c->d_part, c->part_cap};
+    SpmvArgs a{A->nrows, A->Ap, A->Aj, A->Ax, x, y, z, alpha, beta, w0, w1, c->d_part, c->part_cap,
+               A->Ad, A->d_off, A->ndiag};
     switch (epi) {
     case EPI_MXY: spmv_dispatch<EPI_MXY>(a, nred, nb, c->stream, A->nnz + 4L); break;
     case EPI_AMXY: spmv_dispatch<EPI_AMXY>(a, nred, nb, c->stream, A->nnz + 4L); break;

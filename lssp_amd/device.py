@@ -213,6 +213,13 @@ class DMat:
         """length a vector multiplied by this matrix must have (owned + halo)"""
         return self.nrows + self.nhalo
 
+    @property
+    def ndiag(self) -> int:
+        """> 0: the SpMV reads 1-byte diagonal ids (that many offsets) instead of columns"""
+        v = ctypes.c_int()
+        _ck(self.dev.L.lssp_amd_mat_layout(self.h, ctypes.byref(v)), "mat_layout")
+        return v.value
+
     def close(self):
         if self.h:
             self.dev.L.lssp_amd_mat_destroy(self.h)

@@ -259,3 +259,21 @@ def test_spmv_scattered_bitwise_vs_oracle(dev, which):
         o = O.solve(lssp_amd.CG, A, np.ones(A.n), maxit=60, mode=O.TREE)
         assert r.nits == o.nits and np.array_equal(r.trace, o.trace)
         assert np.array_equal(xs.download(), o.x)
+
+
+def test_spmv_column_coding_chosen_by_structure(dev):
+    """Stencil matrices get the 1-byte diagonal-id column stream (5-pt: 5
+    offsets, 7-pt: 7), scattered ones keep int32 columns; both bitwise vs the
+    oracle (the golden SpMV cases cover both layouts against the reference)."""
+    import lssp_amd
+    from inputs import conv_rand
+    for (Ap, Aj, Ax), want in ((lssp_amd.poisson(2, 40), 5), (lssp_amd.poisson(3, 20), 7),
+                               (conv_rand(3000, 3000, 8, 5), 0)):
+        n = Ap.size - 1
+        M = lssp_amd.DMat(dev, Ap, Aj, Ax)
+        assert M.ndiag == want
+        xv = uniform(0x5EED, n)
+        x, z = dev.vec(n, xv), dev.vec(n)
+        M.mv_mxy(x, z)
+        ref = O.spmv(0, O.CSR(n, Ap, Aj, Ax), xv)
+        assert np.array_equal(z.download().view(np.int64), ref.view(np.int64))
