@@ -67,6 +67,14 @@ int reduce_dots(lssp_amd_ctx *c, long n, int nslot, const double *const *a, cons
             e.r1a = a[1];
             e.r1b = b[1];
         }
+        if (nslot > 2) {
+            e.r2a = a[2];
+            e.r2b = b[2];
+        }
+        if (nslot > 3) {
+            e.r3a = a[3];
+            e.r3b = b[3];
+        }
         LSSP_TRY(launch_ew(c, e));
     }
     return finish_reduce(c, n, nslot, a, b, f);

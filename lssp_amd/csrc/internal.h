@@ -138,7 +138,11 @@ constexpr int PK3_CAP = 4096;    // v6: packets per block (descriptors staged in
 constexpr int PK4_PAD = -1 - 4096;  // v6 padding code: the value-ring slot past the end (holds +0.0)
 
 // ---- line sweeps of structured ILU(0) factors (linesweep.hip) ----------------
+#ifndef LINE_P_OVERRIDE
 constexpr int LINE_P = 4;  // planes per tile
+#else
+constexpr int LINE_P = LINE_P_OVERRIDE;  // tuning builds (tools/build_variant.sh)
+#endif
 enum { LT_KIN = 1, LT_JIN = 2, LT_KOUT = 4, LT_JOUT = 8 };
 struct LineGeom {
     int nx = 0, ny = 0, nz = 0;
@@ -226,11 +230,13 @@ struct Ew {
     const double *scal = nullptr;   // device scalars
     int nred = 0;
     const double *r0a = nullptr, *r0b = nullptr, *r1a = nullptr, *r1b = nullptr;
+    const double *r2a = nullptr, *r2b = nullptr, *r3a = nullptr, *r3b = nullptr;  // nred 3, 4
     const double *vbase = nullptr;  // GMRES basis [k][n]
     int k = 0;
     int sidx = 0;                   // scalar index for device-scalar kinds
 };
 int launch_ew(lssp_amd_ctx *c, const Ew &e);
+
 // finish a reduction whose level-1 partials (tree) or operands (serial) are set:
 // tree: level-2 over nslot partial rows of C entries; then the finalize program
 int launch_reduce_tree(lssp_amd_ctx *c, long C, int nslot, const Fin &f);

@@ -476,7 +476,7 @@ struct EwArgs {
     const double *x, *y, *u, *v;
     double *out0, *out1;
     const double *scal;
-    const double *r0a, *r0b, *r1a, *r1b;
+    const double *r0a, *r0b, *r1a, *r1b, *r2a, *r2b, *r3a, *r3b;
     const double *vbase;
     int k, sidx;
     double *part;
@@ -496,6 +496,7 @@ __global__ __launch_bounds__(256) void k_ew(EwArgs g)
         // (the compiler may not move a load above the output stores it might alias)
         bool w0 = false, w1 = false;  // this element's out0 / out1 written by the kind below
         double o0 = 0.0, o1 = 0.0, p0a = 0.0, p0b = 0.0, p1a = 0.0, p1b = 0.0;
+        double p2a = 0.0, p2b = 0.0, p3a = 0.0, p3b = 0.0;
         auto pre = [&](const double *q) { return (in && q != g.out0 && q != g.out1) ? q[i] : 0.0; };
         if (NRED > 0) {
             p0a = pre(g.r0a);
@@ -503,6 +504,12 @@ __global__ __launch_bounds__(256) void k_ew(EwArgs g)
             if (NRED > 1) {
                 p1a = pre(g.r1a);
                 p1b = pre(g.r1b);
+            }
+            if (NRED > 2) {
+                p2a = pre(g.r2a);
+                p2b = pre(g.r2b);
+                p3a = g.r3a ? pre(g.r3a) : 0.0;
+                p3b = g.r3b ? pre(g.r3b) : 0.0;
             }
         }
         if (in) {
@@ -582,6 +589,10 @@ __global__ __launch_bounds__(256) void k_ew(EwArgs g)
             };
             v[0] = in ? val(g.r0a, p0a) * val(g.r0b, p0b) : 0.0;
             if (NRED > 1) v[NRED > 1 ? 1 : 0] = in ? val(g.r1a, p1a) * val(g.r1b, p1b) : 0.0;
+            if (NRED > 2) {
+                v[NRED > 2 ? 2 : 0] = in ? val(g.r2a, p2a) * val(g.r2b, p2b) : 0.0;
+                v[NRED > 3 ? 3 : 0] = (in && g.r3a) ? val(g.r3a, p3a) * val(g.r3b, p3b) : 0.0;
+            }
             chunk_reduce<NRED>(v, g.part, g.pcap, c, lds);
         }
     }
@@ -593,12 +604,13 @@ int launch_ew(lssp_amd_ctx *c, const Ew &e)
     long C = num_chunks(e.n);
     LSSP_TRY(ensure_part(c, C));
     EwArgs g{e.kind, e.n, e.a, e.b, e.x, e.y, e.u, e.v, e.out0, e.out1, e.scal,
-             e.r0a, e.r0b, e.r1a, e.r1b, e.vbase, e.k, e.sidx, c->d_part, c->part_cap, C};
+             e.r0a, e.r0b, e.r1a, e.r1b, e.r2a, e.r2b, e.r3a, e.r3b, e.vbase, e.k, e.sidx, c->d_part, c->part_cap, C};
     // one chunk per block up to a cap; the cap keeps >= 8 blocks per CU resident
     long grid = C < 8L * c->num_cus * 4 ? C : 8L * c->num_cus * 4;
     if (e.nred == 0) k_ew<0><<<grid, 256, 0, c->stream>>>(g);
     else if (e.nred == 1) k_ew<1><<<grid, 256, 0, c->stream>>>(g);
-    else k_ew<2><<<grid, 256, 0, c->stream>>>(g);
+    else if (e.nred == 2) k_ew<2><<<grid, 256, 0, c->stream>>>(g);
+    else k_ew<4><<<grid, 256, 0, c->stream>>>(g);  // 3 or 4 (r3a == nullptr: slot 3 sums zeros)
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;
 }

@@ -886,7 +886,12 @@ constexpr int LINE_DH = 2;
 #else
 constexpr int LINE_DH = LINE_DH_OVERRIDE;
 #endif
-constexpr int LINE_CW = 2, LINE_NL = 4, LINE_D = 10, LINE_SW = 2;
+#ifndef LINE_D_OVERRIDE
+constexpr int LINE_D = 10;
+#else
+constexpr int LINE_D = LINE_D_OVERRIDE;
+#endif
+constexpr int LINE_CW = LINE_P / 2, LINE_NL = 4, LINE_SW = 2;  // two planes per compute wave
 
 template <int NA, bool RHS_NAT, int OUT, bool TRACE>
 static int launch_line_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)

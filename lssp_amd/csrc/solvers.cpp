@@ -900,11 +900,21 @@ int lgmres(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, i
 struct L1K {
     Run &R;
     int st = LSSP_AMD_OK;  // first failure; every later call is a no-op
+    // the last vector update is held back: when dots follow it, they are
+    // reduced in the same pass (k_ew with partial sums of its results)
+    Ew pend;
+    bool has_pend = false;
     explicit L1K(Run &r) : R(r) {}
+    ~L1K() { flush(); }  // a driver's last update (x) before it returns
     bool ok() const { return st == LSSP_AMD_OK; }
     void chk(int s)
     {
         if (st == LSSP_AMD_OK && s != LSSP_AMD_OK) st = s;
+    }
+    void flush()
+    {
+        if (has_pend && ok()) chk(R.ew(pend));
+        has_pend = false;
     }
     double *vec()
     {
@@ -915,15 +925,16 @@ struct L1K {
     }
     void ew(int kind, double a, double b, const double *x, const double *y, double *out)
     {
+        flush();
         if (!ok()) return;
-        Ew e;
-        e.kind = kind;
-        e.a = a;
-        e.b = b;
-        e.x = x;
-        e.y = y;
-        e.out0 = out;
-        chk(R.ew(e));
+        pend = Ew();
+        pend.kind = kind;
+        pend.a = a;
+        pend.b = b;
+        pend.x = x;
+        pend.y = y;
+        pend.out0 = out;
+        has_pend = true;
     }
     // vector.cxx:98-107 y = y*b + x*a;  :110-120 z = y*b + x*a
     void axpby(double a, const double *x, double b, double *y) { ew(K_AXPBY, a, b, x, nullptr, y); }
@@ -933,25 +944,75 @@ struct L1K {
     void scale(double *x, double a) { ew(K_SCALE, a, 0, nullptr, nullptr, x); }       // :141-146
     void mxy(double *x, double *y)  // mvops.cxx:118-150
     {
+        flush();
         if (ok()) chk(R.spmv(EPI_MXY, 1, x, 0, nullptr, y));
     }
     void resid(double *x, const double *b, double *r)  // lssp_mv_amxpbyz(-1, A, x, 1, b, r), :42-78
     {
+        flush();
         if (ok()) chk(R.spmv(EPI_AXPBY, -1, x, 1, b, r));
     }
     void pc(double *x, const double *rhs)
     {
+        flush();
         if (ok()) chk(R.pc(x, rhs));
     }
-    double fetch(int op, const double *x, const double *y)
+    // m <= MAX_SLOTS dots / norms the reference evaluates back to back
+    // (vector.cxx:123-139): one pass -- the pending updates with the products
+    // reduced at their end -- and one host round trip.  The trace gets each
+    // value at its position in the reference's call order.
+    void fetchn(int m, const bool *isnorm, const double *const *xs, const double *const *ys, double *out)
     {
-        if (!ok()) return NAN;
-        chk(R.dot1(x, y, R.fin(op, 1, R.T(), -1, S_TMP)));
-        if (ok()) chk(R.sync(0, 16));
-        return ok() ? R.h(S_TMP) : NAN;
+        int pos[MAX_SLOTS];
+        for (int q = 0; q < m; q++) pos[q] = R.T();
+        if (ok()) {
+            Fin f = R.fin(FIN_STORE, m);
+            if (R.tree && has_pend) {  // the held-back update's pass also reduces
+                const double **ra[MAX_SLOTS] = {&pend.r0a, &pend.r1a, &pend.r2a, &pend.r3a};
+                const double **rb[MAX_SLOTS] = {&pend.r0b, &pend.r1b, &pend.r2b, &pend.r3b};
+                for (int q = 0; q < m; q++) {
+                    *ra[q] = xs[q];
+                    *rb[q] = ys[q];
+                }
+                pend.nred = m;
+                flush();
+                if (ok()) chk(finish_reduce(R.c, R.n, m, xs, ys, f));
+            } else {
+                flush();
+                if (ok()) chk(reduce_dots(R.c, R.n, m, xs, ys, f));
+            }
+            if (ok()) chk(R.sync(0, 32));
+        }
+        for (int q = 0; q < m; q++) {
+            out[q] = ok() ? (isnorm[q] ? sqrt(R.h(S_SUM0 + q)) : R.h(S_SUM0 + q)) : NAN;
+            if (ok() && pos[q] >= 0) R.patches.push_back({pos[q], out[q]});
+        }
     }
-    double dot(const double *x, const double *y) { return fetch(FIN_STORE, x, y); }  // vector.cxx:123-133
-    double norm(const double *x) { return fetch(FIN_NORM, x, x); }                    // :135-139
+    // two back-to-back evaluations (norm: n0 / n1), one pass and one round trip
+    void pair(double &o0, const double *x0, const double *y0, bool n0, double &o1, const double *x1,
+              const double *y1, bool n1)
+    {
+        const bool nm[2] = {n0, n1};
+        const double *xs[2] = {x0, x1}, *ys[2] = {y0, y1};
+        double v[2];
+        fetchn(2, nm, xs, ys, v);
+        o0 = v[0];
+        o1 = v[1];
+    }
+    double dot(const double *x, const double *y)  // vector.cxx:123-133
+    {
+        const bool nm[1] = {false};
+        double v;
+        fetchn(1, nm, &x, &y, &v);
+        return v;
+    }
+    double norm(const double *x)  // :135-139
+    {
+        const bool nm[1] = {true};
+        double v;
+        fetchn(1, nm, &x, &x, &v);
+        return v;
+    }
 };
 
 void tol_setup(const lssp_amd_solve_params &P, double nrm2, double bnorm_rb, double &tol)
@@ -967,6 +1028,7 @@ void tol_setup(const lssp_amd_solve_params &P, double nrm2, double bnorm_rb, dou
 
 #define L1_DONE()                      \
     do {                               \
+        K.flush();                     \
         if (!K.ok()) return K.st;      \
         *nits = iter;                  \
         *res_out = nrm2;               \
@@ -1142,8 +1204,7 @@ int bicrstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
         }
         K.axpbyz(-alpha, map, 1, z, ms);
         K.mxy(ms, ams);
-        tdot1 = K.dot(ams, s);
-        tdot2 = K.dot(ams, ams);
+        K.pair(tdot1, ams, s, false, tdot2, ams, ams, false);
         omega = tdot1 / tdot2;
         K.axpby(alpha, p, 1, x);
         K.axpby(omega, ms, 1, x);
@@ -1169,11 +1230,12 @@ static void safe_coef(L1K &K, int iter, const double *y, const double *a, const 
                       double &eta)
 {
     double tdot[5], tmp;
-    tdot[0] = K.dot(y, y);
-    tdot[1] = K.dot(a, r);
-    tdot[2] = K.dot(y, r);
-    tdot[3] = K.dot(a, y);
-    tdot[4] = K.dot(a, a);
+    {  // the five dots back to back: one pass of four, then the fifth
+        const bool nm[4] = {false, false, false, false};
+        const double *xs[4] = {y, a, y, a}, *ys[4] = {y, r, r, y};
+        K.fetchn(4, nm, xs, ys, tdot);
+        tdot[4] = K.dot(a, a);
+    }
     if (iter == 1) {
         qsi = tdot[1] / tdot[4];
         eta = 0.0;
@@ -1452,8 +1514,9 @@ int qmrcgstab(Run &R, const lssp_amd_solve_params &P, double *xk, const double *
         K.pc(tk, r);
         {
             // :146 -- operand evaluation order as g++ -O2 built it (the golden traces)
-            const double num = K.dot(sk, tk);
-            omega = num / K.dot(tk, tk);
+            double num, den;
+            K.pair(num, sk, tk, false, den, tk, tk, false);
+            omega = num / den;
         }
         K.axpbyz(1., sk, -omega, tk, rk);
         theta = K.norm(rk) / btau;
@@ -1509,8 +1572,7 @@ int tfqmr(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, in
     K.set(d, 0.);
     K.pc(t, p);
     K.mxy(t, v);
-    rhoold = K.dot(r, rtld);
-    tau = K.norm(r);
+    K.pair(rhoold, r, rtld, false, tau, r, r, true);
     wold = tau;
     theta = 0.0;
     eta = 0.0;
@@ -1606,8 +1668,7 @@ int orthomin(Run &R, const lssp_amd_solve_params &P, double *x, const double *rh
         j = itr_out % k;
         K.set(q[j], 0.);
         K.pc(q[j], s);
-        a_j = K.dot(r, q[j]);
-        c_j[j] = K.dot(q[j], q[j]);
+        K.pair(a_j, r, q[j], false, c_j[j], q[j], q[j], false);
         if (!K.ok()) return K.st;
         if (fabs(c_j[j]) <= BREAKDOWN) break;
         a_j = a_j / c_j[j];
@@ -1724,8 +1785,7 @@ int bicgstabl(Run &R, const lssp_amd_solve_params &P, double *x, const double *b
                 tau[i * zd + j] = nu;
                 K.axpby(-nu, r[i], 1, r[j]);
             }
-            sigma[j] = K.dot(r[j], r[j]);
-            nu = K.dot(r[0], r[j]);
+            K.pair(sigma[j], r[j], r[j], false, nu, r[0], r[j], false);
             gamma1[j] = nu / sigma[j];
         }
         if (!K.ok()) return K.st;

@@ -59,12 +59,20 @@ def main():
 
 
 def timings(M, r, x, y, diags, timeit, N, dev):
+    import lssp_amd
+
+    def t(fn):
+        try:
+            return round(timeit(fn), 1)
+        except lssp_amd.LsspError:  # e.g. a variant whose standalone sweep exceeds the LDS
+            return None
+
     for d in diags:
         os.environ["LSSP_AMD_LINE_DIAG"] = str(d)
         out = {"N": N, "diag": d,
-               "L_us": round(timeit(lambda: M.trisolve(0, y, r)), 1),
-               "U_us": round(timeit(lambda: M.trisolve(1, x, y)), 1),
-               "apply_us": round(timeit(lambda: M.apply(x, r)), 1)}
+               "L_us": t(lambda: M.trisolve(0, y, r)),
+               "U_us": t(lambda: M.trisolve(1, x, y)),
+               "apply_us": t(lambda: M.apply(x, r))}
         print(json.dumps(out), flush=True)
     os.environ["LSSP_AMD_LINE_DIAG"] = "0"
     dev.close()
