@@ -26,6 +26,7 @@ constexpr uint64_t TRI_SENTINEL = 0xFFF7DEADBEEFCAFEull;
 // scalar slots of the Krylov drivers (device memory, ctx->d_scal)
 enum Scal {
     S_RHO0 = 0, S_RHO1, S_ALPHA, S_BETA, S_OMEGA, S_RES, S_SNORM, S_BREAK, S_BNORM, S_TMP,
+    S_DONE, S_TOL, S_NIT,  // batched iterations (solvers.cpp cg): stop flag, tolerance, iterations run
     S_SUM0 = 16,   // raw reduced sums of the last reduction
     S_H = 32,      // GMRES Hessenberg column (up to NSCAL - 32 entries)
 };
@@ -44,6 +45,7 @@ enum FinOp {
     FIN_CG_ALPHA,        // alpha = rho1 / s0; rho0 = rho1
     FIN_CG_RES,          // res = sqrt(s0)
     FIN_CG_RES_RHO,      // res = sqrt(s0); rho1 = s0; beta = rho1/rho0  (PC_NON: z == r)
+    FIN_CG_RES_RHO_B,    // FIN_CG_RES_RHO, then res -> history S_H + nit, nit += 1, done = res <= tol
 };
 
 struct Fin {
@@ -71,6 +73,9 @@ struct lssp_amd_ctx {
     double *d_trace = nullptr; // device trace buffer
     long trace_cap = 0;
     int *d_err = nullptr;      // error word (trisolve timeouts)
+    // while set: every k_ew / k_spmv3 / reduction launch returns at once when
+    // *guard != 0 (batched iterations past the one that converged)
+    const double *guard = nullptr;
     // multi-GPU (RCCL)
     int nranks = 1, rank = 0;
     void *comm = nullptr;      // ncclComm_t

@@ -112,12 +112,19 @@ __device__ void finalize(const Fin &f, const double *s, double *scal, double *tr
         t0 = sqrt(s[0]);
         scal[S_RES] = t0;
         break;
-    case FIN_CG_RES_RHO: {  // :106, then the next :80 with z == r (PC_NON)
+    case FIN_CG_RES_RHO:  // :106, then the next :80 with z == r (PC_NON)
+    case FIN_CG_RES_RHO_B: {
         t0 = sqrt(s[0]);
         scal[S_RES] = t0;
         t1 = s[0];
         scal[S_RHO1] = s[0];
         scal[S_BETA] = s[0] / scal[S_RHO0];
+        if (f.op == FIN_CG_RES_RHO_B) {  // :109 decided here; the host reads the batch afterwards
+            const int k = (int)scal[S_NIT];
+            scal[S_H + k] = t0;
+            scal[S_NIT] = k + 1;
+            if (t0 <= scal[S_TOL]) scal[S_DONE] = 1.0;
+        }
         break;
     }
     }
@@ -149,8 +156,9 @@ __device__ __forceinline__ double ld_sc1(const double *p)
 
 __global__ __launch_bounds__(64) void k_reduce2m(const double *__restrict__ part, long pcap, long C, int nslot,
                                                 double *sums, double *scal, double *trace, Fin f, int do_fin,
-                                                double *wsum, unsigned *cnt)
+                                                double *wsum, unsigned *cnt, const double *guard)
 {
+    if (guard && *guard != 0.0) return;
     const int q = blockIdx.x, t = q * 64 + threadIdx.x;  // lane t of the 1024-lane level 2
     for (int s = 0; s < nslot; s++) {
         const double *p = part + s * pcap;
@@ -206,8 +214,10 @@ constexpr int SER_C = 2048;
 // carry (multi-rank): the running sums of the ranks before this one, so the
 // chain continues theirs and the P ranks add in global index order.
 __global__ __launch_bounds__(1024) void k_dot_serial(SerialArgs g, long n, int nslot, double *sums, double *scal,
-                                                     double *trace, Fin f, int do_fin, const double *carry)
+                                                     double *trace, Fin f, int do_fin, const double *carry,
+                                                     const double *guard)
 {
+    if (guard && *guard != 0.0) return;
     __shared__ double buf[2][MAX_SLOTS][SER_C];
     const int tid = threadIdx.x;
     const long nch = (n + SER_C - 1) / SER_C;
@@ -290,6 +300,7 @@ struct SpmvArgs {
     const uint8_t *Ad;  // diagonal-id column coding (lssp_amd_mat::Ad), CMP kernels
     const int *off;
     int ndiag;
+    const double *guard;  // lssp_amd_ctx::guard
 };
 
 // The 256-row blocks are dealt so that each of the 8 XCDs owns one contiguous
@@ -312,6 +323,7 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
     __shared__ __attribute__((aligned(16))) int sj[CMP ? SPMV_CAP / 4 + 8 : SPMV_CAP + 4];
     __shared__ int soff[CMP ? 256 : 1];
     __shared__ double lds[MAX_SLOTS][4];
+    if (a.guard && *a.guard != 0.0) return;
     const long per = gridDim.x / 8;
     const long blk = (blockIdx.x % 8) * per + blockIdx.x / 8;
     if (blk >= nblk) return;
@@ -429,7 +441,7 @@ int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, c
     long nb = num_chunks(A->nrows);
     LSSP_TRY(ensure_part(c, nb));
     SpmvArgs a{A->nrows, A->Ap, A->Aj, A->Ax, x, y, z, alpha, beta, w0, w1, c->d_part, c->part_cap,
-               A->Ad, A->d_off, A->ndiag};
+               A->Ad, A->d_off, A->ndiag, c->guard};
     switch (epi) {
     case EPI_MXY: spmv_dispatch<EPI_MXY>(a, nred, nb, c->stream, A->nnz + 4L); break;
     case EPI_AMXY: spmv_dispatch<EPI_AMXY>(a, nred, nb, c->stream, A->nnz + 4L); break;
@@ -482,12 +494,14 @@ struct EwArgs {
     double *part;
     long pcap;
     long nchunks;
+    const double *guard;
 };
 
 template <int NRED>
 __global__ __launch_bounds__(256) void k_ew(EwArgs g)
 {
     __shared__ double lds[MAX_SLOTS][4];
+    if (g.guard && *g.guard != 0.0) return;
     for (long c = blockIdx.x; c < g.nchunks; c += gridDim.x) {
         const long i = c * 256 + threadIdx.x;
         const bool in = i < g.n;
@@ -604,7 +618,8 @@ int launch_ew(lssp_amd_ctx *c, const Ew &e)
     long C = num_chunks(e.n);
     LSSP_TRY(ensure_part(c, C));
     EwArgs g{e.kind, e.n, e.a, e.b, e.x, e.y, e.u, e.v, e.out0, e.out1, e.scal,
-             e.r0a, e.r0b, e.r1a, e.r1b, e.r2a, e.r2b, e.r3a, e.r3b, e.vbase, e.k, e.sidx, c->d_part, c->part_cap, C};
+             e.r0a, e.r0b, e.r1a, e.r1b, e.r2a, e.r2b, e.r3a, e.r3b, e.vbase, e.k, e.sidx, c->d_part, c->part_cap, C,
+             c->guard};
     // one chunk per block up to a cap; the cap keeps >= 8 blocks per CU resident
     long grid = C < 8L * c->num_cus * 4 ? C : 8L * c->num_cus * 4;
     if (e.nred == 0) k_ew<0><<<grid, 256, 0, c->stream>>>(g);
@@ -620,7 +635,7 @@ int launch_reduce_tree(lssp_amd_ctx *c, long C, int nslot, const Fin &f)
     int do_fin = c->nranks > 1 ? 0 : 1;
     static_assert(L2_LANES == 16 * 64, "k_reduce2m runs the 16 waves of the level-2 workgroup");
     k_reduce2m<<<L2_LANES / 64, 64, 0, c->stream>>>(c->d_part, c->part_cap, C, nslot, c->d_sums, c->d_scal,
-                                                         c->d_trace, f, do_fin, c->d_wsum, c->d_rcnt);
+                                                         c->d_trace, f, do_fin, c->d_wsum, c->d_rcnt, c->guard);
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;
 }
@@ -634,7 +649,8 @@ int launch_reduce_serial(lssp_amd_ctx *c, long n, int nslot, const double *const
         g.b[s] = b[s];
     }
     int do_fin = c->nranks > 1 ? 0 : 1;
-    k_dot_serial<<<1, 1024, 0, c->stream>>>(g, n, nslot, c->d_sums, c->d_scal, c->d_trace, f, do_fin, carry);
+    k_dot_serial<<<1, 1024, 0, c->stream>>>(g, n, nslot, c->d_sums, c->d_scal, c->d_trace, f, do_fin, carry,
+                                            c->guard);
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;
 }

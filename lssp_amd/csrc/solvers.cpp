@@ -322,50 +322,119 @@ int cg(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *
     if (tol < tol_rb) tol = tol_rb;
     bool pending_rho = false;
 
-    for (it = 0; it < maxit; it++) {
-        pending_rho = false;
-        if (R.M) {
-            LSSP_TRY(R.pc(z, r));                                   // :79
-            LSSP_TRY(R.dot1(z, r, R.fin(FIN_CG_RHO, 1, R.T())));   // :80
-        } else if (it == 0) {
-            LSSP_TRY(R.dot1(r, r, R.fin(FIN_CG_RHO, 1, R.T())));
-        }
-        Ew e;
-        if (it == 0) {
-            e.kind = K_COPY;  // :83-86
-            e.x = z;
-            e.out0 = p;
-        } else {
-            e.kind = K_CG_P;  // :88-92
-            e.x = z;
-            e.out0 = p;
-        }
-        LSSP_TRY(R.ew(e));
-        LSSP_TRY(R.spmv(EPI_MXY, 1, p, 0, nullptr, q, 1, p));        // :95
-        LSSP_TRY(R.fin1(q, p, R.fin(FIN_CG_ALPHA, 1, R.T())));      // :96-99
-        e = Ew();
-        e.kind = K_CG_XR;  // :101-104
-        e.out0 = x;
-        e.x = p;
-        e.out1 = r;
-        e.y = q;
-        e.nred = 1;
-        e.r0a = r;
-        e.r0b = r;
-        LSSP_TRY(R.ew(e));
-        if (R.M) {
-            LSSP_TRY(R.fin1(r, r, R.fin(FIN_CG_RES, 1, R.T())));  // :106
-        } else {
-            int t0 = R.T(), t1 = R.T();
-            LSSP_TRY(R.fin1(r, r, R.fin(FIN_CG_RES_RHO, 1, t0, t1)));  // :106, next :80 (z == r)
+    if (!R.M && R.c->nranks == 1) {
+        // PC_NON on one rank: iterations are queued in batches and the stop
+        // test :109 runs on the device (FIN_CG_RES_RHO_B); the launches of the
+        // iterations after the one that converged return at once (ctx guard),
+        // and the host reads a batch's residuals with ONE round trip instead of
+        // one per iteration.  Same kernels, same arithmetic.
+        constexpr int BATCH = 16;
+        lssp_amd_ctx *c = R.c;
+        it = 0;
+        bool stop = false;
+        while (it < maxit && !stop) {
+            const int nb = std::min(BATCH, maxit - it);
+            c->h_scal[S_DONE] = 0.0;
+            c->h_scal[S_TOL] = tol;
+            c->h_scal[S_NIT] = 0.0;
+            LSSP_HIP(hipMemcpyAsync(c->d_scal + S_DONE, c->h_scal + S_DONE, 3 * sizeof(double),
+                                    hipMemcpyHostToDevice, c->stream));
+            long tl_after[BATCH];
+            c->guard = c->d_scal + S_DONE;
+            int st = LSSP_AMD_OK;
+            for (int j = 0; j < nb && st == LSSP_AMD_OK; j++) {
+                const int k = it + j;
+                Ew e;
+                if (k == 0) {
+                    st = R.dot1(r, r, R.fin(FIN_CG_RHO, 1, R.T()));  // :80 (z == r)
+                    e.kind = K_COPY;                                  // :83-86
+                } else {
+                    e.kind = K_CG_P;  // :88-92
+                }
+                e.x = z;
+                e.out0 = p;
+                if (st == LSSP_AMD_OK) st = R.ew(e);
+                if (st == LSSP_AMD_OK) st = R.spmv(EPI_MXY, 1, p, 0, nullptr, q, 1, p);  // :95
+                if (st == LSSP_AMD_OK) st = R.fin1(q, p, R.fin(FIN_CG_ALPHA, 1, R.T()));  // :96-99
+                e = Ew();
+                e.kind = K_CG_XR;  // :101-104
+                e.out0 = x;
+                e.x = p;
+                e.out1 = r;
+                e.y = q;
+                e.nred = 1;
+                e.r0a = r;
+                e.r0b = r;
+                if (st == LSSP_AMD_OK) st = R.ew(e);
+                int t0 = R.T(), t1 = R.T();
+                if (st == LSSP_AMD_OK) st = R.fin1(r, r, R.fin(FIN_CG_RES_RHO_B, 1, t0, t1));  // :106-109, next :80
+                tl_after[j] = R.tl;
+            }
+            c->guard = nullptr;
+            LSSP_TRY(st);
+            LSSP_TRY(R.sync(0, S_H + nb));
+            const int ran = std::max(1, std::min(nb, (int)R.h(S_NIT)));
+            for (int q = 0; q < ran; q++) {
+                res = R.h(S_H + q);
+                if (P.verb >= 1 && R.rank == 0)
+                    lprint("cg: itr: %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", it + q, res,
+                           (err_rel == 0 ? 0 : res / err_rel), (b_norm == 0 ? 0 : res / b_norm));
+            }
             pending_rho = true;
+            if (R.h(S_DONE) != 0.0) {  // :109 held at iteration it + ran - 1
+                R.tl = tl_after[ran - 1];
+                it += ran - 1;
+                stop = true;
+            } else {
+                it += nb;
+            }
         }
-        LSSP_TRY(R.sync(0, 16));
-        res = R.h(S_RES);
-        if (P.verb >= 1 && R.rank == 0)
-            lprint("cg: itr: %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", it, res,
-                   (err_rel == 0 ? 0 : res / err_rel), (b_norm == 0 ? 0 : res / b_norm));
-        if (res <= tol) break;  // :109
+    } else {
+        for (it = 0; it < maxit; it++) {
+            pending_rho = false;
+            if (R.M) {
+                LSSP_TRY(R.pc(z, r));                                   // :79
+                LSSP_TRY(R.dot1(z, r, R.fin(FIN_CG_RHO, 1, R.T())));   // :80
+            } else if (it == 0) {
+                LSSP_TRY(R.dot1(r, r, R.fin(FIN_CG_RHO, 1, R.T())));
+            }
+            Ew e;
+            if (it == 0) {
+                e.kind = K_COPY;  // :83-86
+                e.x = z;
+                e.out0 = p;
+            } else {
+                e.kind = K_CG_P;  // :88-92
+                e.x = z;
+                e.out0 = p;
+            }
+            LSSP_TRY(R.ew(e));
+            LSSP_TRY(R.spmv(EPI_MXY, 1, p, 0, nullptr, q, 1, p));        // :95
+            LSSP_TRY(R.fin1(q, p, R.fin(FIN_CG_ALPHA, 1, R.T())));      // :96-99
+            e = Ew();
+            e.kind = K_CG_XR;  // :101-104
+            e.out0 = x;
+            e.x = p;
+            e.out1 = r;
+            e.y = q;
+            e.nred = 1;
+            e.r0a = r;
+            e.r0b = r;
+            LSSP_TRY(R.ew(e));
+            if (R.M) {
+                LSSP_TRY(R.fin1(r, r, R.fin(FIN_CG_RES, 1, R.T())));  // :106
+            } else {
+                int t0 = R.T(), t1 = R.T();
+                LSSP_TRY(R.fin1(r, r, R.fin(FIN_CG_RES_RHO, 1, t0, t1)));  // :106, next :80 (z == r)
+                pending_rho = true;
+            }
+            LSSP_TRY(R.sync(0, 16));
+            res = R.h(S_RES);
+            if (P.verb >= 1 && R.rank == 0)
+                lprint("cg: itr: %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", it, res,
+                       (err_rel == 0 ? 0 : res / err_rel), (b_norm == 0 ? 0 : res / b_norm));
+            if (res <= tol) break;  // :109
+        }
     }
     if (pending_rho) R.tl--;
     if (it < maxit) it += 1;
