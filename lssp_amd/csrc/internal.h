@@ -41,6 +41,8 @@ enum FinOp {
     FIN_BICG_S,          // snorm = sqrt(s0); break = snorm <= 1e-40
     FIN_BICG_OMEGA,      // omega = s0 / s1
     FIN_BICG_RES_RHO,    // res = sqrt(s0); then FIN_BICG_RHO on s1
+    FIN_BICG_RES_RHO_B,  // FIN_BICG_RES_RHO, then res -> history S_H + nit, nit += 1, done = 2 breakdown
+                         // (S_BREAK), 1 res <= tol, 3 the next iteration's rho1 == 0
     FIN_CG_RHO,          // rho1 = s0; beta = rho1 / rho0
     FIN_CG_ALPHA,        // alpha = rho1 / s0; rho0 = rho1
     FIN_CG_RES,          // res = sqrt(s0)

@@ -90,7 +90,8 @@ __device__ void finalize(const Fin &f, const double *s, double *scal, double *tr
     case FIN_BICG_OMEGA:  // :135
         scal[S_OMEGA] = s[0] / s[1];
         break;
-    case FIN_BICG_RES_RHO: {  // :141 then the next iteration's :87
+    case FIN_BICG_RES_RHO:  // :141 then the next iteration's :87
+    case FIN_BICG_RES_RHO_B: {
         t0 = sqrt(s[0]);
         scal[S_RES] = t0;
         double rho1 = s[1];
@@ -98,6 +99,14 @@ __device__ void finalize(const Fin &f, const double *s, double *scal, double *tr
         scal[S_RHO1] = rho1;
         scal[S_BETA] = (rho1 * scal[S_ALPHA]) / (scal[S_RHO0] * scal[S_OMEGA]);
         scal[S_RHO0] = rho1;
+        if (f.op == FIN_BICG_RES_RHO_B) {  // :117 / :149 / :89 decided here; the host reads the batch afterwards
+            const int k = (int)scal[S_NIT];
+            scal[S_H + k] = t0;
+            scal[S_NIT] = k + 1;
+            if (scal[S_BREAK] != 0.0) scal[S_DONE] = 2.0;
+            else if (t0 <= scal[S_TOL]) scal[S_DONE] = 1.0;
+            else if (rho1 == 0) scal[S_DONE] = 3.0;
+        }
         break;
     }
     case FIN_CG_RHO:  // solver-cg.cxx:80, :88

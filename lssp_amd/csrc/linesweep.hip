@@ -357,6 +357,7 @@ struct LineArgs {
     unsigned long long *trace;
     int ttile;
     int diag;  // LSSP_AMD_LINE_DIAG timing experiments (wrong results when != 0)
+    const double *guard;  // lssp_amd_ctx::guard
 };
 
 __device__ __forceinline__ void dma16(const void *g, unsigned lds)
@@ -498,6 +499,10 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int nx = a.nx;
+    if (a.guard && *a.guard != 0.0) {  // a batched iteration past the stop: consume the launch's tile claims
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.claim, (unsigned long long)a.ntiles + gridDim.x);
+        return;
+    }
 
     for (;;) {
         __syncthreads();
@@ -965,6 +970,7 @@ static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const doub
     a.base = ls.base;
     a.mirror = which;
     a.err = c->d_err;
+    a.guard = c->guard;
     {
         const char *dg = getenv("LSSP_AMD_LINE_DIAG");
         a.diag = dg ? atoi(dg) : 0;

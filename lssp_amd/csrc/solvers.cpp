@@ -198,14 +198,11 @@ int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
     double rho1 = R.h(S_RHO1);
     bool pending_rho = false;  // a fused next-iteration rho1 sits in the trace
 
-    for (it = 0; it < maxit; it++) {
-        pending_rho = false;
-        if (rho1 == 0) {  // :89-92
-            if (R.rank == 0) lprint("bicgstab: method failed.!\n");
-            break;
-        }
+    // one iteration :94-141 queued on the stream; fin_res: the finalize of its
+    // last reduction; *pos_s: the trace position before its ||s|| (:117)
+    auto enqueue = [&](int k, int fin_res, long *pos_s) -> int {
         Ew e;
-        if (it == 0) {
+        if (k == 0) {
             e.kind = K_COPY;  // :96
             e.x = r;
             e.out0 = p;
@@ -228,7 +225,7 @@ int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
         e.r0a = s;
         e.r0b = s;
         LSSP_TRY(R.ew(e));
-        const long pos_s = R.tl;
+        *pos_s = R.tl;
         LSSP_TRY(R.fin1(s, s, R.fin(FIN_BICG_S, 1, R.T())));  // :117
         LSSP_TRY(R.pc(sh, s));                                 // :130-131
         LSSP_TRY(R.spmv(EPI_AMX, 1, sh, 0, p, t, 2, s, nullptr));  // :133
@@ -250,29 +247,103 @@ int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
         e.r1a = r;
         e.r1b = rh;
         LSSP_TRY(R.ew(e));
-        {
-            int t0 = R.T(), t1 = R.T();
-            LSSP_TRY(R.fin2(r, r, r, rh, R.fin(FIN_BICG_RES_RHO, 2, t0, t1)));  // :141, next :87
-        }
+        int t0 = R.T(), t1 = R.T();
+        return R.fin2(r, r, r, rh, R.fin(fin_res, 2, t0, t1));  // :141, next :87
+    };
+    // :117-128 after the device took x += alpha*ph: the reference evaluates
+    // ||s|| again (trace), then r = b - A x and its norm
+    auto breakdown = [&](long pos_s) -> int {
+        if (R.rank == 0) lprint("bicgstab: ||s|| is too small: %f, terminated.\n", R.h(S_SNORM));
+        R.tl = pos_s + 1;
+        long q = R.tl++;
+        R.patches.push_back({q, R.h(S_SNORM)});
+        LSSP_TRY(R.spmv(EPI_AXPBY, -1, x, 1, b, r));  // :124
+        LSSP_TRY(R.dot1(r, r, R.fin(FIN_NORM, 1, R.T(), -1, S_RES)));
         LSSP_TRY(R.sync(0, 16));
-        if (R.h(S_BREAK) != 0.0) {  // :117-128 -- x += alpha*ph already done on the device
-            if (R.rank == 0) lprint("bicgstab: ||s|| is too small: %f, terminated.\n", R.h(S_SNORM));
-            R.tl = pos_s + 1;
-            long q = R.tl++;
-            R.patches.push_back({q, R.h(S_SNORM)});  // the reference evaluates the norm again (:118)
-            LSSP_TRY(R.spmv(EPI_AXPBY, -1, x, 1, b, r));  // :124
-            LSSP_TRY(R.dot1(r, r, R.fin(FIN_NORM, 1, R.T(), -1, S_RES)));
-            LSSP_TRY(R.sync(0, 16));
-            res = R.h(S_RES);
-            break;
-        }
-        pending_rho = true;
         res = R.h(S_RES);
+        return LSSP_AMD_OK;
+    };
+    auto itr_line = [&](int k, double rk) {
         if (P.verb >= 1 && R.rank == 0)
-            lprint("bicgstab: itr: %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", it, res,
-                   (err_rel == 0 ? 0 : res / err_rel), (b_norm == 0 ? 0 : res / b_norm));
-        if (res <= tol) break;  // :149
-        rho1 = R.h(S_RHO1);
+            lprint("bicgstab: itr: %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", k, rk,
+                   (err_rel == 0 ? 0 : rk / err_rel), (b_norm == 0 ? 0 : rk / b_norm));
+    };
+    const bool batched = R.c->nranks == 1 && (!R.M || R.M->line.ntiles > 0);
+    if (batched && rho1 == 0) {  // :89-92 at the first iteration
+        if (R.rank == 0) lprint("bicgstab: method failed.!\n");
+        it = 0;
+    } else if (batched) {
+        // One rank, line-swept or no preconditioner: iterations are queued in
+        // batches and the stop tests run on the device (FIN_BICG_RES_RHO_B:
+        // breakdown :117, res <= tol :149, rho1 == 0 :89 of the next); the
+        // launches past the stop return at once (ctx guard), and the host reads a
+        // batch's residuals with one round trip.  Same kernels, same arithmetic.
+        constexpr int BATCH = 8;
+        lssp_amd_ctx *c = R.c;
+        it = 0;
+        bool stop = false;
+        while (it < maxit && !stop) {
+            const int nb = std::min(BATCH, maxit - it);
+            c->h_scal[S_DONE] = 0.0;
+            c->h_scal[S_TOL] = tol;
+            c->h_scal[S_NIT] = 0.0;
+            LSSP_HIP(hipMemcpyAsync(c->d_scal + S_DONE, c->h_scal + S_DONE, 3 * sizeof(double),
+                                    hipMemcpyHostToDevice, c->stream));
+            long tl_after[BATCH], pos_s[BATCH];
+            c->guard = c->d_scal + S_DONE;
+            int st = LSSP_AMD_OK;
+            for (int j = 0; j < nb && st == LSSP_AMD_OK; j++) {
+                st = enqueue(it + j, FIN_BICG_RES_RHO_B, &pos_s[j]);
+                tl_after[j] = R.tl;
+            }
+            c->guard = nullptr;
+            LSSP_TRY(st);
+            LSSP_TRY(R.sync(0, S_H + nb));
+            const int ran = std::max(1, std::min(nb, (int)R.h(S_NIT)));
+            const int code = (int)R.h(S_DONE);
+            for (int q = 0; q < ran - (code == 2 ? 1 : 0); q++) itr_line(it + q, R.h(S_H + q));
+            res = R.h(S_H + ran - 1);
+            pending_rho = true;
+            if (code == 2) {  // breakdown in iteration it + ran - 1
+                it += ran - 1;
+                pending_rho = false;
+                LSSP_TRY(breakdown(pos_s[ran - 1]));
+                stop = true;
+            } else if (code == 1) {  // converged
+                R.tl = tl_after[ran - 1];
+                it += ran - 1;
+                stop = true;
+            } else if (code == 3) {  // the next iteration's rho1 == 0
+                R.tl = tl_after[ran - 1];
+                it += ran;
+                pending_rho = false;
+                if (it < maxit && R.rank == 0) lprint("bicgstab: method failed.!\n");
+                if (it < maxit) stop = true;
+                else pending_rho = true;
+            } else {
+                it += nb;
+            }
+        }
+    } else {
+        for (it = 0; it < maxit; it++) {
+            pending_rho = false;
+            if (rho1 == 0) {  // :89-92
+                if (R.rank == 0) lprint("bicgstab: method failed.!\n");
+                break;
+            }
+            long pos_s = 0;
+            LSSP_TRY(enqueue(it, FIN_BICG_RES_RHO, &pos_s));
+            LSSP_TRY(R.sync(0, 16));
+            if (R.h(S_BREAK) != 0.0) {  // :117-128 -- x += alpha*ph already done on the device
+                LSSP_TRY(breakdown(pos_s));
+                break;
+            }
+            pending_rho = true;
+            res = R.h(S_RES);
+            itr_line(it, res);
+            if (res <= tol) break;  // :149
+            rho1 = R.h(S_RHO1);
+        }
     }
     if (pending_rho) R.tl--;  // the fused next-iteration rho1 is not part of the reference's run
     if (it < maxit) it += 1;  // :152
