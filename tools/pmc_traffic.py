@@ -32,7 +32,7 @@ def main(fetch_dir, write_dir, out):
         return [k for k in fe if sub in k]
 
     res = {}
-    for k in find("k_spmv3<0, 0>"):
+    for k in find("k_spmv3<0, 0"):  # y = A x (any column coding)
         res["k_spmv3"] = int(2 * fe[k] + wr.get(k, 0))
     line = find("k_line<")  # line sweeps: the apply is one L and one U launch
     if line:
