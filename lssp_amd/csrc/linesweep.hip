@@ -473,6 +473,31 @@ constexpr int LINE_RW = 6;  // rhs wave: a run block's loads land LINE_RW steps 
 // compute waves (P/CW planes each), NL loader waves, D loader lead (steps),
 // DH poller lead (steps), SW storer waves; OUT 1: natural-order output, 2: the
 // U rhs stream (the L sweep of an apply); TRACE: diagnostics.
+// The apply's two sweeps (L -> U rhs stream, U from it) raise the poller's
+// wave priority and hold the loaders' DMA issue back ~6 x 64 clk after each
+// barrier, so the step's hand-off polls enter the CU's memory queue ahead of
+// the 10 KB of coefficient DMAs (whose lead is 10 steps): 216^3 apply 957 ->
+// 922 us (tools/gpu_exp.sh; the standalone natural-order sweeps got slower with
+// it, so they keep 0 / 0).  -DLINE_POLL_PRIO / -DLINE_LOAD_SLEEP override both.
+template <bool RHS_NAT, int OUT>
+constexpr int line_poll_prio()
+{
+#ifdef LINE_POLL_PRIO
+    return LINE_POLL_PRIO;
+#else
+    return (OUT == 2 || !RHS_NAT) ? 3 : 0;
+#endif
+}
+template <bool RHS_NAT, int OUT>
+constexpr int line_load_sleep()
+{
+#ifdef LINE_LOAD_SLEEP
+    return LINE_LOAD_SLEEP;
+#else
+    return (OUT == 2 || !RHS_NAT) ? 6 : 0;
+#endif
+}
+
 template <int P, int NA, bool RHS_NAT, int OUT, int CW, int NL, int D, int DH, int SW, bool TRACE>
 __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_line(LineArgs a)
 {
@@ -665,6 +690,7 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
             };
             for (int s = S0; s <= T; s++) {
                 const unsigned long long i0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
+                if constexpr (line_load_sleep<RHS_NAT, OUT>() > 0) __builtin_amdgcn_s_sleep(line_load_sleep<RHS_NAT, OUT>());
                 if (!(a.diag & 2)) issue(s + D);  // dummies past T keep the wait counts exact
                 const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
                 // steps s+LA+1 .. s+D were issued after step s+LA's
@@ -708,6 +734,7 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                     if (!jin && lane < P) reinterpret_cast<double *>(ring + q * SL::BYTES + SL::JFIN)[lane] = 0.0;
                 }
             }
+            if constexpr (line_poll_prio<RHS_NAT, OUT>() > 0) __builtin_amdgcn_s_setprio(line_poll_prio<RHS_NAT, OUT>());
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             unsigned polls = 0;
             for (int s = S0; s <= T; s++) {
