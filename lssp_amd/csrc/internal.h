@@ -180,6 +180,7 @@ struct LineILU {
     int W = 0, S = 0, tmax = 0, ntiles = 0;
     LineSweep L, U;
     double *d_ustream = nullptr;  // the U sweep's rhs, written by the L sweep
+    double *d_lstream = nullptr;  // the L sweep's rhs in its stream layout (k_line_rhs)
     double *d_hk = nullptr, *d_hj = nullptr;  // hand-off buffers (armed with TRI_SENTINEL)
     long hk_stride = 0, hj_stride = 0, hk_n = 0, hj_n = 0;
 };

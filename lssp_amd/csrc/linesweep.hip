@@ -301,6 +301,9 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
     // both sweeps (they never run at once) and armed with the sentinel
     LSSP_HIP(hipMalloc(&li.d_ustream, sizeof(double) * (li.U.rows_total + 16 * 1024 / 8)));
     LSSP_HIP(hipMemset(li.d_ustream, 0, sizeof(double) * (li.U.rows_total + 16 * 1024 / 8)));  // invalid rows stay +0.0
+    // the apply's L sweep reads its rhs as a stream too (k_line_rhs fills the valid rows)
+    LSSP_HIP(hipMalloc(&li.d_lstream, sizeof(double) * (li.L.rows_total + 16 * 1024 / 8)));
+    LSSP_HIP(hipMemset(li.d_lstream, 0, sizeof(double) * (li.L.rows_total + 16 * 1024 / 8)));
     li.tmax = std::max(li.L.tmax, li.U.tmax);
     li.hk_stride = (long)li.tmax * 64;
     li.hj_stride = (long)li.tmax * LINE_P;
@@ -329,9 +332,10 @@ void free_line_sweep(LineILU &li)
         *s = LineSweep{};
     }
     if (li.d_ustream) (void)hipFree(li.d_ustream);
+    if (li.d_lstream) (void)hipFree(li.d_lstream);
     if (li.d_hk) (void)hipFree(li.d_hk);
     if (li.d_hj) (void)hipFree(li.d_hj);
-    li.d_ustream = li.d_hk = li.d_hj = nullptr;
+    li.d_ustream = li.d_lstream = li.d_hk = li.d_hj = nullptr;
     li.ntiles = 0;
 }
 
@@ -479,6 +483,15 @@ constexpr int LINE_RW = 6;  // rhs wave: a run block's loads land LINE_RW steps 
 // the 10 KB of coefficient DMAs (whose lead is 10 steps): 216^3 apply 957 ->
 // 922 us (tools/gpu_exp.sh; the standalone natural-order sweeps got slower with
 // it, so they keep 0 / 0).  -DLINE_POLL_PRIO / -DLINE_LOAD_SLEEP override both.
+#ifndef LINE_STORE_SLEEP
+#define LINE_STORE_SLEEP 0  // tuning: storers' delay before their stores (64 clk units)
+#endif
+#ifndef LINE_COMP_PRIO
+#define LINE_COMP_PRIO 0  // tuning: compute waves' priority
+#endif
+#ifndef LINE_RHS_SLEEP
+#define LINE_RHS_SLEEP 0  // tuning: rhs wave's delay before its loads
+#endif
 template <bool RHS_NAT, int OUT>
 constexpr int line_poll_prio()
 {
@@ -551,6 +564,7 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
         const bool trs = TRACE && t == a.ttile && lane == 0;
 
         if (wave < CW) {
+            if (LINE_COMP_PRIO) __builtin_amdgcn_s_setprio(LINE_COMP_PRIO);
             // ---------------- compute: planes p0 .. p0+PC-1 ----------------
             // Coefficients and rhs of step s+1 are read from LDS at the start of
             // step s (their slot was completed before the barrier that ended step
@@ -829,6 +843,7 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                 constexpr int u = decltype(U)::value;  // set u: issued at step s, written at s + LINE_RW
                 if (s > T) return;
                 write(s, ring_v[u]);
+                if (LINE_RHS_SLEEP) __builtin_amdgcn_s_sleep(LINE_RHS_SLEEP);
                 issue(s + LINE_RW, ring_v[u]);
                 line_barrier();
             };
@@ -872,6 +887,7 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                 };
                 for (int s = S0; s <= T; s++) {
                     const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
+                    if (LINE_STORE_SLEEP) __builtin_amdgcn_s_sleep(LINE_STORE_SLEEP);
                     if (s >= 0) slice(s);
                     if (s >= 1 && s <= T) rearm(s - 1);
                     if (trs && w == 0 && s >= 0 && s < T) ts[8 * s + 5] = __builtin_amdgcn_s_memtime() - w0;
@@ -892,6 +908,7 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                 }
                 for (int s = S0; s <= T; s++) {
                     const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
+                    if (LINE_STORE_SLEEP) __builtin_amdgcn_s_sleep(LINE_STORE_SLEEP);
                     const int q = s - 1;
                     if (q >= 0 && q < T) {
                         const double *rs = res + (q & (RS - 1)) * P * 64;
@@ -976,8 +993,41 @@ static int launch_line_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a
 // which: 0 = L sweep, 1 = U sweep.  The rhs is natural order unless u_in (the
 // U rhs stream); the output goes to out (natural order) or, when out_u, to the
 // U rhs stream (the L sweep of an apply)
+// The apply's rhs (natural order) into the L sweep's stream layout.  A block
+// moves 8 consecutive steps of one tile: thread (plane p, line l) loads the 8
+// consecutive rows i .. i+7 of its line (one 64-byte run of the natural-order
+// vector) and writes them to the 8 step blocks, where the block's 256 threads
+// write 256 consecutive stream entries per step.  Block b runs on XCD b % 8 and
+// the XCD's blocks walk whole tiles in step order.
+constexpr int LRHS_RUN = 8;
+__global__ __launch_bounds__(LINE_P * 64) void k_line_rhs(const LineTile *__restrict__ tiles, int ntiles, int nq,
+                                                         int nx, int ny, const double *__restrict__ rhs,
+                                                         double *__restrict__ out, const double *guard)
+{
+    if (guard && *guard != 0.0) return;  // a batched iteration past the stop (lssp_amd_ctx::guard)
+    const long b = blockIdx.x, j = b >> 3;
+    const int t = (int)(b & 7) + 8 * (int)(j / nq), q0 = (int)(j % nq) * LRHS_RUN;
+    if (t >= ntiles) return;
+    const LineTile d = tiles[t];
+    const int p = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (q0 >= d.T || p >= d.np || l >= d.nj) return;
+    const long row0 = ((long)(d.k0 + p) * ny + (d.j0 + l)) * nx;
+    double v[LRHS_RUN];
+#pragma unroll
+    for (int m = 0; m < LRHS_RUN; m++) {
+        const int i = q0 + m - l - p;
+        v[m] = (q0 + m < d.T && (unsigned)i < (unsigned)nx) ? rhs[row0 + i] : 0.0;
+    }
+    double *o = out + d.cbase + (long)q0 * LINE_P * d.nj + p * d.nj + l;
+#pragma unroll
+    for (int m = 0; m < LRHS_RUN; m++) {
+        const int i = q0 + m - l - p;
+        if (q0 + m < d.T && (unsigned)i < (unsigned)nx) o[(long)m * LINE_P * d.nj] = v[m];
+    }
+}
+
 static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const double *rhs, bool u_in, double *out,
-                       bool out_u)
+                       bool out_u, bool l_in = false)
 {
     const LineSweep &ls = which ? li.U : li.L;
     LineArgs a{};
@@ -987,7 +1037,7 @@ static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const doub
     a.n = (long)ls.nx * ls.ny * ls.nz;
     a.tiles = ls.d_tiles;
     a.coef = ls.d_coef;
-    a.rhs = u_in ? li.d_ustream : rhs;
+    a.rhs = u_in ? li.d_ustream : l_in ? li.d_lstream : rhs;
     a.out = out_u ? li.d_ustream : out;
     a.hk = li.d_hk;
     a.hj = li.d_hj;
@@ -1003,13 +1053,20 @@ static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const doub
         a.diag = dg ? atoi(dg) : 0;
     }
     if (u_in) return launch_line_t<4, false, 1>(c, ls, a);
+    if (l_in) return ls.NA == 3 ? launch_line_t<3, false, 2>(c, ls, a) : launch_line_t<4, false, 2>(c, ls, a);
     if (out_u) return ls.NA == 3 ? launch_line_t<3, true, 2>(c, ls, a) : launch_line_t<4, true, 2>(c, ls, a);
     return ls.NA == 3 ? launch_line_t<3, true, 1>(c, ls, a) : launch_line_t<4, true, 1>(c, ls, a);
 }
 
 int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs)
 {
-    LSSP_TRY(launch_line(c, li, 0, rhs, false, nullptr, true));
+    const LineSweep &L = li.L;
+    const int nq = (L.tmax + LRHS_RUN - 1) / LRHS_RUN;
+    const long grid = 8L * ((L.ntiles + 7) / 8) * nq;
+    k_line_rhs<<<grid, LINE_P * 64, 0, c->stream>>>(L.d_tiles, L.ntiles, nq, L.nx, L.ny, rhs, li.d_lstream,
+                                                    c->guard);
+    LSSP_HIP(hipGetLastError());
+    LSSP_TRY(launch_line(c, li, 0, nullptr, false, nullptr, true, true));
     return launch_line(c, li, 1, nullptr, true, x, false);
 }
 
