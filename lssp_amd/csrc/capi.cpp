@@ -109,7 +109,7 @@ void setup_mark(const char *phase)
     last = t;
 }
 
-void parallel_for(long n, const std::function<void(long, long)> &f)
+int host_threads()
 {
     static const int nt = [] {
         int t = (int)std::thread::hardware_concurrency();
@@ -117,7 +117,13 @@ void parallel_for(long n, const std::function<void(long, long)> &f)
         if (e && atoi(e) > 0) t = std::min(t, atoi(e));
         return std::max(1, std::min(t, 16));
     }();
-    const int k = (int)std::min<long>(nt, std::max<long>(1, n / 4096));
+    return nt;
+}
+
+void parallel_for(long n, const std::function<void(long, long)> &f, long grain)
+{
+    const int nt = host_threads();
+    const int k = (int)std::min<long>(nt, std::max<long>(1, n / std::max<long>(grain, 1)));
     if (k <= 1) {
         f(0, n);
         return;

@@ -280,7 +280,9 @@ double wall_time();  // seconds, lssp_get_time() (utils.cxx:40-46)
 void setup_mark(const char *phase);
 // host setup loops: f(lo, hi) over [0, n) in contiguous chunks on up to 16
 // threads (OMP_NUM_THREADS / the hardware concurrency, whichever is smaller)
-void parallel_for(long n, const std::function<void(long, long)> &f);
+int host_threads();  // worker threads for host setup: <= 16, <= OMP_NUM_THREADS
+// [0, n) cut into at most 16 contiguous ranges of >= grain items, one thread each
+void parallel_for(long n, const std::function<void(long, long)> &f, long grain = 4096);
 
 // ILU setup (ilu_setup.cpp), exact restatement of pc-iluk.cxx / pc-ilut.cxx
 struct HostCSR {

@@ -12,9 +12,11 @@
 // arithmetic is untouched (entries in the reference's order), so the sweep
 // stays bitwise.
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 
 #include "internal.h"
 
@@ -31,83 +33,104 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
     auto strict_end = [&](int i) { return upper ? Tp[i + 1] : Tp[i + 1] - 1; };
     bool unit = true;
     int bw = 1;
-    for (int i = 0; i < n; i++) {
-        unit &= (upper ? Tx[Tp[i]] : Tx[Tp[i + 1] - 1]) == 1.0;
-        for (int k = strict_begin(i); k < strict_end(i); k++) bw = std::max(bw, std::abs(i - Tj[k]));
+    {
+        std::mutex mu;
+        parallel_for(n, [&](long i0, long i1) {
+            bool u = true;
+            int w = 1;
+            for (long i = i0; i < i1; i++) {
+                u &= (upper ? Tx[Tp[i]] : Tx[Tp[i + 1] - 1]) == 1.0;
+                for (int k = strict_begin((int)i); k < strict_end((int)i); k++) w = std::max(w, std::abs((int)i - Tj[k]));
+            }
+            std::lock_guard<std::mutex> g(mu);
+            unit &= u;
+            bw = std::max(bw, w);
+        });
     }
-    long B = std::max(64L, (long)bw);  // one bandwidth per block: measured best (DESIGN.md 3.4)
+    long B = std::max(64L, (long)bw);  // one bandwidth per block: measured best (DESIGN.md 3.5)
     if (B > n) B = n;
     const int nb = (int)((n + B - 1) / B);
 
-    // rows of each block ordered by (level, q)
+    // rows of each block ordered by (level, q); blocks are independent (threads),
+    // their step lists are concatenated in block order
     std::vector<int> perm(n), pos(n);
-    std::vector<int> step_pos, step_lev, blk_step(nb + 1, 0);
-    for (int b = 0; b < nb; b++) {
-        const long q0 = (long)b * B, q1 = std::min<long>(q0 + B, n);
-        int lmin = INT_MAX, lmax = 0;
-        for (long q = q0; q < q1; q++) {
-            const int r = upper ? n - 1 - (int)q : (int)q;
-            lmin = std::min(lmin, lev[r]);
-            lmax = std::max(lmax, lev[r]);
-        }
-        std::vector<int> cnt(lmax - lmin + 2, 0);
-        for (long q = q0; q < q1; q++) cnt[lev[upper ? n - 1 - (int)q : (int)q] - lmin + 1]++;
-        for (size_t l = 1; l < cnt.size(); l++) cnt[l] += cnt[l - 1];
-        blk_step[b] = (int)step_lev.size();
-        for (int l = 0; l <= lmax - lmin; l++)
-            if (cnt[l + 1] > cnt[l]) {
-                step_pos.push_back((int)q0 + cnt[l]);
-                step_lev.push_back(l + lmin);
+    std::vector<std::vector<int>> bsp(nb), bsl(nb);
+    parallel_for(nb, [&](long b0, long b1) {
+        for (long b = b0; b < b1; b++) {
+            const long q0 = b * B, q1 = std::min<long>(q0 + B, n);
+            int lmin = INT_MAX, lmax = 0;
+            for (long q = q0; q < q1; q++) {
+                const int r = upper ? n - 1 - (int)q : (int)q;
+                lmin = std::min(lmin, lev[r]);
+                lmax = std::max(lmax, lev[r]);
             }
-        for (long q = q0; q < q1; q++) {
-            const int r = upper ? n - 1 - (int)q : (int)q;
-            const int p = (int)q0 + cnt[lev[r] - lmin]++;
-            perm[p] = r;
-            pos[r] = p;
+            std::vector<int> cnt(lmax - lmin + 2, 0);
+            for (long q = q0; q < q1; q++) cnt[lev[upper ? n - 1 - (int)q : (int)q] - lmin + 1]++;
+            for (size_t l = 1; l < cnt.size(); l++) cnt[l] += cnt[l - 1];
+            for (int l = 0; l <= lmax - lmin; l++)
+                if (cnt[l + 1] > cnt[l]) {
+                    bsp[b].push_back((int)q0 + cnt[l]);
+                    bsl[b].push_back(l + lmin);
+                }
+            for (long q = q0; q < q1; q++) {
+                const int r = upper ? n - 1 - (int)q : (int)q;
+                const int p = (int)q0 + cnt[lev[r] - lmin]++;
+                perm[p] = r;
+                pos[r] = p;
+            }
         }
+    }, 1);
+    std::vector<int> step_pos, blk_step(nb + 1, 0);
+    for (int b = 0; b < nb; b++) {
+        blk_step[b] = (int)step_pos.size();
+        step_pos.insert(step_pos.end(), bsp[b].begin(), bsp[b].end());
     }
-    const int nsteps = (int)step_lev.size();
+    const int nsteps = (int)step_pos.size();
     blk_step[nb] = nsteps;
     step_pos.push_back(n);
     std::vector<int> step_of(n);
-    for (int s = 0; s < nsteps; s++)
-        for (int p = step_pos[s]; p < step_pos[s + 1]; p++) step_of[p] = s;
+    parallel_for(nsteps, [&](long s0, long s1) {
+        for (long s = s0; s < s1; s++)
+            for (int p = step_pos[s]; p < step_pos[s + 1]; p++) step_of[p] = (int)s;
+    }, 64);
 
     // entries in summation order; intra-block dependencies still inside the
     // ring window come from LDS (code -1 - slot), everything else from HBM
-    std::vector<int> rp(n + 1, 0), cols;
-    std::vector<double> vals, diag;
+    std::vector<int> rp(n + 1, 0);
+    for (int p = 0; p < n; p++) rp[p + 1] = rp[p] + strict_end(perm[p]) - strict_begin(perm[p]);
+    std::vector<int> cols(rp[n]);
+    std::vector<double> vals(rp[n]), diag;
     if (!unit) diag.resize(n);
-    cols.reserve(Tj.size());
-    vals.reserve(Tj.size());
-    for (int p = 0; p < n; p++) {
-        const int i = perm[p], b = (int)(Q(i) / B), s = step_of[p];
-        // within the ring window (the last BP_RING positions of the block)
-        // the value comes from LDS; everything else (earlier blocks, far back
-        // in this one) from HBM
-        auto take = [&](int k) {
-            const int j = Tj[k];
-            const int bj = (int)(Q(j) / B);
-            int code = j;
-            if (bj == b) {
-                const int pd = pos[j];
-                if (step_pos[s + 1] - pd <= BP_RING) code = -1 - (int)((pd - (long)b * B) % BP_RING);
-            }
-            cols.push_back(code);
-            vals.push_back(Tx[k]);
-        };
-        if (!upper)
-            for (int k = Tp[i]; k < Tp[i + 1] - 1; k++) take(k);
-        else
-            for (int k = Tp[i + 1] - 1; k > Tp[i]; k--) take(k);
-        if (!unit) diag[p] = upper ? Tx[Tp[i]] : Tx[Tp[i + 1] - 1];
-        rp[p + 1] = (int)cols.size();
-    }
+    parallel_for(n, [&](long p0, long p1) {
+        for (long p = p0; p < p1; p++) {
+            const int i = perm[p], b = (int)(Q(i) / B), s = step_of[p];
+            int o = rp[p];
+            auto take = [&](int k) {
+                const int j = Tj[k];
+                const int bj = (int)(Q(j) / B);
+                int code = j;
+                if (bj == b) {
+                    const int pd = pos[j];
+                    if (step_pos[s + 1] - pd <= BP_RING) code = -1 - (int)((pd - (long)b * B) % BP_RING);
+                }
+                cols[o] = code;
+                vals[o] = Tx[k];
+                o++;
+            };
+            if (!upper)
+                for (int k = Tp[i]; k < Tp[i + 1] - 1; k++) take(k);
+            else
+                for (int k = Tp[i + 1] - 1; k > Tp[i]; k--) take(k);
+            if (!unit) diag[p] = upper ? Tx[Tp[i]] : Tx[Tp[i + 1] - 1];
+        }
+    });
     {
         // v6 packets; the rhs of the U sweep is the L sweep's output, read in
         // L's schedule order (the L sweep's rhs is permuted into L order first)
         std::vector<int> rhs_index(n);
-        for (int r = 0; r < n; r++) rhs_index[r] = prod && !prod->h_pos.empty() ? prod->h_pos[r] : pos[r];
+        parallel_for(n, [&](long r0, long r1) {
+            for (long r = r0; r < r1; r++) rhs_index[r] = prod && !prod->h_pos.empty() ? prod->h_pos[r] : pos[r];
+        });
         const int st6 = build_packets6(n, perm, pos, rp, cols, vals, diag, unit, step_pos, blk_step, nb, B,
                                        rhs_index, t);
         // a row longer than the longest record: the sync-free sweep serves the factor
@@ -162,77 +185,110 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
         return p4((long)(EP / 2) * nrow) + 2L * EP * nrow + p4(2 * nrow) + p4(nrow);
     };
     constexpr long PK6_REC_WORDS16 = 1024;  // 16-byte units (trisolve.hip PK6_REC16)
-    std::vector<int> blk(nb + 1, 0);
-    std::vector<int> desc;
-    std::vector<uint32_t> rec;  // 4-byte words, 16-byte aligned packets
-    std::vector<int> idx;
-    std::vector<int> stamp(n, -1), slot(n, 0), xl;
     auto pack = [](int a, int b) { return (uint32_t)((a & 0xffff) | ((uint32_t)(b & 0xffff) << 16)); };
-    int pid = 0;
-    for (int b = 0; b < nb; b++) {
-        blk[b] = (int)desc.size() / 4;
-        for (int s = blk_step[b]; s < blk_step[b + 1]; s++) {
-            int p = step_pos[s];
-            while (p < step_pos[s + 1]) {
-                int nr = 0, emax = 0;
-                xl.clear();
-                while (p + nr < step_pos[s + 1] && nr < ROWS) {
-                    const int r = p + nr;
-                    if (EP >= 16 && rec_words(nr + 1) > 4 * PK6_REC_WORDS16) break;  // LDS record slot
-                    int newx = 0;
-                    for (int k = rp[r]; k < rp[r + 1]; k++)
-                        if (cols[k] >= 0 && stamp[cols[k]] != pid) newx++;
-                    if ((long)xl.size() + newx > (long)ROWS * PK3_EXT) break;
-                    for (int k = rp[r]; k < rp[r + 1]; k++) {
-                        const int g = cols[k];
-                        if (g >= 0 && stamp[g] != pid) {
-                            stamp[g] = pid;
-                            slot[g] = (int)xl.size();
-                            xl.push_back(g);
+    // blocks are independent: each thread builds its blocks' packets with
+    // block-relative record / index offsets and its own operand stamps; the
+    // blocks are then laid out in order and the offsets made absolute
+    struct BlkPk {
+        std::vector<int> desc;
+        std::vector<uint32_t> rec;
+        std::vector<int> idx;
+    };
+    std::vector<BlkPk> bp(nb);
+    std::atomic<int> status{LSSP_AMD_OK};
+    parallel_for(nb, [&](long b0, long b1) {
+        std::vector<int> stamp(n, -1), slot(n, 0), xl;
+        int pid = 0;
+        for (long b = b0; b < b1 && status.load() == LSSP_AMD_OK; b++) {
+            std::vector<int> &desc = bp[b].desc, &idx = bp[b].idx;
+            std::vector<uint32_t> &rec = bp[b].rec;
+            for (int s = blk_step[b]; s < blk_step[b + 1]; s++) {
+                int p = step_pos[s];
+                while (p < step_pos[s + 1]) {
+                    int nr = 0, emax = 0;
+                    xl.clear();
+                    while (p + nr < step_pos[s + 1] && nr < ROWS) {
+                        const int r = p + nr;
+                        if (EP >= 16 && rec_words(nr + 1) > 4 * PK6_REC_WORDS16) break;  // LDS record slot
+                        int newx = 0;
+                        for (int k = rp[r]; k < rp[r + 1]; k++)
+                            if (cols[k] >= 0 && stamp[cols[k]] != pid) newx++;
+                        if ((long)xl.size() + newx > (long)ROWS * PK3_EXT) break;
+                        for (int k = rp[r]; k < rp[r + 1]; k++) {
+                            const int g = cols[k];
+                            if (g >= 0 && stamp[g] != pid) {
+                                stamp[g] = pid;
+                                slot[g] = (int)xl.size();
+                                xl.push_back(g);
+                            }
                         }
+                        emax = std::max(emax, rp[r + 1] - rp[r]);
+                        nr++;
                     }
-                    emax = std::max(emax, rp[r + 1] - rp[r]);
-                    nr++;
-                }
-                const int nx = (int)xl.size();
-                const long ro = (long)rec.size() / 4, io = (long)idx.size();
-                if (ro > INT_MAX || io > INT_MAX) return LSSP_AMD_EUNSUPPORTED;
-                desc.push_back((int)ro);
-                desc.push_back((int)io);
-                desc.push_back(nr | (nx << 10) | (emax << 21));
-                desc.push_back(p);
-                // C: (EP/2) words per row, V: 2*EP, D: 2, ROW: 1 -- each array padded to 4 words
-                auto pad4 = [](long w) { return (w + 3) & ~3L; };
-                const long wc = pad4((long)(EP / 2) * nr), wv = 2L * EP * nr, wd = pad4(2L * nr), wr = pad4(nr);
-                rec.resize(rec.size() + wc + wv + wd + wr, 0u);
-                uint32_t *w = rec.data() + 4 * ro;
-                double *V = reinterpret_cast<double *>(w + wc);
-                double *D = V + (long)EP * nr;
-                uint32_t *ROW = w + wc + wv + wd;
-                for (int r = 0; r < nr; r++) {
-                    const int k0 = rp[p + r], len = rp[p + r + 1] - k0;
-                    int c[24];
-                    for (int e = 0; e < 24; e++) c[e] = PK4_PAD;
-                    for (int e = 0; e < len; e++) {
-                        const int g = cols[k0 + e];
-                        c[e] = g < 0 ? g : slot[g];
-                        V[2L * ((long)(e / 2) * nr + r) + (e & 1)] = vals[k0 + e];
+                    const int nx = (int)xl.size();
+                    const long ro = (long)rec.size() / 4, io = (long)idx.size();  // block-relative
+                    desc.push_back((int)ro);
+                    desc.push_back((int)io);
+                    desc.push_back(nr | (nx << 10) | (emax << 21));
+                    desc.push_back(p);
+                    // C: (EP/2) words per row, V: 2*EP, D: 2, ROW: 1 -- each array padded to 4 words
+                    auto pad4 = [](long w) { return (w + 3) & ~3L; };
+                    const long wc = pad4((long)(EP / 2) * nr), wv = 2L * EP * nr, wd = pad4(2L * nr), wr = pad4(nr);
+                    rec.resize(rec.size() + wc + wv + wd + wr, 0u);
+                    uint32_t *w = rec.data() + 4 * ro;
+                    double *V = reinterpret_cast<double *>(w + wc);
+                    double *D = V + (long)EP * nr;
+                    uint32_t *ROW = w + wc + wv + wd;
+                    for (int r = 0; r < nr; r++) {
+                        const int k0 = rp[p + r], len = rp[p + r + 1] - k0;
+                        int cc[24];
+                        for (int e = 0; e < 24; e++) cc[e] = PK4_PAD;
+                        for (int e = 0; e < len; e++) {
+                            const int g = cols[k0 + e];
+                            cc[e] = g < 0 ? g : slot[g];
+                            V[2L * ((long)(e / 2) * nr + r) + (e & 1)] = vals[k0 + e];
+                        }
+                        for (int q = 0; q < EP / 2; q++) w[(long)(EP / 2) * r + q] = pack(cc[2 * q], cc[2 * q + 1]);
+                        D[r] = unit ? 1.0 : diag[p + r];
+                        ROW[r] = (uint32_t)perm[p + r];
                     }
-                    for (int q = 0; q < EP / 2; q++) w[(long)(EP / 2) * r + q] = pack(c[2 * q], c[2 * q + 1]);
-                    D[r] = unit ? 1.0 : diag[p + r];
-                    ROW[r] = (uint32_t)perm[p + r];
+                    for (int r = 0; r < nr; r++) idx.push_back(rhs_index[perm[p + r]]);
+                    for (int x = 0; x < nx; x++) idx.push_back(pos[xl[x]]);
+                    p += nr;
+                    pid++;
                 }
-                for (int r = 0; r < nr; r++) idx.push_back(rhs_index[perm[p + r]]);
-                for (int x = 0; x < nx; x++) idx.push_back(pos[xl[x]]);
-                p += nr;
-                pid++;
             }
+            if ((int)desc.size() / 4 > PK3_CAP) status = LSSP_AMD_EUNSUPPORTED;
         }
-        if ((int)desc.size() / 4 - blk[b] > PK3_CAP) return LSSP_AMD_EUNSUPPORTED;
+    }, 1);
+    if (status.load() != LSSP_AMD_OK) return status.load();
+    // lay the blocks out in order; offsets absolute
+    std::vector<int> blk(nb + 1, 0);
+    std::vector<long> rec_off(nb + 1, 0), idx_off(nb + 1, 0);
+    for (int b = 0; b < nb; b++) {
+        blk[b + 1] = blk[b] + (int)bp[b].desc.size() / 4;
+        rec_off[b + 1] = rec_off[b] + (long)bp[b].rec.size();
+        idx_off[b + 1] = idx_off[b] + (long)bp[b].idx.size();
     }
-    blk[nb] = (int)desc.size() / 4;
-    rec.resize(rec.size() + 4, 0u);
-    idx.push_back(0);
+    if (rec_off[nb] / 4 > INT_MAX || idx_off[nb] > INT_MAX) return LSSP_AMD_EUNSUPPORTED;
+    std::vector<int> desc(4L * blk[nb]);
+    std::vector<uint32_t> rec(rec_off[nb] + 4, 0u);
+    std::vector<int> idx(idx_off[nb] + 1, 0);
+    parallel_for(nb, [&](long b0, long b1) {
+        for (long b = b0; b < b1; b++) {
+            const BlkPk &k = bp[b];
+            int *d = desc.data() + 4L * blk[b];
+            for (size_t e = 0; e < k.desc.size(); e += 4) {
+                d[e] = k.desc[e] + (int)(rec_off[b] / 4);
+                d[e + 1] = k.desc[e + 1] + (int)idx_off[b];
+                d[e + 2] = k.desc[e + 2];
+                d[e + 3] = k.desc[e + 3];
+            }
+            std::copy(k.rec.begin(), k.rec.end(), rec.begin() + rec_off[b]);
+            std::copy(k.idx.begin(), k.idx.end(), idx.begin() + idx_off[b]);
+        }
+    }, 1);
+    bp.clear();
     t.pk6_n = blk[nb];
     t.pk6_ep = EP;
     t.pk6_rows = ROWS;
