@@ -994,35 +994,38 @@ static int launch_line_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a
 // U rhs stream); the output goes to out (natural order) or, when out_u, to the
 // U rhs stream (the L sweep of an apply)
 // The apply's rhs (natural order) into the L sweep's stream layout.  A block
-// moves 8 consecutive steps of one tile: thread (plane p, line l) loads the 8
-// consecutive rows i .. i+7 of its line (one 64-byte run of the natural-order
-// vector) and writes them to the 8 step blocks, where the block's 256 threads
-// write 256 consecutive stream entries per step.  Block b runs on XCD b % 8 and
-// the XCD's blocks walk whole tiles in step order.
+// moves 8 consecutive steps of one tile (P x 64 x 8 values): value v of the
+// block is (plane p, line l, step q0 + m) with m = v & 7, so 8 neighbouring
+// lanes load one 64-byte run of a line from the natural-order vector and, per
+// step, 8 lanes store 8 consecutive stream entries.  Block b runs on XCD b % 8
+// and the XCD's blocks walk whole tiles in step order.
 constexpr int LRHS_RUN = 8;
-__global__ __launch_bounds__(LINE_P * 64) void k_line_rhs(const LineTile *__restrict__ tiles, int ntiles, int nq,
-                                                         int nx, int ny, const double *__restrict__ rhs,
-                                                         double *__restrict__ out, const double *guard)
+__global__ __launch_bounds__(256) void k_line_rhs(const LineTile *__restrict__ tiles, int ntiles, int nq, int nx,
+                                                 int ny, const double *__restrict__ rhs, double *__restrict__ out,
+                                                 const double *guard)
 {
     if (guard && *guard != 0.0) return;  // a batched iteration past the stop (lssp_amd_ctx::guard)
     const long b = blockIdx.x, j = b >> 3;
     const int t = (int)(b & 7) + 8 * (int)(j / nq), q0 = (int)(j % nq) * LRHS_RUN;
     if (t >= ntiles) return;
     const LineTile d = tiles[t];
-    const int p = threadIdx.x >> 6, l = threadIdx.x & 63;
-    if (q0 >= d.T || p >= d.np || l >= d.nj) return;
-    const long row0 = ((long)(d.k0 + p) * ny + (d.j0 + l)) * nx;
-    double v[LRHS_RUN];
+    if (q0 >= d.T) return;
+    constexpr int NV = LINE_P * 64 * LRHS_RUN / 256;  // values per thread
+    double v[NV];
 #pragma unroll
-    for (int m = 0; m < LRHS_RUN; m++) {
+    for (int it = 0; it < NV; it++) {
+        const int k = it * 256 + threadIdx.x, m = k & 7, l = (k >> 3) & 63, p = k >> 9;
         const int i = q0 + m - l - p;
-        v[m] = (q0 + m < d.T && (unsigned)i < (unsigned)nx) ? rhs[row0 + i] : 0.0;
+        const bool ok = q0 + m < d.T && p < d.np && l < d.nj && (unsigned)i < (unsigned)nx;
+        v[it] = ok ? rhs[((long)(d.k0 + p) * ny + (d.j0 + l)) * nx + i] : 0.0;
     }
-    double *o = out + d.cbase + (long)q0 * LINE_P * d.nj + p * d.nj + l;
+    const long SB = (long)LINE_P * d.nj;
 #pragma unroll
-    for (int m = 0; m < LRHS_RUN; m++) {
+    for (int it = 0; it < NV; it++) {
+        const int k = it * 256 + threadIdx.x, m = k & 7, l = (k >> 3) & 63, p = k >> 9;
         const int i = q0 + m - l - p;
-        if (q0 + m < d.T && (unsigned)i < (unsigned)nx) o[(long)m * LINE_P * d.nj] = v[m];
+        if (q0 + m < d.T && p < d.np && l < d.nj && (unsigned)i < (unsigned)nx)
+            out[d.cbase + (q0 + m) * SB + p * d.nj + l] = v[it];
     }
 }
 
@@ -1063,8 +1066,7 @@ int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const doubl
     const LineSweep &L = li.L;
     const int nq = (L.tmax + LRHS_RUN - 1) / LRHS_RUN;
     const long grid = 8L * ((L.ntiles + 7) / 8) * nq;
-    k_line_rhs<<<grid, LINE_P * 64, 0, c->stream>>>(L.d_tiles, L.ntiles, nq, L.nx, L.ny, rhs, li.d_lstream,
-                                                    c->guard);
+    k_line_rhs<<<grid, 256, 0, c->stream>>>(L.d_tiles, L.ntiles, nq, L.nx, L.ny, rhs, li.d_lstream, c->guard);
     LSSP_HIP(hipGetLastError());
     LSSP_TRY(launch_line(c, li, 0, nullptr, false, nullptr, true, true));
     return launch_line(c, li, 1, nullptr, true, x, false);
