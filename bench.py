@@ -254,8 +254,8 @@ def main():
                      "csr_int32_equivalent_gbps": round(csr_equiv_gbs, 1)},
             "roofline": {"bound": "hbm", "achieved": round(apply_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(apply_gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("ilu_apply"),
-                         "kernel": "ILU(0) apply = k_line (L sweep, rhs in natural order -> the U sweep's "
-                                   "rhs stream) + k_line (U sweep -> x in natural order); "
+                         "kernel": "ILU(0) apply = k_line_rhs (rhs -> the L sweep's stream) + k_line (L sweep "
+                                   "-> the U sweep's rhs stream) + k_line (U sweep -> x in natural order); "
                                    "latency-bound: 2 x 646 dependent levels",
                          "bytes_per_launch": apply_b, "ms_per_launch": round(apply_ms, 5)},
             "roofline_spmv": {"bound": "hbm", "achieved": round(spmv_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
