@@ -424,38 +424,34 @@ int lssp_amd_mat_local_rows(const lssp_amd_mat *A, int *row0, int *nlocal, int *
 
 // ---- SpMV (mvops.cxx) ----------------------------------------------------------
 // x must hold nrows + nhalo entries on a distributed matrix; its halo part is
-// refreshed here (halo_exchange is a no-op on one rank).
+// refreshed here, overlapped with the halo-free rows (spmv_halo, comm.cpp).
 int lssp_amd_mv_amxpby(lssp_amd_ctx *c, double alpha, const lssp_amd_mat *A, double *x,
                        double beta, double *y)
 {
     if (!c || !A || !x || !y) return LSSP_AMD_EINVAL;
-    LSSP_TRY(halo_exchange(A, x));
-    return launch_spmv(c, A, EPI_AXPBY, alpha, x, beta, y, y, 0, nullptr, nullptr);
+    return spmv_halo(c, A, EPI_AXPBY, alpha, x, beta, y, y, 0, nullptr, nullptr);
 }
 
 int lssp_amd_mv_amxpbyz(lssp_amd_ctx *c, double alpha, const lssp_amd_mat *A, double *x,
                         double beta, const double *y, double *z)
 {
     if (!c || !A || !x || !y || !z) return LSSP_AMD_EINVAL;
-    LSSP_TRY(halo_exchange(A, x));
     // y is read even when beta == 0, as the reference does (mvops.cxx:61): a NaN / Inf
     // in y propagates into z (tests/test_gpu_edge.py); only the drivers use the
     // y-free epilogue
-    return launch_spmv(c, A, EPI_AXPBY, alpha, x, beta, y, z, 0, nullptr, nullptr);
+    return spmv_halo(c, A, EPI_AXPBY, alpha, x, beta, y, z, 0, nullptr, nullptr);
 }
 
 int lssp_amd_mv_amxy(lssp_amd_ctx *c, double a, const lssp_amd_mat *A, double *x, double *y)
 {
     if (!c || !A || !x || !y) return LSSP_AMD_EINVAL;
-    LSSP_TRY(halo_exchange(A, x));
-    return launch_spmv(c, A, EPI_AMXY, a, x, 0, nullptr, y, 0, nullptr, nullptr);
+    return spmv_halo(c, A, EPI_AMXY, a, x, 0, nullptr, y, 0, nullptr, nullptr);
 }
 
 int lssp_amd_mv_mxy(lssp_amd_ctx *c, const lssp_amd_mat *A, double *x, double *y)
 {
     if (!c || !A || !x || !y) return LSSP_AMD_EINVAL;
-    LSSP_TRY(halo_exchange(A, x));
-    return launch_spmv(c, A, EPI_MXY, 1.0, x, 0, nullptr, y, 0, nullptr, nullptr);
+    return spmv_halo(c, A, EPI_MXY, 1.0, x, 0, nullptr, y, 0, nullptr, nullptr);
 }
 
 // ---- BLAS-1 (vector.cxx) -----------------------------------------------------------

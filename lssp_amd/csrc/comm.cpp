@@ -57,15 +57,17 @@ static int xfer_allgather(lssp_amd_ctx *c, const void *dsend, void *drecv, long 
     return LSSP_AMD_OK;
 }
 
-// one grouped point-to-point round
-static int xfer_group(lssp_amd_ctx *c, const std::vector<Msg> &sends, const std::vector<Msg> &recvs)
+// one grouped point-to-point round (RCCL: on stream st, default the context's)
+static int xfer_group(lssp_amd_ctx *c, const std::vector<Msg> &sends, const std::vector<Msg> &recvs,
+                      hipStream_t st = nullptr)
 {
     if (!host_mode(c)) {
+        if (!st) st = c->stream;
         LSSP_NCCL(ncclGroupStart());
         for (const Msg &m : sends)
-            LSSP_NCCL(ncclSend(m.dbuf, (size_t)m.bytes, ncclInt8, m.peer, (ncclComm_t)c->comm, c->stream));
+            LSSP_NCCL(ncclSend(m.dbuf, (size_t)m.bytes, ncclInt8, m.peer, (ncclComm_t)c->comm, st));
         for (const Msg &m : recvs)
-            LSSP_NCCL(ncclRecv(m.dbuf, (size_t)m.bytes, ncclInt8, m.peer, (ncclComm_t)c->comm, c->stream));
+            LSSP_NCCL(ncclRecv(m.dbuf, (size_t)m.bytes, ncclInt8, m.peer, (ncclComm_t)c->comm, st));
         LSSP_NCCL(ncclGroupEnd());
         return LSSP_AMD_OK;
     }
@@ -121,6 +123,14 @@ int comm_carry_out(lssp_amd_ctx *c)
     return xfer_group(c, {{c->rank + 1, c->d_sums, (long)sizeof(double) * MAX_SLOTS}}, {});
 }
 
+static void halo_msgs(const lssp_amd_mat *A, double *x, std::vector<Msg> &s, std::vector<Msg> &r)
+{
+    for (size_t q = 0; q < A->send_peer.size(); q++)
+        s.push_back({A->send_peer[q], A->d_send_buf + A->send_off[q], (long)sizeof(double) * A->send_cnt[q]});
+    for (size_t q = 0; q < A->recv_peer.size(); q++)
+        r.push_back({A->recv_peer[q], x + A->nrows + A->recv_off[q], (long)sizeof(double) * A->recv_cnt[q]});
+}
+
 int halo_exchange(const lssp_amd_mat *A, double *x)
 {
     if (!A || A->ctx == nullptr || A->ctx->nranks <= 1) return LSSP_AMD_OK;
@@ -128,11 +138,42 @@ int halo_exchange(const lssp_amd_mat *A, double *x)
     lssp_amd_ctx *c = A->ctx;
     LSSP_TRY(launch_pack(c, A->d_send_idx, x, A->d_send_buf, A->nsend));
     std::vector<Msg> s, r;
-    for (size_t q = 0; q < A->send_peer.size(); q++)
-        s.push_back({A->send_peer[q], A->d_send_buf + A->send_off[q], (long)sizeof(double) * A->send_cnt[q]});
-    for (size_t q = 0; q < A->recv_peer.size(); q++)
-        r.push_back({A->recv_peer[q], x + A->nrows + A->recv_off[q], (long)sizeof(double) * A->recv_cnt[q]});
+    halo_msgs(A, x, s, r);
     return xfer_group(c, s, r);
+}
+
+// z = op(A x) with the halo round overlapped: the chunks [ich0, ich1) read no
+// halo column, so their product runs while the round is in flight -- on the
+// RCCL path the round goes to comm_stream between two events (pack -> round ->
+// boundary chunks); on the host transport, which stages through the host
+// synchronously, the interior product is simply queued before the round.  Each
+// chunk writes its level-1 partials at its own index, so the split product and
+// its fused dots are bitwise those of one launch.
+int spmv_halo(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, double *x, double beta,
+              const double *y, double *z, int nred, const double *w0, const double *w1)
+{
+    const bool xch = c->nranks > 1 && !(A->send_peer.empty() && A->recv_peer.empty());
+    if (!xch || A->ich1 <= A->ich0) {
+        LSSP_TRY(halo_exchange(A, x));
+        return launch_spmv(c, A, epi, alpha, x, beta, y, z, nred, w0, w1);
+    }
+    const long nall = num_chunks(A->nrows);
+    LSSP_TRY(launch_pack(c, A->d_send_idx, x, A->d_send_buf, A->nsend));
+    std::vector<Msg> s, r;
+    halo_msgs(A, x, s, r);
+    if (!host_mode(c)) {
+        LSSP_HIP(hipEventRecord(c->ev_pack, c->stream));
+        LSSP_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_pack, 0));
+        LSSP_TRY(xfer_group(c, s, r, c->comm_stream));
+        LSSP_HIP(hipEventRecord(c->ev_halo, c->comm_stream));
+        LSSP_TRY(launch_spmv(c, A, epi, alpha, x, beta, y, z, nred, w0, w1, A->ich0, A->ich1));
+        LSSP_HIP(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+    } else {
+        LSSP_TRY(launch_spmv(c, A, epi, alpha, x, beta, y, z, nred, w0, w1, A->ich0, A->ich1));
+        LSSP_TRY(xfer_group(c, s, r));
+    }
+    LSSP_TRY(launch_spmv(c, A, epi, alpha, x, beta, y, z, nred, w0, w1, 0, A->ich0));
+    return launch_spmv(c, A, epi, alpha, x, beta, y, z, nred, w0, w1, A->ich1, nall);
 }
 
 int comm_destroy(lssp_amd_ctx *c)
@@ -149,6 +190,11 @@ int comm_destroy(lssp_amd_ctx *c)
         (void)hipFree(c->d_carry);
         c->d_carry = nullptr;
     }
+    if (c->ev_pack) (void)hipEventDestroy(c->ev_pack);
+    if (c->ev_halo) (void)hipEventDestroy(c->ev_halo);
+    if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
+    c->ev_pack = c->ev_halo = nullptr;
+    c->comm_stream = nullptr;
     c->host = lssp_amd_host_transport{};
     c->nranks = 1;
     c->rank = 0;
@@ -187,6 +233,9 @@ int lssp_amd_comm_init(lssp_amd_ctx *c, int nranks, int rank, const void *idp)
     c->rank = rank;
     LSSP_HIP(hipMalloc(&c->d_gather, sizeof(double) * MAX_SLOTS * nranks));
     LSSP_HIP(hipMalloc(&c->d_carry, sizeof(double) * MAX_SLOTS));
+    LSSP_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+    LSSP_HIP(hipEventCreateWithFlags(&c->ev_pack, hipEventDisableTiming));
+    LSSP_HIP(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
     return LSSP_AMD_OK;
 }
 
@@ -293,6 +342,25 @@ int lssp_amd_mat_upload_dist(lssp_amd_ctx *c, int n_global, int row0, int nlocal
     M->nnz = nnz;
     M->n_global = n_global;
     M->row0 = row0;
+    {  // the longest run of chunks without a halo-reading row (spmv_halo)
+        const long nch = num_chunks(nlocal);
+        long run0 = 0, best0 = 0, best1 = 0;
+        for (long ch = 0; ch <= nch; ch++) {
+            bool halo_free = ch < nch;
+            for (long i = ch * 256; halo_free && i < std::min<long>((ch + 1) * 256, nlocal); i++)
+                for (int k = Ap[i]; k < Ap[i + 1]; k++)
+                    if (lj[k] >= nlocal) {
+                        halo_free = false;
+                        break;
+                    }
+            if (!halo_free) {
+                if (ch - run0 > best1 - best0) best0 = run0, best1 = ch;
+                run0 = ch + 1;
+            }
+        }
+        M->ich0 = best0;
+        M->ich1 = best1;
+    }
     // receive plan (per owner)
     std::vector<int> need(P, 0);
     for (int g : hcols) need[g / blk]++;

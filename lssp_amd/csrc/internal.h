@@ -84,6 +84,10 @@ struct lssp_amd_ctx {
     lssp_amd_host_transport host{};  // host-staged transport (comm == nullptr, nranks > 1)
     double *d_gather = nullptr;  // [nranks][MAX_SLOTS]
     double *d_carry = nullptr;   // [MAX_SLOTS] serial mode: running sums of the ranks before this one
+    // RCCL mode: the halo round runs on comm_stream while the interior rows'
+    // product runs on stream (ev_pack: send buffer packed; ev_halo: halo landed)
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t ev_pack = nullptr, ev_halo = nullptr;
     int tri_blocks_per_cu = 1;  // the sync-free sweep's grid (k_trisolve)
     // Krylov work vectors, kept across solves (no hipMalloc on the solve path)
     struct WsBuf {
@@ -113,6 +117,9 @@ struct lssp_amd_mat {
     int *d_send_idx = nullptr;
     double *d_send_buf = nullptr;
     int nsend = 0;
+    // the longest run of 256-row chunks [ich0, ich1) none of whose rows reads a
+    // halo column: their product does not wait for the halo round (spmv_halo)
+    long ich0 = 0, ich1 = 0;
 };
 
 namespace lssp_amd {
@@ -227,7 +234,7 @@ enum Epi { EPI_MXY = 0, EPI_AMXY, EPI_AXPBY, EPI_AMX };  // see spmv kernel
 int build_diag_ids(lssp_amd_mat *M, const int *Ap, const int *Aj);
 int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, const double *x,
                 double beta, const double *y, double *z, int nred, const double *w0,
-                const double *w1);
+                const double *w1, long cb = 0, long ce = -1);  // chunks [cb, ce); ce < 0: all
 // elementwise + optional partials; kinds in kernels.hip (EwKind)
 struct Ew {
     int kind = 0;
@@ -324,6 +331,9 @@ int comm_allgather_sums(lssp_amd_ctx *c, int nslot);
 int comm_carry_in(lssp_amd_ctx *c);
 int comm_carry_out(lssp_amd_ctx *c);
 int halo_exchange(const lssp_amd_mat *A, double *x);
+// halo round + product, the halo-free chunks overlapped with the round
+int spmv_halo(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, double *x, double beta,
+              const double *y, double *z, int nred, const double *w0, const double *w1);
 int comm_destroy(lssp_amd_ctx *c);
 
 }  // namespace lssp_amd

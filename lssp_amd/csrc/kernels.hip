@@ -277,8 +277,9 @@ __global__ void k_finalize(const double *sums, double *scal, double *trace, Fin 
 // multi-rank: gathered [P][MAX_SLOTS] rank sums, summed in rank order (tree
 // mode), or the last rank's running sums, which are the global sums (serial)
 __global__ void k_sum_ranks(const double *gath, int P, int nslot, double *sums, double *scal,
-                            double *trace, Fin f, int serial)
+                            double *trace, Fin f, int serial, const double *guard)
 {
+    if (guard && *guard != 0.0) return;
     double r[MAX_SLOTS] = {0, 0, 0, 0};
     for (int s = 0; s < nslot; s++) {
         double t = serial ? gath[(P - 1) * MAX_SLOTS + s] : gath[s];
@@ -310,6 +311,7 @@ struct SpmvArgs {
     const int *off;
     int ndiag;
     const double *guard;  // lssp_amd_ctx::guard
+    long blk0;            // first chunk of this launch (spmv_halo splits a product)
 };
 
 // The 256-row blocks are dealt so that each of the 8 XCDs owns one contiguous
@@ -334,8 +336,9 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
     __shared__ double lds[MAX_SLOTS][4];
     if (a.guard && *a.guard != 0.0) return;
     const long per = gridDim.x / 8;
-    const long blk = (blockIdx.x % 8) * per + blockIdx.x / 8;
-    if (blk >= nblk) return;
+    const long lb = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    if (lb >= nblk) return;
+    const long blk = a.blk0 + lb;
     const int r0 = (int)(blk * 256);
     const int tid = threadIdx.x;
     const int r = r0 + tid;
@@ -444,13 +447,17 @@ static void spmv_dispatch(const SpmvArgs &a, int nred, long nblocks, hipStream_t
 
 int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, const double *x,
                 double beta, const double *y, double *z, int nred, const double *w0,
-                const double *w1)
+                const double *w1, long cb, long ce)
 {
     if (A->nrows == 0) return LSSP_AMD_OK;
-    long nb = num_chunks(A->nrows);
-    LSSP_TRY(ensure_part(c, nb));
+    const long nall = num_chunks(A->nrows);
+    LSSP_TRY(ensure_part(c, nall));
+    if (ce < 0) ce = nall;
+    if (cb < 0 || cb > ce || ce > nall) return LSSP_AMD_EINVAL;
+    const long nb = ce - cb;
+    if (nb == 0) return LSSP_AMD_OK;
     SpmvArgs a{A->nrows, A->Ap, A->Aj, A->Ax, x, y, z, alpha, beta, w0, w1, c->d_part, c->part_cap,
-               A->Ad, A->d_off, A->ndiag, c->guard};
+               A->Ad, A->d_off, A->ndiag, c->guard, cb};
     switch (epi) {
     case EPI_MXY: spmv_dispatch<EPI_MXY>(a, nred, nb, c->stream, A->nnz + 4L); break;
     case EPI_AMXY: spmv_dispatch<EPI_AMXY>(a, nred, nb, c->stream, A->nnz + 4L); break;
@@ -675,7 +682,7 @@ int launch_finalize(lssp_amd_ctx *c, const double *sums, int nslot, const Fin &f
 int launch_sum_ranks(lssp_amd_ctx *c, int nslot, const Fin &f)
 {
     k_sum_ranks<<<1, 1, 0, c->stream>>>(c->d_gather, c->nranks, nslot, c->d_sums, c->d_scal,
-                                         c->d_trace, f, c->reduce_mode == LSSP_AMD_REDUCE_SERIAL);
+                                         c->d_trace, f, c->reduce_mode == LSSP_AMD_REDUCE_SERIAL, c->guard);
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;
 }

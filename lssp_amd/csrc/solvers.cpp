@@ -115,8 +115,7 @@ struct Run {
     int spmv(int epi, double alpha, double *x, double beta, const double *y, double *z, int nred = 0,
              const double *w0 = nullptr, const double *w1 = nullptr)
     {
-        LSSP_TRY(halo_exchange(A, x));
-        return launch_spmv(c, A, epi, alpha, x, beta, y, z, tree ? nred : 0, w0, w1);
+        return spmv_halo(c, A, epi, alpha, x, beta, y, z, tree ? nred : 0, w0, w1);
     }
     int ew(Ew e)
     {
@@ -268,12 +267,12 @@ int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
             lprint("bicgstab: itr: %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", k, rk,
                    (err_rel == 0 ? 0 : rk / err_rel), (b_norm == 0 ? 0 : rk / b_norm));
     };
-    const bool batched = R.c->nranks == 1 && (!R.M || R.M->line.ntiles > 0);
+    const bool batched = !R.M || R.M->line.ntiles > 0;
     if (batched && rho1 == 0) {  // :89-92 at the first iteration
         if (R.rank == 0) lprint("bicgstab: method failed.!\n");
         it = 0;
     } else if (batched) {
-        // One rank, line-swept or no preconditioner: iterations are queued in
+        // Line-swept or no preconditioner: iterations are queued in
         // batches and the stop tests run on the device (FIN_BICG_RES_RHO_B:
         // breakdown :117, res <= tol :149, rho1 == 0 :89 of the next); the
         // launches past the stop return at once (ctx guard), and the host reads a
@@ -393,8 +392,8 @@ int cg(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *
     if (tol < tol_rb) tol = tol_rb;
     bool pending_rho = false;
 
-    if (!R.M && R.c->nranks == 1) {
-        // PC_NON on one rank: iterations are queued in batches and the stop
+    if (!R.M) {
+        // PC_NON: iterations are queued in batches and the stop
         // test :109 runs on the device (FIN_CG_RES_RHO_B); the launches of the
         // iterations after the one that converged return at once (ctx guard),
         // and the host reads a batch's residuals with ONE round trip instead of
