@@ -89,8 +89,11 @@ int lssp_amd_mat_info(const lssp_amd_mat *A, int *nrows, int *ncols, int *nnz);
 /* Device layout of the SpMV's column stream: *ndiag > 0 when every entry's
  * offset col - row is one of ndiag (<= 255) distinct values (stencil
  * matrices); the SpMV then reads a 1-byte offset id per entry instead of the
- * 4-byte column (same entries, same summation order).  0: plain CSR columns. */
-int lssp_amd_mat_layout(const lssp_amd_mat *A, int *ndiag);
+ * 4-byte column (same entries, same summation order).  0: plain CSR columns.
+ * *windowed (may be NULL) = 1 when the columns of every 1024-row block span
+ * at most 16384 entries and the product stages that span of x in LDS instead
+ * of gathering it from memory (locally numbered meshes); 0 otherwise. */
+int lssp_amd_mat_layout(const lssp_amd_mat *A, int *ndiag, int *windowed);
 
 /* ---- SpMV: mvops.h:9-19 (mvops.cxx:5-150), bitwise per row --------------
  * x: for a matrix from lssp_amd_mat_upload the first ncols entries are read.

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cstdarg>
 #include <atomic>
 #include <cstring>
@@ -210,6 +211,37 @@ int build_diag_ids(lssp_amd_mat *M, const int *Ap, const int *Aj)
     return LSSP_AMD_OK;
 }
 
+// The x spans of the 1024-row blocks of k_spmv_win (kernels.hip), for matrices
+// the diagonal-id coding does not cover (more than 255 offsets) whose rows
+// nevertheless stay near the diagonal (locally renumbered meshes: config 5).
+int build_windows(lssp_amd_mat *M, const int *Ap, const int *Aj)
+{
+    static const bool off = getenv("LSSP_AMD_SPMV_WIN") && atoi(getenv("LSSP_AMD_SPMV_WIN")) == 0;
+    const int n = M->nrows;
+    if (off || M->ndiag > 0 || M->nnz == 0 || n == 0) return LSSP_AMD_OK;
+    const long nb = (n + WIN_ROWS - 1) / WIN_ROWS;
+    std::vector<int> win(2 * nb);
+    std::atomic<bool> wide{false};
+    parallel_for(nb, [&](long b0, long b1) {
+        for (long b = b0; b < b1 && !wide.load(std::memory_order_relaxed); b++) {
+            int lo = INT_MAX, hi = INT_MIN;
+            const int r1 = (int)std::min<long>((b + 1) * WIN_ROWS, n);
+            for (int k = Ap[b * WIN_ROWS]; k < Ap[r1]; k++) {
+                lo = std::min(lo, Aj[k]);
+                hi = std::max(hi, Aj[k] + 1);
+            }
+            if (lo > hi) lo = hi = 0;  // a block of empty rows
+            if ((long)hi - lo > WIN_CAP) wide = true;
+            win[2 * b] = lo;
+            win[2 * b + 1] = hi;
+        }
+    }, 16);
+    if (wide) return LSSP_AMD_OK;
+    LSSP_HIP(hipMalloc(&M->d_win, sizeof(int) * win.size()));
+    LSSP_HIP(hipMemcpy(M->d_win, win.data(), sizeof(int) * win.size(), hipMemcpyHostToDevice));
+    return LSSP_AMD_OK;
+}
+
 double wall_time()
 {
     return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
@@ -358,7 +390,8 @@ static int upload_csr(lssp_amd_mat *M, const int *Ap, const int *Aj, const doubl
         LSSP_HIP(hipMemcpy(M->Aj, Aj, sizeof(int) * M->nnz, hipMemcpyHostToDevice));
         LSSP_HIP(hipMemcpy(M->Ax, Ax, sizeof(double) * M->nnz, hipMemcpyHostToDevice));
     }
-    return build_diag_ids(M, Ap, Aj);
+    LSSP_TRY(build_diag_ids(M, Ap, Aj));
+    return build_windows(M, Ap, Aj);
 }
 
 int lssp_amd_mat_upload(lssp_amd_ctx *c, int nrows, int ncols, int nnz, const int *Ap, const int *Aj,
@@ -391,6 +424,7 @@ int lssp_amd_mat_destroy(lssp_amd_mat *M)
     if (M->Ax) (void)hipFree(M->Ax);
     if (M->Ad) (void)hipFree(M->Ad);
     if (M->d_off) (void)hipFree(M->d_off);
+    if (M->d_win) (void)hipFree(M->d_win);
     if (M->d_send_idx) (void)hipFree(M->d_send_idx);
     if (M->d_send_buf) (void)hipFree(M->d_send_buf);
     delete M;
@@ -406,10 +440,11 @@ int lssp_amd_mat_info(const lssp_amd_mat *A, int *nrows, int *ncols, int *nnz)
     return LSSP_AMD_OK;
 }
 
-int lssp_amd_mat_layout(const lssp_amd_mat *A, int *ndiag)
+int lssp_amd_mat_layout(const lssp_amd_mat *A, int *ndiag, int *windowed)
 {
     if (!A || !ndiag) return LSSP_AMD_EINVAL;
     *ndiag = A->ndiag;
+    if (windowed) *windowed = A->d_win != nullptr;
     return LSSP_AMD_OK;
 }
 

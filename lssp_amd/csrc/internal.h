@@ -109,6 +109,10 @@ struct lssp_amd_mat {
     uint8_t *Ad = nullptr;
     int *d_off = nullptr;
     int ndiag = 0;
+    // windowed x (k_spmv_win): when every 1024-row block's columns fall in a
+    // span of at most WIN_CAP entries, d_win[2b], d_win[2b+1] = that span
+    // [lo, hi) and the product stages x[lo, hi) in LDS; nullptr: not windowed
+    int *d_win = nullptr;
     // distributed layout
     int n_global = 0, row0 = 0, nhalo = 0;
     // halo exchange plan: for each peer, indices (local) to send and the count to receive
@@ -232,6 +236,8 @@ namespace lssp_amd {
 // ---- kernel launchers (kernels.hip) ------------------------------------------
 enum Epi { EPI_MXY = 0, EPI_AMXY, EPI_AXPBY, EPI_AMX };  // see spmv kernel
 int build_diag_ids(lssp_amd_mat *M, const int *Ap, const int *Aj);
+int build_windows(lssp_amd_mat *M, const int *Ap, const int *Aj);
+constexpr int WIN_ROWS = 1024, WIN_CAP = 16384;
 int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, const double *x,
                 double beta, const double *y, double *z, int nred, const double *w0,
                 const double *w1, long cb = 0, long ce = -1);  // chunks [cb, ce); ce < 0: all

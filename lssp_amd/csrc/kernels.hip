@@ -429,6 +429,121 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
     }
 }
 
+// Windowed-x product for matrices without the diagonal-id coding whose rows
+// stay near the diagonal (build_windows, capi.cpp): a 1024-row workgroup (4
+// reduction chunks) first stages its x span [lo, hi) (<= WIN_CAP entries)
+// into LDS with coalesced loads, then each lane forms its row's products from
+// LDS.  The gathers of a locally shuffled numbering (config 5) each hit a
+// separate L2 line when read from memory; from LDS they cost a bank access.
+// Same per-row arithmetic as k_spmv3 (products in CSR order onto 0.0), same
+// 256-row chunk partials.  Rows' Aj / Ax are read straight from memory, issued
+// with the x span before the one barrier: staging them through LDS as well
+// (coalesced 16-byte loads, a second LDS phase) measured slower, 37 -> 47 us
+// on config 5 -- with 128 KB of LDS one workgroup holds a CU, and every extra
+// barrier phase is exposed latency.
+#ifndef WIN_DIAG
+#define WIN_DIAG 0  // timing experiments only: 1 = no x staging, 2 = no matrix loads
+#endif
+template <int EPI, int NRED>
+__global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *win, long nblk)
+{
+    __shared__ double sxw[WIN_CAP];
+    __shared__ double lds[4][MAX_SLOTS][4];
+    if (a.guard && *a.guard != 0.0) return;
+    const long per = gridDim.x / 8;
+    const long blk = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    if (blk >= nblk) return;
+    const int tid = threadIdx.x;
+    const int r = (int)(blk * WIN_ROWS) + tid;
+    const int lo = win[2 * blk], span = win[2 * blk + 1] - lo;
+    // x span, row bounds, the row's first 8 entries and the dot operands, all in flight at once
+    constexpr int NS = WIN_CAP / WIN_ROWS;
+    double xs[NS];
+#pragma unroll
+    for (int u = 0; u < NS; u++)
+        xs[u] = WIN_DIAG != 1 && tid + WIN_ROWS * u < span ? a.x[lo + tid + WIN_ROWS * u] : 0.0;
+    const int rr = min(r, a.nrows - 1);
+    const int rb = a.Ap[rr], re = a.Ap[rr + 1];
+    const int len = r < a.nrows ? re - rb : 0;
+    int cj[8];
+    double cx[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        cj[u] = lo;
+        cx[u] = 0.0;
+        if (WIN_DIAG == 2) {
+            cj[u] = lo + ((tid * 7 + u * 131) & 8191);
+            cx[u] = 1.0;
+        } else if (u < len) {
+            cj[u] = a.Aj[rb + u];
+            cx[u] = a.Ax[rb + u];
+        }
+    }
+    double w0p = 0.0, w1p = 0.0;
+    if (NRED > 0) {
+        if (a.w0 != a.z) w0p = a.w0[rr];
+        if (NRED > 1 && a.w1 && a.w1 != a.z) w1p = a.w1[rr];
+    }
+#pragma unroll
+    for (int u = 0; u < NS; u++)
+        if (tid + WIN_ROWS * u < span) sxw[tid + WIN_ROWS * u] = xs[u];
+    __syncthreads();
+    double sum = 0;
+    if (len <= 8) {
+        double pr[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) pr[u] = sxw[cj[u] - lo] * cx[u];
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (u < len) sum += pr[u];
+    } else {
+        for (int k = rb; k < re; k++) sum += sxw[a.Aj[k] - lo] * a.Ax[k];
+    }
+    double zv = 0;
+    if (r < a.nrows) {
+        if (EPI == EPI_MXY) zv = sum;
+        else if (EPI == EPI_AMXY) zv = sum * a.alpha;
+        else if (EPI == EPI_AXPBY) zv = a.y[r] * a.beta + a.alpha * sum;
+        else zv = a.alpha * sum;
+        a.z[r] = zv;
+    }
+    if (NRED > 0) {
+        double v[NRED > 0 ? NRED : 1];
+        if (r < a.nrows) {
+            v[0] = zv * (a.w0 == a.z ? zv : w0p);
+            if (NRED > 1) v[NRED > 1 ? 1 : 0] = zv * (a.w1 && a.w1 != a.z ? w1p : zv);
+        } else {
+#pragma unroll
+            for (int q = 0; q < NRED; q++) v[q] = 0.0;
+        }
+        // chunk_reduce's order for each of the 4 chunks (waves 4q .. 4q+3)
+        const int lane = tid & 63, wave = tid >> 6, q = wave >> 2;
+#pragma unroll
+        for (int t = 0; t < NRED; t++) {
+            const double s = wave_sum(v[t]);
+            if (lane == 0) lds[q][t][wave & 3] = s;
+        }
+        __syncthreads();
+        const long chunk = blk * 4 + (tid >> 8);
+        if ((tid & 255) == 0 && chunk * 256 < a.nrows) {
+            const int cq = tid >> 8;
+#pragma unroll
+            for (int t = 0; t < NRED; t++)
+                a.part[t * a.pcap + chunk] = (lds[cq][t][0] + lds[cq][t][1]) + (lds[cq][t][2] + lds[cq][t][3]);
+        }
+    }
+}
+
+template <int EPI>
+static void spmv_win_dispatch(const SpmvArgs &a, const int *win, int nred, hipStream_t s)
+{
+    const long nb = (a.nrows + WIN_ROWS - 1) / WIN_ROWS;
+    const long g = (nb + 7) / 8 * 8;
+    if (nred == 0) k_spmv_win<EPI, 0><<<g, WIN_ROWS, 0, s>>>(a, win, nb);
+    else if (nred == 1) k_spmv_win<EPI, 1><<<g, WIN_ROWS, 0, s>>>(a, win, nb);
+    else k_spmv_win<EPI, 2><<<g, WIN_ROWS, 0, s>>>(a, win, nb);
+}
+
 template <int EPI, bool CMP>
 static void spmv_dispatch(const SpmvArgs &a, int nred, long nblocks, hipStream_t s, long nnz_pad)
 {
@@ -458,6 +573,16 @@ int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, c
     if (nb == 0) return LSSP_AMD_OK;
     SpmvArgs a{A->nrows, A->Ap, A->Aj, A->Ax, x, y, z, alpha, beta, w0, w1, c->d_part, c->part_cap,
                A->Ad, A->d_off, A->ndiag, c->guard, cb};
+    if (A->d_win && nb == nall) {
+        switch (epi) {
+        case EPI_MXY: spmv_win_dispatch<EPI_MXY>(a, A->d_win, nred, c->stream); break;
+        case EPI_AMXY: spmv_win_dispatch<EPI_AMXY>(a, A->d_win, nred, c->stream); break;
+        case EPI_AXPBY: spmv_win_dispatch<EPI_AXPBY>(a, A->d_win, nred, c->stream); break;
+        default: spmv_win_dispatch<EPI_AMX>(a, A->d_win, nred, c->stream); break;
+        }
+        LSSP_HIP(hipGetLastError());
+        return LSSP_AMD_OK;
+    }
     switch (epi) {
     case EPI_MXY: spmv_dispatch<EPI_MXY>(a, nred, nb, c->stream, A->nnz + 4L); break;
     case EPI_AMXY: spmv_dispatch<EPI_AMXY>(a, nred, nb, c->stream, A->nnz + 4L); break;

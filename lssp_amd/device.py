@@ -216,9 +216,16 @@ class DMat:
     @property
     def ndiag(self) -> int:
         """> 0: the SpMV reads 1-byte diagonal ids (that many offsets) instead of columns"""
-        v = ctypes.c_int()
-        _ck(self.dev.L.lssp_amd_mat_layout(self.h, ctypes.byref(v)), "mat_layout")
+        v, w = ctypes.c_int(), ctypes.c_int()
+        _ck(self.dev.L.lssp_amd_mat_layout(self.h, ctypes.byref(v), ctypes.byref(w)), "mat_layout")
         return v.value
+
+    @property
+    def windowed(self) -> bool:
+        """the SpMV stages each 1024-row block's x span in LDS (k_spmv_win)"""
+        v, w = ctypes.c_int(), ctypes.c_int()
+        _ck(self.dev.L.lssp_amd_mat_layout(self.h, ctypes.byref(v), ctypes.byref(w)), "mat_layout")
+        return bool(w.value)
 
     def close(self):
         if self.h:

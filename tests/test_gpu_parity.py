@@ -228,19 +228,30 @@ def _scattered(n, seed, maxlen=20, reach=3000):
     return O.CSR(n, Ap.astype(np.int32), Aj.astype(np.int32), Ax)
 
 
-@pytest.mark.parametrize("which", ["thermal", "scattered"])
+@pytest.mark.parametrize("which", ["thermal", "thermal-big", "scattered", "wide"])
 def test_spmv_scattered_bitwise_vs_oracle(dev, which):
-    """k_spmv3 gives the oracle's sums bit for bit (mvops.cxx:42-78, 118-150) on
-    scattered-column matrices (the thermal-like matrix of config 5, random
-    rows of up to 11 entries)."""
+    """The uncoded products give the oracle's sums bit for bit (mvops.cxx:42-78,
+    118-150) on scattered-column matrices: the thermal-like matrix of config 5
+    and random rows of 0..20 entries within +-3000 of the diagonal take the
+    windowed-x kernel (k_spmv_win); columns over the whole range ("wide") and
+    the window switched off (LSSP_AMD_SPMV_WIN=0 is read once per process, so
+    a 1024-row block spanning > 16384 columns stands in for it) take the
+    gathering k_spmv3."""
     import lssp_amd
     from lssp_amd.synthetic import thermal_like
     if which == "thermal":
         Ap, Aj, Ax = thermal_like(m=150, window=512)
         A = O.CSR(Ap.size - 1, Ap, Aj, Ax)
+    elif which == "thermal-big":
+        Ap, Aj, Ax = thermal_like(m=330, window=4096)  # 108,900 rows: 107 windowed blocks
+        A = O.CSR(Ap.size - 1, Ap, Aj, Ax)
+    elif which == "wide":
+        A = _scattered(40000, 12, maxlen=12, reach=40000)
     else:
         A = _scattered(5000, 11)
     M = lssp_amd.DMat(dev, A.Ap, A.Aj, A.Ax)
+    assert M.ndiag == 0
+    assert M.windowed == (which != "wide")
     xh, yh = uniform(0x5EED, A.n), uniform(3, A.n)
     x, y, z = dev.vec(A.n, xh), dev.vec(A.n, yh), dev.vec(A.n, yh)
     M.mv_mxy(x, z)
@@ -252,13 +263,13 @@ def test_spmv_scattered_bitwise_vs_oracle(dev, which):
     M.mv_amxpby(1.5, x, 0.25, y)
     assert np.array_equal(y.download(), O.spmv(2, A, xh, alpha=1.5, beta=0.25, z=yh.copy()))
     # CG (fused q.p in the SpMV epilogue) in tree mode vs the oracle
-    if which == "thermal":
+    if which in ("thermal", "thermal-big", "wide"):
         b = dev.vec(A.n, np.ones(A.n))
         xs = dev.vec(A.n, np.zeros(A.n))
         r = lssp_amd.solve(dev, M, None, xs, b, solver=lssp_amd.CG, maxit=60, trace_cap=100000)
         o = O.solve(lssp_amd.CG, A, np.ones(A.n), maxit=60, mode=O.TREE)
-        assert r.nits == o.nits and np.array_equal(r.trace, o.trace)
-        assert np.array_equal(xs.download(), o.x)
+        assert r.nits == o.nits and np.array_equal(r.trace, o.trace, equal_nan=True)
+        assert np.array_equal(xs.download(), o.x, equal_nan=True)
 
 
 def test_spmv_column_coding_chosen_by_structure(dev):
