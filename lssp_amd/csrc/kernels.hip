@@ -436,16 +436,21 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
 // LDS.  The gathers of a locally shuffled numbering (config 5) each hit a
 // separate L2 line when read from memory; from LDS they cost a bank access.
 // Same per-row arithmetic as k_spmv3 (products in CSR order onto 0.0), same
-// 256-row chunk partials.  Rows' Aj / Ax are read straight from memory, issued
-// with the x span before the one barrier: staging them through LDS as well
+// 256-row chunk partials.  Rows' Aj / Ax are read straight from memory as
+// 16-byte vectors (5 + 3 per lane, shifted into place by the row's alignment:
+// 35.8 -> 33.5 us on config 5 against 8 + 8 scalar loads), issued with the x
+// span before the one barrier: staging them through LDS as well
 // (coalesced 16-byte loads, a second LDS phase) measured slower, 37 -> 47 us
 // on config 5 -- with 128 KB of LDS one workgroup holds a CU, and every extra
 // barrier phase is exposed latency.
 #ifndef WIN_DIAG
 #define WIN_DIAG 0  // timing experiments only: 1 = no x staging, 2 = no matrix loads
 #endif
+#ifndef WIN_VEC
+#define WIN_VEC 1
+#endif
 template <int EPI, int NRED>
-__global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *win, long nblk)
+__global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *win, long nblk, long nnz_pad)
 {
     __shared__ double sxw[WIN_CAP];
     __shared__ double lds[4][MAX_SLOTS][4];
@@ -467,6 +472,52 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *wi
     const int len = r < a.nrows ? re - rb : 0;
     int cj[8];
     double cx[8];
+#if WIN_VEC
+    {
+        // the row's first 8 entries as 16-byte vectors (5 for Ax, 3 for Aj,
+        // clamped to the padded arrays), then shifted by the row's alignment
+        typedef double dbl2_t __attribute__((ext_vector_type(2)));
+        typedef int int4_t __attribute__((ext_vector_type(4)));
+        const dbl2_t *X2 = reinterpret_cast<const dbl2_t *>(a.Ax);
+        const int4_t *J4 = reinterpret_cast<const int4_t *>(a.Aj);
+        const long x0 = rb >> 1, j0 = rb >> 2;
+        dbl2_t vx[5];
+        int4_t vj[3];
+#pragma unroll
+        for (int u = 0; u < 5; u++) vx[u] = X2[min(x0 + u, (nnz_pad >> 1) - 1)];
+#pragma unroll
+        for (int u = 0; u < 3; u++) vj[u] = J4[min(j0 + u, (nnz_pad >> 2) - 1)];
+        double ex[10];
+        int ej[12];
+#pragma unroll
+        for (int u = 0; u < 5; u++) {
+            ex[2 * u] = vx[u].x;
+            ex[2 * u + 1] = vx[u].y;
+        }
+#pragma unroll
+        for (int u = 0; u < 3; u++) {
+            ej[4 * u] = vj[u].x;
+            ej[4 * u + 1] = vj[u].y;
+            ej[4 * u + 2] = vj[u].z;
+            ej[4 * u + 3] = vj[u].w;
+        }
+        // shifts as bit blends between fixed registers: a select the compiler
+        // may fold into an indexed read of the array, which would spill it
+        const int m1 = -(rb & 1), m2 = -((rb >> 1) & 1);
+        const uint64_t q1 = (uint64_t)(int64_t)m1;
+        int tj[10];
+#pragma unroll
+        for (int u = 0; u < 10; u++) tj[u] = ej[u] ^ ((ej[u] ^ ej[u + 2]) & m2);
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint64_t b0 = __builtin_bit_cast(uint64_t, ex[u]), b1 = __builtin_bit_cast(uint64_t, ex[u + 1]);
+            const double xv = __builtin_bit_cast(double, b0 ^ ((b0 ^ b1) & q1));
+            const int jv = tj[u] ^ ((tj[u] ^ tj[u + 1]) & m1);
+            cj[u] = u < len ? jv : lo;
+            cx[u] = u < len ? xv : 0.0;
+        }
+    }
+#else
 #pragma unroll
     for (int u = 0; u < 8; u++) {
         cj[u] = lo;
@@ -479,6 +530,7 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *wi
             cx[u] = a.Ax[rb + u];
         }
     }
+#endif
     double w0p = 0.0, w1p = 0.0;
     if (NRED > 0) {
         if (a.w0 != a.z) w0p = a.w0[rr];
@@ -535,13 +587,13 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *wi
 }
 
 template <int EPI>
-static void spmv_win_dispatch(const SpmvArgs &a, const int *win, int nred, hipStream_t s)
+static void spmv_win_dispatch(const SpmvArgs &a, const int *win, int nred, hipStream_t s, long nnz_pad)
 {
     const long nb = (a.nrows + WIN_ROWS - 1) / WIN_ROWS;
     const long g = (nb + 7) / 8 * 8;
-    if (nred == 0) k_spmv_win<EPI, 0><<<g, WIN_ROWS, 0, s>>>(a, win, nb);
-    else if (nred == 1) k_spmv_win<EPI, 1><<<g, WIN_ROWS, 0, s>>>(a, win, nb);
-    else k_spmv_win<EPI, 2><<<g, WIN_ROWS, 0, s>>>(a, win, nb);
+    if (nred == 0) k_spmv_win<EPI, 0><<<g, WIN_ROWS, 0, s>>>(a, win, nb, nnz_pad);
+    else if (nred == 1) k_spmv_win<EPI, 1><<<g, WIN_ROWS, 0, s>>>(a, win, nb, nnz_pad);
+    else k_spmv_win<EPI, 2><<<g, WIN_ROWS, 0, s>>>(a, win, nb, nnz_pad);
 }
 
 template <int EPI, bool CMP>
@@ -575,10 +627,10 @@ int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, c
                A->Ad, A->d_off, A->ndiag, c->guard, cb};
     if (A->d_win && nb == nall) {
         switch (epi) {
-        case EPI_MXY: spmv_win_dispatch<EPI_MXY>(a, A->d_win, nred, c->stream); break;
-        case EPI_AMXY: spmv_win_dispatch<EPI_AMXY>(a, A->d_win, nred, c->stream); break;
-        case EPI_AXPBY: spmv_win_dispatch<EPI_AXPBY>(a, A->d_win, nred, c->stream); break;
-        default: spmv_win_dispatch<EPI_AMX>(a, A->d_win, nred, c->stream); break;
+        case EPI_MXY: spmv_win_dispatch<EPI_MXY>(a, A->d_win, nred, c->stream, A->nnz + 4L); break;
+        case EPI_AMXY: spmv_win_dispatch<EPI_AMXY>(a, A->d_win, nred, c->stream, A->nnz + 4L); break;
+        case EPI_AXPBY: spmv_win_dispatch<EPI_AXPBY>(a, A->d_win, nred, c->stream, A->nnz + 4L); break;
+        default: spmv_win_dispatch<EPI_AMX>(a, A->d_win, nred, c->stream, A->nnz + 4L); break;
         }
         LSSP_HIP(hipGetLastError());
         return LSSP_AMD_OK;
