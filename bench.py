@@ -119,8 +119,8 @@ def cpu_baseline(N: int, iters: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--grid", type=int, default=216)
     ap.add_argument("--spmv-reps", type=int, default=50)
     ap.add_argument("--apply-reps", type=int, default=10)
