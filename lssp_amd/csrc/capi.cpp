@@ -231,7 +231,7 @@ int build_windows(lssp_amd_mat *M, const int *Ap, const int *Aj)
                 hi = std::max(hi, Aj[k] + 1);
             }
             if (lo > hi) lo = hi = 0;  // a block of empty rows
-            if ((long)hi - lo > WIN_CAP) wide = true;
+            if ((long)hi - (lo & ~1) > WIN_CAP) wide = true;  // staged from lo rounded down to even
             win[2 * b] = lo;
             win[2 * b + 1] = hi;
         }

@@ -439,7 +439,7 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
 // 256-row chunk partials.  Rows' Aj / Ax are read straight from memory as
 // 16-byte vectors (5 + 3 per lane, shifted into place by the row's alignment:
 // 35.8 -> 33.5 us on config 5 against 8 + 8 scalar loads), issued with the x
-// span before the one barrier: staging them through LDS as well
+// span (16-byte vectors too: 32.4 -> 31.1 us) before the one barrier: staging them through LDS as well
 // (coalesced 16-byte loads, a second LDS phase) measured slower, 37 -> 47 us
 // on config 5 -- with 128 KB of LDS one workgroup holds a CU, and every extra
 // barrier phase is exposed latency.
@@ -449,10 +449,13 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
 #ifndef WIN_VEC
 #define WIN_VEC 1
 #endif
+#ifndef WIN_XVEC
+#define WIN_XVEC 1
+#endif
 template <int EPI, int NRED>
 __global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *win, long nblk, long nnz_pad)
 {
-    __shared__ double sxw[WIN_CAP];
+    __shared__ __attribute__((aligned(16))) double sxw[WIN_CAP];
     __shared__ double lds[4][MAX_SLOTS][4];
     if (a.guard && *a.guard != 0.0) return;
     const long per = gridDim.x / 8;
@@ -463,10 +466,21 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *wi
     const int lo = win[2 * blk], span = win[2 * blk + 1] - lo;
     // x span, row bounds, the row's first 8 entries and the dot operands, all in flight at once
     constexpr int NS = WIN_CAP / WIN_ROWS;
-    double xs[NS];
+    // staged from lo2 = lo rounded down to even, as 16-byte vectors when x is
+    // 16-byte aligned (uniform); the last odd entry alone (nothing past hi is read)
+    typedef double dbl2w_t __attribute__((ext_vector_type(2)));
+    const int hi = lo + span, lo2 = lo & ~1;
+    const bool xv16 = WIN_XVEC && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0);
+    dbl2w_t xs[NS / 2];
 #pragma unroll
-    for (int u = 0; u < NS; u++)
-        xs[u] = WIN_DIAG != 1 && tid + WIN_ROWS * u < span ? a.x[lo + tid + WIN_ROWS * u] : 0.0;
+    for (int u = 0; u < NS / 2; u++) {
+        const int e = lo2 + 2 * (tid + WIN_ROWS * u);
+        xs[u] = dbl2w_t{0.0, 0.0};
+        if (WIN_DIAG != 1 && e < hi) {
+            if (xv16 && e + 1 < hi) xs[u] = *reinterpret_cast<const dbl2w_t *>(a.x + e);
+            else xs[u] = dbl2w_t{e >= lo ? a.x[e] : 0.0, e + 1 < hi ? a.x[e + 1] : 0.0};
+        }
+    }
     const int rr = min(r, a.nrows - 1);
     const int rb = a.Ap[rr], re = a.Ap[rr + 1];
     const int len = r < a.nrows ? re - rb : 0;
@@ -537,19 +551,19 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *wi
         if (NRED > 1 && a.w1 && a.w1 != a.z) w1p = a.w1[rr];
     }
 #pragma unroll
-    for (int u = 0; u < NS; u++)
-        if (tid + WIN_ROWS * u < span) sxw[tid + WIN_ROWS * u] = xs[u];
+    for (int u = 0; u < NS / 2; u++)
+        if (lo2 + 2 * (tid + WIN_ROWS * u) < hi) reinterpret_cast<dbl2w_t *>(sxw)[tid + WIN_ROWS * u] = xs[u];
     __syncthreads();
     double sum = 0;
     if (len <= 8) {
         double pr[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) pr[u] = sxw[cj[u] - lo] * cx[u];
+        for (int u = 0; u < 8; u++) pr[u] = sxw[cj[u] - lo2] * cx[u];
 #pragma unroll
         for (int u = 0; u < 8; u++)
             if (u < len) sum += pr[u];
     } else {
-        for (int k = rb; k < re; k++) sum += sxw[a.Aj[k] - lo] * a.Ax[k];
+        for (int k = rb; k < re; k++) sum += sxw[a.Aj[k] - lo2] * a.Ax[k];
     }
     double zv = 0;
     if (r < a.nrows) {
