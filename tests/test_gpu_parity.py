@@ -256,6 +256,12 @@ def test_spmv_scattered_bitwise_vs_oracle(dev, which):
     x, y, z = dev.vec(A.n, xh), dev.vec(A.n, yh), dev.vec(A.n, yh)
     M.mv_mxy(x, z)
     assert np.array_equal(z.download(), O.spmv(0, A, xh))
+    # an x that is not 16-byte aligned (a C caller's x + 1): the windowed
+    # kernel stages it with scalar loads instead
+    xo = dev.vec(A.n + 1, np.concatenate([[np.nan], xh]))
+    import ctypes
+    assert dev.L.lssp_amd_mv_mxy(dev.h, M.h, ctypes.c_void_p(xo.ptr.value + 8), z.ptr) == 0
+    assert np.array_equal(z.download(), O.spmv(0, A, xh))
     M.mv_amxy(-0.75, x, z)
     assert np.array_equal(z.download(), O.spmv(1, A, xh, alpha=-0.75))
     M.mv_amxpbyz(-1.0, x, 1.0, y, z)
