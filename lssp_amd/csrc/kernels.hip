@@ -436,22 +436,14 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
 // LDS.  The gathers of a locally shuffled numbering (config 5) each hit a
 // separate L2 line when read from memory; from LDS they cost a bank access.
 // Same per-row arithmetic as k_spmv3 (products in CSR order onto 0.0), same
-// 256-row chunk partials.  Rows' Aj / Ax are read straight from memory as
-// 16-byte vectors (5 + 3 per lane, shifted into place by the row's alignment:
-// 35.8 -> 33.5 us on config 5 against 8 + 8 scalar loads), issued with the x
-// span (16-byte vectors too: 32.4 -> 31.1 us) before the one barrier: staging them through LDS as well
-// (coalesced 16-byte loads, a second LDS phase) measured slower, 37 -> 47 us
-// on config 5 -- with 128 KB of LDS one workgroup holds a CU, and every extra
-// barrier phase is exposed latency.
-#ifndef WIN_DIAG
-#define WIN_DIAG 0  // timing experiments only: 1 = no x staging, 2 = no matrix loads
-#endif
-#ifndef WIN_VEC
-#define WIN_VEC 1
-#endif
-#ifndef WIN_XVEC
-#define WIN_XVEC 1
-#endif
+// 256-row chunk partials.  Every global load is issued before the one
+// barrier, as 16-byte vectors: the x span (from lo rounded down to even;
+// 32.4 -> 31.1 us on config 5 against scalar loads) and each lane's first 8
+// row entries (5 Ax + 3 Aj vectors shifted into place by the row's alignment;
+// 35.8 -> 33.5 us against 8 + 8 scalar loads).  Staging the block's Aj / Ax
+// through LDS as well (a second LDS phase) measured slower, 37 -> 47 us: with
+// 128 KB of LDS one workgroup holds a CU, and every extra barrier phase is
+// exposed latency.
 template <int EPI, int NRED>
 __global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *win, long nblk, long nnz_pad)
 {
@@ -470,13 +462,13 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *wi
     // 16-byte aligned (uniform); the last odd entry alone (nothing past hi is read)
     typedef double dbl2w_t __attribute__((ext_vector_type(2)));
     const int hi = lo + span, lo2 = lo & ~1;
-    const bool xv16 = WIN_XVEC && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0);
+    const bool xv16 = (reinterpret_cast<uintptr_t>(a.x) & 15) == 0;
     dbl2w_t xs[NS / 2];
 #pragma unroll
     for (int u = 0; u < NS / 2; u++) {
         const int e = lo2 + 2 * (tid + WIN_ROWS * u);
         xs[u] = dbl2w_t{0.0, 0.0};
-        if (WIN_DIAG != 1 && e < hi) {
+        if (e < hi) {
             if (xv16 && e + 1 < hi) xs[u] = *reinterpret_cast<const dbl2w_t *>(a.x + e);
             else xs[u] = dbl2w_t{e >= lo ? a.x[e] : 0.0, e + 1 < hi ? a.x[e + 1] : 0.0};
         }
@@ -486,7 +478,6 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *wi
     const int len = r < a.nrows ? re - rb : 0;
     int cj[8];
     double cx[8];
-#if WIN_VEC
     {
         // the row's first 8 entries as 16-byte vectors (5 for Ax, 3 for Aj,
         // clamped to the padded arrays), then shifted by the row's alignment
@@ -531,20 +522,6 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *wi
             cx[u] = u < len ? xv : 0.0;
         }
     }
-#else
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-        cj[u] = lo;
-        cx[u] = 0.0;
-        if (WIN_DIAG == 2) {
-            cj[u] = lo + ((tid * 7 + u * 131) & 8191);
-            cx[u] = 1.0;
-        } else if (u < len) {
-            cj[u] = a.Aj[rb + u];
-            cx[u] = a.Ax[rb + u];
-        }
-    }
-#endif
     double w0p = 0.0, w1p = 0.0;
     if (NRED > 0) {
         if (a.w0 != a.z) w0p = a.w0[rr];
