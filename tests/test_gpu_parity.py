@@ -228,7 +228,28 @@ def _scattered(n, seed, maxlen=20, reach=3000):
     return O.CSR(n, Ap.astype(np.int32), Aj.astype(np.int32), Ax)
 
 
-@pytest.mark.parametrize("which", ["thermal", "thermal-big", "scattered", "wide"])
+def _jumpy(n, seed):
+    """random CSR whose 1024-row blocks read either near their own rows or a
+    narrow band around another block's rows (spans of 100..12,000 columns
+    that overlap, extend or jump between consecutive blocks; rows of 0..12
+    entries): the windowed kernel over many more blocks than CUs"""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 13, n)
+    Ap = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=Ap[1:])
+    row = np.repeat(np.arange(n), lens)
+    nb = (n + 1023) // 1024
+    mode = rng.integers(0, 3, nb)  # 0, 1: near the diagonal; 2: around another block
+    target = rng.permutation(nb)
+    reach = rng.integers(50, 6000, nb)
+    blk = row // 1024
+    centre = np.where(mode[blk] == 2, target[blk] * 1024 + 512, row)
+    Aj = np.clip(centre + rng.integers(-1, 2, row.size) * rng.integers(0, reach[blk] + 1), 0, n - 1)
+    Ax = uniform(seed + 7, int(Ap[-1]))
+    return O.CSR(n, Ap.astype(np.int32), Aj.astype(np.int32), Ax)
+
+
+@pytest.mark.parametrize("which", ["thermal", "thermal-big", "thermal-ring", "scattered", "jumpy", "wide"])
 def test_spmv_scattered_bitwise_vs_oracle(dev, which):
     """The uncoded products give the oracle's sums bit for bit (mvops.cxx:42-78,
     118-150) on scattered-column matrices: the thermal-like matrix of config 5
@@ -245,6 +266,12 @@ def test_spmv_scattered_bitwise_vs_oracle(dev, which):
     elif which == "thermal-big":
         Ap, Aj, Ax = thermal_like(m=330, window=4096)  # 108,900 rows: 107 windowed blocks
         A = O.CSR(Ap.size - 1, Ap, Aj, Ax)
+    elif which == "thermal-ring":
+        # 518,400 rows: 507 windowed blocks, twice the CU count
+        Ap, Aj, Ax = thermal_like(m=720, window=2048)
+        A = O.CSR(Ap.size - 1, Ap, Aj, Ax)
+    elif which == "jumpy":
+        A = _jumpy(700000, 29)
     elif which == "wide":
         A = _scattered(40000, 12, maxlen=12, reach=40000)
     else:
@@ -269,7 +296,7 @@ def test_spmv_scattered_bitwise_vs_oracle(dev, which):
     M.mv_amxpby(1.5, x, 0.25, y)
     assert np.array_equal(y.download(), O.spmv(2, A, xh, alpha=1.5, beta=0.25, z=yh.copy()))
     # CG (fused q.p in the SpMV epilogue) in tree mode vs the oracle
-    if which in ("thermal", "thermal-big", "wide"):
+    if which in ("thermal", "thermal-big", "thermal-ring", "wide"):
         b = dev.vec(A.n, np.ones(A.n))
         xs = dev.vec(A.n, np.zeros(A.n))
         r = lssp_amd.solve(dev, M, None, xs, b, solver=lssp_amd.CG, maxit=60, trace_cap=100000)
