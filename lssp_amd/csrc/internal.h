@@ -260,7 +260,11 @@ int launch_ew(lssp_amd_ctx *c, const Ew &e);
 
 // finish a reduction whose level-1 partials (tree) or operands (serial) are set:
 // tree: level-2 over nslot partial rows of C entries; then the finalize program
-int launch_reduce_tree(lssp_amd_ctx *c, long C, int nslot, const Fin &f);
+int launch_reduce_tree(lssp_amd_ctx *c, long C, int nslot, const Fin &f, int slot0 = 0);  // partial rows slot0 ..
+// CG's vector updates with the preceding reduction's level 2 folded in (k_cg_fused)
+enum { CGF_P = 0, CGF_XR = 1 };
+int launch_cg_fused(lssp_amd_ctx *c, int kind, long n, double *x, double *p, double *r, const double *z,
+                    const double *q, int pin_slot, int pout_slot, const Fin &f);
 // serial: sums of products a_k[i]*b_k[i] in index order (== vector.cxx:123-133)
 int launch_reduce_serial(lssp_amd_ctx *c, long n, int nslot, const double *const *a,
                          const double *const *b, const Fin &f, const double *carry = nullptr);

@@ -814,11 +814,123 @@ int launch_ew(lssp_amd_ctx *c, const Ew &e)
     return LSSP_AMD_OK;
 }
 
-int launch_reduce_tree(lssp_amd_ctx *c, long C, int nslot, const Fin &f)
+// CG (PC_NON, one rank, tree reductions) with the level 2 of the reduction
+// before a vector update folded into that update: every 1024-thread
+// workgroup redoes k_reduce2m's level 2 over the C partials at pin (lane t adds
+// partials t, t+1024, ... onto 0.0, 16 halving waves, the 16 wave sums halved:
+// the same order and sum on every workgroup), derives the scalar its update
+// needs exactly as finalize does, and workgroup 0 alone runs the finalize
+// program (scalars, trace, residual history, stop flag).  This removes the
+// dependent level-2 launch between the reduction's producer and its consumer.
+//   CGF_XR: alpha = rho1 / (q.p) [FIN_CG_ALPHA]; x += alpha p, r -= alpha q,
+//           r.r partials -> pout (solver-cg.cxx:96-104)
+//   CGF_P:  beta = (r.r) / rho0 [FIN_CG_RES_RHO(_B)]; when the stop test
+//           (:109) holds no workgroup updates p; else p = r + beta p (:88-92)
+// pin and pout are different partial rows: a workgroup still reading pin
+// never races another one writing its chunk partials.
+struct CgFusedArgs {
+    int kind;
+    long n, C;
+    double *x, *p, *r;
+    const double *z, *q;
+    const double *pin;
+    double *pout;
+    double *sums, *scal, *trace;
+    Fin f;
+    const double *guard;
+};
+
+__global__ __launch_bounds__(1024) void k_cg_fused(CgFusedArgs a)
+{
+    __shared__ double wl[16];
+    __shared__ double red[2][4][4];
+    __shared__ double sc[2];
+    if (a.guard && *a.guard != 0.0) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    {
+        double acc = 0.0;
+        for (long k = tid; k < a.C; k += L2_LANES) acc += a.pin[k];
+        acc = wave_sum(acc);
+        if (lane == 0) wl[wave] = acc;
+        __syncthreads();
+        if (tid == 0) {
+            double u[16];
+#pragma unroll
+            for (int w = 0; w < 16; w++) u[w] = wl[w];
+#pragma unroll
+            for (int off = 8; off >= 1; off >>= 1)
+#pragma unroll
+                for (int l = 0; l < off; l++) u[l] = u[l] + u[l + off];
+            const double s = u[0];
+            double v;
+            bool stop = false;
+            if (a.kind == CGF_XR) {
+                v = a.scal[S_RHO1] / s;  // finalize FIN_CG_ALPHA's alpha (S_RHO1 is not written below)
+            } else {
+                v = s / a.scal[S_RHO0];  // FIN_CG_RES_RHO's beta (S_RHO0 is not written below)
+                stop = a.f.op == FIN_CG_RES_RHO_B && sqrt(s) <= a.scal[S_TOL];
+            }
+            if (blockIdx.x == 0) {
+                a.sums[0] = s;
+                finalize(a.f, &s, a.scal, a.trace);
+            }
+            sc[0] = v;
+            sc[1] = stop ? 1.0 : 0.0;
+        }
+        __syncthreads();
+    }
+    if (sc[1] != 0.0) return;
+    const double v = sc[0];
+    int par = 0;
+    for (long g = blockIdx.x; g * 1024 < a.n; g += gridDim.x, par ^= 1) {
+        const long i = g * 1024 + tid;
+        if (a.kind == CGF_P) {
+            if (i < a.n) a.p[i] = a.z[i] + v * a.p[i];
+        } else {
+            double rr = 0.0;
+            if (i < a.n) {
+                const double pv = a.p[i], qv = a.q[i];
+                a.x[i] = a.x[i] + v * pv;
+                const double rn = a.r[i] - v * qv;
+                a.r[i] = rn;
+                rr = rn * rn;
+            }
+            // chunk_reduce's order for the 4 chunks of this 1024-element group
+            const double w = wave_sum(rr);
+            if (lane == 0) red[par][wave >> 2][wave & 3] = w;
+            __syncthreads();
+            const long chunk = g * 4 + (tid >> 8);
+            if ((tid & 255) == 0 && chunk * 256 < a.n) {
+                const int cq = tid >> 8;
+                a.pout[chunk] = (red[par][cq][0] + red[par][cq][1]) + (red[par][cq][2] + red[par][cq][3]);
+            }
+        }
+    }
+}
+
+int launch_cg_fused(lssp_amd_ctx *c, int kind, long n, double *x, double *p, double *r, const double *z,
+                    const double *q, int pin_slot, int pout_slot, const Fin &f)
+{
+    if (n <= 0) return LSSP_AMD_OK;
+    const long C = num_chunks(n);
+    LSSP_TRY(ensure_part(c, C));
+    CgFusedArgs g{kind, n, C, x, p, r, z, q, c->d_part + pin_slot * c->part_cap,
+                  c->d_part + pout_slot * c->part_cap, c->d_sums, c->d_scal, c->d_trace, f, c->guard};
+#ifndef CGF_WG_PER_CU
+#define CGF_WG_PER_CU 2
+#endif
+    const long grid = std::min<long>((n + 1023) / 1024, (long)CGF_WG_PER_CU * c->num_cus);
+    k_cg_fused<<<grid, 1024, 0, c->stream>>>(g);
+    LSSP_HIP(hipGetLastError());
+    return LSSP_AMD_OK;
+}
+
+int launch_reduce_tree(lssp_amd_ctx *c, long C, int nslot, const Fin &f, int slot0)
 {
     int do_fin = c->nranks > 1 ? 0 : 1;
     static_assert(L2_LANES == 16 * 64, "k_reduce2m runs the 16 waves of the level-2 workgroup");
-    k_reduce2m<<<L2_LANES / 64, 64, 0, c->stream>>>(c->d_part, c->part_cap, C, nslot, c->d_sums, c->d_scal,
+    k_reduce2m<<<L2_LANES / 64, 64, 0, c->stream>>>(c->d_part + slot0 * c->part_cap, c->part_cap, C, nslot,
+                                                         c->d_sums, c->d_scal,
                                                          c->d_trace, f, do_fin, c->d_wsum, c->d_rcnt, c->guard);
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;

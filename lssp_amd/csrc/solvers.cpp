@@ -400,6 +400,8 @@ int cg(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *
         // one per iteration.  Same kernels, same arithmetic.
         constexpr int BATCH = 16;
         lssp_amd_ctx *c = R.c;
+        static const bool no_fuse = getenv("LSSP_AMD_CG_FUSE_L2") && atoi(getenv("LSSP_AMD_CG_FUSE_L2")) == 0;
+        const bool fuse_l2 = R.tree && c->nranks == 1 && R.n > 0 && !no_fuse;
         it = 0;
         bool stop = false;
         while (it < maxit && !stop) {
@@ -412,6 +414,12 @@ int cg(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *
             long tl_after[BATCH];
             c->guard = c->d_scal + S_DONE;
             int st = LSSP_AMD_OK;
+            // one rank, tree reductions: each reduction's level 2 runs inside
+            // the vector update that consumes it (k_cg_fused): q.p (partial
+            // row 0, from the product) in the x/r update, r.r (row 1) in the
+            // next iteration's p update; the batch's last r.r on its own
+            Fin held;
+            bool have_held = false;
             for (int j = 0; j < nb && st == LSSP_AMD_OK; j++) {
                 const int k = it + j;
                 Ew e;
@@ -423,21 +431,38 @@ int cg(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *
                 }
                 e.x = z;
                 e.out0 = p;
-                if (st == LSSP_AMD_OK) st = R.ew(e);
+                if (st == LSSP_AMD_OK) {
+                    if (have_held) st = launch_cg_fused(c, CGF_P, R.n, nullptr, p, nullptr, z, nullptr, 1, 1, held);
+                    else st = R.ew(e);
+                }
+                have_held = false;
                 if (st == LSSP_AMD_OK) st = R.spmv(EPI_MXY, 1, p, 0, nullptr, q, 1, p);  // :95
-                if (st == LSSP_AMD_OK) st = R.fin1(q, p, R.fin(FIN_CG_ALPHA, 1, R.T()));  // :96-99
-                e = Ew();
-                e.kind = K_CG_XR;  // :101-104
-                e.out0 = x;
-                e.x = p;
-                e.out1 = r;
-                e.y = q;
-                e.nred = 1;
-                e.r0a = r;
-                e.r0b = r;
-                if (st == LSSP_AMD_OK) st = R.ew(e);
+                const Fin fa = R.fin(FIN_CG_ALPHA, 1, R.T());                            // :96-99
+                if (fuse_l2) {
+                    if (st == LSSP_AMD_OK) st = launch_cg_fused(c, CGF_XR, R.n, x, p, r, nullptr, q, 0, 1, fa);
+                } else {
+                    if (st == LSSP_AMD_OK) st = R.fin1(q, p, fa);
+                    e = Ew();
+                    e.kind = K_CG_XR;  // :101-104
+                    e.out0 = x;
+                    e.x = p;
+                    e.out1 = r;
+                    e.y = q;
+                    e.nred = 1;
+                    e.r0a = r;
+                    e.r0b = r;
+                    if (st == LSSP_AMD_OK) st = R.ew(e);
+                }
                 int t0 = R.T(), t1 = R.T();
-                if (st == LSSP_AMD_OK) st = R.fin1(r, r, R.fin(FIN_CG_RES_RHO_B, 1, t0, t1));  // :106-109, next :80
+                const Fin fr = R.fin(FIN_CG_RES_RHO_B, 1, t0, t1);  // :106-109, next :80
+                if (fuse_l2 && j + 1 < nb) {
+                    held = fr;
+                    have_held = true;
+                } else if (fuse_l2) {
+                    if (st == LSSP_AMD_OK) st = launch_reduce_tree(c, num_chunks(R.n), 1, fr, 1);
+                } else {
+                    if (st == LSSP_AMD_OK) st = R.fin1(r, r, fr);
+                }
                 tl_after[j] = R.tl;
             }
             c->guard = nullptr;
