@@ -564,6 +564,16 @@ int lssp_amd_vec_norm(lssp_amd_ctx *c, const double *x, long n, double *result)
 }
 
 // ---- ILU -------------------------------------------------------------------------
+// the sync-free sweeps' level-ordered arrays (k_trisolve) of a general factor,
+// built on first use: the apply's fallback when a factor has no packet
+// schedule, and the single sweeps of lssp_amd_ilu_trisolve
+static int ensure_sync_free(lssp_amd_ctx *c, lssp_amd_ilu *M)
+{
+    if (M->lower.rp && M->upper.rp) return LSSP_AMD_OK;
+    LSSP_TRY(build_trisched(c, M->n, M->Lp, M->Lj, M->Lx, false, M->lower, nullptr, false, true));
+    return build_trisched(c, M->n, M->Up, M->Uj, M->Ux, true, M->upper, nullptr, false, true);
+}
+
 static int ilu_upload(lssp_amd_ctx *c, lssp_amd_ilu *M)
 {
     // structured ILU(0) of a 5-/7-point grid: line sweeps (linesweep.hip); the
@@ -575,13 +585,18 @@ static int ilu_upload(lssp_amd_ctx *c, lssp_amd_ilu *M)
     // line sweeps serve every sweep of a structured factor: the packet and
     // sync-free schedules are then not built (only the level counts)
     const bool general = ls != LSSP_AMD_OK;
-    LSSP_TRY(build_trisched(c, M->n, M->Lp, M->Lj, M->Lx, false, M->lower, nullptr, general, general));
+    LSSP_TRY(build_trisched(c, M->n, M->Lp, M->Lj, M->Lx, false, M->lower, nullptr, general, false));
     LSSP_TRY(build_trisched(c, M->n, M->Up, M->Uj, M->Ux, true, M->upper, general ? &M->lower : nullptr, general,
-                            general));
+                            false));
+    // the sync-free sweeps' level-ordered arrays only when a factor has no
+    // packet schedule (launch_ilu_apply falls back to them): at 256^3 ILUT they
+    // are ~8 GB of host copies and uploads nothing else reads
+    const bool fallback = general && !(M->lower.pk6_n > 0 && M->upper.pk6_n > 0);
+    if (fallback) LSSP_TRY(ensure_sync_free(c, M));
     setup_mark("sweep schedules (L, U)");
     M->lower.h_pos.clear();
     M->lower.h_pos.shrink_to_fit();
-    if (general) {  // the sync-free sweeps' intermediate vector
+    if (fallback) {  // the sync-free sweeps' intermediate vector
         LSSP_HIP(hipMalloc(&M->d_cache, sizeof(double) * std::max(M->n, 1)));
         LSSP_TRY(launch_fill(c, M->d_cache, M->n, TRI_SENTINEL));
     }
@@ -705,6 +720,7 @@ int lssp_amd_ilu_trisolve(lssp_amd_ctx *c, const lssp_amd_ilu *M, int which, dou
         LSSP_TRY(launch_line_sweep(c, M->line, which ? 1 : 0, x, rhs));
         return check_err(c, M);
     }
+    LSSP_TRY(ensure_sync_free(c, const_cast<lssp_amd_ilu *>(M)));
     LSSP_TRY(launch_fill(c, x, M->n, TRI_SENTINEL));
     LSSP_TRY(launch_trisolve(c, which ? M->upper : M->lower, rhs, x, nullptr));
     return check_err(c);

@@ -230,8 +230,13 @@ HostCSR ilut_factor(const HostCSR &A, double tol, int p)
     M.n = n;
     M.ncols = n;
     M.Ap.assign(n + 1, 0);
-    M.Aj.reserve(A.Aj.size() * 3);
-    M.Ax.reserve(A.Aj.size() * 3);
+    // a row keeps at most p L and p U entries plus its diagonal (:256-274):
+    // reserving that bound (address space only; pages are touched as rows are
+    // appended) means the factor is never regrown and copied mid-way -- at
+    // 256^3 a regrowth moved ~4 GB and first-touched ~8 GB more
+    const size_t cap = p >= 0 ? (size_t)n * (2 * (size_t)p + 1) : A.Aj.size() * 3;
+    M.Aj.reserve(cap);
+    M.Ax.reserve(cap);
     std::vector<double> w(n), diag(n);
     std::vector<int> jr(n, -1), jw(n);
     for (int k = A.Ap[0]; k < A.Ap[1]; k++) {  // row 0 as is (:89-96)
