@@ -1,10 +1,10 @@
+#!/bin/bash
+# GPU box A/B of config 5's CG (tools/bench_configs.py cg-thermal) over library
+# variants: default plus build/<v>.so for each argument (tools/build_variant.sh)
 set -o pipefail
-mkdir -p gpurun_out
-B="python -u tools/bench_configs.py cg-thermal --ref-iters 10"
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gputest2.log 2>&1 || { tail -30 gpurun_out/gputest2.log; exit 1; }
-tail -2 gpurun_out/gputest2.log
-timeout -k 10 200 $B > gpurun_out/c5_fused2.json 2>/dev/null || exit 1
-LSSP_AMD_CG_FUSE_L2=0 timeout -k 10 200 $B > gpurun_out/c5_unfused.json 2>/dev/null || exit 1
-LSSP_AMD_LIB=$PWD/build/cgf1.so timeout -k 10 200 $B > gpurun_out/c5_fused1.json 2>/dev/null || exit 1
-LSSP_AMD_LIB=$PWD/build/cgf4.so timeout -k 10 200 $B > gpurun_out/c5_fused4.json 2>/dev/null || exit 1
-for f in fused2 unfused fused1 fused4; do python -c "import json,sys; d=json.load(open('gpurun_out/c5_$f.json')); print('$f', d['gpu'], d['spmv']['ms'])"; done
+mkdir -p gpurun_out/c5
+for v in default "$@" default "$@"; do
+  if [ $v = default ]; then unset LSSP_AMD_LIB; else export LSSP_AMD_LIB=$PWD/build/$v.so; fi
+  timeout -k 10 200 python -u tools/bench_configs.py cg-thermal --ref-iters 10 > gpurun_out/c5/$v.json 2>/dev/null || exit 1
+  python -c "import json; d=json.load(open('gpurun_out/c5/$v.json')); print('$v', d['gpu']['ms_per_iter'], d['gpu']['residual'], d['parity_serial_vs_reference']['trace_bitwise'])"
+done
