@@ -48,13 +48,14 @@ enum FinOp {
     FIN_CG_RES,          // res = sqrt(s0)
     FIN_CG_RES_RHO,      // res = sqrt(s0); rho1 = s0; beta = rho1/rho0  (PC_NON: z == r)
     FIN_CG_RES_RHO_B,    // FIN_CG_RES_RHO, then res -> history S_H + nit, nit += 1, done = res <= tol
+    FIN_BICG_S_OMEGA,    // sums (t.s, t.t, s.s): FIN_BICG_S on s2 (traced at tpos[2]), then FIN_BICG_OMEGA
 };
 
 struct Fin {
     int op = FIN_STORE;
     int nsum = 1;
     int dst[MAX_SLOTS] = {S_SUM0, S_SUM0 + 1, S_SUM0 + 2, S_SUM0 + 3};
-    int tpos[2] = {-1, -1};  // trace positions of the (up to two) traced values
+    int tpos[3] = {-1, -1, -1};  // trace positions of the (up to three) traced values
 };
 
 }  // namespace lssp_amd
@@ -255,6 +256,7 @@ struct Ew {
     const double *vbase = nullptr;  // GMRES basis [k][n]
     int k = 0;
     int sidx = 0;                   // scalar index for device-scalar kinds
+    int pslot = 0;                  // first partial row the pass's reductions write
 };
 int launch_ew(lssp_amd_ctx *c, const Ew &e);
 

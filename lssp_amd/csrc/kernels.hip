@@ -109,6 +109,14 @@ __device__ void finalize(const Fin &f, const double *s, double *scal, double *tr
         }
         break;
     }
+    case FIN_BICG_S_OMEGA: {  // solver-bicgstab.cxx:117, then :135 (one reduction round for both)
+        const double sn = sqrt(s[2]);
+        scal[S_SNORM] = sn;
+        scal[S_BREAK] = sn <= 1e-40 ? 1.0 : 0.0;
+        scal[S_OMEGA] = s[0] / s[1];
+        if (trace && f.tpos[2] >= 0) trace[f.tpos[2]] = sn;
+        break;
+    }
     case FIN_CG_RHO:  // solver-cg.cxx:80, :88
         scal[S_RHO1] = s[0];
         scal[S_BETA] = s[0] / scal[S_RHO0];
@@ -802,7 +810,8 @@ int launch_ew(lssp_amd_ctx *c, const Ew &e)
     long C = num_chunks(e.n);
     LSSP_TRY(ensure_part(c, C));
     EwArgs g{e.kind, e.n, e.a, e.b, e.x, e.y, e.u, e.v, e.out0, e.out1, e.scal,
-             e.r0a, e.r0b, e.r1a, e.r1b, e.r2a, e.r2b, e.r3a, e.r3b, e.vbase, e.k, e.sidx, c->d_part, c->part_cap, C,
+             e.r0a, e.r0b, e.r1a, e.r1b, e.r2a, e.r2b, e.r3a, e.r3b, e.vbase, e.k, e.sidx,
+             c->d_part + (long)e.pslot * c->part_cap, c->part_cap, C,
              c->guard};
     // one chunk per block up to a cap; the cap keeps >= 8 blocks per CU resident
     long grid = C < 8L * c->num_cus * 4 ? C : 8L * c->num_cus * 4;

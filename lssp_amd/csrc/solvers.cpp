@@ -197,6 +197,8 @@ int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
     double rho1 = R.h(S_RHO1);
     bool pending_rho = false;  // a fused next-iteration rho1 sits in the trace
 
+    static const bool no_merge = getenv("LSSP_AMD_BICG_MERGE_S") && atoi(getenv("LSSP_AMD_BICG_MERGE_S")) == 0;
+    const bool merge_s = R.tree && !no_merge;
     // one iteration :94-141 queued on the stream; fin_res: the finalize of its
     // last reduction; *pos_s: the trace position before its ||s|| (:117)
     auto enqueue = [&](int k, int fin_res, long *pos_s) -> int {
@@ -223,14 +225,28 @@ int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
         e.nred = 1;
         e.r0a = s;
         e.r0b = s;
+        // tree mode: ||s||^2's partials go to row 2 and ride with the omega
+        // round (t.s, t.t in rows 0, 1 from the product): one level 2 and, on P
+        // ranks, one all-gather fewer per iteration.  The break test (:117)
+        // only steers the x/r update, which follows the omega round anyway;
+        // the preconditioner apply and product on s run in either case.
+        if (merge_s) e.pslot = 2;
         LSSP_TRY(R.ew(e));
         *pos_s = R.tl;
-        LSSP_TRY(R.fin1(s, s, R.fin(FIN_BICG_S, 1, R.T())));  // :117
+        const Fin fs = R.fin(FIN_BICG_S, 1, R.T());          // :117
+        if (!merge_s) LSSP_TRY(R.fin1(s, s, fs));
         LSSP_TRY(R.pc(sh, s));                                 // :130-131
         LSSP_TRY(R.spmv(EPI_AMX, 1, sh, 0, p, t, 2, s, nullptr));  // :133
         {
             int t0 = R.T(), t1 = R.T();
-            LSSP_TRY(R.fin2(t, s, t, t, R.fin(FIN_BICG_OMEGA, 2, t0, t1)));  // :135
+            if (merge_s) {
+                Fin f = R.fin(FIN_BICG_S_OMEGA, 3, t0, t1);
+                f.tpos[2] = fs.tpos[0];
+                const double *A_[3] = {t, t, s}, *B_[3] = {s, t, s};
+                LSSP_TRY(finish_reduce(R.c, R.n, 3, A_, B_, f));  // :117 + :135
+            } else {
+                LSSP_TRY(R.fin2(t, s, t, t, R.fin(FIN_BICG_OMEGA, 2, t0, t1)));  // :135
+            }
         }
         e = Ew();
         e.kind = K_BICG_XR;  // :136-139
