@@ -9,5 +9,9 @@ timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_bench -o bench -- python3 bench.py --steps 30 > $O/prof_bench.log 2>&1 || { tail -20 $O/prof_bench.log; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_cg -o cg -- python3 tools/bench_configs.py cg-thermal --ref-iters 10 > $O/prof_cg.log 2>&1 || { tail -20 $O/prof_cg.log; exit 1; }
 timeout -k 10 300 python -u tools/bench_configs.py cg-thermal > $O/config5_cg.json 2> $O/config5_cg.err || { tail -20 $O/config5_cg.err; exit 1; }
-find $O -name "*stats.csv" | sort
+for d in prof_bench prof_cg; do
+  db=$(find $O/$d -name "*results.db" | head -1)
+  [ -n "$db" ] && timeout -k 10 120 rocpd2summary -i "$db" -d $O/$d/summary --format csv > /dev/null 2>&1
+done
+find $O -name "*summary.csv" | sort
 tail -c 400 $O/bench.json; tail -c 600 $O/config5_cg.json
