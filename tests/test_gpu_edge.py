@@ -172,3 +172,27 @@ def test_solvers_on_trivial_systems_bitwise_vs_oracle(dev, solver, system):
     assert _same([r.residual], [o.residual])
     assert _same(r.trace, o.trace)
     assert _same(x.download(), o.x)
+
+
+@pytest.mark.parametrize("mode", ["tree", "serial"])
+@pytest.mark.parametrize("n", [1, 300])
+def test_bicgstab_breakdown_without_pc_bitwise_vs_oracle(dev, mode, n):
+    """A = 2I, no preconditioner: alpha = (r.r)/(r.2r) = 1/2 exactly, so s = r - alpha v
+    is exactly 0 in the first iteration and ||s|| <= 1e-40 stops the run
+    (solver-bicgstab.cxx:117-128) inside a batch of queued iterations -- in
+    tree mode the ||s|| sum rides with the omega round (FIN_BICG_S_OMEGA)."""
+    import lssp_amd
+    Ap, Aj, Ax = np.arange(n + 1, dtype=np.int32), np.arange(n, dtype=np.int32), np.full(n, 2.0)
+    b = uniform(0xBD, n)
+    D = lssp_amd.DMat(dev, Ap, Aj, Ax)
+    x = dev.vec(n, np.zeros(n))
+    dev.set_reduction(lssp_amd.TREE if mode == "tree" else lssp_amd.SERIAL)
+    try:
+        r = lssp_amd.solve(dev, D, None, x, dev.vec(n, b), solver=lssp_amd.BICGSTAB, maxit=50, trace_cap=10000)
+    finally:
+        dev.set_reduction(lssp_amd.TREE)
+    o = O.solve(O.BICGSTAB, O.CSR(n, Ap, Aj, Ax), b, maxit=50, mode=O.TREE if mode == "tree" else O.SERIAL)
+    assert r.nits == o.nits == 1
+    assert _same([r.residual], [o.residual])
+    assert _same(r.trace, o.trace)
+    assert _same(x.download(), o.x)
