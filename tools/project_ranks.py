@@ -5,7 +5,7 @@ block-Jacobi ILU(0) of its diagonal block, exactly what bench.py --gpus P
 builds on rank 0; the halo columns are dropped, so the SpMV is a little
 lighter than the real one) is solved alone for --steps BiCGSTAB iterations.
 The time per iteration is a lower bound of bench.py's ms/step at N = P: it
-leaves out the per-SpMV halo exchange and the four dot all-gathers per
+leaves out the per-SpMV halo exchange and the three reduction all-gathers per
 iteration that RCCL adds.  One JSON line per P."""
 import argparse
 import json
