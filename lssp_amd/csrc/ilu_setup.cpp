@@ -239,6 +239,11 @@ HostCSR ilut_factor(const HostCSR &A, double tol, int p)
     M.Ax.reserve(cap);
     std::vector<double> w(n), diag(n);
     std::vector<int> jr(n, -1), jw(n);
+    // ustart[r]: where row r's entries past its diagonal begin.  Rows >= 1 are
+    // stored L part, diagonal, U part, so the elimination below visits exactly
+    // the entries with col > jrow, in the same order, without walking the L
+    // part; row 0 (A's row as is) is scanned whole
+    std::vector<int> ustart(n, 0);
     for (int k = A.Ap[0]; k < A.Ap[1]; k++) {  // row 0 as is (:89-96)
         M.Aj.push_back(A.Aj[k]);
         M.Ax.push_back(A.Ax[k]);
@@ -290,7 +295,7 @@ HostCSR ilut_factor(const HostCSR &A, double tol, int p)
             }
             jr[jrow] = -1;
             const double aik = w[j] = w[j] / diag[jrow];
-            for (int k = M.Ap[jrow]; k < M.Ap[jrow + 1]; k++) {
+            for (int k = ustart[jrow]; k < M.Ap[jrow + 1]; k++) {
                 const int col = M.Aj[k];
                 if (col <= jrow) continue;
                 const int q = jr[col];
@@ -330,6 +335,7 @@ HostCSR ilut_factor(const HostCSR &A, double tol, int p)
         }
         M.Ax.push_back(diag[i]);
         M.Aj.push_back(i);
+        ustart[i] = (int)M.Aj.size();
         len = std::min(nu, p);
         qsplit(w.data() + i + 1, jw.data() + i + 1, nu, len);
         for (int k = 0; k < len; k++) {
