@@ -585,9 +585,17 @@ static int ilu_upload(lssp_amd_ctx *c, lssp_amd_ilu *M)
     // line sweeps serve every sweep of a structured factor: the packet and
     // sync-free schedules are then not built (only the level counts)
     const bool general = ls != LSSP_AMD_OK;
-    LSSP_TRY(build_trisched(c, M->n, M->Lp, M->Lj, M->Lx, false, M->lower, nullptr, general, false));
+    // U's level pass (a sequential walk of the whole factor) runs beside L's
+    // schedule build; U's build needs L's finished schedule
+    std::vector<int> levU;
+    int stU = LSSP_AMD_OK;
+    std::thread tu([&] { stU = tri_levels(M->n, M->Up, M->Uj, true, levU); });
+    const int stL = build_trisched(c, M->n, M->Lp, M->Lj, M->Lx, false, M->lower, nullptr, general, false);
+    tu.join();
+    LSSP_TRY(stL);
+    LSSP_TRY(stU);
     LSSP_TRY(build_trisched(c, M->n, M->Up, M->Uj, M->Ux, true, M->upper, general ? &M->lower : nullptr, general,
-                            false));
+                            false, &levU));
     // the sync-free sweeps' level-ordered arrays only when a factor has no
     // packet schedule (launch_ilu_apply falls back to them): at 256^3 ILUT they
     // are ~8 GB of host copies and uploads nothing else reads

@@ -500,22 +500,14 @@ void ilu_factor(lssp_amd_ctx *c, int kind, HostCSR &&A0, int level, double tol, 
 //   upper: diagonal is the FIRST entry; strict entries summed in DESCENDING
 //          storage order (solver-tri.cxx:35-41) -- stored reversed here so the
 //          kernel always walks forward.
-int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std::vector<int> &Tj,
-                   const std::vector<double> &Tx, bool upper, TriSched &t, const TriSched *prod, bool packets,
-                   bool arrays)
+// dependency levels of a triangular factor's rows (forward for L, backward for
+// U); dependencies must point strictly below (lower) / above (upper): a row is
+// only ever waited on by later-scheduled rows
+int tri_levels(int n, const std::vector<int> &Tp, const std::vector<int> &Tj, bool upper, std::vector<int> &lev)
 {
-    t.n = n;
-    std::vector<int> lev(n, 0);
-    long nstrict = 0;
-    bool unit = true;
-    for (int i = 0; i < n; i++) {
+    lev.assign(n, 0);
+    for (int i = 0; i < n; i++)
         if (Tp[i + 1] - Tp[i] < 1) return LSSP_AMD_EINVAL;  // no diagonal slot
-        nstrict += Tp[i + 1] - Tp[i] - 1;
-        const double d = upper ? Tx[Tp[i]] : Tx[Tp[i + 1] - 1];
-        unit &= d == 1.0;
-    }
-    // dependencies must point strictly below (lower) / above (upper): a row is
-    // only ever waited on by later-scheduled rows
     if (!upper) {
         for (int i = 0; i < n; i++) {
             int l = 0;
@@ -536,6 +528,25 @@ int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std
             }
             lev[i] = l;
         }
+    }
+    return LSSP_AMD_OK;
+}
+
+int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std::vector<int> &Tj,
+                   const std::vector<double> &Tx, bool upper, TriSched &t, const TriSched *prod, bool packets,
+                   bool arrays, std::vector<int> *lev_in)
+{
+    t.n = n;
+    std::vector<int> lev;
+    if (lev_in) lev.swap(*lev_in);
+    else LSSP_TRY(tri_levels(n, Tp, Tj, upper, lev));
+    if ((int)lev.size() != n) return LSSP_AMD_EINVAL;
+    long nstrict = 0;
+    bool unit = true;
+    for (int i = 0; i < n; i++) {
+        nstrict += Tp[i + 1] - Tp[i] - 1;
+        const double d = upper ? Tx[Tp[i]] : Tx[Tp[i + 1] - 1];
+        unit &= d == 1.0;
     }
     int nlev = 0;
     for (int i = 0; i < n; i++) nlev = std::max(nlev, lev[i] + 1);

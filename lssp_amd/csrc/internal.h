@@ -319,7 +319,10 @@ int ilu0_factor_gpu(lssp_amd_ctx *c, int n, int blk, const std::vector<int> &Ap,
                     std::vector<double> &Ax);
 int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std::vector<int> &Tj,
                    const std::vector<double> &Tx, bool upper, TriSched &t, const TriSched *prod = nullptr,
-                   bool packets = true, bool arrays = true);
+                   bool packets = true, bool arrays = true, std::vector<int> *lev_in = nullptr);
+// the rows' dependency levels alone (build_trisched's first pass; lev_in above
+// takes them precomputed, e.g. on another thread)
+int tri_levels(int n, const std::vector<int> &Tp, const std::vector<int> &Tj, bool upper, std::vector<int> &lev);
 // line sweeps (linesweep.hip): LSSP_AMD_EUNSUPPORTED when the factors are not
 // the structured ILU(0) of a 5-/7-point grid
 int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std::vector<int> &Lj,
