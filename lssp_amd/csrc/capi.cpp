@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <atomic>
 #include <cstring>
+#include <exception>
 #include <mutex>
 #include <thread>
 
@@ -216,9 +217,8 @@ int build_diag_ids(lssp_amd_mat *M, const int *Ap, const int *Aj)
 // nevertheless stay near the diagonal (locally renumbered meshes: config 5).
 int build_windows(lssp_amd_mat *M, const int *Ap, const int *Aj)
 {
-    static const bool off = getenv("LSSP_AMD_SPMV_WIN") && atoi(getenv("LSSP_AMD_SPMV_WIN")) == 0;
     const int n = M->nrows;
-    if (off || M->ndiag > 0 || M->nnz == 0 || n == 0) return LSSP_AMD_OK;
+    if (M->ndiag > 0 || M->nnz == 0 || n == 0) return LSSP_AMD_OK;
     const long nb = (n + WIN_ROWS - 1) / WIN_ROWS;
     std::vector<int> win(2 * nb);
     std::atomic<bool> wide{false};
@@ -567,11 +567,33 @@ int lssp_amd_vec_norm(lssp_amd_ctx *c, const double *x, long n, double *result)
 // the sync-free sweeps' level-ordered arrays (k_trisolve) of a general factor,
 // built on first use: the apply's fallback when a factor has no packet
 // schedule, and the single sweeps of lssp_amd_ilu_trisolve
+// (the first lssp_amd_ilu_trisolve on a general factor builds them: the handle
+// is mutated then, under its own lock).  Each factor is built on its own, and a
+// build that fails part-way frees what it allocated, so a retry never
+// overwrites live buffers.
+static int sync_free_one(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std::vector<int> &Tj,
+                         const std::vector<double> &Tx, bool upper, TriSched &t)
+{
+    if (t.rp) return LSSP_AMD_OK;
+    int st;
+    try {
+        st = build_trisched(c, n, Tp, Tj, Tx, upper, t, nullptr, false, true);
+    } catch (const std::exception &) {
+        st = LSSP_AMD_ENOMEM;
+    }
+    if (st != LSSP_AMD_OK) {
+        for (void *p : {(void *)t.perm, (void *)t.rp, (void *)t.cols, (void *)t.vals, (void *)t.diag})
+            if (p) (void)hipFree(p);
+        t.perm = t.rp = t.cols = nullptr;
+        t.vals = t.diag = nullptr;
+    }
+    return st;
+}
 static int ensure_sync_free(lssp_amd_ctx *c, lssp_amd_ilu *M)
 {
-    if (M->lower.rp && M->upper.rp) return LSSP_AMD_OK;
-    LSSP_TRY(build_trisched(c, M->n, M->Lp, M->Lj, M->Lx, false, M->lower, nullptr, false, true));
-    return build_trisched(c, M->n, M->Up, M->Uj, M->Ux, true, M->upper, nullptr, false, true);
+    std::lock_guard<std::mutex> lk(M->sync_free_mu);
+    LSSP_TRY(sync_free_one(c, M->n, M->Lp, M->Lj, M->Lx, false, M->lower));
+    return sync_free_one(c, M->n, M->Up, M->Uj, M->Ux, true, M->upper);
 }
 
 static int ilu_upload(lssp_amd_ctx *c, lssp_amd_ilu *M)
@@ -588,9 +610,19 @@ static int ilu_upload(lssp_amd_ctx *c, lssp_amd_ilu *M)
     // U's level pass (a sequential walk of the whole factor) runs beside L's
     // schedule build; U's build needs L's finished schedule
     std::vector<int> levU;
-    int stU = LSSP_AMD_OK;
-    std::thread tu([&] { stU = tri_levels(M->n, M->Up, M->Uj, true, levU); });
-    const int stL = build_trisched(c, M->n, M->Lp, M->Lj, M->Lx, false, M->lower, nullptr, general, false);
+    int stU = LSSP_AMD_OK, stL = LSSP_AMD_OK;
+    std::thread tu([&] {
+        try {
+            stU = tri_levels(M->n, M->Up, M->Uj, true, levU);
+        } catch (const std::exception &) {
+            stU = LSSP_AMD_ENOMEM;
+        }
+    });
+    try {  // the thread is joined on every path
+        stL = build_trisched(c, M->n, M->Lp, M->Lj, M->Lx, false, M->lower, nullptr, general, false);
+    } catch (const std::exception &) {
+        stL = LSSP_AMD_ENOMEM;
+    }
     tu.join();
     LSSP_TRY(stL);
     LSSP_TRY(stU);
@@ -612,8 +644,35 @@ static int ilu_upload(lssp_amd_ctx *c, lssp_amd_ilu *M)
     return LSSP_AMD_OK;
 }
 
+static int ilu_create(lssp_amd_ctx *c, int kind, int n, const int *Ap, const int *Aj, const double *Ax, int level,
+                      double tol, int p, int blk, lssp_amd_ilu **out);
+static int ilu_from_factors(lssp_amd_ctx *c, int n, const int *Lp, const int *Lj, const double *Lx, const int *Up,
+                            const int *Uj, const double *Ux, lssp_amd_ilu **out);
+
+// host setup allocates multi-GB vectors: an allocation the host refuses
+// becomes LSSP_AMD_ENOMEM at the C-ABI instead of an exception
 int lssp_amd_ilu_create(lssp_amd_ctx *c, int kind, int n, const int *Ap, const int *Aj,
                         const double *Ax, int level, double tol, int p, int blk, lssp_amd_ilu **out)
+{
+    try {
+        return ilu_create(c, kind, n, Ap, Aj, Ax, level, tol, p, blk, out);
+    } catch (const std::exception &) {
+        return LSSP_AMD_ENOMEM;
+    }
+}
+
+int lssp_amd_ilu_from_factors(lssp_amd_ctx *c, int n, const int *Lp, const int *Lj, const double *Lx,
+                              const int *Up, const int *Uj, const double *Ux, lssp_amd_ilu **out)
+{
+    try {
+        return ilu_from_factors(c, n, Lp, Lj, Lx, Up, Uj, Ux, out);
+    } catch (const std::exception &) {
+        return LSSP_AMD_ENOMEM;
+    }
+}
+
+static int ilu_create(lssp_amd_ctx *c, int kind, int n, const int *Ap, const int *Aj, const double *Ax, int level,
+                      double tol, int p, int blk, lssp_amd_ilu **out)
 {
     if (!c || !out || n <= 0 || (kind != LSSP_AMD_ILUK && kind != LSSP_AMD_ILUT)) return LSSP_AMD_EINVAL;
     LSSP_TRY(check_csr(n, n, Ap[n], Ap, Aj));
@@ -653,8 +712,8 @@ int lssp_amd_ilu_create(lssp_amd_ctx *c, int kind, int n, const int *Ap, const i
     return LSSP_AMD_OK;
 }
 
-int lssp_amd_ilu_from_factors(lssp_amd_ctx *c, int n, const int *Lp, const int *Lj, const double *Lx,
-                              const int *Up, const int *Uj, const double *Ux, lssp_amd_ilu **out)
+static int ilu_from_factors(lssp_amd_ctx *c, int n, const int *Lp, const int *Lj, const double *Lx, const int *Up,
+                            const int *Uj, const double *Ux, lssp_amd_ilu **out)
 {
     if (!c || !out || n <= 0) return LSSP_AMD_EINVAL;
     LSSP_TRY(check_csr(n, n, Lp[n], Lp, Lj));

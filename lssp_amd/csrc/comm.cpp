@@ -423,18 +423,22 @@ int lssp_amd_mat_upload_dist(lssp_amd_ctx *c, int n_global, int row0, int nlocal
         g -= row0;
     }
     LSSP_TRY(agree_status(c, st));
-    LSSP_HIP(hipMalloc(&M->d_send_idx, sizeof(int) * std::max(nsend, 1)));
-    LSSP_HIP(hipMalloc(&M->d_send_buf, sizeof(double) * std::max(nsend, 1)));
-    if (nsend)
-        LSSP_HIP(hipMemcpy(M->d_send_idx, sendg.data(), sizeof(int) * nsend, hipMemcpyHostToDevice));
-    LSSP_HIP(hipMalloc(&M->Ap, sizeof(int) * (nlocal + 1)));
-    LSSP_HIP(hipMalloc(&M->Aj, sizeof(int) * (nnz + 4)));  // +4: see upload_csr (capi.cpp)
-    LSSP_HIP(hipMalloc(&M->Ax, sizeof(double) * (nnz + 4)));
-    LSSP_HIP(hipMemcpy(M->Ap, Ap, sizeof(int) * (nlocal + 1), hipMemcpyHostToDevice));
-    if (nnz) {
-        LSSP_HIP(hipMemcpy(M->Aj, lj.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
-        LSSP_HIP(hipMemcpy(M->Ax, Ax, sizeof(double) * nnz, hipMemcpyHostToDevice));
-    }
+    // the matrix's own buffers (the largest allocations of the upload): a
+    // failure becomes a status that every rank agrees on, and MatGuard frees
+    // whatever was allocated
+    auto dev_ok = [](hipError_t e) { return e == hipSuccess; };
+    const bool ok =
+        dev_ok(hipMalloc(&M->d_send_idx, sizeof(int) * std::max(nsend, 1))) &&
+        dev_ok(hipMalloc(&M->d_send_buf, sizeof(double) * std::max(nsend, 1))) &&
+        (!nsend || dev_ok(hipMemcpy(M->d_send_idx, sendg.data(), sizeof(int) * nsend, hipMemcpyHostToDevice))) &&
+        dev_ok(hipMalloc(&M->Ap, sizeof(int) * (nlocal + 1))) &&
+        dev_ok(hipMalloc(&M->Aj, sizeof(int) * ((size_t)nnz + 4))) &&  // +4: see upload_csr (capi.cpp)
+        dev_ok(hipMalloc(&M->Ax, sizeof(double) * ((size_t)nnz + 4))) &&
+        dev_ok(hipMemcpy(M->Ap, Ap, sizeof(int) * (nlocal + 1), hipMemcpyHostToDevice)) &&
+        (!nnz || (dev_ok(hipMemcpy(M->Aj, lj.data(), sizeof(int) * (size_t)nnz, hipMemcpyHostToDevice)) &&
+                  dev_ok(hipMemcpy(M->Ax, Ax, sizeof(double) * (size_t)nnz, hipMemcpyHostToDevice))));
+    if (!ok) (void)hipGetLastError();  // clear the sticky error of a failed allocation
+    LSSP_TRY(agree_status(c, ok ? LSSP_AMD_OK : LSSP_AMD_ENOMEM));
     LSSP_TRY(agree_status(c, build_diag_ids(M, Ap, lj.data())));  // the SpMV's column coding (capi.cpp)
     guard.m = nullptr;
     *out = M;

@@ -8,7 +8,7 @@
 // The reference orders entries with counting sorts whose sequential loops
 // make them STABLE (coo_to_csr keeps the input order inside a row, transpose
 // the row order inside a column).  On the GPU the same orders come from
-// stable LSD radix sorts (hipCUB / rocPRIM onesweep, keys limited to the bits
+// stable LSD radix sorts (rocPRIM's device radix sort, keys limited to the bits
 // the row / column range needs) of (key, entry index) pairs followed by a
 // coalesced gather, and row pointers are lower bounds in the sorted keys.
 // Block patterns (csr_to_bcsr) come from one radix sort of packed
@@ -19,7 +19,8 @@
 // by construction.  These kernels are HBM-bound streaming passes; none of
 // them is on the solve path.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
 #include <cstdint>
@@ -276,13 +277,15 @@ int checked(hipStream_t s, const int *err)
     return h ? LSSP_AMD_EINVAL : LSSP_AMD_OK;
 }
 
+// rocPRIM's device-wide primitives (the library's own API): the LSD radix
+// sort is stable, which is what reproduces the reference's counting sorts
 template <class K, class V>
 int sort_pairs(Scratch &S, const K *kin, K *kout, const V *vin, V *vout, long n, int bits)
 {
     size_t bytes = 0;
-    LSSP_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kin, kout, vin, vout, (int)n, 0, bits, S.s));
+    LSSP_HIP(rocprim::radix_sort_pairs(nullptr, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, S.s));
     SCRATCH(t, char, (long)bytes);
-    LSSP_HIP(hipcub::DeviceRadixSort::SortPairs(t, bytes, kin, kout, vin, vout, (int)n, 0, bits, S.s));
+    LSSP_HIP(rocprim::radix_sort_pairs(t, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, S.s));
     return LSSP_AMD_OK;
 }
 
@@ -290,18 +293,18 @@ template <class K>
 int sort_keys(Scratch &S, const K *kin, K *kout, long n, int bits)
 {
     size_t bytes = 0;
-    LSSP_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, kin, kout, (int)n, 0, bits, S.s));
+    LSSP_HIP(rocprim::radix_sort_keys(nullptr, bytes, kin, kout, (size_t)n, 0u, (unsigned)bits, S.s));
     SCRATCH(t, char, (long)bytes);
-    LSSP_HIP(hipcub::DeviceRadixSort::SortKeys(t, bytes, kin, kout, (int)n, 0, bits, S.s));
+    LSSP_HIP(rocprim::radix_sort_keys(t, bytes, kin, kout, (size_t)n, 0u, (unsigned)bits, S.s));
     return LSSP_AMD_OK;
 }
 
 int exclusive_sum(Scratch &S, const int *in, int *out, long n)
 {
     size_t bytes = 0;
-    LSSP_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, (int)n, S.s));
+    LSSP_HIP(rocprim::exclusive_scan(nullptr, bytes, in, out, 0, (size_t)n, rocprim::plus<int>(), S.s));
     SCRATCH(t, char, (long)bytes);
-    LSSP_HIP(hipcub::DeviceScan::ExclusiveSum(t, bytes, in, out, (int)n, S.s));
+    LSSP_HIP(rocprim::exclusive_scan(t, bytes, in, out, 0, (size_t)n, rocprim::plus<int>(), S.s));
     return LSSP_AMD_OK;
 }
 

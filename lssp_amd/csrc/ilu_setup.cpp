@@ -9,6 +9,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <exception>
 
 #include "internal.h"
 
@@ -234,9 +235,19 @@ HostCSR ilut_factor(const HostCSR &A, double tol, int p)
     // reserving that bound (address space only; pages are touched as rows are
     // appended) means the factor is never regrown and copied mid-way -- at
     // 256^3 a regrowth moved ~4 GB and first-touched ~8 GB more
-    const size_t cap = p >= 0 ? (size_t)n * (2 * (size_t)p + 1) : A.Aj.size() * 3;
-    M.Aj.reserve(cap);
-    M.Ax.reserve(cap);
+    // p beyond n-1 keeps no more than a full row; a reservation the host
+    // refuses falls back to a modest one and the vectors grow as the
+    // reference's realloc does (pc-ilut.cxx:71, :215-222)
+    const size_t pc = p >= 0 ? (size_t)std::min(p, std::max(n - 1, 0)) : 0;
+    const size_t cap = p >= 0 ? (size_t)n * (2 * pc + 1) : A.Aj.size() * 3;
+    try {
+        M.Aj.reserve(cap);
+        M.Ax.reserve(cap);
+    } catch (const std::exception &) {
+        const size_t small = std::max(A.Aj.size() * 3, (size_t)n * 8);
+        M.Aj.reserve(std::min(cap, small));
+        M.Ax.reserve(std::min(cap, small));
+    }
     std::vector<double> w(n), diag(n);
     std::vector<int> jr(n, -1), jw(n);
     // ustart[r]: where row r's entries past its diagonal begin.  Rows >= 1 are

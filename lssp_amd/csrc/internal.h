@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <functional>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -212,6 +213,7 @@ struct lssp_amd_ilu {
     mutable double *d_rperm = nullptr;  // the apply's rhs in L order
     mutable unsigned epoch = 0;
     lssp_amd::LineILU line;  // structured factors: line sweeps (ntiles > 0)
+    std::mutex sync_free_mu;  // the sync-free arrays, built on first use (ensure_sync_free)
     double setup_seconds = 0;
 };
 

@@ -197,8 +197,9 @@ int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
     double rho1 = R.h(S_RHO1);
     bool pending_rho = false;  // a fused next-iteration rho1 sits in the trace
 
-    static const bool no_merge = getenv("LSSP_AMD_BICG_MERGE_S") && atoi(getenv("LSSP_AMD_BICG_MERGE_S")) == 0;
-    const bool merge_s = R.tree && !no_merge;
+    // tree mode merges ||s||^2 into the omega round (below); SERIAL mode keeps
+    // the reference's order of reductions
+    const bool merge_s = R.tree;
     // one iteration :94-141 queued on the stream; fin_res: the finalize of its
     // last reduction; *pos_s: the trace position before its ||s|| (:117)
     auto enqueue = [&](int k, int fin_res, long *pos_s) -> int {
@@ -416,8 +417,7 @@ int cg(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *
         // one per iteration.  Same kernels, same arithmetic.
         constexpr int BATCH = 16;
         lssp_amd_ctx *c = R.c;
-        static const bool no_fuse = getenv("LSSP_AMD_CG_FUSE_L2") && atoi(getenv("LSSP_AMD_CG_FUSE_L2")) == 0;
-        const bool fuse_l2 = R.tree && c->nranks == 1 && R.n > 0 && !no_fuse;
+        const bool fuse_l2 = R.tree && c->nranks == 1 && R.n > 0;
         it = 0;
         bool stop = false;
         while (it < maxit && !stop) {

@@ -254,10 +254,8 @@ def test_spmv_scattered_bitwise_vs_oracle(dev, which):
     """The uncoded products give the oracle's sums bit for bit (mvops.cxx:42-78,
     118-150) on scattered-column matrices: the thermal-like matrix of config 5
     and random rows of 0..20 entries within +-3000 of the diagonal take the
-    windowed-x kernel (k_spmv_win); columns over the whole range ("wide") and
-    the window switched off (LSSP_AMD_SPMV_WIN=0 is read once per process, so
-    a 1024-row block spanning > 16384 columns stands in for it) take the
-    gathering k_spmv3."""
+    windowed-x kernel (k_spmv_win); columns over the whole range ("wide": a
+    1024-row block spanning > 16384 columns) take the gathering k_spmv3."""
     import lssp_amd
     from lssp_amd.synthetic import thermal_like
     if which == "thermal":
