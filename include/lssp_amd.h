@@ -189,6 +189,15 @@ int lssp_amd_comm_unique_id_size(void);
 int lssp_amd_comm_get_unique_id(void *id_out);
 int lssp_amd_comm_init(lssp_amd_ctx *ctx, int nranks, int rank, const void *id);
 int lssp_amd_comm_barrier(lssp_amd_ctx *ctx);
+/* Transport check (collective): an all-gather of every rank's id and a ring
+ * round of grouped send/recv (rank r -> r+1, r-1 -> r; a 1-rank communicator
+ * sends to itself) driven exactly as the SpMV's halo round is -- packed on the
+ * compute stream, the round on the communication stream between two events,
+ * the compute stream waiting for it -- then every received word checked.
+ * LSSP_AMD_OK, or LSSP_AMD_ECOMM when a value did not arrive.  With nranks = 1
+ * lssp_amd_comm_init still creates the (1-rank) RCCL communicator, so a single
+ * GPU can run this before a multi-GPU job. */
+int lssp_amd_comm_selftest(lssp_amd_ctx *ctx);
 
 /* Host-staged transport: the same protocol with the collective carried by the
  * caller (an MPI library, a torch.distributed gloo group, ...) instead of

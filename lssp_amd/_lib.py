@@ -76,6 +76,7 @@ SIGNATURES = {
     "lssp_amd_comm_get_unique_id": (_ci, [_vp]),
     "lssp_amd_comm_init": (_ci, [_vp, _ci, _ci, _vp]),
     "lssp_amd_comm_barrier": (_ci, [_vp]),
+    "lssp_amd_comm_selftest": (_ci, [_vp]),
     "lssp_amd_comm_init_host": (_ci, [_vp, _ci, _ci, _vp]),
     "lssp_amd_mat_upload_dist": (_ci, [_vp, _ci, _ci, _ci, _vp, _vp, _vp, _pvp]),
     "lssp_amd_mat_local_rows": (_ci, [_vp, _vp, _vp, _vp]),

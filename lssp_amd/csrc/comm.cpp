@@ -207,6 +207,20 @@ using namespace lssp_amd;
 
 extern "C" {
 
+namespace {
+struct DevMem {  // device scratch, freed when the upload returns
+    void *p = nullptr;
+    ~DevMem()
+    {
+        if (p) (void)hipFree(p);
+    }
+};
+struct MatGuard {  // the half-built matrix, destroyed unless released
+    lssp_amd_mat *m;
+    ~MatGuard() { lssp_amd_mat_destroy(m); }
+};
+}  // namespace
+
 int lssp_amd_comm_unique_id_size(void) { return (int)sizeof(ncclUniqueId); }
 
 int lssp_amd_comm_get_unique_id(void *out)
@@ -223,7 +237,8 @@ int lssp_amd_comm_init(lssp_amd_ctx *c, int nranks, int rank, const void *idp)
     if (!c || !idp || nranks < 1 || rank < 0 || rank >= nranks) return LSSP_AMD_EINVAL;
     LSSP_HIP(hipSetDevice(c->device));
     comm_destroy(c);
-    if (nranks == 1) return LSSP_AMD_OK;
+    // nranks == 1: a 1-rank communicator (the solvers take their single-rank
+    // paths; lssp_amd_comm_selftest can drive the RCCL transport on one GPU)
     ncclUniqueId id;
     memcpy(&id, idp, sizeof(id));
     ncclComm_t comm;
@@ -237,6 +252,55 @@ int lssp_amd_comm_init(lssp_amd_ctx *c, int nranks, int rank, const void *idp)
     LSSP_HIP(hipEventCreateWithFlags(&c->ev_pack, hipEventDisableTiming));
     LSSP_HIP(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
     return LSSP_AMD_OK;
+}
+
+int lssp_amd_comm_selftest(lssp_amd_ctx *c)
+{
+    if (!c) return LSSP_AMD_EINVAL;
+    if (!c->comm && !host_mode(c)) return LSSP_AMD_EINVAL;  // no transport
+    LSSP_HIP(hipSetDevice(c->device));
+    const int P = c->nranks, r = c->rank;
+    const long n = 4096 + 8 * r;                              // message sizes differ per rank
+    const long nprev = 4096 + 8 * ((r + P - 1) % P);          // what rank r-1 sends
+    std::vector<double> h(std::max(n, nprev));
+    DevMem d_send, d_recv, d_id, d_ids;
+    LSSP_HIP(hipMalloc(&d_send.p, sizeof(double) * n));
+    LSSP_HIP(hipMalloc(&d_recv.p, sizeof(double) * nprev));
+    LSSP_HIP(hipMalloc(&d_id.p, sizeof(double) * MAX_SLOTS));
+    LSSP_HIP(hipMalloc(&d_ids.p, sizeof(double) * MAX_SLOTS * P));
+    for (long i = 0; i < n; i++) h[i] = r * 1e6 + i;
+    LSSP_HIP(hipMemcpyAsync(d_send.p, h.data(), sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    LSSP_HIP(hipMemsetAsync(d_recv.p, 0xff, sizeof(double) * nprev, c->stream));
+    double mine[MAX_SLOTS] = {(double)r, 1.0 + r, 2.0 * r, -1.0 - r};
+    LSSP_HIP(hipMemcpyAsync(d_id.p, mine, sizeof(mine), hipMemcpyHostToDevice, c->stream));
+    LSSP_TRY(xfer_allgather(c, d_id.p, d_ids.p, (long)sizeof(mine)));
+    // the halo round's plumbing (spmv_halo): event after the pack, the round on
+    // comm_stream, the compute stream waits for its event
+    const std::vector<Msg> sends{{(r + 1) % P, d_send.p, (long)sizeof(double) * n}};
+    const std::vector<Msg> recvs{{(r + P - 1) % P, d_recv.p, (long)sizeof(double) * nprev}};
+    if (!host_mode(c)) {
+        LSSP_HIP(hipEventRecord(c->ev_pack, c->stream));
+        LSSP_HIP(hipStreamWaitEvent(c->comm_stream, c->ev_pack, 0));
+        LSSP_TRY(xfer_group(c, sends, recvs, c->comm_stream));
+        LSSP_HIP(hipEventRecord(c->ev_halo, c->comm_stream));
+        LSSP_HIP(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+    } else {
+        LSSP_TRY(xfer_group(c, sends, recvs));
+    }
+    std::vector<double> ids(MAX_SLOTS * P);
+    LSSP_HIP(hipMemcpyAsync(h.data(), d_recv.p, sizeof(double) * nprev, hipMemcpyDeviceToHost, c->stream));
+    LSSP_HIP(hipMemcpyAsync(ids.data(), d_ids.p, sizeof(double) * ids.size(), hipMemcpyDeviceToHost, c->stream));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    int st = LSSP_AMD_OK;
+    const int rp = (r + P - 1) % P;
+    for (long i = 0; i < nprev; i++)
+        if (h[i] != rp * 1e6 + i) st = LSSP_AMD_ECOMM;
+    for (int q = 0; q < P; q++) {
+        const double want[MAX_SLOTS] = {(double)q, 1.0 + q, 2.0 * q, -1.0 - q};
+        for (int k = 0; k < MAX_SLOTS; k++)
+            if (ids[q * MAX_SLOTS + k] != want[k]) st = LSSP_AMD_ECOMM;
+    }
+    return st;
 }
 
 int lssp_amd_comm_init_host(lssp_amd_ctx *c, int nranks, int rank, const lssp_amd_host_transport *t)
@@ -271,19 +335,6 @@ int lssp_amd_comm_barrier(lssp_amd_ctx *c)
 // rank fails together with the same status and none is left waiting in an
 // all-gather or send/recv.  Temporary device buffers and the half-built matrix
 // are released on every path.
-namespace {
-struct DevMem {  // device scratch, freed when the upload returns
-    void *p = nullptr;
-    ~DevMem()
-    {
-        if (p) (void)hipFree(p);
-    }
-};
-struct MatGuard {  // the half-built matrix, destroyed unless released
-    lssp_amd_mat *m;
-    ~MatGuard() { lssp_amd_mat_destroy(m); }
-};
-}  // namespace
 
 // every rank's status -> the first non-zero one (rank order), identical on all ranks
 static int agree_status(lssp_amd_ctx *c, int st)

@@ -439,6 +439,38 @@ __device__ __forceinline__ void static_for(F &&f)
     }
 }
 
+#ifndef LINE_FASTDIV
+#define LINE_FASTDIV 0
+#endif
+#ifndef LINE_FASTCOMP
+#define LINE_FASTCOMP 0
+#endif
+#ifndef LINE_KOUT_BF
+#define LINE_KOUT_BF 0
+#endif
+// a / b correctly rounded from y = RN(1 / b) (formed off the critical path):
+// q0 = RN(a y) is within 1.5 ulp of a / b; one correction with the exact
+// remainder (FMA) brings it within 1 ulp, and a second one rounds correctly
+// (Markstein: y within 1/2 ulp of 1/b, q within 1 ulp of a/b, r = a - b q
+// exact => RN(q + r y) = RN(a / b)).  Exact only without underflow or
+// overflow anywhere: the callers take it for |a|, |b| in [2^-300, 2^300]
+// (a != 0) and use the true division otherwise.
+__device__ __forceinline__ double div_rn(double a, double b, double y)
+{
+    double q = a * y;
+    double r = __builtin_fma(-b, q, a);
+    q = __builtin_fma(r, y, q);
+    r = __builtin_fma(-b, q, a);
+    return __builtin_fma(r, y, q);
+}
+__device__ __forceinline__ bool div_range_ok(double v)
+{
+    const unsigned e = ((unsigned)(__double_as_longlong(v) >> 52)) & 0x7ffu;
+    return e - (1023u - 300u) <= 600u;
+}
+__device__ __forceinline__ bool div_num_ok(double a) { return div_range_ok(a); }
+__device__ __forceinline__ bool div_den_ok(double b) { return div_range_ok(b); }
+
 // slot layout (bytes): the step's coefficient block, its rhs, the hand-off inputs
 template <int P, int NA, bool RHS_NAT>
 struct LineSlot {
@@ -563,7 +595,140 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
         unsigned long long *ts = TRACE ? a.trace + 8 * (long)a.ntiles : nullptr;
         const bool trs = TRACE && t == a.ttile && lane == 0;
 
-        if (wave < CW) {
+        constexpr bool LEAN = LINE_FASTCOMP && !RHS_NAT;  // the lean step reads its rhs from the slot
+        if (LEAN && wave < CW) {
+          if constexpr (LEAN) {
+            // ---------------- compute (lean step): planes p0 .. p0+PC-1 ----------------
+            // The same recurrence as below with the per-step overhead taken off
+            // the critical path: ring offsets advance by adds (no modulo), the
+            // rows valid at a step come from a lane-mask shift register (plane 0's
+            // mask at step s is its mask at s-1 shifted one lane up, plus lane 0
+            // while 0 <= s < nx; plane p's is plane 0's of step s-p), every plane
+            // is computed in one straight-line block, and the hand-off stores
+            // drop the lanes that publish nothing through out-of-range offsets.
+            // Published values need no canonicalisation: every one is the result
+            // of an f64 add or division, and those never return the sentinel (a
+            // signalling NaN) in IEEE mode.
+            const int p0 = wave * PC;
+            struct In {
+                double ck[PC], cj[PC], ci[PC], dg[PC], rh[PC], jv[PC];
+            };
+            auto load = [&](unsigned so, In &in) {
+                const char *slot = ring + so;
+#pragma unroll
+                for (int u = 0; u < PC; u++) {
+                    const int p = p0 + u;
+                    const double *b = reinterpret_cast<const double *>(slot + SL::COEF) + (p * nj + lc) * NA;
+                    in.ck[u] = b[0];
+                    in.cj[u] = b[1];
+                    in.ci[u] = b[2];
+                    if constexpr (NA == 4) in.dg[u] = b[3];
+                    in.rh[u] = reinterpret_cast<const double *>(slot + SL::RHS)[p * nj + lc];
+                    in.jv[u] = reinterpret_cast<const double *>(slot + SL::JFIN)[p];
+                }
+            };
+            double xc[PC];
+#pragma unroll
+            for (int u = 0; u < PC; u++) xc[u] = 0.0;
+            In A, B;
+            constexpr int OOB = 0x40000000;  // + any soffset below stays < 2^31: dropped, never wraps
+            const __amdgpu_buffer_rsrc_t hko =
+                __builtin_amdgcn_make_buffer_rsrc(a.hk + (long)t * a.hk_stride, 0, (int)(a.hk_stride * 8), 0x00020000);
+            const __amdgpu_buffer_rsrc_t hjo =
+                __builtin_amdgcn_make_buffer_rsrc(a.hj + (long)t * a.hj_stride, 0, (int)(a.hj_stride * 8), 0x00020000);
+            const uint64_t njm = nj >= 64 ? ~0ull : ((1ull << nj) - 1);
+            // the plane this wave publishes to the next k-tile (-1: none)
+            const int uk = (kout && np - 1 >= p0 && np - 1 < p0 + PC) ? np - 1 - p0 : -1;
+            const int jl_off = lane == nj - 1 ? 0 : OOB;  // lane nj-1 feeds the next j-tile
+            // hw[u]: the lanes whose row of plane p0+u exists at the current step
+            // (lane l's row i = s - p - l is valid iff lane l-1's was at s-1, and
+            // lane 0's iff 0 <= s - p < nx), pm[u]: 0 for planes past the tile
+            uint64_t hw[PC], pm[PC];
+#pragma unroll
+            for (int u = 0; u < PC; u++) hw[u] = 0, pm[u] = p0 + u < np ? njm : 0ull;
+            unsigned so = (unsigned)(((S0 % R) + R) % R) * SL::BYTES;  // slot of step s
+            constexpr unsigned RB = (unsigned)(R * SL::BYTES);
+            auto body = [&](int s, In &cur, In &nxt) {
+                if (TRACE && lane == 0 && wave == 0 && s == 0) a.trace[8 * t + 1] = __builtin_amdgcn_s_memrealtime();
+                if (trs && wave == 0 && s >= 0 && s < T) ts[8 * s] = __builtin_amdgcn_s_memtime();
+                const unsigned sn = so + SL::BYTES == RB ? 0u : so + SL::BYTES;  // slot of step s+1
+                const double kx = wave == 0 ? reinterpret_cast<const double *>(ring + so + SL::KFIN)[lane]
+                                            : res[((s - 1) & (RS - 1)) * P * 64 + (p0 - 1) * 64 + lane];
+                asm volatile("" ::: "memory");  // kx's read is issued first (LDS returns in order)
+                load(sn, nxt);
+#pragma unroll
+                for (int u = 0; u < PC; u++) {
+                    const int y = s - p0 - u;  // lane 0's row; bit = 0 <= y < nx, in integer ops (SALU)
+                    const unsigned bit = ((unsigned)((y - nx) & ~y)) >> 31;
+                    hw[u] = ((hw[u] << 1) | (uint64_t)bit) & pm[u];
+                }
+                if (s >= 0 && s < T) {
+                    double xn[PC];
+#pragma unroll
+                    for (int u = PC - 1; u >= 0; u--) {
+                        const uint64_t m = hw[u];
+                        const double xk = u > 0 ? xc[u - 1] : kx;
+                        const double xj = dpp_shr1(xc[u], cur.jv[u]);
+                        double v = cur.rh[u] - cur.ck[u] * xk;
+                        v = v - cur.cj[u] * xj;
+                        v = v - cur.ci[u] * xc[u];
+                        if constexpr (NA == 4) v = v / cur.dg[u];
+                        xn[u] = sel_lanes(m, v, xc[u]);
+                    }
+                    if (uk >= 0) {  // uniform
+                        const int q = s + 1 - np;
+                        uint64_t m = hw[0];
+                        double v = xn[0];
+#pragma unroll
+                        for (int u = 1; u < PC; u++)
+                            if (uk == u) m = hw[u], v = xn[u];
+                        int vo = lane * 8;
+                        asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(vo) : "v"(OOB), "v"(vo), "s"(m));
+                        __builtin_amdgcn_raw_buffer_store_b64(split64((uint64_t)__double_as_longlong(v)), hko, vo,
+                                                              q >= 0 ? q * 512 : OOB, 16);  // sc1
+                    }
+                    if (jout) {
+                        const int q = s + 1 - nj;
+                        const int sof = q >= 0 ? (q * P + p0) * 8 : OOB;
+                        if constexpr (PC == 2) {
+                            const uint64_t b0 = (uint64_t)__double_as_longlong(xn[0]);
+                            const uint64_t b1 = (uint64_t)__double_as_longlong(xn[1]);
+                            line_v4u d4;
+                            d4.x = (unsigned)b0;
+                            d4.y = (unsigned)(b0 >> 32);
+                            d4.z = (unsigned)b1;
+                            d4.w = (unsigned)(b1 >> 32);
+                            __builtin_amdgcn_raw_buffer_store_b128(d4, hjo, jl_off, sof, 16);
+                        } else {
+#pragma unroll
+                            for (int u = 0; u < PC; u++)
+                                __builtin_amdgcn_raw_buffer_store_b64(split64((uint64_t)__double_as_longlong(xn[u])), hjo,
+                                                                      jl_off + 8 * u, sof, 16);
+                        }
+                    }
+                    if (trs && wave == 0 && s >= 0 && s < T) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
+#pragma unroll
+                    for (int u = 0; u < PC; u++) {
+                        xc[u] = xn[u];
+                        res[((s & (RS - 1)) * P + p0 + u) * 64 + lane] = xc[u];
+                    }
+                }
+                so = sn;
+                if (trs && s >= 0 && s < T) ts[8 * s + (wave == 0 ? 1 : 7)] = __builtin_amdgcn_s_memtime();
+                line_barrier();
+            };
+            for (int s = S0; s <= T; s += 2) {
+                body(s, A, B);
+                if (s + 1 <= T) body(s + 1, B, A);
+            }
+            if (TRACE && lane == 0 && wave == 0) {
+                a.trace[8 * t + 2] = __builtin_amdgcn_s_memrealtime();
+                unsigned xcc;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                a.trace[8 * t + 4] = xcc;
+            }
+          }
+        } else if (wave < CW) {
             if (LINE_COMP_PRIO) __builtin_amdgcn_s_setprio(LINE_COMP_PRIO);
             // ---------------- compute: planes p0 .. p0+PC-1 ----------------
             // Coefficients and rhs of step s+1 are read from LDS at the start of
@@ -575,6 +740,8 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
             const int p0 = wave * PC;
             struct In {
                 double ck[PC], cj[PC], ci[PC], dg[PC], rh[PC], jv[PC];
+                double rc[PC];  // LINE_FASTDIV: RN(1 / dg), formed one step ahead
+                bool dok[PC];   // dg inside the range where the fast quotient is exact
             };
             auto load = [&](int s, In &in) {
                 const char *slot = ring + (s % R) * SL::BYTES;
@@ -597,6 +764,9 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
             double xc[PC];
 #pragma unroll
             for (int u = 0; u < PC; u++) xc[u] = 0.0;
+            In A, B;  // step s uses the set loaded at step s-1: even steps A, odd steps B
+#pragma unroll
+            for (int u = 0; u < PC; u++) A.rc[u] = B.rc[u] = 1.0, A.dg[u] = B.dg[u] = 1.0, A.dok[u] = B.dok[u] = true;
             // hand-off outputs, stored here (sc1) as soon as computed: this wave
             // never waits on its VMEM queue, so the stores cost it nothing.  Buffer
             // stores: a lane with nothing to store gets an out-of-range offset and
@@ -632,9 +802,20 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                         double v = cur.rh[u] - cur.ck[u] * xk;
                         v = v - cur.cj[u] * xj;
                         v = v - cur.ci[u] * xc[u];
-                        if constexpr (NA == 4) v = v / cur.dg[u];
+                        if constexpr (NA == 4) {
+                            if constexpr (LINE_FASTDIV) {
+                                const double q = div_rn(v, cur.dg[u], cur.rc[u]);
+                                const bool ok = !valid || (cur.dok[u] && div_num_ok(v));  // rows that do not exist keep their old value
+                                v = __builtin_expect(__all(ok), 1) ? q : (ok ? q : v / cur.dg[u]);
+                            } else {
+                                v = v / cur.dg[u];
+                            }
+                        }
                         xn[u] = sel_lanes(__builtin_amdgcn_ballot_w64(valid), v, xc[u]);
-                        if (kout && p == np - 1) {  // uniform: the tile's last plane feeds the next k-tile
+                        if (LINE_KOUT_BF) {  // branch-free: off-tile lanes and tiles without a k-output drop the store
+                            const int ko = (kout && p == np - 1 && valid) ? ((s + 1 - np) * 64 + lane) * 8 : OOB;
+                            __builtin_amdgcn_raw_buffer_store_b64(split64(canon_bits(xn[u])), hko, ko, 0, 16);  // sc1
+                        } else if (kout && p == np - 1) {  // uniform: the tile's last plane feeds the next k-tile
                             const int ko = valid ? ((s + 1 - np) * 64 + lane) * 8 : OOB;
                             __builtin_amdgcn_raw_buffer_store_b64(split64(canon_bits(xn[u])), hko, ko, 0, 16);  // sc1
                         }
@@ -664,10 +845,17 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                         res[((s & (RS - 1)) * P + p0 + u) * 64 + lane] = xc[u];
                     }
                 }
+                if constexpr (NA == 4 && LINE_FASTDIV) {
+                    // the next step's reciprocals, off this step's dependency chain
+#pragma unroll
+                    for (int u = 0; u < PC; u++) {
+                        nxt.rc[u] = 1.0 / nxt.dg[u];
+                        nxt.dok[u] = div_den_ok(nxt.dg[u]);
+                    }
+                }
                 if (trs && s >= 0 && s < T) ts[8 * s + (wave == 0 ? 1 : 7)] = __builtin_amdgcn_s_memtime();
                 line_barrier();
             };
-            In A, B;  // step s uses the set loaded at step s-1: even steps A, odd steps B
             for (int s = S0; s <= T; s += 2) {
                 body(s, A, B);
                 if (s + 1 <= T) body(s + 1, B, A);
@@ -940,7 +1128,11 @@ constexpr int LINE_D = 10;
 #else
 constexpr int LINE_D = LINE_D_OVERRIDE;
 #endif
+#ifndef LINE_PC_OVERRIDE
 constexpr int LINE_CW = LINE_P / 2, LINE_NL = 4, LINE_SW = 2;  // two planes per compute wave
+#else
+constexpr int LINE_CW = LINE_P / LINE_PC_OVERRIDE, LINE_NL = 4, LINE_SW = 2;
+#endif
 
 template <int NA, bool RHS_NAT, int OUT, bool TRACE>
 static int launch_line_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)

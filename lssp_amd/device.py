@@ -112,6 +112,10 @@ class Device:
     def barrier(self):
         _ck(self.L.lssp_amd_comm_barrier(self.h), "barrier")
 
+    def comm_selftest(self):
+        """all-gather + grouped send/recv ring through the configured transport, checked"""
+        _ck(self.L.lssp_amd_comm_selftest(self.h), "comm_selftest")
+
 
 def comm_unique_id() -> bytes:
     L = _lib.load()

@@ -190,3 +190,26 @@ def test_dist_upload_bad_input_fails_on_every_rank(bad_rank):
             p.join(timeout=30)
     assert got == {0: 1, 1: 1}
     assert all(p.exitcode == 0 for p in procs)
+
+
+def test_rccl_one_rank_transport_selftest():
+    """The RCCL branch of the transport on one GPU: a real 1-rank communicator
+    (lssp_amd_comm_init with nranks = 1), then lssp_amd_comm_selftest drives
+    ncclAllGather and a grouped ncclSend/ncclRecv round to itself on the
+    communication stream between the same two events spmv_halo uses, and
+    checks every word.  A single-rank solve on the same context afterwards is
+    still bitwise the oracle (the communicator does not change its path)."""
+    import lssp_amd
+    dev = lssp_amd.Device(0)
+    try:
+        dev.comm_init(1, 0, lssp_amd.comm_unique_id())
+        dev.comm_selftest()
+        dev.comm_selftest()  # the events and comm stream are reusable
+        A = O.poisson(3, 16)
+        Ad = lssp_amd.DMat(dev, A.Ap, A.Aj, A.Ax)
+        x, b = dev.vec(A.n, np.zeros(A.n)), dev.vec(A.n, np.ones(A.n))
+        r = lssp_amd.solve(dev, Ad, None, x, b, solver=lssp_amd.CG, maxit=30, trace_cap=256)
+        o = O.solve(O.CG, A, np.ones(A.n), maxit=30, mode=O.TREE)
+        assert r.nits == o.nits and np.array_equal(r.trace, o.trace) and np.array_equal(x.download(), o.x)
+    finally:
+        dev.close()
