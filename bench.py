@@ -198,6 +198,33 @@ def main():
     apply_b = ilu_apply_bytes(M.nnzL, M.nnzU, nl)
     apply_gbs = apply_b / (apply_ms * 1e-3) / 1e9
 
+    # ---- measured HBM copy peak ("also record a measured copy-kernel
+    # peak"): 2^27 doubles (1 GiB) copied, read + write bytes over HIP-event
+    # time; the best of torch's vectorised copy and the library's vec_copy ----
+    peak_measured = None
+    if rank == 0:
+        nc = 1 << 27
+        src = torch.empty(nc, dtype=torch.float64, device=f"cuda:{gpu}").uniform_(-1, 1)
+        dst = torch.empty_like(src)
+        best = 0.0
+        for how in ("torch", "lssp"):
+            def cp():
+                if how == "torch":
+                    dst.copy_(src)
+                else:
+                    dev.L.lssp_amd_vec_copy(dev.h, dst.data_ptr(), src.data_ptr(), nc)
+            st = torch.cuda.current_stream() if how == "torch" else stream
+            for _ in range(3):
+                cp()
+            e0.record(st)
+            for _ in range(10):
+                cp()
+            e1.record(st)
+            e1.synchronize()
+            best = max(best, 16.0 * nc / (e0.elapsed_time(e1) / 10 * 1e-3) / 1e9)
+        peak_measured = round(best, 1)
+        del src, dst
+
     # ---- BiCGSTAB steps ----
     def run(iters):
         return lssp_amd.solve(dev, A, M, x, b, solver=lssp_amd.BICGSTAB, tol_rel=0.0, tol_abs=0.0, tol_rb=0.0,
@@ -257,11 +284,15 @@ def main():
                          "kernel": "ILU(0) apply = k_line_rhs (rhs -> the L sweep's stream) + k_line (L sweep "
                                    "-> the U sweep's rhs stream) + k_line (U sweep -> x in natural order); "
                                    "latency-bound: 2 x 646 dependent levels",
-                         "bytes_per_launch": apply_b, "ms_per_launch": round(apply_ms, 5)},
+                         "bytes_per_launch": apply_b, "ms_per_launch": round(apply_ms, 5),
+                         "peak_measured": peak_measured,
+                         "frac_of_measured_peak": round(apply_gbs / peak_measured, 4) if peak_measured else None},
             "roofline_spmv": {"bound": "hbm", "achieved": round(spmv_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(spmv_gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("k_spmv3"),
                               "kernel": f"k_spmv3<EPI_MXY,0,{'true' if ndiag else 'false'}> (y = A x)",
-                              "bytes_per_launch": spmv_b, "ms_per_launch": round(spmv_ms, 5)},
+                              "bytes_per_launch": spmv_b, "ms_per_launch": round(spmv_ms, 5),
+                              "peak_measured": peak_measured,
+                              "frac_of_measured_peak": round(spmv_gbs / peak_measured, 4) if peak_measured else None},
             "ilu": {"levels_L": M.levelsL, "levels_U": M.levelsU, "setup_s": round(M.setup_seconds, 3)},
             "setup_s": round(t_setup, 2),
         }

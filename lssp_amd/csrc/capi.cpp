@@ -215,7 +215,7 @@ int build_diag_ids(lssp_amd_mat *M, const int *Ap, const int *Aj)
 // The x spans of the 1024-row blocks of k_spmv_win (kernels.hip), for matrices
 // the diagonal-id coding does not cover (more than 255 offsets) whose rows
 // nevertheless stay near the diagonal (locally renumbered meshes: config 5).
-int build_windows(lssp_amd_mat *M, const int *Ap, const int *Aj)
+int build_windows(lssp_amd_mat *M, const int *Ap, const int *Aj, const double *Ax)
 {
     const int n = M->nrows;
     if (M->ndiag > 0 || M->nnz == 0 || n == 0) return LSSP_AMD_OK;
@@ -237,9 +237,67 @@ int build_windows(lssp_amd_mat *M, const int *Ap, const int *Aj)
         }
     }, 16);
     if (wide) return LSSP_AMD_OK;
-    LSSP_HIP(hipMalloc(&M->d_win, sizeof(int) * win.size()));
-    LSSP_HIP(hipMemcpy(M->d_win, win.data(), sizeof(int) * win.size(), hipMemcpyHostToDevice));
-    return LSSP_AMD_OK;
+    // the sliced copy (lssp_amd_mat::s_ax ...): rows of a block stably sorted
+    // by descending length, so a 64-row slice pads to its longest row and every
+    // load of k_spmv_sell is one coalesced wave access
+    constexpr int NS = WIN_ROWS / 64;
+    std::vector<uint16_t> order((size_t)nb * WIN_ROWS);
+    std::vector<int> slen((size_t)nb * NS);
+    std::vector<uint32_t> srow((size_t)nb * WIN_ROWS);
+    parallel_for(nb, [&](long b0, long b1) {
+        std::vector<int> len(WIN_ROWS);
+        for (long b = b0; b < b1; b++) {
+            const long r0 = b * WIN_ROWS;
+            const int cnt = (int)std::min<long>(WIN_ROWS, n - r0);
+            uint16_t *ord = order.data() + r0;
+            for (int q = 0; q < WIN_ROWS; q++) {
+                len[q] = q < cnt ? Ap[r0 + q + 1] - Ap[r0 + q] : 0;
+                ord[q] = (uint16_t)q;
+            }
+            std::stable_sort(ord, ord + WIN_ROWS, [&](uint16_t x, uint16_t y) { return len[x] > len[y]; });
+            for (int t = 0; t < WIN_ROWS; t++) srow[r0 + t] = (uint32_t)ord[t] | ((uint32_t)len[ord[t]] << 10);
+            for (int w = 0; w < NS; w++) slen[b * NS + w] = len[ord[64 * w]];
+        }
+    }, 16);
+    std::vector<int> meta(2 * slen.size());
+    long tot = 0;
+    for (size_t q = 0; q < slen.size(); q++) {
+        meta[2 * q] = (int)tot;
+        meta[2 * q + 1] = slen[q];
+        tot += 64L * ((slen[q] + 1) & ~1);
+        if (tot > INT_MAX / 2) return LSSP_AMD_OK;  // too large for 32-bit slice offsets: k_spmv3 serves it
+    }
+    constexpr int NPAD = 64 * 16;  // the kernel's unconditional preload may read past the last slice
+    std::vector<double> sax((size_t)tot + NPAD, 0.0);
+    std::vector<uint32_t> scol((size_t)tot / 2 + NPAD / 2, 0u);
+    parallel_for(nb, [&](long b0, long b1) {
+        for (long b = b0; b < b1; b++) {
+            const long r0 = b * WIN_ROWS;
+            const int lo2 = win[2 * b] & ~1;
+            for (int w = 0; w < NS; w++) {
+                const long base = meta[2 * (b * NS + w)];
+                for (int l = 0; l < 64; l++) {
+                    const int q = order[r0 + 64 * w + l];
+                    if (r0 + q >= n) continue;
+                    const int e0 = Ap[r0 + q], len = Ap[r0 + q + 1] - e0;
+                    for (int k = 0; k < len; k++) {
+                        sax[base + 64L * k + l] = Ax[e0 + k];
+                        scol[base / 2 + 64L * (k >> 1) + l] |= (uint32_t)(Aj[e0 + k] - lo2) << (16 * (k & 1));
+                    }
+                }
+            }
+        }
+    }, 16);
+    auto up = [](void **d, const void *h, size_t bytes) -> int {
+        LSSP_HIP(hipMalloc(d, bytes));
+        LSSP_HIP(hipMemcpy(*d, h, bytes, hipMemcpyHostToDevice));
+        return LSSP_AMD_OK;
+    };
+    LSSP_TRY(up((void **)&M->d_win, win.data(), sizeof(int) * win.size()));
+    LSSP_TRY(up((void **)&M->s_meta, meta.data(), sizeof(int) * meta.size()));
+    LSSP_TRY(up((void **)&M->s_row, srow.data(), sizeof(uint32_t) * srow.size()));
+    LSSP_TRY(up((void **)&M->s_ax, sax.data(), sizeof(double) * sax.size()));
+    return up((void **)&M->s_col, scol.data(), sizeof(uint32_t) * scol.size());
 }
 
 double wall_time()
@@ -391,7 +449,7 @@ static int upload_csr(lssp_amd_mat *M, const int *Ap, const int *Aj, const doubl
         LSSP_HIP(hipMemcpy(M->Ax, Ax, sizeof(double) * M->nnz, hipMemcpyHostToDevice));
     }
     LSSP_TRY(build_diag_ids(M, Ap, Aj));
-    return build_windows(M, Ap, Aj);
+    return build_windows(M, Ap, Aj, Ax);
 }
 
 int lssp_amd_mat_upload(lssp_amd_ctx *c, int nrows, int ncols, int nnz, const int *Ap, const int *Aj,
@@ -425,6 +483,8 @@ int lssp_amd_mat_destroy(lssp_amd_mat *M)
     if (M->Ad) (void)hipFree(M->Ad);
     if (M->d_off) (void)hipFree(M->d_off);
     if (M->d_win) (void)hipFree(M->d_win);
+    for (void *p : {(void *)M->s_ax, (void *)M->s_col, (void *)M->s_row, (void *)M->s_meta})
+        if (p) (void)hipFree(p);
     if (M->d_send_idx) (void)hipFree(M->d_send_idx);
     if (M->d_send_buf) (void)hipFree(M->d_send_buf);
     delete M;

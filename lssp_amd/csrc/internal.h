@@ -115,6 +115,17 @@ struct lssp_amd_mat {
     // span of at most WIN_CAP entries, d_win[2b], d_win[2b+1] = that span
     // [lo, hi) and the product stages x[lo, hi) in LDS; nullptr: not windowed
     int *d_win = nullptr;
+    // the sliced copy of a windowed matrix that k_spmv_sell reads (build_windows):
+    // each 1024-row block's rows sorted by length (stable, descending) into 16
+    // slices of 64 rows; slice s keeps entry k of lane l's row at
+    // s_meta[2s] + 64 k + l (s_ax) and its column, as a 16-bit offset from the
+    // block's staging base (lo rounded down to even), in half (k & 1) of the
+    // 32-bit word s_meta[2s] / 2 + 64 (k >> 1) + l (s_col); s_meta[2s + 1] is
+    // the slice's longest row; s_row[64 w + l] = local row | length << 10 of
+    // thread 64 w + l of its block
+    double *s_ax = nullptr;
+    uint32_t *s_col = nullptr, *s_row = nullptr;
+    int *s_meta = nullptr;
     // distributed layout
     int n_global = 0, row0 = 0, nhalo = 0;
     // halo exchange plan: for each peer, indices (local) to send and the count to receive
@@ -239,7 +250,7 @@ namespace lssp_amd {
 // ---- kernel launchers (kernels.hip) ------------------------------------------
 enum Epi { EPI_MXY = 0, EPI_AMXY, EPI_AXPBY, EPI_AMX };  // see spmv kernel
 int build_diag_ids(lssp_amd_mat *M, const int *Ap, const int *Aj);
-int build_windows(lssp_amd_mat *M, const int *Ap, const int *Aj);
+int build_windows(lssp_amd_mat *M, const int *Ap, const int *Aj, const double *Ax);
 constexpr int WIN_ROWS = 1024, WIN_CAP = 16384;
 int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, const double *x,
                 double beta, const double *y, double *z, int nred, const double *w0,

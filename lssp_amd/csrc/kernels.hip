@@ -443,19 +443,24 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
 // into LDS with coalesced loads, then each lane forms its row's products from
 // LDS.  The gathers of a locally shuffled numbering (config 5) each hit a
 // separate L2 line when read from memory; from LDS they cost a bank access.
-// Same per-row arithmetic as k_spmv3 (products in CSR order onto 0.0), same
-// 256-row chunk partials.  Every global load is issued before the one
-// barrier, as 16-byte vectors: the x span (from lo rounded down to even;
-// 32.4 -> 31.1 us on config 5 against scalar loads) and each lane's first 8
-// row entries (5 Ax + 3 Aj vectors shifted into place by the row's alignment;
-// 35.8 -> 33.5 us against 8 + 8 scalar loads).  Staging the block's Aj / Ax
-// through LDS as well (a second LDS phase) measured slower, 37 -> 47 us: with
-// 128 KB of LDS one workgroup holds a CU, and every extra barrier phase is
-// exposed latency.
+// The entries come from the matrix's sliced copy (lssp_amd_mat::s_ax ...):
+// the block's rows sorted by length into 64-row slices, entry k of every row
+// of a slice in one contiguous 64-lane column, so each load is one coalesced
+// wave access (the CSR rows of a wave start at scattered offsets, and their
+// per-lane loads were the larger half of the kernel's time).  The column is a
+// 16-bit offset into the staged span.  A lane adds its row's products in CSR
+// order onto 0.0 -- the arithmetic of k_spmv3 -- and writes the sum to LDS at
+// the row's place in the block; after a barrier thread t takes row t, so the
+// output store and the fused dots' 256-row chunk partials are those of the
+// natural order.  Every global load is issued before the first barrier.
 template <int EPI, int NRED>
-__global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *win, long nblk, long nnz_pad)
+__global__ __launch_bounds__(WIN_ROWS) void k_spmv_sell(SpmvArgs a, const int *win, const double *__restrict__ sax,
+                                                        const uint32_t *__restrict__ scol,
+                                                        const uint32_t *__restrict__ srow,
+                                                        const int *__restrict__ smeta, long nblk)
 {
     __shared__ __attribute__((aligned(16))) double sxw[WIN_CAP];
+    __shared__ double zb[WIN_ROWS];
     __shared__ double lds[4][MAX_SLOTS][4];
     if (a.guard && *a.guard != 0.0) return;
     const long per = gridDim.x / 8;
@@ -464,10 +469,9 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *wi
     const int tid = threadIdx.x;
     const int r = (int)(blk * WIN_ROWS) + tid;
     const int lo = win[2 * blk], span = win[2 * blk + 1] - lo;
-    // x span, row bounds, the row's first 8 entries and the dot operands, all in flight at once
+    // x span: staged from lo2 = lo rounded down to even, as 16-byte vectors when
+    // x is 16-byte aligned (uniform); the last odd entry alone (nothing past hi is read)
     constexpr int NS = WIN_CAP / WIN_ROWS;
-    // staged from lo2 = lo rounded down to even, as 16-byte vectors when x is
-    // 16-byte aligned (uniform); the last odd entry alone (nothing past hi is read)
     typedef double dbl2w_t __attribute__((ext_vector_type(2)));
     const int hi = lo + span, lo2 = lo & ~1;
     const bool xv16 = (reinterpret_cast<uintptr_t>(a.x) & 15) == 0;
@@ -481,55 +485,21 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *wi
             else xs[u] = dbl2w_t{e >= lo ? a.x[e] : 0.0, e + 1 < hi ? a.x[e + 1] : 0.0};
         }
     }
+    // this wave's slice; its first NK entries per lane, unconditionally (the
+    // arrays are padded past the last slice)
+    const int lane = tid & 63;
+    const long sl = blk * (WIN_ROWS / 64) + (tid >> 6);
+    const int sbase = __builtin_amdgcn_readfirstlane(smeta[2 * sl]);
+    const uint32_t ri = srow[blk * WIN_ROWS + tid];
+    const int len = (int)(ri >> 10), lr = (int)(ri & 1023);
+    constexpr int NK = 10;
+    double ax[NK];
+    uint32_t cw[NK / 2];
+#pragma unroll
+    for (int k = 0; k < NK / 2; k++) cw[k] = scol[sbase / 2 + 64 * k + lane];
+#pragma unroll
+    for (int k = 0; k < NK; k++) ax[k] = sax[sbase + 64 * k + lane];
     const int rr = min(r, a.nrows - 1);
-    const int rb = a.Ap[rr], re = a.Ap[rr + 1];
-    const int len = r < a.nrows ? re - rb : 0;
-    int cj[8];
-    double cx[8];
-    {
-        // the row's first 8 entries as 16-byte vectors (5 for Ax, 3 for Aj,
-        // clamped to the padded arrays), then shifted by the row's alignment
-        typedef double dbl2_t __attribute__((ext_vector_type(2)));
-        typedef int int4_t __attribute__((ext_vector_type(4)));
-        const dbl2_t *X2 = reinterpret_cast<const dbl2_t *>(a.Ax);
-        const int4_t *J4 = reinterpret_cast<const int4_t *>(a.Aj);
-        const long x0 = rb >> 1, j0 = rb >> 2;
-        dbl2_t vx[5];
-        int4_t vj[3];
-#pragma unroll
-        for (int u = 0; u < 5; u++) vx[u] = X2[min(x0 + u, (nnz_pad >> 1) - 1)];
-#pragma unroll
-        for (int u = 0; u < 3; u++) vj[u] = J4[min(j0 + u, (nnz_pad >> 2) - 1)];
-        double ex[10];
-        int ej[12];
-#pragma unroll
-        for (int u = 0; u < 5; u++) {
-            ex[2 * u] = vx[u].x;
-            ex[2 * u + 1] = vx[u].y;
-        }
-#pragma unroll
-        for (int u = 0; u < 3; u++) {
-            ej[4 * u] = vj[u].x;
-            ej[4 * u + 1] = vj[u].y;
-            ej[4 * u + 2] = vj[u].z;
-            ej[4 * u + 3] = vj[u].w;
-        }
-        // shifts as bit blends between fixed registers: a select the compiler
-        // may fold into an indexed read of the array, which would spill it
-        const int m1 = -(rb & 1), m2 = -((rb >> 1) & 1);
-        const uint64_t q1 = (uint64_t)(int64_t)m1;
-        int tj[10];
-#pragma unroll
-        for (int u = 0; u < 10; u++) tj[u] = ej[u] ^ ((ej[u] ^ ej[u + 2]) & m2);
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const uint64_t b0 = __builtin_bit_cast(uint64_t, ex[u]), b1 = __builtin_bit_cast(uint64_t, ex[u + 1]);
-            const double xv = __builtin_bit_cast(double, b0 ^ ((b0 ^ b1) & q1));
-            const int jv = tj[u] ^ ((tj[u] ^ tj[u + 1]) & m1);
-            cj[u] = u < len ? jv : lo;
-            cx[u] = u < len ? xv : 0.0;
-        }
-    }
     double w0p = 0.0, w1p = 0.0;
     if (NRED > 0) {
         if (a.w0 != a.z) w0p = a.w0[rr];
@@ -540,16 +510,16 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *wi
         if (lo2 + 2 * (tid + WIN_ROWS * u) < hi) reinterpret_cast<dbl2w_t *>(sxw)[tid + WIN_ROWS * u] = xs[u];
     __syncthreads();
     double sum = 0;
-    if (len <= 8) {
-        double pr[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) pr[u] = sxw[cj[u] - lo2] * cx[u];
-#pragma unroll
-        for (int u = 0; u < 8; u++)
-            if (u < len) sum += pr[u];
-    } else {
-        for (int k = rb; k < re; k++) sum += sxw[a.Aj[k] - lo2] * a.Ax[k];
+    for (int k = 0; k < NK; k++)
+        if (k < len) sum += sxw[(cw[k >> 1] >> (16 * (k & 1))) & 0xffffu] * ax[k];
+    for (int k = NK; k < len; k++) {  // rows longer than NK entries
+        const uint32_t c = scol[sbase / 2 + 64 * (k >> 1) + lane];
+        sum += sxw[(c >> (16 * (k & 1))) & 0xffffu] * sax[sbase + 64L * k + lane];
     }
+    zb[lr] = sum;
+    __syncthreads();
+    sum = zb[tid];
     double zv = 0;
     if (r < a.nrows) {
         if (EPI == EPI_MXY) zv = sum;
@@ -568,11 +538,11 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *wi
             for (int q = 0; q < NRED; q++) v[q] = 0.0;
         }
         // chunk_reduce's order for each of the 4 chunks (waves 4q .. 4q+3)
-        const int lane = tid & 63, wave = tid >> 6, q = wave >> 2;
+        const int wave = tid >> 6, q = wave >> 2;
 #pragma unroll
         for (int t = 0; t < NRED; t++) {
-            const double s = wave_sum(v[t]);
-            if (lane == 0) lds[q][t][wave & 3] = s;
+            const double sv = wave_sum(v[t]);
+            if (lane == 0) lds[q][t][wave & 3] = sv;
         }
         __syncthreads();
         const long chunk = blk * 4 + (tid >> 8);
@@ -586,13 +556,13 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_win(SpmvArgs a, const int *wi
 }
 
 template <int EPI>
-static void spmv_win_dispatch(const SpmvArgs &a, const int *win, int nred, hipStream_t s, long nnz_pad)
+static void spmv_sell_dispatch(const SpmvArgs &a, const lssp_amd_mat *A, int nred, hipStream_t s)
 {
     const long nb = (a.nrows + WIN_ROWS - 1) / WIN_ROWS;
     const long g = (nb + 7) / 8 * 8;
-    if (nred == 0) k_spmv_win<EPI, 0><<<g, WIN_ROWS, 0, s>>>(a, win, nb, nnz_pad);
-    else if (nred == 1) k_spmv_win<EPI, 1><<<g, WIN_ROWS, 0, s>>>(a, win, nb, nnz_pad);
-    else k_spmv_win<EPI, 2><<<g, WIN_ROWS, 0, s>>>(a, win, nb, nnz_pad);
+    if (nred == 0) k_spmv_sell<EPI, 0><<<g, WIN_ROWS, 0, s>>>(a, A->d_win, A->s_ax, A->s_col, A->s_row, A->s_meta, nb);
+    else if (nred == 1) k_spmv_sell<EPI, 1><<<g, WIN_ROWS, 0, s>>>(a, A->d_win, A->s_ax, A->s_col, A->s_row, A->s_meta, nb);
+    else k_spmv_sell<EPI, 2><<<g, WIN_ROWS, 0, s>>>(a, A->d_win, A->s_ax, A->s_col, A->s_row, A->s_meta, nb);
 }
 
 template <int EPI, bool CMP>
@@ -626,10 +596,10 @@ int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, c
                A->Ad, A->d_off, A->ndiag, c->guard, cb};
     if (A->d_win && nb == nall) {
         switch (epi) {
-        case EPI_MXY: spmv_win_dispatch<EPI_MXY>(a, A->d_win, nred, c->stream, A->nnz + 4L); break;
-        case EPI_AMXY: spmv_win_dispatch<EPI_AMXY>(a, A->d_win, nred, c->stream, A->nnz + 4L); break;
-        case EPI_AXPBY: spmv_win_dispatch<EPI_AXPBY>(a, A->d_win, nred, c->stream, A->nnz + 4L); break;
-        default: spmv_win_dispatch<EPI_AMX>(a, A->d_win, nred, c->stream, A->nnz + 4L); break;
+        case EPI_MXY: spmv_sell_dispatch<EPI_MXY>(a, A, nred, c->stream); break;
+        case EPI_AMXY: spmv_sell_dispatch<EPI_AMXY>(a, A, nred, c->stream); break;
+        case EPI_AXPBY: spmv_sell_dispatch<EPI_AXPBY>(a, A, nred, c->stream); break;
+        default: spmv_sell_dispatch<EPI_AMX>(a, A, nred, c->stream); break;
         }
         LSSP_HIP(hipGetLastError());
         return LSSP_AMD_OK;

@@ -1129,10 +1129,16 @@ constexpr int LINE_D = 10;
 constexpr int LINE_D = LINE_D_OVERRIDE;
 #endif
 #ifndef LINE_PC_OVERRIDE
-constexpr int LINE_CW = LINE_P / 2, LINE_NL = 4, LINE_SW = 2;  // two planes per compute wave
+constexpr int LINE_CW = LINE_P / 2;  // two planes per compute wave
 #else
-constexpr int LINE_CW = LINE_P / LINE_PC_OVERRIDE, LINE_NL = 4, LINE_SW = 2;
+constexpr int LINE_CW = LINE_P / LINE_PC_OVERRIDE;
 #endif
+#ifndef LINE_NL_OVERRIDE
+constexpr int LINE_NL = 4;
+#else
+constexpr int LINE_NL = LINE_NL_OVERRIDE;
+#endif
+constexpr int LINE_SW = 2;
 
 template <int NA, bool RHS_NAT, int OUT, bool TRACE>
 static int launch_line_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)
