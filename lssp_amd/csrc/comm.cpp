@@ -107,6 +107,11 @@ int comm_allgather_sums(lssp_amd_ctx *c, int nslot)
     return xfer_allgather(c, c->d_sums, c->d_gather, (long)sizeof(double) * MAX_SLOTS);
 }
 
+int comm_allgather(lssp_amd_ctx *c, const void *send, void *recv, long bytes)
+{
+    return xfer_allgather(c, send, recv, bytes);
+}
+
 int comm_carry_in(lssp_amd_ctx *c)
 {
     const long bytes = (long)sizeof(double) * MAX_SLOTS;

@@ -354,6 +354,9 @@ int reduce_dots(lssp_amd_ctx *c, long n, int nslot, const double *const *a,
                 const double *const *b, const Fin &f);
 // multi-rank: all-gather rank sums and sum in rank order, then the finalize
 int comm_allgather_sums(lssp_amd_ctx *c, int nslot);
+// recv (nranks * bytes, rank order) = every rank's send (bytes), through the
+// context's transport (RCCL or the host hooks)
+int comm_allgather(lssp_amd_ctx *c, const void *send, void *recv, long bytes);
 // serial mode, P ranks: receive the running sums of rank-1 (zeros on rank 0)
 // into c->d_carry / pass this rank's on to rank+1
 int comm_carry_in(lssp_amd_ctx *c);

@@ -406,12 +406,6 @@ __device__ __forceinline__ double sel_lanes(uint64_t m, double t, double f)
     asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(hi) : "v"((int)(fb >> 32)), "v"((int)(tb >> 32)), "s"(m));
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
-// a published value never carries the flag pattern
-__device__ __forceinline__ uint64_t canon_bits(double v)
-{
-    const uint64_t b = (uint64_t)__double_as_longlong(v);
-    return b == TRI_SENTINEL ? 0x7FF8000000000000ull : b;
-}
 typedef unsigned int line_v2u __attribute__((ext_vector_type(2)));
 typedef unsigned int line_v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ line_v2u split64(uint64_t b)
@@ -438,38 +432,6 @@ __device__ __forceinline__ void static_for(F &&f)
         static_for<I + 1, N>(f);
     }
 }
-
-#ifndef LINE_FASTDIV
-#define LINE_FASTDIV 0
-#endif
-#ifndef LINE_FASTCOMP
-#define LINE_FASTCOMP 0
-#endif
-#ifndef LINE_KOUT_BF
-#define LINE_KOUT_BF 0
-#endif
-// a / b correctly rounded from y = RN(1 / b) (formed off the critical path):
-// q0 = RN(a y) is within 1.5 ulp of a / b; one correction with the exact
-// remainder (FMA) brings it within 1 ulp, and a second one rounds correctly
-// (Markstein: y within 1/2 ulp of 1/b, q within 1 ulp of a/b, r = a - b q
-// exact => RN(q + r y) = RN(a / b)).  Exact only without underflow or
-// overflow anywhere: the callers take it for |a|, |b| in [2^-300, 2^300]
-// (a != 0) and use the true division otherwise.
-__device__ __forceinline__ double div_rn(double a, double b, double y)
-{
-    double q = a * y;
-    double r = __builtin_fma(-b, q, a);
-    q = __builtin_fma(r, y, q);
-    r = __builtin_fma(-b, q, a);
-    return __builtin_fma(r, y, q);
-}
-__device__ __forceinline__ bool div_range_ok(double v)
-{
-    const unsigned e = ((unsigned)(__double_as_longlong(v) >> 52)) & 0x7ffu;
-    return e - (1023u - 300u) <= 600u;
-}
-__device__ __forceinline__ bool div_num_ok(double a) { return div_range_ok(a); }
-__device__ __forceinline__ bool div_den_ok(double b) { return div_range_ok(b); }
 
 // slot layout (bytes): the step's coefficient block, its rhs, the hand-off inputs
 template <int P, int NA, bool RHS_NAT>
@@ -517,9 +479,6 @@ constexpr int LINE_RW = 6;  // rhs wave: a run block's loads land LINE_RW steps 
 // it, so they keep 0 / 0).  -DLINE_POLL_PRIO / -DLINE_LOAD_SLEEP override both.
 #ifndef LINE_STORE_SLEEP
 #define LINE_STORE_SLEEP 0  // tuning: storers' delay before their stores (64 clk units)
-#endif
-#ifndef LINE_COMP_PRIO
-#define LINE_COMP_PRIO 0  // tuning: compute waves' priority
 #endif
 #ifndef LINE_RHS_SLEEP
 #define LINE_RHS_SLEEP 0  // tuning: rhs wave's delay before its loads
@@ -595,12 +554,16 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
         unsigned long long *ts = TRACE ? a.trace + 8 * (long)a.ntiles : nullptr;
         const bool trs = TRACE && t == a.ttile && lane == 0;
 
-        constexpr bool LEAN = LINE_FASTCOMP && !RHS_NAT;  // the lean step reads its rhs from the slot
-        if (LEAN && wave < CW) {
-          if constexpr (LEAN) {
-            // ---------------- compute (lean step): planes p0 .. p0+PC-1 ----------------
-            // The same recurrence as below with the per-step overhead taken off
-            // the critical path: ring offsets advance by adds (no modulo), the
+        if (wave < CW) {
+          {
+            // ---------------- compute: planes p0 .. p0+PC-1 ----------------
+            // Coefficients, rhs and j-inputs of step s+1 are read from LDS at the
+            // start of step s (their slot was completed before the barrier that
+            // ended step s-1), so that latency overlaps step s's arithmetic.  The
+            // k-input of the first plane (the poller's, or the previous compute
+            // wave's result) is read first; planes run in descending order, so it
+            // is needed last.  The per-step overhead is kept off the critical
+            // path: ring offsets advance by adds (no modulo), the
             // rows valid at a step come from a lane-mask shift register (plane 0's
             // mask at step s is its mask at s-1 shifted one lane up, plus lane 0
             // while 0 <= s < nx; plane p's is plane 0's of step s-p), every plane
@@ -613,7 +576,7 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
             struct In {
                 double ck[PC], cj[PC], ci[PC], dg[PC], rh[PC], jv[PC];
             };
-            auto load = [&](unsigned so, In &in) {
+            auto load = [&](int s, unsigned so, In &in) {
                 const char *slot = ring + so;
 #pragma unroll
                 for (int u = 0; u < PC; u++) {
@@ -623,7 +586,11 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                     in.cj[u] = b[1];
                     in.ci[u] = b[2];
                     if constexpr (NA == 4) in.dg[u] = b[3];
-                    in.rh[u] = reinterpret_cast<const double *>(slot + SL::RHS)[p * nj + lc];
+                    if constexpr (RHS_NAT) {
+                        in.rh[u] = rhsblk[((s >> 3) & 1) * line_rhs_blk<P>() + (s & 7) * (P * 64 + 1) + p * 64 + lane];
+                    } else {
+                        in.rh[u] = reinterpret_cast<const double *>(slot + SL::RHS)[p * nj + lc];
+                    }
                     in.jv[u] = reinterpret_cast<const double *>(slot + SL::JFIN)[p];
                 }
             };
@@ -655,7 +622,7 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                 const double kx = wave == 0 ? reinterpret_cast<const double *>(ring + so + SL::KFIN)[lane]
                                             : res[((s - 1) & (RS - 1)) * P * 64 + (p0 - 1) * 64 + lane];
                 asm volatile("" ::: "memory");  // kx's read is issued first (LDS returns in order)
-                load(sn, nxt);
+                load(s + 1, sn, nxt);
 #pragma unroll
                 for (int u = 0; u < PC; u++) {
                     const int y = s - p0 - u;  // lane 0's row; bit = 0 <= y < nx, in integer ops (SALU)
@@ -728,144 +695,6 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                 a.trace[8 * t + 4] = xcc;
             }
           }
-        } else if (wave < CW) {
-            if (LINE_COMP_PRIO) __builtin_amdgcn_s_setprio(LINE_COMP_PRIO);
-            // ---------------- compute: planes p0 .. p0+PC-1 ----------------
-            // Coefficients and rhs of step s+1 are read from LDS at the start of
-            // step s (their slot was completed before the barrier that ended step
-            // s-1), so that latency overlaps step s's arithmetic.  The k-input
-            // of the first plane (the poller's, or the previous compute wave's
-            // result) is read at the step start; planes run in descending order,
-            // so it is needed last.
-            const int p0 = wave * PC;
-            struct In {
-                double ck[PC], cj[PC], ci[PC], dg[PC], rh[PC], jv[PC];
-                double rc[PC];  // LINE_FASTDIV: RN(1 / dg), formed one step ahead
-                bool dok[PC];   // dg inside the range where the fast quotient is exact
-            };
-            auto load = [&](int s, In &in) {
-                const char *slot = ring + (s % R) * SL::BYTES;
-#pragma unroll
-                for (int u = 0; u < PC; u++) {
-                    const int p = p0 + u;
-                    const double *b = reinterpret_cast<const double *>(slot + SL::COEF) + (p * nj + lc) * NA;
-                    in.ck[u] = b[0];
-                    in.cj[u] = b[1];
-                    in.ci[u] = b[2];
-                    if constexpr (NA == 4) in.dg[u] = b[3];
-                    if constexpr (RHS_NAT) {
-                        in.rh[u] = rhsblk[((s >> 3) & 1) * line_rhs_blk<P>() + (s & 7) * (P * 64 + 1) + p * 64 + lane];
-                    } else {
-                        in.rh[u] = reinterpret_cast<const double *>(slot + SL::RHS)[p * nj + lc];
-                    }
-                    in.jv[u] = reinterpret_cast<const double *>(slot + SL::JFIN)[p];
-                }
-            };
-            double xc[PC];
-#pragma unroll
-            for (int u = 0; u < PC; u++) xc[u] = 0.0;
-            In A, B;  // step s uses the set loaded at step s-1: even steps A, odd steps B
-#pragma unroll
-            for (int u = 0; u < PC; u++) A.rc[u] = B.rc[u] = 1.0, A.dg[u] = B.dg[u] = 1.0, A.dok[u] = B.dok[u] = true;
-            // hand-off outputs, stored here (sc1) as soon as computed: this wave
-            // never waits on its VMEM queue, so the stores cost it nothing.  Buffer
-            // stores: a lane with nothing to store gets an out-of-range offset and
-            // its store is dropped, so the step has no branch.
-            const __amdgpu_buffer_rsrc_t hko =
-                __builtin_amdgcn_make_buffer_rsrc(a.hk + (long)t * a.hk_stride, 0, (int)(a.hk_stride * 8), 0x00020000);
-            const __amdgpu_buffer_rsrc_t hjo =
-                __builtin_amdgcn_make_buffer_rsrc(a.hj + (long)t * a.hj_stride, 0, (int)(a.hj_stride * 8), 0x00020000);
-            constexpr int OOB = 0x7ffffff0;
-            auto body = [&](int s, In &cur, In &nxt) {
-                if (TRACE && lane == 0 && wave == 0 && s == 0) a.trace[8 * t + 1] = __builtin_amdgcn_s_memrealtime();
-                if (trs && wave == 0 && s >= 0 && s < T) ts[8 * s] = __builtin_amdgcn_s_memtime();
-                // the same LDS reads on every step (clamped before 0 and at the end: the
-                // values are then unused), so the compiler's wait for kx leaves the
-                // next step's operands in flight
-                const int sc = min(max(s, 0), T - 1);
-                const char *slot = ring + (sc % R) * SL::BYTES;
-                const double kx = wave == 0 ? reinterpret_cast<const double *>(slot + SL::KFIN)[lane]
-                                            : res[((sc - 1) & (RS - 1)) * P * 64 + (p0 - 1) * 64 + lane];
-                asm volatile("" ::: "memory");  // kx's read is issued first (LDS returns in order)
-                load(min(max(s + 1, 0), T - 1), nxt);
-                if (s >= 0 && s < T) {
-                    // every lane computes every plane; rows that do not exist at this
-                    // step keep their old value (a lane-mask select, not a branch)
-                    double xn[PC];
-#pragma unroll
-                    for (int u = PC - 1; u >= 0; u--) {
-                        const int p = p0 + u;
-                        const int i = s - p - lane;
-                        const bool valid = p < np && lane < nj && i >= 0 && i < nx;
-                        const double xk = u > 0 ? xc[u - 1] : kx;
-                        const double xj = dpp_shr1(xc[u], cur.jv[u]);
-                        double v = cur.rh[u] - cur.ck[u] * xk;
-                        v = v - cur.cj[u] * xj;
-                        v = v - cur.ci[u] * xc[u];
-                        if constexpr (NA == 4) {
-                            if constexpr (LINE_FASTDIV) {
-                                const double q = div_rn(v, cur.dg[u], cur.rc[u]);
-                                const bool ok = !valid || (cur.dok[u] && div_num_ok(v));  // rows that do not exist keep their old value
-                                v = __builtin_expect(__all(ok), 1) ? q : (ok ? q : v / cur.dg[u]);
-                            } else {
-                                v = v / cur.dg[u];
-                            }
-                        }
-                        xn[u] = sel_lanes(__builtin_amdgcn_ballot_w64(valid), v, xc[u]);
-                        if (LINE_KOUT_BF) {  // branch-free: off-tile lanes and tiles without a k-output drop the store
-                            const int ko = (kout && p == np - 1 && valid) ? ((s + 1 - np) * 64 + lane) * 8 : OOB;
-                            __builtin_amdgcn_raw_buffer_store_b64(split64(canon_bits(xn[u])), hko, ko, 0, 16);  // sc1
-                        } else if (kout && p == np - 1) {  // uniform: the tile's last plane feeds the next k-tile
-                            const int ko = valid ? ((s + 1 - np) * 64 + lane) * 8 : OOB;
-                            __builtin_amdgcn_raw_buffer_store_b64(split64(canon_bits(xn[u])), hko, ko, 0, 16);  // sc1
-                        }
-                    }
-                    if (jout) {
-                        // lane nj-1 feeds the next j-tile: this wave's PC planes in one store
-                        // (entries of planes whose row does not exist are never polled)
-                        const int jo = lane == nj - 1 ? ((s + 1 - nj) * P + p0) * 8 : OOB;
-                        if constexpr (PC == 2) {
-                            const uint64_t b0 = canon_bits(xn[0]), b1 = canon_bits(xn[1]);
-                            line_v4u d4;
-                            d4.x = (unsigned)b0;
-                            d4.y = (unsigned)(b0 >> 32);
-                            d4.z = (unsigned)b1;
-                            d4.w = (unsigned)(b1 >> 32);
-                            __builtin_amdgcn_raw_buffer_store_b128(d4, hjo, jo, 0, 16);
-                        } else {
-#pragma unroll
-                            for (int u = 0; u < PC; u++)
-                                __builtin_amdgcn_raw_buffer_store_b64(split64(canon_bits(xn[u])), hjo, jo + 8 * u, 0, 16);
-                        }
-                    }
-                    if (trs && wave == 0 && s >= 0 && s < T) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
-#pragma unroll
-                    for (int u = 0; u < PC; u++) {
-                        xc[u] = xn[u];
-                        res[((s & (RS - 1)) * P + p0 + u) * 64 + lane] = xc[u];
-                    }
-                }
-                if constexpr (NA == 4 && LINE_FASTDIV) {
-                    // the next step's reciprocals, off this step's dependency chain
-#pragma unroll
-                    for (int u = 0; u < PC; u++) {
-                        nxt.rc[u] = 1.0 / nxt.dg[u];
-                        nxt.dok[u] = div_den_ok(nxt.dg[u]);
-                    }
-                }
-                if (trs && s >= 0 && s < T) ts[8 * s + (wave == 0 ? 1 : 7)] = __builtin_amdgcn_s_memtime();
-                line_barrier();
-            };
-            for (int s = S0; s <= T; s += 2) {
-                body(s, A, B);
-                if (s + 1 <= T) body(s + 1, B, A);
-            }
-            if (TRACE && lane == 0 && wave == 0) {
-                a.trace[8 * t + 2] = __builtin_amdgcn_s_memrealtime();
-                unsigned xcc;
-                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-                a.trace[8 * t + 4] = xcc;
-            }
         } else if (wave < CW + NL) {
             // ---------------- loaders: every step's DMAs spread over the NL waves ----------------
             const int w = wave - CW;

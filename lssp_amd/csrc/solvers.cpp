@@ -43,6 +43,11 @@ struct Run {
     std::vector<std::pair<long, double>> patches;
     std::vector<double *> bufs;
     int rank = 0;
+    // global preconditioner on P ranks (pc-iluk.cxx:574, blk_size = n): M holds
+    // the factors of the WHOLE matrix on every rank; an apply all-gathers the
+    // rhs blocks, sweeps the global system and keeps the rank's rows
+    bool gpc = false;
+    double *g_send = nullptr, *g_rhs = nullptr, *g_x = nullptr;
 
     ~Run()
     {
@@ -93,7 +98,31 @@ struct Run {
             e.out0 = x;
             return launch_ew(c, e);
         }
+        if (gpc) return pc_global(x, rhs);
         return launch_ilu_apply(c, M, x, rhs);
+    }
+    // the rank's rows of U^-1 L^-1 rhs for the global factors: the rows are
+    // the canonical blocks of ceil(n/P) (the last one shorter, its send padded),
+    // so the gathered blocks are the global rhs in row order
+    int pc_global(double *x, const double *rhs)
+    {
+        const long ng = A->n_global, blk = (ng + c->nranks - 1) / c->nranks;
+        if (!g_send) {
+            g_send = vec(blk);
+            g_rhs = vec(blk * c->nranks);
+            g_x = vec(ng);
+            if (!g_send || !g_rhs || !g_x) return LSSP_AMD_ENOMEM;
+        }
+        Ew e;
+        e.kind = K_COPY;
+        e.x = rhs;
+        e.out0 = g_send;
+        LSSP_TRY(ew(e));
+        LSSP_TRY(comm_allgather(c, g_send, g_rhs, (long)sizeof(double) * blk));
+        LSSP_TRY(launch_ilu_apply(c, M, g_x, g_rhs));
+        e.x = g_x + A->row0;
+        e.out0 = x;
+        return ew(e);
     }
     int sync(int first, int count)
     {
@@ -2182,12 +2211,16 @@ extern "C" int lssp_amd_solve(lssp_amd_ctx *c, const lssp_amd_mat *A, const lssp
 {
     if (!c || !A || !prm || !x || !b) return LSSP_AMD_EINVAL;
     if (A->nrows != A->ncols - A->nhalo) return LSSP_AMD_EINVAL;  // square (lssp.cxx:152)
-    if (M && M->n != A->nrows) return LSSP_AMD_EINVAL;
+    // M: the rank's own rows (a block-Jacobi block on P ranks), or on P ranks
+    // the factors of the whole matrix (the reference's global ILU)
+    const bool gpc = M && c->nranks > 1 && M->n == A->n_global && M->n != A->nrows;
+    if (M && M->n != A->nrows && !gpc) return LSSP_AMD_EINVAL;
     LSSP_HIP(hipSetDevice(c->device));
     Run R;
     R.c = c;
     R.A = A;
     R.M = M;
+    R.gpc = gpc;
     R.n = A->nrows;
     R.nx = (long)A->nrows + A->nhalo;
     R.tree = c->reduce_mode == LSSP_AMD_REDUCE_TREE;

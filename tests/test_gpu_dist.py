@@ -29,7 +29,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, N, maxit, seed, out, solver="bicgstab", mode=1):
+def _worker(rank, world, port, N, maxit, seed, out, solver="bicgstab", mode=1, pc="bj"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -47,8 +47,12 @@ def _worker(rank, world, port, N, maxit, seed, out, solver="bicgstab", mode=1):
         nl = min(blk, n - r0)
         Ap, Aj, Ax = lssp_amd.poisson(3, N, r0, nl)
         A = lssp_amd.DMat(dev, Ap, Aj, Ax, dist=(n, r0))
-        bp, bj, bx = local_block(Ap, Aj, Ax, r0, nl)
-        M = lssp_amd.DILU.create(dev, bp, bj, bx, kind=lssp_amd.ILUK, level=0)
+        if pc == "global":  # every rank holds the ILU(0) of the WHOLE matrix (pc-iluk.cxx:574)
+            gp, gj, gx = lssp_amd.poisson(3, N)
+            M = lssp_amd.DILU.create(dev, gp, gj, gx, kind=lssp_amd.ILUK, level=0)
+        else:
+            bp, bj, bx = local_block(Ap, Aj, Ax, r0, nl)
+            M = lssp_amd.DILU.create(dev, bp, bj, bx, kind=lssp_amd.ILUK, level=0)
         # SpMV with a halo: y = A x for a seeded global x
         xg = uniform(seed, n)
         xv = dev.vec(A.nx, np.concatenate([xg[r0:r0 + nl], np.zeros(A.nhalo)]))
@@ -74,12 +78,12 @@ def _worker(rank, world, port, N, maxit, seed, out, solver="bicgstab", mode=1):
         dist.destroy_process_group()
 
 
-def _run(world, N, solver, mode, maxit=500):
+def _run(world, N, solver, mode, maxit=500, pc="bj"):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, N, maxit, 0x5EED, q, solver, mode))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, maxit, 0x5EED, q, solver, mode, pc))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -213,3 +217,26 @@ def test_rccl_one_rank_transport_selftest():
         assert r.nits == o.nits and np.array_equal(r.trace, o.trace) and np.array_equal(x.download(), o.x)
     finally:
         dev.close()
+
+
+@pytest.mark.parametrize("world,N,mode", [(2, 32, O.SERIAL), (3, 20, O.SERIAL), (4, 16, O.TREE), (2, 24, O.TREE)],
+                         ids=["2r32-serial", "3r20-serial", "4r16-tree", "2r24-tree"])
+def test_global_ilu_on_p_ranks(world, N, mode):
+    """The reference's own preconditioner on P ranks: every rank holds the
+    ILU(0) factors of the whole matrix (pc-iluk.cxx:574, blk_size = n) and an
+    apply all-gathers the rhs blocks, sweeps the global system and keeps the
+    rank's rows.  SERIAL: the ranks continue each other's running sums, so the
+    run is bitwise the single-process reference order -- the same iteration
+    count as one GPU, unlike block-Jacobi.  TREE: bitwise the oracle's P-rank
+    reduction order with the global factors."""
+    nits, res, trace, y, x = _run(world, N, "bicgstab", mode, maxit=5000, pc="global")
+    A = O.poisson(3, N)
+    L, U = O.ilu(A, "iluk", level=0)
+    o = O.solve(O.BICGSTAB, A, np.ones(A.n), L=L, U=U, mode=mode, nranks=1 if mode == O.SERIAL else world,
+                maxit=5000)
+    assert nits == o.nits
+    assert res == o.residual
+    assert np.array_equal(trace, o.trace)
+    assert np.array_equal(x, o.x)
+    if mode == O.SERIAL and N == 32:  # SURVEY A1: the reference takes 21 iterations at 32^3
+        assert nits == 21
