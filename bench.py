@@ -201,28 +201,33 @@ def main():
     # ---- measured HBM copy peak ("also record a measured copy-kernel
     # peak"): 2^27 doubles (1 GiB) copied, read + write bytes over HIP-event
     # time; the best of torch's vectorised copy and the library's vec_copy ----
-    peak_measured = None
+    peak_measured, peak_detail = None, None
     if rank == 0:
         nc = 1 << 27
         src = torch.empty(nc, dtype=torch.float64, device=f"cuda:{gpu}").uniform_(-1, 1)
         dst = torch.empty_like(src)
-        best = 0.0
-        for how in ("torch", "lssp"):
-            def cp():
-                if how == "torch":
+        best = {}
+        for how in ("copy-torch", "copy-lssp", "read-torch"):
+            def op():
+                if how == "copy-torch":
                     dst.copy_(src)
-                else:
+                elif how == "copy-lssp":
                     dev.L.lssp_amd_vec_copy(dev.h, dst.data_ptr(), src.data_ptr(), nc)
-            st = torch.cuda.current_stream() if how == "torch" else stream
+                else:
+                    torch.sum(src, out=red)
+            st = stream if how == "copy-lssp" else torch.cuda.current_stream()
+            red = torch.empty((), dtype=torch.float64, device=src.device)
             for _ in range(3):
-                cp()
+                op()
             e0.record(st)
             for _ in range(10):
-                cp()
+                op()
             e1.record(st)
             e1.synchronize()
-            best = max(best, 16.0 * nc / (e0.elapsed_time(e1) / 10 * 1e-3) / 1e9)
-        peak_measured = round(best, 1)
+            nbytes = 8.0 * nc * (1 if how == "read-torch" else 2)
+            best[how] = round(nbytes / (e0.elapsed_time(e1) / 10 * 1e-3) / 1e9, 1)
+        peak_measured = max(best.values())
+        peak_detail = best
         del src, dst
 
     # ---- BiCGSTAB steps ----
@@ -285,7 +290,7 @@ def main():
                                    "-> the U sweep's rhs stream) + k_line (U sweep -> x in natural order); "
                                    "latency-bound: 2 x 646 dependent levels",
                          "bytes_per_launch": apply_b, "ms_per_launch": round(apply_ms, 5),
-                         "peak_measured": peak_measured,
+                         "peak_measured": peak_measured, "peak_measured_detail": peak_detail,
                          "frac_of_measured_peak": round(apply_gbs / peak_measured, 4) if peak_measured else None},
             "roofline_spmv": {"bound": "hbm", "achieved": round(spmv_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(spmv_gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("k_spmv3"),

@@ -571,8 +571,8 @@ int lssp_amd_vec_set_value(lssp_amd_ctx *c, double *x, long n, double v)
 }
 int lssp_amd_vec_copy(lssp_amd_ctx *c, double *x, const double *y, long n)
 {
-    if (!y && n > 0) return LSSP_AMD_EINVAL;
-    return ew_simple(c, 1, n, 0, 0, y, nullptr, x);
+    if (!c || n < 0 || (n > 0 && (!x || !y))) return LSSP_AMD_EINVAL;
+    return launch_copy(c, x, y, n);
 }
 int lssp_amd_vec_axy(lssp_amd_ctx *c, double alpha, const double *x, double *y, long n)
 {

@@ -272,6 +272,8 @@ struct Ew {
     int pslot = 0;                  // first partial row the pass's reductions write
 };
 int launch_ew(lssp_amd_ctx *c, const Ew &e);
+// x = y (vector.cxx:73-83): 16-byte vector copy when both are 16-byte aligned
+int launch_copy(lssp_amd_ctx *c, double *x, const double *y, long n);
 
 // finish a reduction whose level-1 partials (tree) or operands (serial) are set:
 // tree: level-2 over nslot partial rows of C entries; then the finalize program

@@ -774,6 +774,47 @@ __global__ __launch_bounds__(256) void k_ew(EwArgs g)
     }
 }
 
+// lssp_vec_copy (vector.cxx:73-83) for 16-byte aligned vectors: four 16-byte
+// loads per lane in flight, then the four stores (grid-strided).  It is also
+// what bench.py prices HBM with (roofline peak_measured).
+typedef double line_dbl2v __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(256) void k_copy16(const line_dbl2v *__restrict__ s2, line_dbl2v *__restrict__ d2, long n2)
+{
+    typedef line_dbl2v dbl2v;
+    const long stride = (long)gridDim.x * 256;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n2; i += 4 * stride) {
+        dbl2v v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = i + u * stride < n2 ? __builtin_nontemporal_load(s2 + i + u * stride) : dbl2v{0, 0};
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (i + u * stride < n2) __builtin_nontemporal_store(v[u], d2 + i + u * stride);
+    }
+}
+
+int launch_copy(lssp_amd_ctx *c, double *x, const double *y, long n)
+{
+    if (n <= 0) return LSSP_AMD_OK;
+    const bool al = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0;
+    if (!al || c->guard) {
+        Ew e;
+        e.kind = EW_COPY;
+        e.n = n;
+        e.x = y;
+        e.out0 = x;
+        return launch_ew(c, e);
+    }
+    const long n2 = n / 2;
+    if (n2 > 0) {
+        const long grid = std::min<long>((n2 + 1023) / 1024, 8L * c->num_cus * 4);
+        k_copy16<<<grid, 256, 0, c->stream>>>(reinterpret_cast<const line_dbl2v *>(y), reinterpret_cast<line_dbl2v *>(x),
+                                              n2);
+        LSSP_HIP(hipGetLastError());
+    }
+    if (n & 1) LSSP_HIP(hipMemcpyAsync(x + n - 1, y + n - 1, sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    return LSSP_AMD_OK;
+}
+
 int launch_ew(lssp_amd_ctx *c, const Ew &e)
 {
     if (e.n <= 0) return LSSP_AMD_OK;

@@ -7,6 +7,8 @@ All comparisons are bitwise except where a test says otherwise:
   * solvers in TREE mode (the fast path) against the oracle restating the same
     canonical reduction order.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -319,3 +321,42 @@ def test_spmv_column_coding_chosen_by_structure(dev):
         M.mv_mxy(x, z)
         ref = O.spmv(0, O.CSR(n, Ap, Aj, Ax), xv)
         assert np.array_equal(z.download().view(np.int64), ref.view(np.int64))
+
+
+def test_env_selected_paths_bitwise_vs_oracle():
+    """The two remaining path selectors, each in a fresh process (they are read
+    once): LSSP_AMD_ILU_HOST=1 runs ILUK's numeric factorization on the host
+    (ilu_setup.cpp, pc-iluk.cxx:347-409) instead of the GPU, and LSSP_AMD_LINE=0
+    gives a 7-pt grid's ILU(0) the general packet sweeps (k_tri_pk6) instead of
+    the line sweeps.  Factors and applies are bitwise the oracle's either way,
+    and a BiCGSTAB solve on them is bitwise the oracle's tree-mode run."""
+    import subprocess
+    import sys
+    code = r'''
+import sys, numpy as np
+sys.path.insert(0, "ROOT"); sys.path.insert(0, "ROOT/tests")
+import lssp_amd, oracle as O
+from inputs import uniform
+A = O.poisson(3, 24)
+dev = lssp_amd.Device(0)
+M = lssp_amd.DILU.create(dev, A.Ap, A.Aj, A.Ax, kind=lssp_amd.ILUK, level=0)
+(Lp, Lj, Lx), (Up, Uj, Ux) = M.factors()
+L, U = O.ilu(A, "iluk", level=0)
+assert np.array_equal(Lj, L.Aj) and np.array_equal(Uj, U.Aj)
+assert np.array_equal(Lx.view(np.int64), L.Ax.view(np.int64)) and np.array_equal(Ux.view(np.int64), U.Ax.view(np.int64))
+rhs = uniform(5, A.n)
+x = dev.vec(A.n)
+for _ in range(2):
+    M.apply(x, dev.vec(A.n, rhs))
+    assert np.array_equal(x.download().view(np.int64), O.ilu_apply(L, U, rhs).view(np.int64))
+Ad = lssp_amd.DMat(dev, A.Ap, A.Aj, A.Ax)
+xs, b = dev.vec(A.n, np.zeros(A.n)), dev.vec(A.n, np.ones(A.n))
+r = lssp_amd.solve(dev, Ad, M, xs, b, solver=lssp_amd.BICGSTAB, trace_cap=1000)
+o = O.solve(O.BICGSTAB, A, np.ones(A.n), L=L, U=U, mode=O.TREE)
+assert r.nits == o.nits and np.array_equal(r.trace, o.trace) and np.array_equal(xs.download(), o.x)
+print("ok", r.nits)
+'''.replace("ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    for env in ({"LSSP_AMD_ILU_HOST": "1"}, {"LSSP_AMD_LINE": "0"}, {"LSSP_AMD_ILU_HOST": "1", "LSSP_AMD_LINE": "0"}):
+        res = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,
+                             timeout=150)
+        assert res.returncode == 0 and "ok" in res.stdout, (env, res.stdout[-2000:], res.stderr[-2000:])
