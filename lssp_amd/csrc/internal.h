@@ -166,7 +166,6 @@ struct TriSched {
 constexpr int PK3_ROWS = 256;    // v6: rows per packet = compute lanes = loader lanes
 constexpr int PK3_EXT = 2;       // v6: HBM x operands per packet row (on average)
 constexpr int PK3_CAP = 4096;    // v6: packets per block (descriptors staged in LDS)
-constexpr int PK4_PAD = -1 - 4096;  // v6 padding code: the value-ring slot past the end (holds +0.0)
 
 // ---- line sweeps of structured ILU(0) factors (linesweep.hip) ----------------
 #ifndef LINE_P_OVERRIDE
@@ -290,6 +289,10 @@ int launch_fill(lssp_amd_ctx *c, double *x, long n, uint64_t bits);
 int launch_trisolve(lssp_amd_ctx *c, const TriSched &t, const double *rhs, double *x,
                     double *reset);
 constexpr int BP_RING = 4096;  // LDS ring of recently computed values (32 KB)
+// k_tri_pk6's LDS operand array: the value ring [0, BP_RING), a +0.0 pad slot
+// at BP_RING, then the two buffers of landed HBM operands (PK3_EXT per packet
+// row of 256).  Byte offset of entry base + par * buffer + k:
+constexpr int pk6_xs_off(int base, int par, int k) { return 8 * (base + par * 256 * PK3_EXT + k); }
 int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std::vector<int> &Tj,
                       const std::vector<double> &Tx, bool upper, const std::vector<int> &lev,
                       TriSched &t, const TriSched *prod = nullptr);

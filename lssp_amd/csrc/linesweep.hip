@@ -947,16 +947,29 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
 // ---------------------------------------------------------------------------
 // launch
 // ---------------------------------------------------------------------------
-#ifndef LINE_DH_OVERRIDE
-constexpr int LINE_DH = 2;
+// Leads (steps): loaders D, poller DH.  The apply's sweeps (rhs from a stream)
+// measured fastest at D = 7, DH = 3 (apply 795-799 us against 818-823 at 10 /
+// 2, three sessions; D 4-6 and 8-10 at DH = 3 and DH 2 or 4 at D = 7 were
+// slower, profiles/r03/r03n_line_leads.txt); the standalone sweeps (natural-
+// order rhs through the rhs wave) keep 10 / 2, where DH = 3 costs 15-30 us.
+template <bool RHS_NAT>
+constexpr int line_d()
+{
+#ifdef LINE_D_OVERRIDE
+    return LINE_D_OVERRIDE;
 #else
-constexpr int LINE_DH = LINE_DH_OVERRIDE;
+    return RHS_NAT ? 10 : 7;
 #endif
-#ifndef LINE_D_OVERRIDE
-constexpr int LINE_D = 10;
+}
+template <bool RHS_NAT>
+constexpr int line_dh()
+{
+#ifdef LINE_DH_OVERRIDE
+    return LINE_DH_OVERRIDE;
 #else
-constexpr int LINE_D = LINE_D_OVERRIDE;
+    return RHS_NAT ? 2 : 3;
 #endif
+}
 #ifndef LINE_PC_OVERRIDE
 constexpr int LINE_CW = LINE_P / 2;  // two planes per compute wave
 #else
@@ -972,7 +985,7 @@ constexpr int LINE_SW = 2;
 template <int NA, bool RHS_NAT, int OUT, bool TRACE>
 static int launch_line_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)
 {
-    auto kern = k_line<LINE_P, NA, RHS_NAT, OUT, LINE_CW, LINE_NL, LINE_D, LINE_DH, LINE_SW, TRACE>;
+    auto kern = k_line<LINE_P, NA, RHS_NAT, OUT, LINE_CW, LINE_NL, line_d<RHS_NAT>(), line_dh<RHS_NAT>(), LINE_SW, TRACE>;
     static int attr = 0;
     if (lds > attr) {
         LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -988,7 +1001,7 @@ static int launch_line_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g
 template <int NA, bool RHS_NAT, int OUT>
 static int launch_line_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a)
 {
-    const int lds = line_lds_bytes<LINE_P, NA, RHS_NAT, OUT, LINE_D>();
+    const int lds = line_lds_bytes<LINE_P, NA, RHS_NAT, OUT, line_d<RHS_NAT>()>();
     if (lds > 160 * 1024) return LSSP_AMD_EUNSUPPORTED;
     // diagnostics only: LSSP_AMD_LINE_TRACE=path[:tile] appends one JSON line per sweep
     static const char *trp = getenv("LSSP_AMD_LINE_TRACE");

@@ -160,8 +160,12 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
 //   desc  int4 {record offset (16 B units), index offset (4 B units),
 //               nr | nx << 10 | emax << 21, schedule position of the first row}
 //   records (compute lanes), arrays over the packet's rows, 16-byte aligned:
-//     C  codes as int16 pairs, EP/2 words per row: uint2 (EP 4) or uint4 chunks (EP 8, 16, 24)
-//        -- -1-slot (value ring), PK4_PAD, or an xidx index
+//     C  operand addresses as uint16 pairs, EP/2 words per row: uint2 (EP 4) or
+//        uint4 chunks (EP 8, 16, 24) -- the operand's byte offset in the
+//        kernel's LDS operand array (pk6_xs_off: a value-ring slot, the +0.0
+//        pad slot, or the packet's landed HBM operand, whose buffer is the
+//        packet's parity within its block), so the compute lanes read each
+//        operand with no decoding
 //     V[EP/2] double2 entry values, D double diagonal, ROW int (natural row)
 //   indices (loader lanes): rhs[nr] (the rhs entry of each row: its L-schedule
 //     position, for both sweeps -- the L sweep reads the rhs permuted into L
@@ -202,6 +206,7 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
         for (long b = b0; b < b1 && status.load() == LSSP_AMD_OK; b++) {
             std::vector<int> &desc = bp[b].desc, &idx = bp[b].idx;
             std::vector<uint32_t> &rec = bp[b].rec;
+            static_assert(pk6_xs_off(BP_RING + 1, 1, ROWS * PK3_EXT - 1) <= 0xffff, "16-bit operand offsets");
             for (int s = blk_step[b]; s < blk_step[b + 1]; s++) {
                 int p = step_pos[s];
                 while (p < step_pos[s + 1]) {
@@ -226,6 +231,7 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
                         nr++;
                     }
                     const int nx = (int)xl.size();
+                    const int par = (int)(desc.size() / 4) & 1;  // the packet's index in its block, mod 2
                     const long ro = (long)rec.size() / 4, io = (long)idx.size();  // block-relative
                     desc.push_back((int)ro);
                     desc.push_back((int)io);
@@ -242,10 +248,10 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
                     for (int r = 0; r < nr; r++) {
                         const int k0 = rp[p + r], len = rp[p + r + 1] - k0;
                         int cc[24];
-                        for (int e = 0; e < 24; e++) cc[e] = PK4_PAD;
+                        for (int e = 0; e < 24; e++) cc[e] = pk6_xs_off(BP_RING, 0, 0);  // the +0.0 pad slot
                         for (int e = 0; e < len; e++) {
                             const int g = cols[k0 + e];
-                            cc[e] = g < 0 ? g : slot[g];
+                            cc[e] = g < 0 ? pk6_xs_off(-1 - g, 0, 0) : pk6_xs_off(BP_RING + 1, par, slot[g]);
                             V[2L * ((long)(e / 2) * nr + r) + (e & 1)] = vals[k0 + e];
                         }
                         for (int q = 0; q < EP / 2; q++) w[(long)(EP / 2) * r + q] = pack(cc[2 * q], cc[2 * q + 1]);

@@ -204,6 +204,11 @@ struct Pk6Args {
     unsigned long long *claim;
     unsigned long long base;
     int *err;
+    // diagnostics (LSSP_AMD_PK6_TRACE): per block {claim, first step, end,
+    // sentinel hits, xcc, packets}; per packet of block tblk {compute start,
+    // compute end, loader wait (clk), loader landing end}
+    unsigned long long *trace;
+    int tblk;
 };
 
 template <int EP>
@@ -215,10 +220,11 @@ struct Pk6Rec {
     double v[EP];
     double dg;
     int nr, pos0;
-    __device__ __forceinline__ int code(int e) const
+    // byte offset of operand e in the LDS operand array (tri_bp.cpp pk6_xs_off)
+    __device__ __forceinline__ unsigned off(int e) const
     {
         const unsigned w = EP == 4 ? c[0][e / 2] : c[e / 8][(e / 2) & 3];
-        return (e & 1) ? ((int)w >> 16) : (int)(short)(w & 0xffff);
+        return (e & 1) ? (w >> 16) : (w & 0xffffu);
     }
 };
 
@@ -242,16 +248,19 @@ __device__ __forceinline__ T &sel4(T &a, T &b, T &c, T &d)
 // registers; the loader lanes fetch it KE steps ahead with the gathers and land
 // it in an LDS slot at the end of the step before, and the compute lanes read
 // it from there (D unused).
-template <int EP, int KE, int IA, int D, int NR, bool LREC = false>
+template <int EP, int KE, int IA, int D, int NR, bool LREC = false, bool TRACE = false>
 __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
 {
     constexpr int Q = 4;
     static_assert(D + 1 <= Q && IA <= Q && KE >= 1 && IA - KE >= 1 && IA - KE <= 2, "pipeline depths");
     constexpr int S0 = (IA > D ? IA : D);
     constexpr int J0 = -((S0 + Q - 1) / Q) * Q;  // first step, a multiple of Q
-    __shared__ double ring[BP_RING + 1];
+    // operands: the value ring, the +0.0 pad slot, the landed HBM operands of
+    // two packets (pk6_xs_off); a record addresses each operand by byte offset
+    static_assert(NR == 256, "pk6_xs_off assumes 256-row packets");
+    __shared__ double xs[BP_RING + 1 + 2 * NR * PK3_EXT];
+    double *const ring = xs;
     __shared__ double rbuf[2][NR];
-    __shared__ double xbuf[2][NR * PK3_EXT];
     __shared__ int4 sdesc[PK3_CAP];
     __shared__ v4u recbuf[LREC ? 2 : 1][LREC ? PK6_REC16 : 1];
     __shared__ int s_blk;
@@ -266,29 +275,39 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
         const int b = s_blk;
         if (b >= a.nb) break;
         const int q0 = a.blk[b], np = a.blk[b + 1] - q0;
+        if (TRACE && tid == 0) {
+            a.trace[8L * b] = __builtin_amdgcn_s_memrealtime();
+            a.trace[8L * b + 5] = np;
+        }
+        unsigned long long *ts = TRACE ? a.trace + 8L * a.nb : nullptr;
+        const bool trs = TRACE && b == a.tblk && t == 0;
         const int bbase = b * a.B;  // first schedule position of the block
         for (int i = tid; i < np; i += blockDim.x) sdesc[i] = a.desc[q0 + i];
         __syncthreads();
         // both roles run steps J0 .. J0+T-1 (T a multiple of Q); out-of-range
         // packets turn into loads from valid dummy addresses
         const int T = (np - J0 + Q - 1) / Q * Q;
-        auto desc = [&](int p) {
-            const int4 d = sdesc[p];
-            return make_int4(__builtin_amdgcn_readfirstlane(d.x), __builtin_amdgcn_readfirstlane(d.y),
-                             __builtin_amdgcn_readfirstlane(d.z), __builtin_amdgcn_readfirstlane(d.w));
-        };
-
         // descriptor of a packet, clamped: out-of-range packets get nr = nx = 0
-        // and read valid dummy records (no branches around the loads)
-        auto descc = [&](int p) {
-            int4 d = desc(min(max(p, 0), max(np - 1, 0)));
+        // and read valid dummy records (no branches around the loads).  Read in
+        // two halves -- the LDS read one step before its use, the move to
+        // scalar registers at the use -- so no step waits for an LDS read at
+        // its start (the step's barrier has drained LDS by then).
+        auto dread = [&](int p) { return sdesc[min(max(p, 0), max(np - 1, 0))]; };
+        auto duni = [&](const int4 r, int p) {
+            int4 d = make_int4(__builtin_amdgcn_readfirstlane(r.x), __builtin_amdgcn_readfirstlane(r.y),
+                               __builtin_amdgcn_readfirstlane(r.z), __builtin_amdgcn_readfirstlane(r.w));
             if (p < 0 || p >= np) d.z = 0;
             return d;
         };
+        auto descc = [&](int p) { return duni(dread(p), p); };
         if (LREC && role == 0) {
             // compute lanes, record from LDS (landed by the loaders one step ahead)
+            int4 draw = dread(J0);
             for (int j = J0; j < J0 + T; j++) {
-                const int4 d = descc(j);
+                if (trs && j >= 0 && j < np) ts[4L * j] = __builtin_amdgcn_s_memtime();
+                if (TRACE && tid == 0 && j == 0) a.trace[8L * b + 1] = __builtin_amdgcn_s_memrealtime();
+                const int4 d = duni(draw, j);
+                draw = dread(j + 1);
                 const int nr = d.z & 0x3ff;
                 if (t < nr) {
                     const unsigned *w = reinterpret_cast<const unsigned *>(recbuf[j & 1]);
@@ -296,17 +315,17 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
                     typedef double v2d __attribute__((ext_vector_type(2)));
                     const v2d *V = reinterpret_cast<const v2d *>(w + wc);
                     const double dg = reinterpret_cast<const double *>(V + (EP / 2) * nr)[t];
-                    const double *xb = xbuf[j & 1];
                     double acc = rbuf[j & 1][t];
                     double xv[EP], vv[EP];
+                    const char *xsb = reinterpret_cast<const char *>(xs);
 #pragma unroll
                     for (int q = 0; q < EP / 8; q++) {
                         const v4u cw = reinterpret_cast<const v4u *>(w)[(EP / 8) * t + q];
 #pragma unroll
                         for (int h = 0; h < 8; h++) {
                             const unsigned ww = cw[h / 2];
-                            const int cd = (h & 1) ? ((int)ww >> 16) : (int)(short)(ww & 0xffff);
-                            xv[8 * q + h] = cd < 0 ? ring[-1 - cd] : xb[cd];
+                            const unsigned o = (h & 1) ? (ww >> 16) : (ww & 0xffffu);
+                            xv[8 * q + h] = *reinterpret_cast<const double *>(xsb + o);
                         }
                     }
 #pragma unroll
@@ -322,8 +341,10 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
                     ring[(pos - bbase) & (BP_RING - 1)] = xi;
                     st_agent(a.sh + pos, xi);
                 }
+                if (trs && j >= 0 && j < np) ts[4L * j + 1] = __builtin_amdgcn_s_memtime();
                 lds_barrier();
             }
+            if (TRACE && tid == 0) a.trace[8L * b + 2] = __builtin_amdgcn_s_memrealtime();
             const long s0 = bbase, s1 = min(s0 + a.B, (long)a.n);
             uint64_t *rs = reinterpret_cast<uint64_t *>(a.sh_next);
             for (long i = s0 + t; i < s1; i += NR) rs[i] = TRI_SENTINEL;
@@ -350,10 +371,14 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
                 Rr.nr = nr;
                 Rr.pos0 = d.w;
             };
-            int4 dn = descc(J0 + D);  // descriptor of packet j+D, read one step ahead
+            int4 dn = descc(J0 + D);    // descriptor of packet j+D, read one step ahead
+            int4 dnr = dread(J0 + D + 1);
             auto step = [&](int j, Pk6Rec<EP> &Rc, Pk6Rec<EP> &Rn) {
+                if (trs && j >= 0 && j < np) ts[4L * j] = __builtin_amdgcn_s_memtime();
+                if (TRACE && tid == 0 && j == 0) a.trace[8L * b + 1] = __builtin_amdgcn_s_memrealtime();
                 issue(dn, Rn);
-                dn = descc(j + D + 1);
+                dn = duni(dnr, j + D + 1);
+                dnr = dread(j + D + 2);
                 // the current record must be complete here, at one fixed point
 #pragma unroll
                 for (int q = 0; q < Pk6Rec<EP>::NCW; q++) asm volatile("" ::"v"(Rc.c[q]));
@@ -361,15 +386,12 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
                 for (int e = 0; e < EP; e++) asm volatile("" ::"v"(Rc.v[e]));
                 asm volatile("" ::"v"(Rc.dg));
                 if (t < Rc.nr) {  // nr == 0 outside the block's packets
-                    const double *xb = xbuf[j & 1];
                     double acc = rbuf[j & 1][t];
                     double xv[EP];
+                    const char *xsb = reinterpret_cast<const char *>(xs);
                     // all EP entries: padded ones read +0.0 and subtract +0.0*+0.0
 #pragma unroll
-                    for (int e = 0; e < EP; e++) {
-                        const int cd = Rc.code(e);
-                        xv[e] = cd < 0 ? ring[-1 - cd] : xb[cd];
-                    }
+                    for (int e = 0; e < EP; e++) xv[e] = *reinterpret_cast<const double *>(xsb + Rc.off(e));
 #pragma unroll
                     for (int e = 0; e < EP; e++) acc = acc - Rc.v[e] * xv[e];
                     const double xi = a.unit ? acc : acc / Rc.dg;
@@ -377,6 +399,7 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
                     ring[(pos - bbase) & (BP_RING - 1)] = xi;
                     st_agent(a.sh + pos, xi);
                 }
+                if (trs && j >= 0 && j < np) ts[4L * j + 1] = __builtin_amdgcn_s_memtime();
                 lds_barrier();
             };
             Pk6Rec<EP> R0, R1, R2, R3;
@@ -387,6 +410,7 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
                 step(j0 + 2, sel4<2>(R0, R1, R2, R3), sel4<(2 + D) % Q>(R0, R1, R2, R3));
                 step(j0 + 3, sel4<3>(R0, R1, R2, R3), sel4<(3 + D) % Q>(R0, R1, R2, R3));
             }
+            if (TRACE && tid == 0) a.trace[8L * b + 2] = __builtin_amdgcn_s_memrealtime();
             // arm the block's positions of the other shadow for the next apply
             const long s0 = bbase, s1 = min(s0 + a.B, (long)a.n);
             uint64_t *rs = reinterpret_cast<uint64_t *>(a.sh_next);
@@ -443,11 +467,18 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
                 asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(L.ev[1]) : "v"(px1) : "memory");
             };
             int4 dl = descc(J0 + IA);  // descriptor of packet j+IA, read one step ahead
+            int4 dlr = dread(J0 + IA + 1);
+            static_assert(!LREC || IA - KE == 1, "LREC: the record's packet j+KE is the index loads' of step j-1");
+            int4 dk = descc(J0 + KE);
+            unsigned hits = 0;
             auto step = [&](int j, PkLd &Li, PkLd &Lg, PkLd &Ll) {
-                issue_rec(descc(j + KE), Lg);
+                issue_rec(dk, Lg);
                 issue_idx(dl, Li);
                 gather(Lg);
-                dl = descc(j + IA + 1);
+                if constexpr (LREC) dk = dl;
+                dl = duni(dlr, j + IA + 1);
+                dlr = dread(j + IA + 2);
+                const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
                 // gathers of packet j+1 were issued at step j+1-KE
                 if constexpr (LREC)
                     asm volatile("s_waitcnt vmcnt(%7)"
@@ -469,9 +500,16 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
                     const int k = t + NR * e;
                     if (k < Ll.nx) {
                         uint64_t bits = Ll.ev[e];
-                        if (bits == TRI_SENTINEL) bits = poll_ready(a.sh + Ll.xi[e], a.err);
-                        xbuf[(j + 1) & 1][k] = __longlong_as_double((long long)bits);
+                        if (bits == TRI_SENTINEL) {
+                            if (TRACE) hits++;
+                            bits = poll_ready(a.sh + Ll.xi[e], a.err);
+                        }
+                        xs[BP_RING + 1 + ((j + 1) & 1) * NR * PK3_EXT + k] = __longlong_as_double((long long)bits);
                     }
+                }
+                if (trs && j + 1 >= 0 && j + 1 < np) {  // the packet landed here is j+1
+                    ts[4L * (j + 1) + 2] = __builtin_amdgcn_s_memtime() - w0;
+                    ts[4L * (j + 1) + 3] = __builtin_amdgcn_s_memtime();
                 }
                 lds_barrier();
             };
@@ -494,6 +532,15 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
             }
 #undef LSSP_PK6_LSTEP
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (TRACE) {
+                for (int o = 32; o >= 1; o >>= 1) hits += __shfl_xor(hits, o);
+                if ((t & 63) == 0 && hits) atomicAdd(a.trace + 8L * b + 3, (unsigned long long)hits);
+                if (t == 0) {
+                    unsigned xcc;
+                    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                    a.trace[8L * b + 4] = xcc;
+                }
+            }
         }
     }
 }
@@ -512,20 +559,50 @@ int launch_trisolve(lssp_amd_ctx *c, const TriSched &t, const double *rhs, doubl
 }
 
 // packet sweep of one factor: its output to the shadow sh (schedule order)
-static int launch_pk6(lssp_amd_ctx *c, const TriSched &t, const double *rhs, double *sh, double *sh_next)
+template <bool TRACE>
+static void launch_pk6_k(lssp_amd_ctx *c, const TriSched &t, const Pk6Args &g, int grid)
 {
-    const int grid = std::min(t.bp_nb, c->num_cus);
-    Pk6Args g{t.bp_nb, t.pk6_blk, reinterpret_cast<const int4 *>(t.pk6_desc), t.pk6_rec, t.pk6_idx, rhs, sh,
-              sh_next, t.n, t.bp_B, t.unit, t.pk6_claim, t.pk6_base, c->d_err};
     // Instantiated: 256-row packets, x operands gathered 2 steps ahead (KE 2);
     // EP 4 / 8 with register records, EP 16 / 24 with LDS records -- the
     // variants whose inline-asm loader tools/check_vmcnt.py
     // (tests/test_isa_vmcnt.py) verifies hazard-free
+    if (t.pk6_ep == 4) k_tri_pk6<4, 2, 4, 3, 256, false, TRACE><<<grid, 512, 0, c->stream>>>(g);
+    else if (t.pk6_ep == 8) k_tri_pk6<8, 2, 4, 3, 256, false, TRACE><<<grid, 512, 0, c->stream>>>(g);
+    else if (t.pk6_ep == 16) k_tri_pk6<16, 3, 4, 1, 256, true, TRACE><<<grid, 512, 0, c->stream>>>(g);
+    else k_tri_pk6<24, 3, 4, 1, 256, true, TRACE><<<grid, 512, 0, c->stream>>>(g);
+}
+
+static int launch_pk6(lssp_amd_ctx *c, const TriSched &t, const double *rhs, double *sh, double *sh_next)
+{
+    const int grid = std::min(t.bp_nb, c->num_cus);
+    Pk6Args g{t.bp_nb, t.pk6_blk, reinterpret_cast<const int4 *>(t.pk6_desc), t.pk6_rec, t.pk6_idx, rhs, sh,
+              sh_next, t.n, t.bp_B, t.unit, t.pk6_claim, t.pk6_base, c->d_err, nullptr, 0};
     if (t.pk6_rows != 256) return LSSP_AMD_EUNSUPPORTED;
-    if (t.pk6_ep == 4) k_tri_pk6<4, 2, 4, 3, 256><<<grid, 512, 0, c->stream>>>(g);
-    else if (t.pk6_ep == 8) k_tri_pk6<8, 2, 4, 3, 256><<<grid, 512, 0, c->stream>>>(g);
-    else if (t.pk6_ep == 16) k_tri_pk6<16, 3, 4, 1, 256, true><<<grid, 512, 0, c->stream>>>(g);
-    else k_tri_pk6<24, 3, 4, 1, 256, true><<<grid, 512, 0, c->stream>>>(g);
+    // diagnostics only: LSSP_AMD_PK6_TRACE=path[:block] appends one JSON line per sweep
+    static const char *trp = getenv("LSSP_AMD_PK6_TRACE");
+    if (!trp) {
+        launch_pk6_k<false>(c, t, g, grid);
+    } else {
+        const char *colon = strrchr(trp, ':');
+        g.tblk = colon ? atoi(colon + 1) : t.bp_nb / 2;
+        const size_t tn = 8 * (size_t)t.bp_nb + 4 * (size_t)PK3_CAP + 64;
+        LSSP_HIP(hipMalloc(&g.trace, sizeof(unsigned long long) * tn));
+        LSSP_HIP(hipMemsetAsync(g.trace, 0, sizeof(unsigned long long) * tn, c->stream));
+        launch_pk6_k<true>(c, t, g, grid);
+        std::vector<unsigned long long> h(tn);
+        LSSP_HIP(hipMemcpyAsync(h.data(), g.trace, sizeof(unsigned long long) * tn, hipMemcpyDeviceToHost, c->stream));
+        LSSP_HIP(hipStreamSynchronize(c->stream));
+        (void)hipFree(g.trace);
+        std::string path(trp, colon ? colon - trp : strlen(trp));
+        FILE *f = fopen(path.c_str(), "a");
+        if (f) {
+            fprintf(f, "{\"upper\": %d, \"nb\": %d, \"B\": %d, \"ep\": %d, \"tblk\": %d, \"grid\": %d, \"data\": [",
+                    (int)t.upper, t.bp_nb, t.bp_B, t.pk6_ep, g.tblk, grid);
+            for (size_t i = 0; i < tn; i++) fprintf(f, "%s%llu", i ? ", " : "", h[i]);
+            fprintf(f, "]}\n");
+            fclose(f);
+        }
+    }
     t.pk6_base += (unsigned long long)t.bp_nb + grid;
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;
