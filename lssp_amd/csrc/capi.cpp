@@ -111,6 +111,15 @@ void setup_mark(const char *phase)
     last = t;
 }
 
+SetupTimer::SetupTimer() : t0(wall_time()) {}
+void SetupTimer::mark(const char *phase)
+{
+    static const bool on = getenv("LSSP_AMD_SETUP_TIMES") && atoi(getenv("LSSP_AMD_SETUP_TIMES"));
+    const double t = wall_time();
+    if (on) fprintf(stderr, "lssp_amd setup:   %-26s %8.3f s\n", phase, t - t0);
+    t0 = t;
+}
+
 int host_threads()
 {
     static const int nt = [] {
@@ -673,7 +682,9 @@ static int ilu_upload(lssp_amd_ctx *c, lssp_amd_ilu *M)
     int stU = LSSP_AMD_OK, stL = LSSP_AMD_OK;
     std::thread tu([&] {
         try {
+            SetupTimer tm;
             stU = tri_levels(M->n, M->Up, M->Uj, true, levU);
+            tm.mark("U levels (thread)");
         } catch (const std::exception &) {
             stU = LSSP_AMD_ENOMEM;
         }

@@ -549,8 +549,10 @@ int build_trisched(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const std
 {
     t.n = n;
     std::vector<int> lev;
+    SetupTimer tm;
     if (lev_in) lev.swap(*lev_in);
     else LSSP_TRY(tri_levels(n, Tp, Tj, upper, lev));
+    tm.mark(upper ? "U levels" : "L levels");
     if ((int)lev.size() != n) return LSSP_AMD_EINVAL;
     long nstrict = 0;
     bool unit = true;

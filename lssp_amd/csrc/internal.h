@@ -111,7 +111,7 @@ struct lssp_amd_mat {
     uint8_t *Ad = nullptr;
     int *d_off = nullptr;
     int ndiag = 0;
-    // windowed x (k_spmv_win): when every 1024-row block's columns fall in a
+    // windowed x (k_spmv_sell): when every 1024-row block's columns fall in a
     // span of at most WIN_CAP entries, d_win[2b], d_win[2b+1] = that span
     // [lo, hi) and the product stages x[lo, hi) in LDS; nullptr: not windowed
     int *d_win = nullptr;
@@ -315,6 +315,12 @@ int lprint(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 double wall_time();  // seconds, lssp_get_time() (utils.cxx:40-46)
 // setup phase timings to stderr when LSSP_AMD_SETUP_TIMES=1 (tuning aid)
 void setup_mark(const char *phase);
+// a sub-phase's own duration (LSSP_AMD_SETUP_TIMES; thread-safe: no shared clock)
+struct SetupTimer {
+    double t0;
+    SetupTimer();
+    void mark(const char *phase);
+};
 // host setup loops: f(lo, hi) over [0, n) in contiguous chunks on up to 16
 // threads (OMP_NUM_THREADS / the hardware concurrency, whichever is smaller)
 int host_threads();  // worker threads for host setup: <= 16, <= OMP_NUM_THREADS

@@ -28,6 +28,13 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
 {
     (void)c;
     if (n <= 0) return LSSP_AMD_OK;
+    SetupTimer tm;
+    const char *side = upper ? "U" : "L";
+    std::string nm;
+    auto mark = [&](const char *what) {
+        nm = std::string(side) + " " + what;
+        tm.mark(nm.c_str());
+    };
     auto Q = [&](int r) { return upper ? n - 1 - r : r; };
     auto strict_begin = [&](int i) { return upper ? Tp[i] + 1 : Tp[i]; };
     auto strict_end = [&](int i) { return upper ? Tp[i + 1] : Tp[i + 1] - 1; };
@@ -47,6 +54,7 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
             bw = std::max(bw, w);
         });
     }
+    mark("bandwidth");
     long B = std::max(64L, (long)bw);  // one bandwidth per block: measured best
     if (B > n) B = n;
     const int nb = (int)((n + B - 1) / B);
@@ -80,6 +88,7 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
             }
         }
     }, 1);
+    mark("block level order");
     std::vector<int> step_pos, blk_step(nb + 1, 0);
     for (int b = 0; b < nb; b++) {
         blk_step[b] = (int)step_pos.size();
@@ -124,6 +133,7 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
             if (!unit) diag[p] = upper ? Tx[Tp[i]] : Tx[Tp[i + 1] - 1];
         }
     });
+    mark("entries in sweep order");
     {
         // v6 packets; the rhs of the U sweep is the L sweep's output, read in
         // L's schedule order (the L sweep's rhs is permuted into L order first)
@@ -138,6 +148,7 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
         else if (st6 != LSSP_AMD_OK) return st6;
         if (!upper) t.h_pos = pos;
     }
+    mark("packets (incl. upload)");
     t.bp_B = (int)B;
     t.upper = upper;
     t.bp_nb = nb;
@@ -150,6 +161,7 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
     };
     LSSP_TRY(up(t.bp_perm, perm));  // position -> row: the apply's permutation kernels
     LSSP_TRY(up(t.bp_pos, pos));    // row -> position: x back to natural order as a gather
+    mark("permutation upload");
     return LSSP_AMD_OK;
 }
 
