@@ -223,43 +223,57 @@ void qsplit(double *a, int *ind, int n, int ncut)
     }
 }
 
-// pc-ilut.cxx:51-286 -- ILUT(tol, p) of one local block
-HostCSR ilut_factor(const HostCSR &A, double tol, int p)
+// pc-ilut.cxx:51-286 -- ILUT(tol, p) of one local block, written straight into
+// the split factors the sweeps use: L (strict entries in the reference's row
+// order, then the unit diagonal LAST) and U (pivot FIRST, then the U part).
+// The reference stores a row as L part, diagonal, U part; splitting that row
+// the way ilu_factor splits any factor (entries before the diagonal to L, the
+// diagonal as 1.0 to L and as the pivot to U, the rest to U) gives exactly
+// these rows, so no combined factor is kept and no split pass runs.  Row 0 is
+// A's row as is (:89-96), so U's row 0 is A's row 0 entry for entry.
+void ilut_factor_lu(const HostCSR &A, double tol, int p, HostCSR &L, HostCSR &U)
 {
     const int n = A.n;
-    HostCSR M;
-    M.n = n;
-    M.ncols = n;
-    M.Ap.assign(n + 1, 0);
+    L = HostCSR();
+    U = HostCSR();
+    L.n = L.ncols = U.n = U.ncols = n;
+    L.Ap.assign(n + 1, 0);
+    U.Ap.assign(n + 1, 0);
     // a row keeps at most p L and p U entries plus its diagonal (:256-274):
     // reserving that bound (address space only; pages are touched as rows are
-    // appended) means the factor is never regrown and copied mid-way -- at
-    // 256^3 a regrowth moved ~4 GB and first-touched ~8 GB more
-    // p beyond n-1 keeps no more than a full row; a reservation the host
-    // refuses falls back to a modest one and the vectors grow as the
-    // reference's realloc does (pc-ilut.cxx:71, :215-222)
+    // appended) means the factors are never regrown and copied mid-way -- at
+    // 256^3 a regrowth moved ~4 GB and first-touched ~8 GB more.  p beyond
+    // n-1 keeps no more than a full row; a reservation the host refuses falls
+    // back to a modest one and the vectors grow as the reference's realloc does
+    // (pc-ilut.cxx:71, :215-222)
     const size_t pc = p >= 0 ? (size_t)std::min(p, std::max(n - 1, 0)) : 0;
-    const size_t cap = p >= 0 ? (size_t)n * (2 * pc + 1) : A.Aj.size() * 3;
+    const size_t row0 = (size_t)(A.Ap[1] - A.Ap[0]);
+    const size_t capl = p >= 0 ? (size_t)n * (pc + 1) : A.Aj.size() * 2;
+    const size_t capu = p >= 0 ? (size_t)n * (pc + 1) + row0 : A.Aj.size() * 2;
     try {
-        M.Aj.reserve(cap);
-        M.Ax.reserve(cap);
+        L.Aj.reserve(capl);
+        L.Ax.reserve(capl);
+        U.Aj.reserve(capu);
+        U.Ax.reserve(capu);
     } catch (const std::exception &) {
-        const size_t small = std::max(A.Aj.size() * 3, (size_t)n * 8);
-        M.Aj.reserve(std::min(cap, small));
-        M.Ax.reserve(std::min(cap, small));
+        const size_t small = std::max(A.Aj.size() * 2, (size_t)n * 4);
+        L.Aj.reserve(std::min(capl, small));
+        L.Ax.reserve(std::min(capl, small));
+        U.Aj.reserve(std::min(capu, small));
+        U.Ax.reserve(std::min(capu, small));
     }
     std::vector<double> w(n), diag(n);
     std::vector<int> jr(n, -1), jw(n);
-    // ustart[r]: where row r's entries past its diagonal begin.  Rows >= 1 are
-    // stored L part, diagonal, U part, so the elimination below visits exactly
-    // the entries with col > jrow, in the same order, without walking the L
-    // part; row 0 (A's row as is) is scanned whole
-    std::vector<int> ustart(n, 0);
     for (int k = A.Ap[0]; k < A.Ap[1]; k++) {  // row 0 as is (:89-96)
-        M.Aj.push_back(A.Aj[k]);
-        M.Ax.push_back(A.Ax[k]);
+        if (A.Aj[k] == 0) {
+            L.Aj.push_back(0);
+            L.Ax.push_back(1.0);
+        }
+        U.Aj.push_back(A.Aj[k]);
+        U.Ax.push_back(A.Ax[k]);
     }
-    M.Ap[1] = (int)M.Aj.size();
+    L.Ap[1] = (int)L.Aj.size();
+    U.Ap[1] = (int)U.Aj.size();
     diag[0] = A.Ax[A.Ap[0]];
     if (std::fabs(diag[0]) < ZERO_DIAG_TOL) diag[0] = diag[0] > 0 ? ZERO_DIAG_VALUE : -ZERO_DIAG_VALUE;
 
@@ -306,11 +320,13 @@ HostCSR ilut_factor(const HostCSR &A, double tol, int p)
             }
             jr[jrow] = -1;
             const double aik = w[j] = w[j] / diag[jrow];
-            for (int k = ustart[jrow]; k < M.Ap[jrow + 1]; k++) {
-                const int col = M.Aj[k];
+            // the pivot row's entries past its diagonal, in stored order: U's row
+            // without its leading pivot (row 0: A's row, filtered by col)
+            for (int k = jrow ? U.Ap[jrow] + 1 : 0; k < U.Ap[jrow + 1]; k++) {
+                const int col = U.Aj[k];
                 if (col <= jrow) continue;
                 const int q = jr[col];
-                const double mx = -aik * M.Ax[k];
+                const double mx = -aik * U.Ax[k];
                 if (q == -1 && std::fabs(mx) < rel) continue;
                 if (col < i) {
                     if (q == -1) {
@@ -341,21 +357,22 @@ HostCSR ilut_factor(const HostCSR &A, double tol, int p)
         int len = std::min(nl, p);
         qsplit(w.data(), jw.data(), nl, len);
         for (int k = 0; k < len; k++) {
-            M.Ax.push_back(w[k]);
-            M.Aj.push_back(jw[k]);
+            L.Ax.push_back(w[k]);
+            L.Aj.push_back(jw[k]);
         }
-        M.Ax.push_back(diag[i]);
-        M.Aj.push_back(i);
-        ustart[i] = (int)M.Aj.size();
+        L.Ax.push_back(1.0);
+        L.Aj.push_back(i);
+        U.Ax.push_back(diag[i]);
+        U.Aj.push_back(i);
         len = std::min(nu, p);
         qsplit(w.data() + i + 1, jw.data() + i + 1, nu, len);
         for (int k = 0; k < len; k++) {
-            M.Ax.push_back(w[i + 1 + k]);
-            M.Aj.push_back(jw[i + 1 + k]);
+            U.Ax.push_back(w[i + 1 + k]);
+            U.Aj.push_back(jw[i + 1 + k]);
         }
-        M.Ap[i + 1] = (int)M.Aj.size();
+        L.Ap[i + 1] = (int)L.Aj.size();
+        U.Ap[i + 1] = (int)U.Aj.size();
     }
-    return M;
 }
 
 HostCSR local_block(const HostCSR &F, int s, int e)
@@ -433,23 +450,51 @@ void ilu_factor(lssp_amd_ctx *c, int kind, HostCSR &&A0, int level, double tol, 
         F = std::move(M);
     }
     F.n = F.ncols = n;
+    if (kind == LSSP_AMD_ILUT) {
+        // ILUT writes L and U directly (ilut_factor_lu); one block (the
+        // reference's default blk_size = n) needs no block copy at all
+        if (blk >= n) {
+            ilut_factor_lu(M, tol, p, L, U);
+        } else {
+            L = HostCSR();
+            U = HostCSR();
+            L.n = L.ncols = U.n = U.ncols = n;
+            L.Ap.assign(n + 1, 0);
+            U.Ap.assign(n + 1, 0);
+            for (int s = 0; s < n; s += blk) {
+                const int e = std::min(s + blk, n);
+                HostCSR Lb, Ub;
+                ilut_factor_lu(local_block(M, s, e), tol, p, Lb, Ub);
+                for (int i = 0; i < Lb.n; i++) {
+                    for (int k = Lb.Ap[i]; k < Lb.Ap[i + 1]; k++) {
+                        L.Aj.push_back(Lb.Aj[k] + s);
+                        L.Ax.push_back(Lb.Ax[k]);
+                    }
+                    for (int k = Ub.Ap[i]; k < Ub.Ap[i + 1]; k++) {
+                        U.Aj.push_back(Ub.Aj[k] + s);
+                        U.Ax.push_back(Ub.Ax[k]);
+                    }
+                    L.Ap[s + i + 1] = (int)L.Aj.size();
+                    U.Ap[s + i + 1] = (int)U.Aj.size();
+                }
+            }
+        }
+        M = HostCSR();
+        setup_mark("numeric factorization (into L, U)");
+        return;
+    }
     if (F.Ap.empty()) {
     F.Ap.assign(n + 1, 0);
     F.Aj.reserve(M.Aj.size());
     F.Ax.reserve(M.Ax.size());
     for (int s = 0; s < n; s += blk) {
         const int e = std::min(s + blk, n);
-        HostCSR B = local_block(M, s, e), T;
-        if (kind == LSSP_AMD_ILUK) {
-            ilu0_factor(B.n, B.Ap.data(), B.Aj.data(), B.Ax.data());
-            T = std::move(B);
-        } else {
-            T = ilut_factor(B, tol, p);
-        }
-        for (int i = 0; i < T.n; i++) {
-            for (int k = T.Ap[i]; k < T.Ap[i + 1]; k++) {
-                F.Aj.push_back(T.Aj[k] + s);
-                F.Ax.push_back(T.Ax[k]);
+        HostCSR B = local_block(M, s, e);
+        ilu0_factor(B.n, B.Ap.data(), B.Aj.data(), B.Ax.data());
+        for (int i = 0; i < B.n; i++) {
+            for (int k = B.Ap[i]; k < B.Ap[i + 1]; k++) {
+                F.Aj.push_back(B.Aj[k] + s);
+                F.Ax.push_back(B.Ax[k]);
             }
             F.Ap[s + i + 1] = (int)F.Aj.size();
         }

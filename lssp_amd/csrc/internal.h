@@ -297,7 +297,7 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
                       const std::vector<double> &Tx, bool upper, const std::vector<int> &lev,
                       TriSched &t, const TriSched *prod = nullptr);
 int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &pos, const std::vector<int> &rp,
-                   const std::vector<int> &cols, const std::vector<double> &vals,
+                   const int *cols, const double *vals,
                    const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
                    const std::vector<int> &blk_step, int nb, long B, const std::vector<int> &rhs_index,
                    TriSched &t);

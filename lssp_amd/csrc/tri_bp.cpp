@@ -16,6 +16,7 @@
 #include <climits>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 
 #include "internal.h"
@@ -107,8 +108,10 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
     // ring window come from LDS (code -1 - slot), everything else from HBM
     std::vector<int> rp(n + 1, 0);
     for (int p = 0; p < n; p++) rp[p + 1] = rp[p] + strict_end(perm[p]) - strict_begin(perm[p]);
-    std::vector<int> cols(rp[n]);
-    std::vector<double> vals(rp[n]), diag;
+    // uninitialised: every slot is written below, by the position threads
+    std::unique_ptr<int[]> cols(new int[std::max(rp[n], 1)]);
+    std::unique_ptr<double[]> vals(new double[std::max(rp[n], 1)]);
+    std::vector<double> diag;
     if (!unit) diag.resize(n);
     parallel_for(n, [&](long p0, long p1) {
         for (long p = p0; p < p1; p++) {
@@ -141,7 +144,7 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
         parallel_for(n, [&](long r0, long r1) {
             for (long r = r0; r < r1; r++) rhs_index[r] = prod && !prod->h_pos.empty() ? prod->h_pos[r] : pos[r];
         });
-        const int st6 = build_packets6(n, perm, pos, rp, cols, vals, diag, unit, step_pos, blk_step, nb, B,
+        const int st6 = build_packets6(n, perm, pos, rp, cols.get(), vals.get(), diag, unit, step_pos, blk_step, nb, B,
                                        rhs_index, t);
         // a row longer than the longest record: the sync-free sweep serves the factor
         if (st6 == LSSP_AMD_EUNSUPPORTED) t.pk6_n = -1;
@@ -184,7 +187,7 @@ int build_bp_schedule(lssp_amd_ctx *c, int n, const std::vector<int> &Tp, const 
 //     order, the U sweep reads the L sweep's shadow), xidx[nx] (schedule
 //     positions of the HBM operands in this sweep's own shadow)
 int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &pos, const std::vector<int> &rp,
-                   const std::vector<int> &cols, const std::vector<double> &vals,
+                   const int *cols, const double *vals,
                    const std::vector<double> &diag, bool unit, const std::vector<int> &step_pos,
                    const std::vector<int> &blk_step, int nb, long B, const std::vector<int> &rhs_index,
                    TriSched &t)
@@ -218,6 +221,15 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
         for (long b = b0; b < b1 && status.load() == LSSP_AMD_OK; b++) {
             std::vector<int> &desc = bp[b].desc, &idx = bp[b].idx;
             std::vector<uint32_t> &rec = bp[b].rec;
+            {
+                // the block's packets at most: one per row, each array padded by
+                // < 4 words -- reserved so the multi-MB vectors never regrow
+                const long rows = std::min<long>((b + 1) * B, n) - b * B;
+                const int steps = blk_step[b + 1] - blk_step[b];
+                rec.reserve((size_t)(rows * ((EP / 2) + 2 * EP + 3) + 12L * (rows / 8 + steps + 1)));
+                idx.reserve((size_t)(rows * (1 + PK3_EXT) + 8));
+                desc.reserve((size_t)4 * (rows / 8 + steps + 1));
+            }
             static_assert(pk6_xs_off(BP_RING + 1, 1, ROWS * PK3_EXT - 1) <= 0xffff, "16-bit operand offsets");
             for (int s = blk_step[b]; s < blk_step[b + 1]; s++) {
                 int p = step_pos[s];
@@ -289,37 +301,47 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
         idx_off[b + 1] = idx_off[b] + (long)bp[b].idx.size();
     }
     if (rec_off[nb] / 4 > INT_MAX || idx_off[nb] > INT_MAX) return LSSP_AMD_EUNSUPPORTED;
-    std::vector<int> desc(4L * blk[nb]);
-    std::vector<uint32_t> rec(rec_off[nb] + 4, 0u);
-    std::vector<int> idx(idx_off[nb] + 1, 0);
+    // the blocks laid out in order (offsets made absolute) in uninitialised
+    // host arrays, filled by the block threads in parallel -- no single-thread
+    // zero fill of the multi-GB record stream -- then one upload each
+    SetupTimer tm;
+    t.pk6_n = blk[nb];
+    t.pk6_ep = EP;
+    t.pk6_rows = ROWS;
+    const size_t ndesc = std::max<size_t>(4L * blk[nb], 1), nrec = rec_off[nb] + 4, nidx = idx_off[nb] + 1;
+    std::unique_ptr<int[]> desc(new int[ndesc]);
+    std::unique_ptr<uint32_t[]> rec(new uint32_t[nrec]);
+    std::unique_ptr<int[]> idx(new int[nidx]);
+    std::fill(rec.get() + rec_off[nb], rec.get() + nrec, 0u);  // the kernels' whole-unit reads past the end
+    idx[nidx - 1] = 0;
+    desc[0] = 0;
     parallel_for(nb, [&](long b0, long b1) {
         for (long b = b0; b < b1; b++) {
-            const BlkPk &k = bp[b];
-            int *d = desc.data() + 4L * blk[b];
+            BlkPk &k = bp[b];
+            int *d = desc.get() + 4L * blk[b];
             for (size_t e = 0; e < k.desc.size(); e += 4) {
                 d[e] = k.desc[e] + (int)(rec_off[b] / 4);
                 d[e + 1] = k.desc[e + 1] + (int)idx_off[b];
                 d[e + 2] = k.desc[e + 2];
                 d[e + 3] = k.desc[e + 3];
             }
-            std::copy(k.rec.begin(), k.rec.end(), rec.begin() + rec_off[b]);
-            std::copy(k.idx.begin(), k.idx.end(), idx.begin() + idx_off[b]);
+            std::copy(k.rec.begin(), k.rec.end(), rec.get() + rec_off[b]);
+            std::copy(k.idx.begin(), k.idx.end(), idx.get() + idx_off[b]);
+            k = BlkPk();  // the block's host copy is done with
         }
     }, 1);
     bp.clear();
-    t.pk6_n = blk[nb];
-    t.pk6_ep = EP;
-    t.pk6_rows = ROWS;
-    auto up = [](auto *&d, const auto &h) -> int {
-        using T = typename std::remove_reference<decltype(h)>::type::value_type;
-        LSSP_HIP(hipMalloc(&d, sizeof(T) * std::max<size_t>(h.size(), 1)));
-        if (!h.empty()) LSSP_HIP(hipMemcpy(d, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
+    auto up = [](auto *&d, const auto *h, size_t cnt) -> int {
+        using T = typename std::remove_const<typename std::remove_pointer<decltype(h)>::type>::type;
+        LSSP_HIP(hipMalloc(&d, sizeof(T) * cnt));
+        LSSP_HIP(hipMemcpy(d, h, sizeof(T) * cnt, hipMemcpyHostToDevice));
         return LSSP_AMD_OK;
     };
-    LSSP_TRY(up(t.pk6_blk, blk));
-    LSSP_TRY(up(t.pk6_desc, desc));
-    LSSP_TRY(up(t.pk6_rec, rec));
-    LSSP_TRY(up(t.pk6_idx, idx));
+    LSSP_TRY(up(t.pk6_blk, blk.data(), blk.size()));
+    LSSP_TRY(up(t.pk6_desc, desc.get(), ndesc));
+    LSSP_TRY(up(t.pk6_rec, rec.get(), nrec));
+    LSSP_TRY(up(t.pk6_idx, idx.get(), nidx));
+    tm.mark("packet upload");
     LSSP_HIP(hipMalloc(&t.pk6_claim, sizeof(unsigned long long)));
     LSSP_HIP(hipMemset(t.pk6_claim, 0, sizeof(unsigned long long)));
     t.pk6_base = 0;

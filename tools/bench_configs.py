@@ -3,6 +3,7 @@
     python tools/bench_configs.py cg-thermal   [--iters 1000] [--ref-iters 1000]
     python tools/bench_configs.py gmres-ilut   [--grid 256]   [--ref-iters 30]
     python tools/bench_configs.py bicgstab-iluk --grid 512     (config 4's matrix on one GPU)
+    python tools/bench_configs.py general-ilu  [--grid 216]   (the packet-sweep ILU path)
 
 Each prints ONE JSON line: GPU throughput (Krylov it/s with HIP-event SpMV
 and ILU-apply rooflines), the reference's own CPU timing on a bounded sample
@@ -15,6 +16,9 @@ compared with the reference's iteration count.
 config 5 (cg-thermal): thermal2-like SPD matrix (lssp_amd.synthetic), CG,
 PC_NON, b = 1, x0 = 0, fixed 1000 iterations.
 config 3 (gmres-ilut): 7-pt Poisson 256^3, GMRES(30) + ILUT(1e-4, p=20).
+general-ilu: the packet-sweep ILU path on a non-grid mesh ILU(0), a 7-pt ILU(1)
+and the 7-pt ILU(0) forced off the line sweeps (tracked number for the
+general path).
 """
 import argparse
 import json
@@ -199,9 +203,62 @@ def bicgstab_iluk(args):
     print(json.dumps(out), flush=True)
 
 
+def general_ilu(args):
+    """The general (packet-sweep) ILU path on matrices the line sweeps do not
+    serve: ILU(0) of the thermal-like mesh matrix (not a grid), ILU(1) of a
+    7-pt grid, and the 7-pt ILU(0) forced onto the packet sweeps (LSSP_AMD_LINE=0)
+    beside its line sweeps.  Per case: apply time (B_ilu GB/s), BiCGSTAB it/s
+    (tree), and for the thermal case a SERIAL-mode run bitwise vs the reference."""
+    import lssp_amd
+    import oracle as O
+    from lssp_amd.synthetic import thermal_like
+    dev = lssp_amd.Device(0)
+    cases = []
+
+    def case(name, Ap, Aj, Ax, level, line, ref_iters=0):
+        n, nnz = Ap.size - 1, int(Ap[-1])
+        log(f"{name}: setup")
+        old = os.environ.get("LSSP_AMD_LINE")
+        if not line:
+            os.environ["LSSP_AMD_LINE"] = "0"
+        t0 = time.perf_counter()
+        M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=level)
+        t_pc = time.perf_counter() - t0
+        if old is None:
+            os.environ.pop("LSSP_AMD_LINE", None)
+        else:
+            os.environ["LSSP_AMD_LINE"] = old
+        A = lssp_amd.DMat(dev, Ap, Aj, Ax)
+        out = {"case": name, "rows": n, "nnz": nnz, "ilu": {"level": level, "nnzL": M.nnzL, "nnzU": M.nnzU,
+                                                            "setup_s": round(t_pc, 2),
+                                                            "sweeps": "line" if line and "7-pt" in name and level == 0
+                                                            else "packet"},
+               "ilu_apply": apply_leg(dev, M, n, reps=10)}
+        timed_solve(dev, A, M, n, lssp_amd.BICGSTAB, 5)
+        r, t = timed_solve(dev, A, M, n, lssp_amd.BICGSTAB, args.iters)
+        out["gpu"] = {"iters": r.nits, "seconds": round(t, 4), "iters_per_s": round(r.nits / t, 2),
+                      "reduction": "tree"}
+        if ref_iters and O.ref_available():
+            parity(dev, A, M, n, O.CSR(n, Ap, Aj, Ax), O.BICGSTAB, dict(pc=O.PC_ILUK, level=level),
+                   ref_iters, 30, out)
+        M.close()
+        A.close()
+        print(json.dumps(out), flush=True)
+        cases.append(out)
+
+    Ap, Aj, Ax = thermal_like()
+    case("thermal-like ILU(0)", Ap, Aj, Ax, 0, True, ref_iters=args.ref_iters)
+    Ap, Aj, Ax = lssp_amd.poisson(3, 128)
+    case("7-pt 128^3 ILU(1)", Ap, Aj, Ax, 1, True)
+    Ap, Aj, Ax = lssp_amd.poisson(3, args.grid)
+    case(f"7-pt {args.grid}^3 ILU(0), packet sweeps", Ap, Aj, Ax, 0, False)
+    case(f"7-pt {args.grid}^3 ILU(0), line sweeps", Ap, Aj, Ax, 0, True)
+    dev.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", choices=["cg-thermal", "gmres-ilut", "bicgstab-iluk"])
+    ap.add_argument("which", choices=["cg-thermal", "gmres-ilut", "bicgstab-iluk", "general-ilu"])
     ap.add_argument("--iters", type=int, default=1000)
     ap.add_argument("--ref-iters", type=int, default=None)
     ap.add_argument("--grid", type=int, default=256)
@@ -214,6 +271,11 @@ def main():
         # bitwise leg is kept to a few Arnoldi steps
         args.ref_iters = 5 if args.ref_iters is None else args.ref_iters
         gmres_ilut(args)
+    elif args.which == "general-ilu":
+        args.iters = min(args.iters, 100)
+        args.ref_iters = 20 if args.ref_iters is None else args.ref_iters
+        args.grid = 216 if args.grid == 256 else args.grid
+        general_ilu(args)
     else:
         args.iters = min(args.iters, 50)
         bicgstab_iluk(args)

@@ -1,5 +1,5 @@
 // ilut_probe.cpp -- tuning aid (not part of the library): times the host ILUT
-// numeric factorization (ilu_setup.cpp ilut_factor, pc-ilut.cxx:51-286) on a
+// numeric factorization (ilu_setup.cpp ilut_factor_lu, pc-ilut.cxx:51-286) on a
 // 7-pt Poisson N^3 matrix and prints a checksum of the factor (variants must
 // keep it bit for bit).
 //   make -C lssp_amd/csrc && hipcc -O2 -std=c++17 -I include -I /opt/rocm/include \
@@ -34,14 +34,16 @@ int main(int argc, char **argv)
                 A.Ap[r + 1] = (int)A.Aj.size();
             }
     const auto t0 = std::chrono::steady_clock::now();
-    HostCSR F = ilut_factor(A, 1e-4, 20);
+    HostCSR L, U;
+    ilut_factor_lu(A, 1e-4, 20, L, U);
     const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     uint64_t h = 1469598103934665603ull;
-    for (size_t k = 0; k < F.Aj.size(); k++) {
-        uint64_t b;
-        memcpy(&b, &F.Ax[k], 8);
-        h = (h ^ b ^ (uint64_t)F.Aj[k]) * 1099511628211ull;
-    }
-    printf("N %d n %d nnz %zu ilut %.3f s hash %016llx\n", N, n, F.Aj.size(), s, (unsigned long long)h);
+    for (const HostCSR *F : {&L, &U})
+        for (size_t k = 0; k < F->Aj.size(); k++) {
+            uint64_t b;
+            memcpy(&b, &F->Ax[k], 8);
+            h = (h ^ b ^ (uint64_t)F->Aj[k]) * 1099511628211ull;
+        }
+    printf("N %d n %d nnz %zu ilut %.3f s hash %016llx\n", N, n, L.Aj.size() + U.Aj.size(), s, (unsigned long long)h);
     return 0;
 }
