@@ -168,11 +168,11 @@ constexpr int PK3_EXT = 2;       // v6: HBM x operands per packet row (on averag
 constexpr int PK3_CAP = 4096;    // v6: packets per block (descriptors staged in LDS)
 
 // ---- line sweeps of structured ILU(0) factors (linesweep.hip) ----------------
-#ifndef LINE_P_OVERRIDE
-constexpr int LINE_P = 4;  // planes per tile
-#else
-constexpr int LINE_P = LINE_P_OVERRIDE;  // tuning builds (tools/build_variant.sh)
-#endif
+// A tile is 256 / P lines x P planes = 256 rows per step, P in {4, 8, 16}
+// (chosen per factor, build_line_sweep): a compute wave's 64 lanes are P / 4
+// groups of 256 / P lines, each lane holds 2 planes, 2 compute waves.  Squarer
+// tiles = fewer tile-to-tile hand-offs on a sweep's critical path (216^3: 56
+// hops with 64 x 4 tiles, 26 with 16 x 16).
 enum { LT_KIN = 1, LT_JIN = 2, LT_KOUT = 4, LT_JOUT = 8 };
 struct LineGeom {
     int nx = 0, ny = 0, nz = 0;
@@ -191,6 +191,7 @@ struct LineTile {  // one workgroup's unit of work, in its sweep's coordinates
 };
 struct LineSweep {
     int nx = 0, ny = 0, nz = 0, ntiles = 0, tmax = 0, NA = 3;
+    int P = 4;  // planes per tile (256 / P lines)
     long rows_total = 0;
     LineTile *d_tiles = nullptr;
     double *d_coef = nullptr;
@@ -200,7 +201,7 @@ struct LineSweep {
 };
 struct LineILU {
     LineGeom g;
-    int W = 0, S = 0, tmax = 0, ntiles = 0;
+    int P = 4, W = 0, S = 0, tmax = 0, ntiles = 0;
     LineSweep L, U;
     double *d_ustream = nullptr;  // the U sweep's rhs, written by the L sweep
     double *d_lstream = nullptr;  // the L sweep's rhs in its stream layout (k_line_rhs)
@@ -278,9 +279,14 @@ int launch_copy(lssp_amd_ctx *c, double *x, const double *y, long n);
 // tree: level-2 over nslot partial rows of C entries; then the finalize program
 int launch_reduce_tree(lssp_amd_ctx *c, long C, int nslot, const Fin &f, int slot0 = 0);  // partial rows slot0 ..
 // CG's vector updates with the preceding reduction's level 2 folded in (k_cg_fused)
-enum { CGF_P = 0, CGF_XR = 1 };
+// CGF_R / CGF_PX / CGF_X: the x update x += alpha p is deferred from the x/r
+// pass into the next p pass (which reads p anyway), or a batch's last pass
+// CGF_X; stamp = the S_DONE value (FIN_CG_RES_RHO_B) that the stop test of
+// this pass's own reduction writes -- a guard equal to it still runs the
+// pass's x update, any other nonzero guard skips the pass
+enum { CGF_P = 0, CGF_XR = 1, CGF_R = 2, CGF_PX = 3, CGF_X = 4 };
 int launch_cg_fused(lssp_amd_ctx *c, int kind, long n, double *x, double *p, double *r, const double *z,
-                    const double *q, int pin_slot, int pout_slot, const Fin &f);
+                    const double *q, int pin_slot, int pout_slot, const Fin &f, int stamp = 0);
 // serial: sums of products a_k[i]*b_k[i] in index order (== vector.cxx:123-133)
 int launch_reduce_serial(lssp_amd_ctx *c, long n, int nslot, const double *const *a,
                          const double *const *b, const Fin &f, const double *carry = nullptr);

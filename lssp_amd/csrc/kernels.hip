@@ -140,7 +140,7 @@ __device__ void finalize(const Fin &f, const double *s, double *scal, double *tr
             const int k = (int)scal[S_NIT];
             scal[S_H + k] = t0;
             scal[S_NIT] = k + 1;
-            if (t0 <= scal[S_TOL]) scal[S_DONE] = 1.0;
+            if (t0 <= scal[S_TOL]) scal[S_DONE] = k + 1;  // the stamp of k_cg_fused's deferred x update
         }
         break;
     }
@@ -500,9 +500,13 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_sell(SpmvArgs a, const int *w
 #pragma unroll
     for (int k = 0; k < NK; k++) ax[k] = sax[sbase + 64 * k + lane];
     const int rr = min(r, a.nrows - 1);
+    // a fused dot with x itself (CG's q.p): when the block's rows lie inside
+    // its x span, x[r] is read from the staged span (uniform), not again from HBM
+    const int r0 = (int)(blk * WIN_ROWS), r1 = min(r0 + WIN_ROWS, a.nrows);
+    const bool w0x = NRED > 0 && a.w0 == a.x && a.w0 != a.z && r0 >= lo && r1 <= hi;
     double w0p = 0.0, w1p = 0.0;
     if (NRED > 0) {
-        if (a.w0 != a.z) w0p = a.w0[rr];
+        if (a.w0 != a.z && !w0x) w0p = a.w0[rr];
         if (NRED > 1 && a.w1 && a.w1 != a.z) w1p = a.w1[rr];
     }
 #pragma unroll
@@ -520,6 +524,7 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_sell(SpmvArgs a, const int *w
     zb[lr] = sum;
     __syncthreads();
     sum = zb[tid];
+    if (w0x && r < a.nrows) w0p = sxw[r - lo2];
     double zv = 0;
     if (r < a.nrows) {
         if (EPI == EPI_MXY) zv = sum;
@@ -846,10 +851,17 @@ int launch_ew(lssp_amd_ctx *c, const Ew &e)
 //           r.r partials -> pout (solver-cg.cxx:96-104)
 //   CGF_P:  beta = (r.r) / rho0 [FIN_CG_RES_RHO(_B)]; when the stop test
 //           (:109) holds no workgroup updates p; else p = r + beta p (:88-92)
+//   CGF_R:  CGF_XR without x (3 vectors instead of 6); CGF_PX: CGF_P that
+//           first adds the previous alpha p to x (also when the stop test
+//           holds) -- p is read once for both; CGF_X: that x update alone (a
+//           batch's last iteration).  x gets the same operands in the same
+//           order, one pass later: every value is unchanged.  The stop test
+//           writes S_DONE = its iteration's stamp, so the pass that finds it
+//           still applies its x update while any later pass returns.
 // pin and pout are different partial rows: a workgroup still reading pin
 // never races another one writing its chunk partials.
 struct CgFusedArgs {
-    int kind;
+    int kind, stamp;
     long n, C;
     double *x, *p, *r;
     const double *z, *q;
@@ -865,8 +877,16 @@ __global__ __launch_bounds__(1024) void k_cg_fused(CgFusedArgs a)
     __shared__ double wl[16];
     __shared__ double red[2][4][4];
     __shared__ double sc[2];
-    if (a.guard && *a.guard != 0.0) return;
+    if (a.guard) {  // a batched iteration past the stop; the stop's own pass keeps its x update
+        const double g = *a.guard;
+        if (g != 0.0 && g != (double)a.stamp) return;
+    }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (a.kind == CGF_X) {  // the batch's deferred x update alone
+        const double al = a.scal[S_ALPHA];
+        for (long i = blockIdx.x * 1024L + tid; i < a.n; i += gridDim.x * 1024L) a.x[i] = a.x[i] + al * a.p[i];
+        return;
+    }
     {
         double acc = 0.0;
         for (long k = tid; k < a.C; k += L2_LANES) acc += a.pin[k];
@@ -884,7 +904,7 @@ __global__ __launch_bounds__(1024) void k_cg_fused(CgFusedArgs a)
             const double s = u[0];
             double v;
             bool stop = false;
-            if (a.kind == CGF_XR) {
+            if (a.kind == CGF_XR || a.kind == CGF_R) {
                 v = a.scal[S_RHO1] / s;  // finalize FIN_CG_ALPHA's alpha (S_RHO1 is not written below)
             } else {
                 v = s / a.scal[S_RHO0];  // FIN_CG_RES_RHO's beta (S_RHO0 is not written below)
@@ -899,7 +919,17 @@ __global__ __launch_bounds__(1024) void k_cg_fused(CgFusedArgs a)
         }
         __syncthreads();
     }
-    if (sc[1] != 0.0) return;
+    const bool stop = sc[1] != 0.0;
+    if (a.kind == CGF_PX) {  // x += alpha p of the previous x/r pass (CGF_R), then p = r + beta p
+        const double al = a.scal[S_ALPHA], v = sc[0];  // workgroup 0's finalize does not write S_ALPHA
+        for (long i = blockIdx.x * 1024L + tid; i < a.n; i += gridDim.x * 1024L) {
+            const double pv = a.p[i];
+            a.x[i] = a.x[i] + al * pv;
+            if (!stop) a.p[i] = a.z[i] + v * pv;
+        }
+        return;
+    }
+    if (stop) return;
     const double v = sc[0];
     int par = 0;
     for (long g = blockIdx.x; g * 1024 < a.n; g += gridDim.x, par ^= 1) {
@@ -909,8 +939,8 @@ __global__ __launch_bounds__(1024) void k_cg_fused(CgFusedArgs a)
         } else {
             double rr = 0.0;
             if (i < a.n) {
-                const double pv = a.p[i], qv = a.q[i];
-                a.x[i] = a.x[i] + v * pv;
+                const double qv = a.q[i];
+                if (a.kind == CGF_XR) a.x[i] = a.x[i] + v * a.p[i];
                 const double rn = a.r[i] - v * qv;
                 a.r[i] = rn;
                 rr = rn * rn;
@@ -929,12 +959,12 @@ __global__ __launch_bounds__(1024) void k_cg_fused(CgFusedArgs a)
 }
 
 int launch_cg_fused(lssp_amd_ctx *c, int kind, long n, double *x, double *p, double *r, const double *z,
-                    const double *q, int pin_slot, int pout_slot, const Fin &f)
+                    const double *q, int pin_slot, int pout_slot, const Fin &f, int stamp)
 {
     if (n <= 0) return LSSP_AMD_OK;
     const long C = num_chunks(n);
     LSSP_TRY(ensure_part(c, C));
-    CgFusedArgs g{kind, n, C, x, p, r, z, q, c->d_part + pin_slot * c->part_cap,
+    CgFusedArgs g{kind, stamp, n, C, x, p, r, z, q, c->d_part + pin_slot * c->part_cap,
                   c->d_part + pout_slot * c->part_cap, c->d_sums, c->d_scal, c->d_trace, f, c->guard};
     const long grid = std::min<long>((n + 1023) / 1024, 2L * c->num_cus);  // 2 per CU
     k_cg_fused<<<grid, 1024, 0, c->stream>>>(g);

@@ -8,20 +8,27 @@
 // same recurrence in mirrored coordinates (i' = nx-1-i, ...), and its
 // descending summation order (solver-tri.cxx:38) is then again k'-1, j'-1, i'-1.
 //
-// Decomposition.  A TILE is nj <= 64 consecutive lines (j) of np <= P
-// consecutive planes (k); one workgroup runs it.  Lane l owns line j0+l; at
-// step s it computes, for each plane p, row i = s - l - p.  Then
+// Decomposition.  A TILE is nj <= NJ consecutive lines (j) of np <= P
+// consecutive planes (k), P * NJ = 256 (G = 64 / NJ lane groups); one
+// workgroup runs it.  A compute wave's lane (g, l) owns line j0+l of the
+// group's planes; at step s it computes, for each of its planes p, row
+// i = s - l - p.  Then
 //   * (i-1, j, k):   the lane's own value of the previous step (a register);
-//   * (i, j-1, k):   lane l-1's value of the previous step (DPP wave_shr:1);
-//   * (i, j, k-1):   the lane's own value of plane p-1 at the previous step;
-// so a step is P rows per lane of pure register arithmetic.  Across tiles the
-// two boundary streams (plane np-1 -> the next tile in k, lane nj-1 -> the next
+//   * (i, j-1, k):   line l-1's value of the previous step (DPP: wave_shr:1,
+//                    or row_shr:1 when the groups are the 16-lane DPP rows);
+//   * (i, j, k-1):   the lane's own value of plane p-1 at the previous step
+//                    (the group's first plane: LDS, written by the group or
+//                    wave holding plane p-1);
+// so a step is pure register arithmetic plus one LDS read.  Across tiles the
+// two boundary streams (plane np-1 -> the next tile in k, line nj-1 -> the next
 // tile in j) go through HBM hand-off buffers with the value as the flag
 // (TRI_SENTINEL), indexed by the consumer's step so both sides access them
-// coalesced.  A path through the grid crosses W + S tiles instead of nz planes.
+// coalesced.  A path through the grid crosses W + S tiles instead of nz
+// planes: squarer tiles (16 x 16 instead of 64 x 4) halve W + S at the same
+// 256 rows per step.
 //
 // Roles (one barrier per step, LDS only):
-//   wave 0          compute: reads the step's slot, writes results to LDS;
+//   waves 0..CW-1   compute: read the step's slot, write results to LDS;
 //   waves 1..NL     loaders: LDS-DMA (global_load_lds) of the step's
 //                   coefficient block (and rhs) D steps ahead, steps q = w mod NL;
 //   wave NL+1       poller: LDS-DMA sc1 reads of the hand-off inputs DH steps
@@ -199,7 +206,7 @@ static int build_tiles(const LineGeom &g, int P, int W, std::vector<LineTile> &t
 static int upload_sweep(lssp_amd_ctx *c, const LineGeom &g, const std::vector<LineTile> &tiles, const CoefSrc &src,
                         int NA, LineSweep &ls)
 {
-    const int nx = g.nx, P = LINE_P;
+    const int nx = g.nx, P = ls.P;
     std::vector<LineTile> tt = tiles;
     long rows_total = 0;
     int tmax = 0;
@@ -246,6 +253,31 @@ static int upload_sweep(lssp_amd_ctx *c, const LineGeom &g, const std::vector<Li
     return LSSP_AMD_OK;
 }
 
+// planes per tile: the P in {4, 8, 16} with the fewest tile hops on a sweep's
+// critical path, (W - 1) + (S - 1) for W tiles across the lines and S down the
+// longest plane segment (ties: the smaller P).  216^3: 64 x 4 tiles 56 hops,
+// 32 x 8 32, 16 x 16 26; a 27-plane block-Jacobi slab of it: 9, 9, 14.
+static int line_choose_P(const LineGeom &g)
+{
+#ifdef LINE_P_FORCE
+    return LINE_P_FORCE;  // tuning builds (tools/build_variant.sh)
+#endif
+    int seg = 1;
+    for (int k = 0; k < g.nz;) {
+        int e = k + 1;
+        while (e < g.nz && g.kin[e]) e++;
+        seg = std::max(seg, e - k);
+        k = e;
+    }
+    int best = 4;
+    long bh = -1;
+    for (int P : {4, 8, 16}) {
+        const long hops = (g.ny + 256 / P - 1) / (256 / P) + (seg + P - 1) / P - 2;
+        if (bh < 0 || hops < bh) best = P, bh = hops;
+    }
+    return best;
+}
+
 int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std::vector<int> &Lj,
                      const std::vector<double> &Lx, const std::vector<int> &Up, const std::vector<int> &Uj,
                      const std::vector<double> &Ux, LineILU &li)
@@ -254,8 +286,8 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
     if (env && !atoi(env)) return LSSP_AMD_EUNSUPPORTED;
     LineGeom g;
     if (!detect_grid(n, Lp, Lj, Lx, Up, Uj, g)) return LSSP_AMD_EUNSUPPORTED;
-    const int P = LINE_P;
-    const int W = (g.ny + 63) / 64;
+    const int P = line_choose_P(g);
+    const int W = (g.ny + 256 / P - 1) / (256 / P);
     std::vector<LineTile> Lt;
     int S = 0;
     LSSP_TRY(build_tiles(g, P, W, Lt, S));
@@ -281,6 +313,7 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
     cl.build(Lp, Lj, Lx, false, n, g.nx, plane, g.unitL ? 3 : 4);
     cu.build(Up, Uj, Ux, true, n, g.nx, plane, 4);
     li.g = g;
+    li.P = li.L.P = li.U.P = P;
     li.W = W;
     li.S = S;
     LSSP_TRY(upload_sweep(c, g, Lt, cl, g.unitL ? 3 : 4, li.L));
@@ -305,8 +338,8 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
     LSSP_HIP(hipMalloc(&li.d_lstream, sizeof(double) * (li.L.rows_total + 16 * 1024 / 8)));
     LSSP_HIP(hipMemset(li.d_lstream, 0, sizeof(double) * (li.L.rows_total + 16 * 1024 / 8)));
     li.tmax = std::max(li.L.tmax, li.U.tmax);
-    li.hk_stride = (long)li.tmax * 64;
-    li.hj_stride = (long)li.tmax * LINE_P;
+    li.hk_stride = (long)li.tmax * (256 / P);
+    li.hj_stride = (long)li.tmax * P;
     li.ntiles = (int)Lt.size();
     li.hk_n = li.hk_stride * li.ntiles;
     li.hj_n = li.hj_stride * li.ntiles;
@@ -424,6 +457,23 @@ __device__ __forceinline__ double dpp_shr1(double v, double old)
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+// the previous line's value within each lane group; a group's line 0 gets old
+// (G = 4: the groups are the DPP rows, row_shr:1 leaves lane 0 of a row alone)
+template <int G>
+__device__ __forceinline__ double dpp_shr1g(double v, double old)
+{
+    if constexpr (G == 4) {
+        const long long b = __double_as_longlong(v), o = __double_as_longlong(old);
+        const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, 0x111, 0xf, 0xf, false);
+        const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), 0x111, 0xf, 0xf, false);
+        return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+    } else if constexpr (G == 2) {
+        return sel_lanes(1ull << 32, old, dpp_shr1(v, old));
+    } else {
+        return dpp_shr1(v, old);
+    }
+}
+
 template <int I, int N, class F>
 __device__ __forceinline__ void static_for(F &&f)
 {
@@ -436,30 +486,31 @@ __device__ __forceinline__ void static_for(F &&f)
 // slot layout (bytes): the step's coefficient block, its rhs, the hand-off inputs
 template <int P, int NA, bool RHS_NAT>
 struct LineSlot {
-    static constexpr int NPC = (P * 64 * NA * 8 + 1023) / 1024;  // 1 KB DMA pieces of the coefficient block
-    static constexpr int NRP = (P * 64 * 8 + 1023) / 1024;       // ... of a U rhs-stream block
+    static constexpr int NJ = 4 * 64 / P;                        // lines per tile (P * NJ = 256 rows per step)
+    static constexpr int NPC = (P * NJ * NA * 8 + 1023) / 1024;  // 1 KB DMA pieces of the coefficient block
+    static constexpr int NRP = (P * NJ * 8 + 1023) / 1024;       // ... of a U rhs-stream block
     static constexpr int NRD = RHS_NAT ? 0 : NRP;                // rhs DMA instructions per step
     static constexpr int COEF = 0;
     static constexpr int RHS = NPC * 1024;
-    static constexpr int KFIN = RHS + (RHS_NAT ? 0 : NRP * 1024);  // double[64]
-    static constexpr int JFIN = KFIN + 512;                                  // double[P]
+    static constexpr int KFIN = RHS + (RHS_NAT ? 0 : NRP * 1024);  // double[NJ]
+    static constexpr int JFIN = KFIN + NJ * 8;                      // double[P]
     static constexpr int BYTES = (JFIN + 8 * P + 15) & ~15;
 };
 
 // LDS after the slot ring: the compute results of the last RS steps
-// ([RS][P][64] doubles: the next compute wave's k-input, and the storers'
+// ([RS][P][NJ] doubles: the next compute group's k-input, and the storers'
 // source -- natural-order output is written in 8-step runs per line, so it
 // keeps two 8-step blocks), the claimed tile, the poller's DMA sink and, for
-// a natural-order rhs, two 8-step rhs blocks ([8][P*64+1] doubles each,
+// a natural-order rhs, two 8-step rhs blocks ([8][P*NJ+1] doubles each,
 // filled by the rhs wave in runs the same way)
 template <int OUT>
 constexpr int line_rs() { return OUT == 1 ? 16 : 2; }
 template <int P>
-constexpr int line_rhs_blk() { return 8 * (P * 64 + 1); }  // doubles per rhs block
+constexpr int line_rhs_blk() { return 8 * (256 + 1); }  // doubles per rhs block (P * NJ = 256)
 template <int P, int NA, bool RHS_NAT, int OUT, int D>
 constexpr int line_lds_bytes()
 {
-    return (D + 1) * LineSlot<P, NA, RHS_NAT>::BYTES + line_rs<OUT>() * P * 64 * 8 + 16 + 512 +
+    return (D + 1) * LineSlot<P, NA, RHS_NAT>::BYTES + line_rs<OUT>() * 256 * 8 + 16 + 512 +
            (RHS_NAT ? 2 * line_rhs_blk<P>() * 8 : 0);
 }
 template <int CW, int NL, int SW, bool RHS_NAT>
@@ -508,22 +559,24 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
     // landing lead: the loaders and the poller complete step s+LA's slot during
     // step s; the compute reads it at step s+LA-1 (into registers, one step ahead)
     constexpr int LA = 2;
-    static_assert(DH >= 2 && DH < D && P % CW == 0 && (OUT == 1 || OUT == 2), "lead");
-    constexpr int PC = P / CW;
+    using SL = LineSlot<P, NA, RHS_NAT>;
+    // a compute wave's lanes are G groups of NJ lines; lane (g, l) holds PC
+    // planes of line l: planes p0 + g*PC .. p0 + g*PC + PC-1 of the wave's PW
+    constexpr int NJ = SL::NJ, G = 64 / NJ, PW = P / CW, PC = PW / G;
+    static_assert(DH >= 2 && DH < D && P % CW == 0 && PW % G == 0 && PC >= 1 && (OUT == 1 || OUT == 2), "lead");
     constexpr int R = D + 1;
     // first step of every role (a multiple of 2, 3 and 4); the rhs wave writes
     // block 0 from step -9 on, its loads LINE_RW steps earlier
     constexpr int S0 = -(((D > 9 + LINE_RW ? D : 9 + LINE_RW) + 11) / 12) * 12;
-    using SL = LineSlot<P, NA, RHS_NAT>;
     constexpr int NITEM = SL::NPC + SL::NRD;          // DMA instructions per step, shared by the loaders
     constexpr int KPER = (NITEM + NL - 1) / NL;
     static_assert((D - LA) * KPER <= 63 && 2 * (DH - 1) <= 63, "vmcnt range");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char *ring = smem;
     constexpr int RS = line_rs<OUT>();
-    double *res = reinterpret_cast<double *>(smem + R * SL::BYTES);  // [RS][P][64]
-    int *s_tile = reinterpret_cast<int *>(res + RS * P * 64);
-    double *rhsblk = reinterpret_cast<double *>(smem + R * SL::BYTES + RS * P * 64 * 8 + 16 + 512);  // [2][8][P*64+1]
+    double *res = reinterpret_cast<double *>(smem + R * SL::BYTES);  // [RS][P][NJ]
+    int *s_tile = reinterpret_cast<int *>(res + RS * P * NJ);
+    double *rhsblk = reinterpret_cast<double *>(smem + R * SL::BYTES + RS * P * NJ * 8 + 16 + 512);  // [2][8][P*NJ+1]
     const unsigned lds0 = (unsigned)(uintptr_t)smem;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -545,7 +598,9 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
         const long SB = (long)P * nj;  // rows per step block
         const bool kin = d.flags & LT_KIN, jin = d.flags & LT_JIN, kout = d.flags & LT_KOUT,
                    jout = d.flags & LT_JOUT;
-        const int lc = min(lane, nj - 1);
+        // compute and storer lanes: group gl (plane offset), line ll
+        const int ll = lane & (NJ - 1), gl = lane / NJ;
+        const int lc = min(ll, nj - 1);
         // natural row of (i, line lane, plane p) = nb(p) + i (mirror: nb(p) - i)
         auto nb = [&](int p, int l) {
             const long r = ((long)(d.k0 + p) * a.ny + (d.j0 + l)) * nx;
@@ -572,7 +627,8 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
             // Published values need no canonicalisation: every one is the result
             // of an f64 add or division, and those never return the sentinel (a
             // signalling NaN) in IEEE mode.
-            const int p0 = wave * PC;
+            const int p0 = wave * PW;     // the wave's first plane
+            const int pg = p0 + gl * PC;  // the lane group's first plane
             struct In {
                 double ck[PC], cj[PC], ci[PC], dg[PC], rh[PC], jv[PC];
             };
@@ -580,14 +636,14 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                 const char *slot = ring + so;
 #pragma unroll
                 for (int u = 0; u < PC; u++) {
-                    const int p = p0 + u;
+                    const int p = pg + u;
                     const double *b = reinterpret_cast<const double *>(slot + SL::COEF) + (p * nj + lc) * NA;
                     in.ck[u] = b[0];
                     in.cj[u] = b[1];
                     in.ci[u] = b[2];
                     if constexpr (NA == 4) in.dg[u] = b[3];
                     if constexpr (RHS_NAT) {
-                        in.rh[u] = rhsblk[((s >> 3) & 1) * line_rhs_blk<P>() + (s & 7) * (P * 64 + 1) + p * 64 + lane];
+                        in.rh[u] = rhsblk[((s >> 3) & 1) * line_rhs_blk<P>() + (s & 7) * (P * NJ + 1) + p * NJ + ll];
                     } else {
                         in.rh[u] = reinterpret_cast<const double *>(slot + SL::RHS)[p * nj + lc];
                     }
@@ -604,30 +660,48 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
             const __amdgpu_buffer_rsrc_t hjo =
                 __builtin_amdgcn_make_buffer_rsrc(a.hj + (long)t * a.hj_stride, 0, (int)(a.hj_stride * 8), 0x00020000);
             const uint64_t njm = nj >= 64 ? ~0ull : ((1ull << nj) - 1);
-            // the plane this wave publishes to the next k-tile (-1: none)
-            const int uk = (kout && np - 1 >= p0 && np - 1 < p0 + PC) ? np - 1 - p0 : -1;
-            const int jl_off = lane == nj - 1 ? 0 : OOB;  // lane nj-1 feeds the next j-tile
-            // hw[u]: the lanes whose row of plane p0+u exists at the current step
-            // (lane l's row i = s - p - l is valid iff lane l-1's was at s-1, and
-            // lane 0's iff 0 <= s - p < nx), pm[u]: 0 for planes past the tile
+            constexpr uint64_t GM = NJ >= 64 ? ~0ull : ((1ull << NJ) - 1);  // group 0's lanes
+            constexpr uint64_t GS = G == 1 ? 1ull : G == 2 ? 0x100000001ull : 0x0001000100010001ull;  // group starts
+            // the plane this wave publishes to the next k-tile: register uk (-1: none) of group gk
+            const int ko = np - 1 - p0;
+            const bool kw = kout && ko >= 0 && ko < PW;
+            const int uk = kw ? ko % PC : -1;
+            const uint64_t kgm = kw ? GM << ((ko / PC) * NJ % 64) : 0ull;
+            const int jl_off = ll == nj - 1 ? gl * PC * 8 : OOB;  // line nj-1 feeds the next j-tile
+            // hw[u]: the lanes whose row of register u's plane exists at the current
+            // step (line l's row i = s - p - l is valid iff line l-1's was at s-1,
+            // and line 0's iff 0 <= s - p < nx), pm[u]: 0 for planes past the tile
             uint64_t hw[PC], pm[PC];
 #pragma unroll
-            for (int u = 0; u < PC; u++) hw[u] = 0, pm[u] = p0 + u < np ? njm : 0ull;
+            for (int u = 0; u < PC; u++) {
+                hw[u] = 0;
+                pm[u] = 0;
+#pragma unroll
+                for (int g = 0; g < G; g++)
+                    if (p0 + g * PC + u < np) pm[u] |= njm << (g * NJ % 64);
+            }
             unsigned so = (unsigned)(((S0 % R) + R) % R) * SL::BYTES;  // slot of step s
             constexpr unsigned RB = (unsigned)(R * SL::BYTES);
             auto body = [&](int s, In &cur, In &nxt) {
                 if (TRACE && lane == 0 && wave == 0 && s == 0) a.trace[8 * t + 1] = __builtin_amdgcn_s_memrealtime();
                 if (trs && wave == 0 && s >= 0 && s < T) ts[8 * s] = __builtin_amdgcn_s_memtime();
                 const unsigned sn = so + SL::BYTES == RB ? 0u : so + SL::BYTES;  // slot of step s+1
-                const double kx = wave == 0 ? reinterpret_cast<const double *>(ring + so + SL::KFIN)[lane]
-                                            : res[((s - 1) & (RS - 1)) * P * 64 + (p0 - 1) * 64 + lane];
+                // k-input of the group's first plane: the poller's (wave 0, group 0),
+                // else plane pg-1 of the previous step (another group or wave)
+                const double kx = (wave == 0 && gl == 0)
+                                      ? reinterpret_cast<const double *>(ring + so + SL::KFIN)[ll]
+                                      : res[((s - 1) & (RS - 1)) * P * NJ + (pg - 1) * NJ + ll];
                 asm volatile("" ::: "memory");  // kx's read is issued first (LDS returns in order)
                 load(s + 1, sn, nxt);
 #pragma unroll
                 for (int u = 0; u < PC; u++) {
-                    const int y = s - p0 - u;  // lane 0's row; bit = 0 <= y < nx, in integer ops (SALU)
-                    const unsigned bit = ((unsigned)((y - nx) & ~y)) >> 31;
-                    hw[u] = ((hw[u] << 1) | (uint64_t)bit) & pm[u];
+                    uint64_t nb = 0;  // line 0 of each group; bit = 0 <= y < nx, in integer ops (SALU)
+#pragma unroll
+                    for (int g = 0; g < G; g++) {
+                        const int y = s - (p0 + g * PC + u);
+                        nb |= (uint64_t)(((unsigned)((y - nx) & ~y)) >> 31) << (g * NJ % 64);
+                    }
+                    hw[u] = (((hw[u] << 1) & ~GS) | nb) & pm[u];
                 }
                 if (s >= 0 && s < T) {
                     double xn[PC];
@@ -635,7 +709,7 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                     for (int u = PC - 1; u >= 0; u--) {
                         const uint64_t m = hw[u];
                         const double xk = u > 0 ? xc[u - 1] : kx;
-                        const double xj = dpp_shr1(xc[u], cur.jv[u]);
+                        const double xj = dpp_shr1g<G>(xc[u], cur.jv[u]);
                         double v = cur.rh[u] - cur.ck[u] * xk;
                         v = v - cur.cj[u] * xj;
                         v = v - cur.ci[u] * xc[u];
@@ -649,12 +723,17 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
 #pragma unroll
                         for (int u = 1; u < PC; u++)
                             if (uk == u) m = hw[u], v = xn[u];
-                        int vo = lane * 8;
+                        m &= kgm;
+                        int vo = ll * 8;
                         asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(vo) : "v"(OOB), "v"(vo), "s"(m));
                         __builtin_amdgcn_raw_buffer_store_b64(split64((uint64_t)__double_as_longlong(v)), hko, vo,
-                                                              q >= 0 ? q * 512 : OOB, 16);  // sc1
+                                                              q >= 0 ? q * (NJ * 8) : OOB, 16);  // sc1
                     }
                     if (jout) {
+                        // planes past the tile (p >= np) publish nothing: the two sweeps
+                        // share the hand-off buffers, and the other sweep's tile of this
+                        // index may have more planes, whose consumer would take a value
+                        // left here for a ready one
                         const int q = s + 1 - nj;
                         const int sof = q >= 0 ? (q * P + p0) * 8 : OOB;
                         if constexpr (PC == 2) {
@@ -665,19 +744,22 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                             d4.y = (unsigned)(b0 >> 32);
                             d4.z = (unsigned)b1;
                             d4.w = (unsigned)(b1 >> 32);
-                            __builtin_amdgcn_raw_buffer_store_b128(d4, hjo, jl_off, sof, 16);
+                            __builtin_amdgcn_raw_buffer_store_b128(d4, hjo, pg + 1 < np ? jl_off : OOB, sof, 16);
+                            if (np & 1)  // uniform: the group whose second plane is past the tile
+                                __builtin_amdgcn_raw_buffer_store_b64(split64(b0), hjo, pg + 1 == np ? jl_off : OOB,
+                                                                      sof, 16);
                         } else {
 #pragma unroll
                             for (int u = 0; u < PC; u++)
                                 __builtin_amdgcn_raw_buffer_store_b64(split64((uint64_t)__double_as_longlong(xn[u])), hjo,
-                                                                      jl_off + 8 * u, sof, 16);
+                                                                      pg + u < np ? jl_off + 8 * u : OOB, sof, 16);
                         }
                     }
                     if (trs && wave == 0 && s >= 0 && s < T) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
 #pragma unroll
                     for (int u = 0; u < PC; u++) {
                         xc[u] = xn[u];
-                        res[((s & (RS - 1)) * P + p0 + u) * 64 + lane] = xc[u];
+                        res[((s & (RS - 1)) * P + pg + u) * NJ + ll] = xc[u];
                     }
                 }
                 so = sn;
@@ -736,7 +818,7 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
         } else if (wave == CW + NL) {
             // ---------------- poller ----------------
             // LDS-DMA sc1 reads of the hand-off inputs straight into their ring
-            // slots, DH steps ahead: at step s the k-input of step s+DH (32 lanes x
+            // slots, DH steps ahead: at step s the k-input of step s+DH (NJ/2 lanes x
             // 16 B) and the j-input of step s+DH+1 (P/2 lanes x 16 B) are issued,
             // and those of steps s+1 (k) and s+2 (j) -- issued DH-1 steps ago -- are
             // waited for and checked (the compute reads k at its step start, j one
@@ -746,22 +828,22 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
             // +0.0 and +0.0 * +0.0 leaves the row's sum bit for bit unchanged.
             const double *hk = a.hk + (long)max(d.tk, 0) * a.hk_stride;
             const double *hj = a.hj + (long)max(d.tj, 0) * a.hj_stride;
-            const int qmax = (int)(a.hk_stride / 64) - 1;
+            const int qmax = (int)(a.hk_stride / NJ) - 1;
             auto kval = [&](int q) { return q >= 0 && q < T && lane < nj && q - lane >= 0 && q - lane < nx; };
             auto jval = [&](int q) { return q >= 0 && q < T && lane < np && q - lane >= 0 && q - lane < nx; };
-            const unsigned sink = lds0 + (unsigned)(R * SL::BYTES + RS * P * 64 * 8 + 16);
+            const unsigned sink = lds0 + (unsigned)(R * SL::BYTES + RS * P * NJ * 8 + 16);
             auto issue = [&](int q) {
-                // k-input of step q (lanes 0..31), j-input of step q+1 (lanes 0..P/2-1)
-                const char *kp = reinterpret_cast<const char *>(hk + (long)min(max(q, 0), qmax) * 64) + lane * 16;
+                // k-input of step q (lanes 0..NJ/2-1), j-input of step q+1 (lanes 0..P/2-1)
+                const char *kp = reinterpret_cast<const char *>(hk + (long)min(max(q, 0), qmax) * NJ) + lane * 16;
                 const char *jp = reinterpret_cast<const char *>(hj + (long)min(max(q + 1, 0), qmax) * P) + lane * 16;
                 const unsigned ks = kin ? lds0 + (unsigned)((((q % R) + R) % R) * SL::BYTES + SL::KFIN) : sink;
                 const unsigned js = jin ? lds0 + (unsigned)(((((q + 1) % R) + R) % R) * SL::BYTES + SL::JFIN) : sink;
-                if (lane < 32) dma16_sc1(kp, ks);
+                if (lane < NJ / 2) dma16_sc1(kp, ks);
                 if (lane < P / 2) dma16_sc1(jp, js);
             };
             if (!kin || !jin) {
                 for (int q = 0; q < R; q++) {
-                    if (!kin) reinterpret_cast<double *>(ring + q * SL::BYTES + SL::KFIN)[lane] = 0.0;
+                    if (!kin && lane < NJ) reinterpret_cast<double *>(ring + q * SL::BYTES + SL::KFIN)[lane] = 0.0;
                     if (!jin && lane < P) reinterpret_cast<double *>(ring + q * SL::BYTES + SL::JFIN)[lane] = 0.0;
                 }
             }
@@ -801,9 +883,9 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                             __builtin_amdgcn_s_sleep(1);
                         }
                     };
-                    if (bk) *kslot = __longlong_as_double((long long)spin(hk + (long)qk * 64 + lane));
+                    if (bk) *kslot = __longlong_as_double((long long)spin(hk + (long)qk * NJ + lane));
                     if (bj) *jslot = __longlong_as_double((long long)spin(hj + (long)qj * P + lane));
-                    if (kin && kval(s + DH)) (void)spin(hk + (long)(s + DH) * 64 + lane);
+                    if (kin && kval(s + DH)) (void)spin(hk + (long)(s + DH) * NJ + lane);
                     if (jin && jval(s + DH + 1)) (void)spin(hj + (long)(s + DH + 1) * P + lane);
                     for (int k = 2; k <= DH; k++) issue(s + k);  // the polls issued at steps s+k-DH
                 }
@@ -820,11 +902,11 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
             // Block b (steps 8b .. 8b+7) of the rhs is loaded as runs -- the 8
             // consecutive rows (i = 8b - l - p + m, m = 0..7) of line l, plane p go
             // to 8 consecutive lanes, so a load touches 8 runs instead of 64 lines
-            // -- in 8 slices of P*64 values; slice k is written to LDS at step
+            // -- in 8 slices of P*NJ values; slice k is written to LDS at step
             // 8b - 9 + k, from loads issued LINE_RW steps earlier (a register ring
             // the compiler tracks: plain loads, no asm).  The compute reads block b
             // from step 8b-1 on; two buffers alternate.
-            constexpr int NI = P * 64 / 64;  // loads per lane per slice
+            constexpr int NI = P * NJ / 64;  // loads per lane per slice
             auto slice_of = [&](int s, int &b, int &k) {
                 b = (s + 9) >> 3;
                 k = (s + 9) & 7;
@@ -835,9 +917,9 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                 slice_of(s, b, k);
 #pragma unroll
                 for (int it = 0; it < NI; it++) {
-                    const int v = k * P * 64 + it * 64 + lane;
+                    const int v = k * P * NJ + it * 64 + lane;
                     const int r = v >> 3, m = v & 7;
-                    const int p = r >> 6, l = r & 63;
+                    const int p = r / NJ, l = r % NJ;
                     const int i = 8 * b + m - l - p;
                     const bool ok = b >= 0 && p < np && l < nj && (unsigned)i < (unsigned)nx;
                     const long row = ok ? (a.mirror ? nb(p, l) - i : nb(p, l) + i) : 0;
@@ -851,9 +933,9 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                 double *blk = rhsblk + (b & 1) * line_rhs_blk<P>();
 #pragma unroll
                 for (int it = 0; it < NI; it++) {
-                    const int v = k * P * 64 + it * 64 + lane;
+                    const int v = k * P * NJ + it * 64 + lane;
                     const int r = v >> 3, m = v & 7;
-                    blk[m * (P * 64 + 1) + r] = src[it];  // r = p*64 + l
+                    blk[m * (P * NJ + 1) + r] = src[it];  // r = p*NJ + l
                 }
             };
             auto rstep = [&](int s, auto U) {
@@ -869,7 +951,7 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
         } else {
             // ---------------- storers: results, re-arms ----------------
             // OUT 2 (the U sweep's rhs stream, contiguous per plane and step):
-            // storer w writes planes w, w+SW, ... of step s-1.  OUT 1 (natural
+            // storer w writes 64-value chunks w, w+SW, ... of step s-1.  OUT 1 (natural
             // order): the results of an 8-step block are written during the next
             // 8 steps as runs -- 8 consecutive rows of one line (one lane, one
             // plane) go to 8 consecutive lanes, so a store touches 8 runs instead
@@ -880,13 +962,13 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
             uint64_t *hji = reinterpret_cast<uint64_t *>(a.hj + (long)max(d.tj, 0) * a.hj_stride) + min(lane, P - 1);
             const bool rk = w == SW - 1 && kin && lane < nj, rj = w == 0 && jin && lane < np;
             auto rearm = [&](int q) {
-                if (rk && (unsigned)(q - lane) < (unsigned)nx) hki[(long)q * 64] = TRI_SENTINEL;
+                if (rk && (unsigned)(q - lane) < (unsigned)nx) hki[(long)q * NJ] = TRI_SENTINEL;
                 if (rj && (unsigned)(q - lane) < (unsigned)nx) hji[(long)q * P] = TRI_SENTINEL;
             };
             if constexpr (OUT == 1) {
                 // block B (steps 8B .. 8B+7) is written during steps 8B+8 .. 8B+15,
                 // slice k = s - 8B - 8 at step s: values k*NV + w*NV/SW + it*64 + lane
-                constexpr int NV = P * 64;  // values per slice (a block holds 8 * NV)
+                constexpr int NV = P * NJ;  // values per slice (a block holds 8 * NV)
                 static_assert(NV % (64 * SW) == 0 && RS == 16, "slices");
                 auto slice = [&](int s) {
                     const int B = (s >> 3) - 1, k = s & 7;
@@ -895,9 +977,9 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                     for (int it = 0; it < NV / (64 * SW); it++) {
                         const int v = k * NV + w * (NV / SW) + it * 64 + lane;
                         const int r = v >> 3, m = v & 7;  // run r = (plane, line), step 8B+m
-                        const int p = r >> 6, l = r & 63, q = 8 * B + m;
+                        const int p = r / NJ, l = r % NJ, q = 8 * B + m;
                         const int i = q - l - p;
-                        const double x = res[((q & (RS - 1)) * P + p) * 64 + l];
+                        const double x = res[((q & (RS - 1)) * P + p) * NJ + l];
                         if (!(a.diag & 1) && p < np && l < nj && (unsigned)i < (unsigned)nx)
                             a.out[a.mirror ? nb(p, l) - i : nb(p, l) + i] = x;
                     }
@@ -913,14 +995,16 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                 // the last blocks' remaining slices (every compute result is in LDS)
                 for (int s = T + 1; s < 8 * ((T >> 3) + 2); s++) slice(s);
             } else {
-                constexpr int PS = (P + SW - 1) / SW;
+                // chunk c of a step's results: 64 lanes = G planes (c*G + gl) x NJ lines (ll)
+                constexpr int PS = P * NJ / 64 / SW;
+                static_assert(P * NJ % (64 * SW) == 0, "chunks");
                 double *po[PS];
                 int vlo[PS];
 #pragma unroll
                 for (int u = 0; u < PS; u++) {
-                    const int p = w + u * SW, pp = min(p, np - 1);
-                    vlo[u] = p < np && lane < nj ? lane + p : 1 << 30;  // valid iff 0 <= q - vlo < nx
-                    // the mirror U tile's row of (step T-1-q, plane np-1-p, lane nj-1-lane) at q = 0
+                    const int p = (w + u * SW) * G + gl, pp = min(p, np - 1);
+                    vlo[u] = p < np && ll < nj ? ll + p : 1 << 30;  // valid iff 0 <= q - vlo < nx
+                    // the mirror U tile's row of (step T-1-q, plane np-1-p, line nj-1-l) at q = 0
                     po[u] = a.out + d.ubase + (long)(T - 1) * SB + (long)(np - 1 - pp) * nj + (nj - 1 - lc);
                 }
                 for (int s = S0; s <= T; s++) {
@@ -928,10 +1012,10 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                     if (LINE_STORE_SLEEP) __builtin_amdgcn_s_sleep(LINE_STORE_SLEEP);
                     const int q = s - 1;
                     if (q >= 0 && q < T) {
-                        const double *rs = res + (q & (RS - 1)) * P * 64;
+                        const double *rs = res + (q & (RS - 1)) * P * NJ;
 #pragma unroll
                         for (int u = 0; u < PS; u++) {
-                            const double v = rs[min(w + u * SW, P - 1) * 64 + lane];
+                            const double v = rs[(w + u * SW) * 64 + lane];
                             if (!(a.diag & 1) && (unsigned)(q - vlo[u]) < (unsigned)nx) po[u][-SB * q] = v;
                         }
                         rearm(q);
@@ -970,11 +1054,7 @@ constexpr int line_dh()
     return RHS_NAT ? 2 : 3;
 #endif
 }
-#ifndef LINE_PC_OVERRIDE
-constexpr int LINE_CW = LINE_P / 2;  // two planes per compute wave
-#else
-constexpr int LINE_CW = LINE_P / LINE_PC_OVERRIDE;
-#endif
+constexpr int LINE_CW = 2;  // two compute waves: P / 4 lane groups x two planes each
 #ifndef LINE_NL_OVERRIDE
 constexpr int LINE_NL = 4;
 #else
@@ -982,10 +1062,10 @@ constexpr int LINE_NL = LINE_NL_OVERRIDE;
 #endif
 constexpr int LINE_SW = 2;
 
-template <int NA, bool RHS_NAT, int OUT, bool TRACE>
+template <int P, int NA, bool RHS_NAT, int OUT, bool TRACE>
 static int launch_line_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)
 {
-    auto kern = k_line<LINE_P, NA, RHS_NAT, OUT, LINE_CW, LINE_NL, line_d<RHS_NAT>(), line_dh<RHS_NAT>(), LINE_SW, TRACE>;
+    auto kern = k_line<P, NA, RHS_NAT, OUT, LINE_CW, LINE_NL, line_d<RHS_NAT>(), line_dh<RHS_NAT>(), LINE_SW, TRACE>;
     static int attr = 0;
     if (lds > attr) {
         LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -998,14 +1078,14 @@ static int launch_line_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g
     return LSSP_AMD_OK;
 }
 
-template <int NA, bool RHS_NAT, int OUT>
-static int launch_line_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a)
+template <int P, int NA, bool RHS_NAT, int OUT>
+static int launch_line_p(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a)
 {
-    const int lds = line_lds_bytes<LINE_P, NA, RHS_NAT, OUT, line_d<RHS_NAT>()>();
+    const int lds = line_lds_bytes<P, NA, RHS_NAT, OUT, line_d<RHS_NAT>()>();
     if (lds > 160 * 1024) return LSSP_AMD_EUNSUPPORTED;
     // diagnostics only: LSSP_AMD_LINE_TRACE=path[:tile] appends one JSON line per sweep
     static const char *trp = getenv("LSSP_AMD_LINE_TRACE");
-    if (!trp) return launch_line_k<NA, RHS_NAT, OUT, false>(c, ls, a, lds);
+    if (!trp) return launch_line_k<P, NA, RHS_NAT, OUT, false>(c, ls, a, lds);
     LineArgs g = a;
     const size_t tn = 8 * (size_t)ls.ntiles + 8 * (size_t)ls.tmax + 64;
     const char *colon = strrchr(trp, ':');
@@ -1013,7 +1093,7 @@ static int launch_line_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a
     LSSP_HIP(hipMalloc(&g.trace, sizeof(unsigned long long) * tn));
     LSSP_HIP(hipMemsetAsync(g.trace, 0, sizeof(unsigned long long) * tn, c->stream));
     const int grid = std::min(ls.ntiles, c->num_cus);
-    LSSP_TRY((launch_line_k<NA, RHS_NAT, OUT, true>(c, ls, g, lds)));
+    LSSP_TRY((launch_line_k<P, NA, RHS_NAT, OUT, true>(c, ls, g, lds)));
     std::vector<unsigned long long> h(tn);
     LSSP_HIP(hipMemcpyAsync(h.data(), g.trace, sizeof(unsigned long long) * tn, hipMemcpyDeviceToHost, c->stream));
     LSSP_HIP(hipStreamSynchronize(c->stream));
@@ -1022,24 +1102,35 @@ static int launch_line_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a
     FILE *f = fopen(path.c_str(), "a");
     if (f) {
         fprintf(f, "{\"mirror\": %d, \"ntiles\": %d, \"W\": %d, \"ttile\": %d, \"T\": %d, \"grid\": %d, \"data\": [",
-                a.mirror, ls.ntiles, (ls.ny + 63) / 64, g.ttile, ls.h_tiles[g.ttile].T, grid);
+                a.mirror, ls.ntiles, (ls.ny + 256 / P - 1) / (256 / P), g.ttile, ls.h_tiles[g.ttile].T, grid);
         for (size_t i = 0; i < tn; i++) fprintf(f, "%s%llu", i ? ", " : "", h[i]);
         fprintf(f, "]}\n");
         fclose(f);
     }
     return LSSP_AMD_OK;
 }
+template <int NA, bool RHS_NAT, int OUT>
+static int launch_line_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a)
+{
+    switch (ls.P) {
+    case 4: return launch_line_p<4, NA, RHS_NAT, OUT>(c, ls, a);
+    case 8: return launch_line_p<8, NA, RHS_NAT, OUT>(c, ls, a);
+    case 16: return launch_line_p<16, NA, RHS_NAT, OUT>(c, ls, a);
+    default: return LSSP_AMD_EUNSUPPORTED;
+    }
+}
 
 // which: 0 = L sweep, 1 = U sweep.  The rhs is natural order unless u_in (the
 // U rhs stream); the output goes to out (natural order) or, when out_u, to the
 // U rhs stream (the L sweep of an apply)
 // The apply's rhs (natural order) into the L sweep's stream layout.  A block
-// moves 8 consecutive steps of one tile (P x 64 x 8 values): value v of the
+// moves 8 consecutive steps of one tile (P x NJ x 8 values): value v of the
 // block is (plane p, line l, step q0 + m) with m = v & 7, so 8 neighbouring
 // lanes load one 64-byte run of a line from the natural-order vector and, per
 // step, 8 lanes store 8 consecutive stream entries.  Block b runs on XCD b % 8
 // and the XCD's blocks walk whole tiles in step order.
 constexpr int LRHS_RUN = 8;
+template <int P>
 __global__ __launch_bounds__(256) void k_line_rhs(const LineTile *__restrict__ tiles, int ntiles, int nq, int nx,
                                                  int ny, const double *__restrict__ rhs, double *__restrict__ out,
                                                  const double *guard)
@@ -1050,19 +1141,19 @@ __global__ __launch_bounds__(256) void k_line_rhs(const LineTile *__restrict__ t
     if (t >= ntiles) return;
     const LineTile d = tiles[t];
     if (q0 >= d.T) return;
-    constexpr int NV = LINE_P * 64 * LRHS_RUN / 256;  // values per thread
+    constexpr int NJ = 256 / P, NV = P * NJ * LRHS_RUN / 256;  // values per thread
     double v[NV];
 #pragma unroll
     for (int it = 0; it < NV; it++) {
-        const int k = it * 256 + threadIdx.x, m = k & 7, l = (k >> 3) & 63, p = k >> 9;
+        const int k = it * 256 + threadIdx.x, m = k & 7, l = (k >> 3) % NJ, p = (k >> 3) / NJ;
         const int i = q0 + m - l - p;
         const bool ok = q0 + m < d.T && p < d.np && l < d.nj && (unsigned)i < (unsigned)nx;
         v[it] = ok ? rhs[((long)(d.k0 + p) * ny + (d.j0 + l)) * nx + i] : 0.0;
     }
-    const long SB = (long)LINE_P * d.nj;
+    const long SB = (long)P * d.nj;
 #pragma unroll
     for (int it = 0; it < NV; it++) {
-        const int k = it * 256 + threadIdx.x, m = k & 7, l = (k >> 3) & 63, p = k >> 9;
+        const int k = it * 256 + threadIdx.x, m = k & 7, l = (k >> 3) % NJ, p = (k >> 3) / NJ;
         const int i = q0 + m - l - p;
         if (q0 + m < d.T && p < d.np && l < d.nj && (unsigned)i < (unsigned)nx)
             out[d.cbase + (q0 + m) * SB + p * d.nj + l] = v[it];
@@ -1106,7 +1197,8 @@ int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const doubl
     const LineSweep &L = li.L;
     const int nq = (L.tmax + LRHS_RUN - 1) / LRHS_RUN;
     const long grid = 8L * ((L.ntiles + 7) / 8) * nq;
-    k_line_rhs<<<grid, 256, 0, c->stream>>>(L.d_tiles, L.ntiles, nq, L.nx, L.ny, rhs, li.d_lstream, c->guard);
+    auto kr = L.P == 16 ? k_line_rhs<16> : L.P == 8 ? k_line_rhs<8> : k_line_rhs<4>;
+    kr<<<grid, 256, 0, c->stream>>>(L.d_tiles, L.ntiles, nq, L.nx, L.ny, rhs, li.d_lstream, c->guard);
     LSSP_HIP(hipGetLastError());
     LSSP_TRY(launch_line(c, li, 0, nullptr, false, nullptr, true, true));
     return launch_line(c, li, 1, nullptr, true, x, false);

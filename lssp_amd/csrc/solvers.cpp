@@ -477,14 +477,16 @@ int cg(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *
                 e.x = z;
                 e.out0 = p;
                 if (st == LSSP_AMD_OK) {
-                    if (have_held) st = launch_cg_fused(c, CGF_P, R.n, nullptr, p, nullptr, z, nullptr, 1, 1, held);
+                    // with the x update of the previous x/r pass (CGF_R): its stop test is stamped j
+                    if (have_held) st = launch_cg_fused(c, CGF_PX, R.n, x, p, nullptr, z, nullptr, 1, 1, held, j);
                     else st = R.ew(e);
                 }
                 have_held = false;
                 if (st == LSSP_AMD_OK) st = R.spmv(EPI_MXY, 1, p, 0, nullptr, q, 1, p);  // :95
                 const Fin fa = R.fin(FIN_CG_ALPHA, 1, R.T());                            // :96-99
                 if (fuse_l2) {
-                    if (st == LSSP_AMD_OK) st = launch_cg_fused(c, CGF_XR, R.n, x, p, r, nullptr, q, 0, 1, fa);
+                    // r only: x += alpha p (:102) rides with the next p pass, or the batch's CGF_X
+                    if (st == LSSP_AMD_OK) st = launch_cg_fused(c, CGF_R, R.n, x, p, r, nullptr, q, 0, 1, fa);
                 } else {
                     if (st == LSSP_AMD_OK) st = R.fin1(q, p, fa);
                     e = Ew();
@@ -505,6 +507,8 @@ int cg(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *
                     have_held = true;
                 } else if (fuse_l2) {
                     if (st == LSSP_AMD_OK) st = launch_reduce_tree(c, num_chunks(R.n), 1, fr, 1);
+                    if (st == LSSP_AMD_OK)
+                        st = launch_cg_fused(c, CGF_X, R.n, x, p, nullptr, nullptr, nullptr, 1, 1, Fin(), j + 1);
                 } else {
                     if (st == LSSP_AMD_OK) st = R.fin1(r, r, fr);
                 }

@@ -195,6 +195,43 @@ def test_trisolve_sweeps_and_levels_vs_oracle(dev, N, kind, kw):
         assert np.array_equal(x.download(), O.ilu_apply(O.CSR(A.n, Lp, Lj, Lx), O.CSR(A.n, Up, Uj, Ux), rhs))
 
 
+def _box7(nx, ny, nz, seed):
+    """7-pt stencil on an nx x ny x nz box (natural order, i fastest), random
+    nonsymmetric diagonally dominant values."""
+    rng = np.random.default_rng(seed)
+    n = nx * ny * nz
+    Ap, Aj, Ax = [0], [], []
+    for r in range(n):
+        i, j, k = r % nx, r // nx % ny, r // (nx * ny)
+        cols = [c for c, ok in ((r - nx * ny, k > 0), (r - nx, j > 0), (r - 1, i > 0), (r, True),
+                                (r + 1, i < nx - 1), (r + nx, j < ny - 1), (r + nx * ny, k < nz - 1)) if ok]
+        vals = rng.uniform(-1, -0.1, len(cols))
+        vals[cols.index(r)] = 7.0 + rng.uniform(0, 1)
+        Aj += cols
+        Ax += list(vals)
+        Ap.append(len(Aj))
+    return np.array(Ap, np.int32), np.array(Aj, np.int32), np.array(Ax)
+
+
+# boxes whose line-sweep tiles are 64 x 4 (planes per tile chosen by hop count:
+# (20, 100, 6)), 32 x 8 ((20, 60, 24)) and 16 x 16 ((20, 40, 40), (13, 37, 35)),
+# with partial tiles in j and k and an odd last plane count
+@pytest.mark.parametrize("nx,ny,nz", [(20, 100, 6), (20, 60, 24), (20, 40, 40), (13, 37, 35)])
+def test_line_sweep_tile_shapes_bitwise_vs_oracle(dev, nx, ny, nz):
+    import lssp_amd
+    Ap, Aj, Ax = _box7(nx, ny, nz, nx + ny + nz)
+    n = Ap.size - 1
+    M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=1, level=0)
+    L, U = O.ilu(O.CSR(n, Ap, Aj, Ax), "iluk", level=0)
+    (Lp, Lj, Lx), (Up, Uj, Ux) = M.factors()
+    assert np.array_equal(Lx, L.Ax) and np.array_equal(Ux, U.Ax)
+    x = dev.vec(n)
+    for rep in range(4):  # repeated applies: the shared hand-off buffers must be re-armed exactly
+        rhs = uniform(200 + rep, n)
+        M.apply(x, dev.vec(n, rhs))
+        assert np.array_equal(x.download(), O.ilu_apply(L, U, rhs)), rep
+
+
 @pytest.mark.parametrize("seed,n,per_row,missing,blk", [(11, 3000, 6, 0, 0), (12, 2500, 9, 7, 0),
                                                         (13, 4000, 5, 0, 1000), (14, 1999, 4, 5, 333)])
 def test_gpu_ilu0_factorization_bitwise_vs_oracle(dev, seed, n, per_row, missing, blk):
