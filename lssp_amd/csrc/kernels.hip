@@ -966,7 +966,10 @@ int launch_cg_fused(lssp_amd_ctx *c, int kind, long n, double *x, double *p, dou
     LSSP_TRY(ensure_part(c, C));
     CgFusedArgs g{kind, stamp, n, C, x, p, r, z, q, c->d_part + pin_slot * c->part_cap,
                   c->d_part + pout_slot * c->part_cap, c->d_sums, c->d_scal, c->d_trace, f, c->guard};
-    const long grid = std::min<long>((n + 1023) / 1024, 2L * c->num_cus);  // 2 per CU
+#ifndef CGF_PER_CU
+#define CGF_PER_CU 2  // tuning builds override it
+#endif
+    const long grid = std::min<long>((n + 1023) / 1024, (long)CGF_PER_CU * c->num_cus);  // 2 per CU
     k_cg_fused<<<grid, 1024, 0, c->stream>>>(g);
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;

@@ -1016,7 +1016,7 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
 #pragma unroll
                         for (int u = 0; u < PS; u++) {
                             const double v = rs[(w + u * SW) * 64 + lane];
-                            if (!(a.diag & 1) && (unsigned)(q - vlo[u]) < (unsigned)nx) po[u][-SB * q] = v;
+                            if (!(a.diag & 33) && (unsigned)(q - vlo[u]) < (unsigned)nx) po[u][-SB * q] = v;
                         }
                         rearm(q);
                     }
@@ -1060,7 +1060,11 @@ constexpr int LINE_NL = 4;
 #else
 constexpr int LINE_NL = LINE_NL_OVERRIDE;
 #endif
-constexpr int LINE_SW = 2;
+#ifndef LINE_SW_OVERRIDE
+constexpr int LINE_SW = 4;  // storer waves (2 -> 4: 216^3 apply 751 -> 693 us, r03ae)
+#else
+constexpr int LINE_SW = LINE_SW_OVERRIDE;  // tuning builds
+#endif
 
 template <int P, int NA, bool RHS_NAT, int OUT, bool TRACE>
 static int launch_line_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)
@@ -1194,6 +1198,10 @@ static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const doub
 
 int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs)
 {
+#ifdef LINE_APPLY_NAT  // tuning builds: the L sweep reads the natural-order rhs itself (rhs wave)
+    LSSP_TRY(launch_line(c, li, 0, rhs, false, nullptr, true));
+    return launch_line(c, li, 1, nullptr, true, x, false);
+#endif
     const LineSweep &L = li.L;
     const int nq = (L.tmax + LRHS_RUN - 1) / LRHS_RUN;
     const long grid = 8L * ((L.ntiles + 7) / 8) * nq;

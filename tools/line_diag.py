@@ -6,7 +6,7 @@
 For each LSSP_AMD_LINE_DIAG value (linesweep.hip; results are WRONG when it is
 non-zero: 1 storers skip the output stores, 2 loaders skip their DMAs,
 4 multiply instead of divide, 8 the poller does not wait for producers,
-16 no hand-off stores (only with 8)) prints the L sweep, U sweep and apply
+16 no hand-off stores (only with 8), 32 the apply's L sweep skips its U rhs-stream stores) prints the L sweep, U sweep and apply
 times (HIP events on the library's stream).
 """
 import json
