@@ -148,6 +148,12 @@ int lssp_amd_ilu_info(const lssp_amd_ilu *M, int *n, int *nnzL, int *nnzU, int *
                       int *levelsU, double *setup_seconds);
 int lssp_amd_ilu_get_factors(const lssp_amd_ilu *M, int *Lp, int *Lj, double *Lx, int *Up,
                              int *Uj, double *Ux);
+/* How an apply sweeps M's factors (no reference counterpart: a query like
+ * lssp_amd_mat_layout).  *line = 1 when the factors are a natural-ordered 5-/7-
+ * point grid's ILU(0) and run as line sweeps, with tiles of *lines lines x
+ * *planes planes (chosen per factor); 0 (and 0 x 0) for the general packet
+ * sweeps.  Any pointer may be NULL. */
+int lssp_amd_ilu_sweep_layout(const lssp_amd_ilu *M, int *line, int *lines, int *planes);
 
 /* ---- Krylov solve: lssp_solver_solve (lssp.cxx:250-414) for BiCGSTAB
  *      (solver-bicgstab.cxx:10-175), GMRES(m) (solver-gmres.cxx:12-255),

@@ -52,6 +52,7 @@ SIGNATURES = {
     "lssp_amd_mat_destroy": (_ci, [_vp]),
     "lssp_amd_mat_info": (_ci, [_vp, _vp, _vp, _vp]),
     "lssp_amd_mat_layout": (_ci, [_vp, _vp, _vp]),
+    "lssp_amd_ilu_sweep_layout": (_ci, [_vp, _vp, _vp, _vp]),
     "lssp_amd_mv_amxpby": (_ci, [_vp, _cd, _vp, _vp, _cd, _vp]),
     "lssp_amd_mv_amxpbyz": (_ci, [_vp, _cd, _vp, _vp, _cd, _vp, _vp]),
     "lssp_amd_mv_amxy": (_ci, [_vp, _cd, _vp, _vp, _vp]),

@@ -877,6 +877,16 @@ int lssp_amd_ilu_info(const lssp_amd_ilu *M, int *n, int *nnzL, int *nnzU, int *
     return LSSP_AMD_OK;
 }
 
+int lssp_amd_ilu_sweep_layout(const lssp_amd_ilu *M, int *line, int *lines, int *planes)
+{
+    if (!M) return LSSP_AMD_EINVAL;
+    const bool ls = M->line.ntiles > 0;
+    if (line) *line = ls ? 1 : 0;
+    if (lines) *lines = ls ? 256 / M->line.P : 0;
+    if (planes) *planes = ls ? M->line.P : 0;
+    return LSSP_AMD_OK;
+}
+
 int lssp_amd_ilu_get_factors(const lssp_amd_ilu *M, int *Lp, int *Lj, double *Lx, int *Up, int *Uj,
                              double *Ux)
 {

@@ -216,12 +216,14 @@ def _box7(nx, ny, nz, seed):
 # boxes whose line-sweep tiles are 64 x 4 (planes per tile chosen by hop count:
 # (20, 100, 6)), 32 x 8 ((20, 60, 24)) and 16 x 16 ((20, 40, 40), (13, 37, 35)),
 # with partial tiles in j and k and an odd last plane count
-@pytest.mark.parametrize("nx,ny,nz", [(20, 100, 6), (20, 60, 24), (20, 40, 40), (13, 37, 35)])
-def test_line_sweep_tile_shapes_bitwise_vs_oracle(dev, nx, ny, nz):
+@pytest.mark.parametrize("nx,ny,nz,tile", [(20, 100, 6, (64, 4)), (20, 60, 24, (32, 8)), (20, 40, 40, (16, 16)),
+                                           (13, 37, 35, (16, 16))])
+def test_line_sweep_tile_shapes_bitwise_vs_oracle(dev, nx, ny, nz, tile):
     import lssp_amd
     Ap, Aj, Ax = _box7(nx, ny, nz, nx + ny + nz)
     n = Ap.size - 1
     M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=1, level=0)
+    assert M.sweep_layout() == (True, *tile)
     L, U = O.ilu(O.CSR(n, Ap, Aj, Ax), "iluk", level=0)
     (Lp, Lj, Lx), (Up, Uj, Ux) = M.factors()
     assert np.array_equal(Lx, L.Ax) and np.array_equal(Ux, U.Ax)
