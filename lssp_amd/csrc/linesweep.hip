@@ -406,27 +406,6 @@ __device__ __forceinline__ void dma16_sc1(const void *g, unsigned lds)
     asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off sc1" ::"v"(g), "s"(__builtin_amdgcn_readfirstlane(lds))
                  : "memory", "m0");
 }
-#ifdef LINE_DIV_RN
-// (tuning builds) a / b correctly rounded from y = RN(1 / b), formed a step
-// ahead: q0 = RN(a y), then two corrections with the exact remainder (FMA)
-// (Markstein: y within 1/2 ulp of 1/b, q within 1 ulp of a/b, r = a - b q
-// exact => RN(q + r y) = RN(a / b)).  Exact only without underflow or overflow
-// and for a != 0 (a = -0 would give +0): the caller takes it when every valid
-// lane's |a|, |b| lie in [2^-300, 2^300] and divides otherwise.
-__device__ __forceinline__ double div_rn(double a, double b, double y)
-{
-    double q = a * y;
-    double r = __builtin_fma(-b, q, a);
-    q = __builtin_fma(r, y, q);
-    r = __builtin_fma(-b, q, a);
-    return __builtin_fma(r, y, q);
-}
-__device__ __forceinline__ bool div_range_ok(double v)
-{
-    const unsigned e = ((unsigned)(__double_as_longlong(v) >> 52)) & 0x7ffu;
-    return e - (1023u - 300u) <= 600u;
-}
-#endif
 // LDS drained, then the workgroup barrier.  The wait is the builtin (not asm),
 // so the compiler's wait-count tracking knows every LDS load is complete after
 // it and does not re-wait for loads issued before the barrier; the empty asm
@@ -652,9 +631,7 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
             const int pg = p0 + gl * PC;  // the lane group's first plane
             struct In {
                 double ck[PC], cj[PC], ci[PC], dg[PC], rh[PC], jv[PC];
-#ifdef LINE_DIV_RN
-                double dy[PC];
-#endif
+
             };
             auto load = [&](int s, unsigned so, In &in) {
                 const char *slot = ring + so;
@@ -666,9 +643,6 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                     in.cj[u] = b[1];
                     in.ci[u] = b[2];
                     if constexpr (NA == 4) in.dg[u] = b[3];
-#ifdef LINE_DIV_RN
-                    if constexpr (NA == 4) in.dy[u] = 1.0 / in.dg[u];
-#endif
                     if constexpr (RHS_NAT) {
                         in.rh[u] = rhsblk[((s >> 3) & 1) * line_rhs_blk<P>() + (s & 7) * (P * NJ + 1) + p * NJ + ll];
                     } else {
@@ -740,15 +714,7 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                         double v = cur.rh[u] - cur.ck[u] * xk;
                         v = v - cur.cj[u] * xj;
                         v = v - cur.ci[u] * xc[u];
-#ifdef LINE_DIV_RN
-                        if constexpr (NA == 4) {
-                            const bool ok = div_range_ok(v) && div_range_ok(cur.dg[u]);
-                            if ((__ballot(!ok) & m) == 0) v = div_rn(v, cur.dg[u], cur.dy[u]);
-                            else v = v / cur.dg[u];
-                        }
-#else
                         if constexpr (NA == 4) v = v / cur.dg[u];
-#endif
                         xn[u] = sel_lanes(m, v, xc[u]);
                     }
                     if (uk >= 0) {  // uniform
