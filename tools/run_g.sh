@@ -1,4 +1,7 @@
 set -o pipefail
-bash tools/gpu_exp.sh 216 x0 > gpurun_out/g_exp8.txt 2>&1 || { tail gpurun_out/g_exp8.txt; exit 1; }
-bash tools/gpu_exp.sh 216 x0 >> gpurun_out/g_exp8.txt 2>&1 || { tail gpurun_out/g_exp8.txt; exit 1; }
-grep -v amdgpu.ids gpurun_out/g_exp8.txt
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/ev2; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+tail -3 $O/pytest.log
+timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+cat $O/bench.json | cut -c1-400
