@@ -361,11 +361,6 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
 int line_rearm(lssp_amd_ctx *c, LineILU &li);
 void free_line_sweep(LineILU &li);
 int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs);
-// BiCGSTAB's p = r + beta (p - omega v) (solver-bicgstab.cxx:99-102) fused with
-// the line-swept apply's rhs gather, then x = M^-1 p; EUNSUPPORTED unless M is
-// line-swept
-int launch_ilu_apply_bicg_p(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const double *r, double *p,
-                            const double *v);
 int launch_line_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs);
 void free_trisched(TriSched &t);
 

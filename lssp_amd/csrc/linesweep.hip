@@ -1134,16 +1134,11 @@ static int launch_line_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a
 // lanes load one 64-byte run of a line from the natural-order vector and, per
 // step, 8 lanes store 8 consecutive stream entries.  Block b runs on XCD b % 8
 // and the XCD's blocks walk whole tiles in step order.
-// BP: BiCGSTAB's p update fused in (solver-bicgstab.cxx:99-102): the value
-// gathered for row r is p[r] = rhs[r] + beta (p[r] - omega v[r]) (k_ew's
-// EW_BICG_P expression), also stored back to p -- every row belongs to exactly
-// one (tile, step, plane, line), so each is read and written once.
 constexpr int LRHS_RUN = 8;
-template <int P, bool BP>
+template <int P>
 __global__ __launch_bounds__(256) void k_line_rhs(const LineTile *__restrict__ tiles, int ntiles, int nq, int nx,
                                                  int ny, const double *__restrict__ rhs, double *__restrict__ out,
-                                                 const double *guard, double *pv, const double *__restrict__ vv,
-                                                 const double *__restrict__ scal)
+                                                 const double *guard)
 {
     if (guard && *guard != 0.0) return;  // a batched iteration past the stop (lssp_amd_ctx::guard)
     const long b = blockIdx.x, j = b >> 3;
@@ -1158,17 +1153,7 @@ __global__ __launch_bounds__(256) void k_line_rhs(const LineTile *__restrict__ t
         const int k = it * 256 + threadIdx.x, m = k & 7, l = (k >> 3) % NJ, p = (k >> 3) / NJ;
         const int i = q0 + m - l - p;
         const bool ok = q0 + m < d.T && p < d.np && l < d.nj && (unsigned)i < (unsigned)nx;
-        const long row = ((long)(d.k0 + p) * ny + (d.j0 + l)) * nx + i;
-        if constexpr (BP) {
-            v[it] = 0.0;
-            if (ok) {
-                const double beta = scal[S_BETA], omega = scal[S_OMEGA];
-                v[it] = rhs[row] + beta * (pv[row] - omega * vv[row]);
-                pv[row] = v[it];
-            }
-        } else {
-            v[it] = ok ? rhs[row] : 0.0;
-        }
+        v[it] = ok ? rhs[((long)(d.k0 + p) * ny + (d.j0 + l)) * nx + i] : 0.0;
     }
     const long SB = (long)P * d.nj;
 #pragma unroll
@@ -1212,32 +1197,20 @@ static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const doub
     return ls.NA == 3 ? launch_line_t<3, true, 1>(c, ls, a) : launch_line_t<4, true, 1>(c, ls, a);
 }
 
-// pv != nullptr: BiCGSTAB's p update p = rhs + beta (p - omega vv) runs in the
-// gather, and the apply's rhs is the updated p
-static int line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs, double *pv, const double *vv)
+int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs)
 {
+#ifdef LINE_APPLY_NAT  // tuning builds: the L sweep reads the natural-order rhs itself (rhs wave)
+    LSSP_TRY(launch_line(c, li, 0, rhs, false, nullptr, true));
+    return launch_line(c, li, 1, nullptr, true, x, false);
+#endif
     const LineSweep &L = li.L;
     const int nq = (L.tmax + LRHS_RUN - 1) / LRHS_RUN;
     const long grid = 8L * ((L.ntiles + 7) / 8) * nq;
-    auto kr = pv ? (L.P == 16 ? k_line_rhs<16, true> : L.P == 8 ? k_line_rhs<8, true> : k_line_rhs<4, true>)
-                 : (L.P == 16 ? k_line_rhs<16, false> : L.P == 8 ? k_line_rhs<8, false> : k_line_rhs<4, false>);
-    kr<<<grid, 256, 0, c->stream>>>(L.d_tiles, L.ntiles, nq, L.nx, L.ny, rhs, li.d_lstream, c->guard, pv, vv,
-                                    c->d_scal);
+    auto kr = L.P == 16 ? k_line_rhs<16> : L.P == 8 ? k_line_rhs<8> : k_line_rhs<4>;
+    kr<<<grid, 256, 0, c->stream>>>(L.d_tiles, L.ntiles, nq, L.nx, L.ny, rhs, li.d_lstream, c->guard);
     LSSP_HIP(hipGetLastError());
     LSSP_TRY(launch_line(c, li, 0, nullptr, false, nullptr, true, true));
     return launch_line(c, li, 1, nullptr, true, x, false);
-}
-
-int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs)
-{
-    return line_apply(c, li, x, rhs, nullptr, nullptr);
-}
-
-int launch_ilu_apply_bicg_p(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const double *r, double *p,
-                            const double *v)
-{
-    if (!M->line.ntiles) return LSSP_AMD_EUNSUPPORTED;
-    return line_apply(c, M->line, x, r, p, v);
 }
 
 int launch_line_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs)

@@ -243,14 +243,8 @@ int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
             e.y = v;
             e.out0 = p;
         }
-        if (k > 0 && R.M && !R.gpc && R.M->line.ntiles) {
-            // line-swept ILU(0): the p update runs inside the apply's rhs gather
-            // (same expression per element; p is read once for both)
-            LSSP_TRY(launch_ilu_apply_bicg_p(R.c, R.M, ph, r, p, v));  // :99-102, :107-108
-        } else {
-            LSSP_TRY(R.ew(e));
-            LSSP_TRY(R.pc(ph, p));  // :107-108
-        }
+        LSSP_TRY(R.ew(e));
+        LSSP_TRY(R.pc(ph, p));                                   // :107-108
         LSSP_TRY(R.spmv(EPI_AMX, 1, ph, 0, p, v, 1, rh));         // :110
         LSSP_TRY(R.fin1(rh, v, R.fin(FIN_BICG_ALPHA, 1, R.T())));  // :112
         e = Ew();
