@@ -1,7 +1,9 @@
 set -o pipefail
-O=gpurun_out/ab; mkdir -p $O
-for v in default nofuse default nofuse; do
-  if [ "$v" = default ]; then unset LSSP_AMD_LIB; else export LSSP_AMD_LIB=$PWD/build/$v.so; fi
-  timeout -k 10 300 python -u bench.py --no-cpu > $O/b_$v.json 2> $O/b_$v.err || { tail -5 $O/b_$v.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$O/b_$v.json')); print('$v', d['value'], d['ms_per_step'])"
-done
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/final; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+tail -3 $O/pytest.log
+timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+cat $O/bench.json | cut -c1-300
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bench -o bench -- python3 bench.py --steps 30 --no-cpu > $O/prof_bench.log 2>&1 || { tail -20 $O/prof_bench.log; exit 1; }
+find $O -name "*kernel_stats.csv"
