@@ -1,3 +1,5 @@
+# GPU box: the round's verification -- full GPU suite, bench line, rocprofv3
+# kernel stats of the bench (outputs under gpurun_out/final/)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/final; mkdir -p $O
