@@ -94,6 +94,13 @@ int lssp_amd_mat_info(const lssp_amd_mat *A, int *nrows, int *ncols, int *nnz);
  * at most 16384 entries and the product stages that span of x in LDS instead
  * of gathering it from memory (locally numbered meshes); 0 otherwise. */
 int lssp_amd_mat_layout(const lssp_amd_mat *A, int *ndiag, int *windowed);
+/* Device memory of a matrix: *csr_bytes = the resident CSR (Ap, Aj, Ax: every
+ * operation but the two SpMV layouts above reads it), *aux_bytes = what the
+ * SpMV layouts add beside it (offset ids + table; window spans and the sliced
+ * copy, about as large as Aj + Ax again).  A windowed matrix whose padded
+ * sliced copy would exceed 2^30 entries is not windowed (32-bit slice
+ * offsets) and runs on the CSR product.  Either pointer may be NULL. */
+int lssp_amd_mat_bytes(const lssp_amd_mat *A, long long *csr_bytes, long long *aux_bytes);
 
 /* ---- SpMV: mvops.h:9-19 (mvops.cxx:5-150), bitwise per row --------------
  * x: for a matrix from lssp_amd_mat_upload the first ncols entries are read.
@@ -115,6 +122,11 @@ int lssp_amd_mv_mxy(lssp_amd_ctx *ctx, const lssp_amd_mat *A, double *x, double 
 /* ---- BLAS-1: vector.h:8-39 (vector.cxx:31-146) -------------------------- */
 int lssp_amd_vec_set_value(lssp_amd_ctx *ctx, double *x, long n, double val);
 int lssp_amd_vec_copy(lssp_amd_ctx *ctx, double *x, const double *y, long n);
+/* Measurement aid (no reference counterpart): read x[0..n) once with 16-byte
+ * non-temporal loads and store the XOR of all its 64-bit words (as bits) in
+ * the device double *sink -- the HBM streaming-read rate quoted beside the
+ * 8 TB/s spec.  n even, x 16-byte aligned (else LSSP_AMD_EINVAL). */
+int lssp_amd_stream_read(lssp_amd_ctx *ctx, const double *x, long n, double *sink);
 int lssp_amd_vec_axy(lssp_amd_ctx *ctx, double alpha, const double *x, double *y, long n);
 int lssp_amd_vec_axpby(lssp_amd_ctx *ctx, double alpha, const double *x, double beta, double *y,
                        long n);
@@ -193,7 +205,13 @@ int lssp_amd_solve(lssp_amd_ctx *ctx, const lssp_amd_mat *A, const lssp_amd_ilu 
  * rank). */
 int lssp_amd_comm_unique_id_size(void);
 int lssp_amd_comm_get_unique_id(void *id_out);
+/* Collective over the nranks processes (ncclCommInitRank).  Every nranks >= 1
+ * creates a real RCCL communicator, nranks == 1 included: the caller must pass
+ * an id from lssp_amd_comm_get_unique_id (a placeholder id blocks or fails in
+ * RCCL).  A context that never calls it runs single-rank with no communicator;
+ * lssp_amd_comm_nranks reports the communicator's rank count (ncclCommCount). */
 int lssp_amd_comm_init(lssp_amd_ctx *ctx, int nranks, int rank, const void *id);
+int lssp_amd_comm_nranks(lssp_amd_ctx *ctx, int *nranks);
 int lssp_amd_comm_barrier(lssp_amd_ctx *ctx);
 /* Transport check (collective): an all-gather of every rank's id and a ring
  * round of grouped send/recv (rank r -> r+1, r-1 -> r; a 1-rank communicator

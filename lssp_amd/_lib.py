@@ -52,6 +52,7 @@ SIGNATURES = {
     "lssp_amd_mat_destroy": (_ci, [_vp]),
     "lssp_amd_mat_info": (_ci, [_vp, _vp, _vp, _vp]),
     "lssp_amd_mat_layout": (_ci, [_vp, _vp, _vp]),
+    "lssp_amd_mat_bytes": (_ci, [_vp, _vp, _vp]),
     "lssp_amd_ilu_sweep_layout": (_ci, [_vp, _vp, _vp, _vp]),
     "lssp_amd_mv_amxpby": (_ci, [_vp, _cd, _vp, _vp, _cd, _vp]),
     "lssp_amd_mv_amxpbyz": (_ci, [_vp, _cd, _vp, _vp, _cd, _vp, _vp]),
@@ -59,6 +60,7 @@ SIGNATURES = {
     "lssp_amd_mv_mxy": (_ci, [_vp, _vp, _vp, _vp]),
     "lssp_amd_vec_set_value": (_ci, [_vp, _vp, _cl, _cd]),
     "lssp_amd_vec_copy": (_ci, [_vp, _vp, _vp, _cl]),
+    "lssp_amd_stream_read": (_ci, [_vp, _vp, _cl, _vp]),
     "lssp_amd_vec_axy": (_ci, [_vp, _cd, _vp, _vp, _cl]),
     "lssp_amd_vec_axpby": (_ci, [_vp, _cd, _vp, _cd, _vp, _cl]),
     "lssp_amd_vec_axpbyz": (_ci, [_vp, _cd, _vp, _cd, _vp, _vp, _cl]),
@@ -78,6 +80,7 @@ SIGNATURES = {
     "lssp_amd_comm_init": (_ci, [_vp, _ci, _ci, _vp]),
     "lssp_amd_comm_barrier": (_ci, [_vp]),
     "lssp_amd_comm_selftest": (_ci, [_vp]),
+    "lssp_amd_comm_nranks": (_ci, [_vp, _vp]),
     "lssp_amd_comm_init_host": (_ci, [_vp, _ci, _ci, _vp]),
     "lssp_amd_mat_upload_dist": (_ci, [_vp, _ci, _ci, _ci, _vp, _vp, _vp, _pvp]),
     "lssp_amd_mat_local_rows": (_ci, [_vp, _vp, _vp, _vp]),

@@ -217,6 +217,7 @@ int build_diag_ids(lssp_amd_mat *M, const int *Ap, const int *Aj)
     LSSP_HIP(hipMalloc(&M->d_off, sizeof(int) * off.size()));
     LSSP_HIP(hipMemcpy(M->Ad, ad.data(), ad.size(), hipMemcpyHostToDevice));
     LSSP_HIP(hipMemcpy(M->d_off, off.data(), sizeof(int) * off.size(), hipMemcpyHostToDevice));
+    M->aux_bytes += (long long)ad.size() + (long long)sizeof(int) * (long long)off.size();
     M->ndiag = (int)off.size();
     return LSSP_AMD_OK;
 }
@@ -224,6 +225,16 @@ int build_diag_ids(lssp_amd_mat *M, const int *Ap, const int *Aj)
 // The x spans of the 1024-row blocks of k_spmv_win (kernels.hip), for matrices
 // the diagonal-id coding does not cover (more than 255 offsets) whose rows
 // nevertheless stay near the diagonal (locally renumbered meshes: config 5).
+// entries (padded) of the sliced copy above which k_spmv3 serves the matrix:
+// its slice offsets are 32-bit (the 16-bit column pairs halve them).
+// LSSP_AMD_SELL_CAP (tests) lowers it to pin the fallback on small matrices.
+static long sell_cap()
+{
+    const char *e = getenv("LSSP_AMD_SELL_CAP");
+    const long v = e ? atol(e) : 0;
+    return v > 0 && v < INT_MAX / 2 ? v : (long)(INT_MAX / 2);
+}
+
 int build_windows(lssp_amd_mat *M, const int *Ap, const int *Aj, const double *Ax)
 {
     const int n = M->nrows;
@@ -274,7 +285,7 @@ int build_windows(lssp_amd_mat *M, const int *Ap, const int *Aj, const double *A
         meta[2 * q] = (int)tot;
         meta[2 * q + 1] = slen[q];
         tot += 64L * ((slen[q] + 1) & ~1);
-        if (tot > INT_MAX / 2) return LSSP_AMD_OK;  // too large for 32-bit slice offsets: k_spmv3 serves it
+        if (tot > sell_cap()) return LSSP_AMD_OK;  // too large for 32-bit slice offsets: k_spmv3 serves it
     }
     constexpr int NPAD = 64 * 16;  // the kernel's unconditional preload may read past the last slice
     std::vector<double> sax((size_t)tot + NPAD, 0.0);
@@ -297,9 +308,10 @@ int build_windows(lssp_amd_mat *M, const int *Ap, const int *Aj, const double *A
             }
         }
     }, 16);
-    auto up = [](void **d, const void *h, size_t bytes) -> int {
+    auto up = [M](void **d, const void *h, size_t bytes) -> int {
         LSSP_HIP(hipMalloc(d, bytes));
         LSSP_HIP(hipMemcpy(*d, h, bytes, hipMemcpyHostToDevice));
+        M->aux_bytes += (long long)bytes;
         return LSSP_AMD_OK;
     };
     LSSP_TRY(up((void **)&M->d_win, win.data(), sizeof(int) * win.size()));
@@ -509,6 +521,14 @@ int lssp_amd_mat_info(const lssp_amd_mat *A, int *nrows, int *ncols, int *nnz)
     return LSSP_AMD_OK;
 }
 
+int lssp_amd_mat_bytes(const lssp_amd_mat *A, long long *csr_bytes, long long *aux_bytes)
+{
+    if (!A) return LSSP_AMD_EINVAL;
+    if (csr_bytes) *csr_bytes = 4LL * (A->nrows + 1) + 12LL * A->nnz;
+    if (aux_bytes) *aux_bytes = A->aux_bytes;
+    return LSSP_AMD_OK;
+}
+
 int lssp_amd_mat_layout(const lssp_amd_mat *A, int *ndiag, int *windowed)
 {
     if (!A || !ndiag) return LSSP_AMD_EINVAL;
@@ -582,6 +602,11 @@ int lssp_amd_vec_copy(lssp_amd_ctx *c, double *x, const double *y, long n)
 {
     if (!c || n < 0 || (n > 0 && (!x || !y))) return LSSP_AMD_EINVAL;
     return launch_copy(c, x, y, n);
+}
+int lssp_amd_stream_read(lssp_amd_ctx *c, const double *x, long n, double *sink)
+{
+    if (!c || !sink || n < 0 || (n & 1) || (n > 0 && !x) || (reinterpret_cast<uintptr_t>(x) & 15)) return LSSP_AMD_EINVAL;
+    return launch_stream_read(c, x, n, sink);
 }
 int lssp_amd_vec_axy(lssp_amd_ctx *c, double alpha, const double *x, double *y, long n)
 {

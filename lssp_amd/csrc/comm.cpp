@@ -206,6 +206,22 @@ int comm_destroy(lssp_amd_ctx *c)
     return LSSP_AMD_OK;
 }
 
+// one int per rank, all-gathered in rank order (collective)
+int comm_gather_int(lssp_amd_ctx *c, int v, std::vector<int> &all)
+{
+    int *d = nullptr;  // [mine | all ranks]
+    LSSP_HIP(hipMalloc(&d, sizeof(int) * (1 + c->nranks)));
+    int st = hipMemcpy(d, &v, sizeof(int), hipMemcpyHostToDevice) == hipSuccess ? LSSP_AMD_OK : LSSP_AMD_EHIP;
+    if (st == LSSP_AMD_OK) st = xfer_allgather(c, d, d + 1, (long)sizeof(int));
+    all.assign(c->nranks, 0);
+    if (st == LSSP_AMD_OK &&
+        (hipMemcpyAsync(all.data(), d + 1, sizeof(int) * c->nranks, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+         hipStreamSynchronize(c->stream) != hipSuccess))
+        st = LSSP_AMD_EHIP;
+    (void)hipFree(d);
+    return st;
+}
+
 }  // namespace lssp_amd
 
 using namespace lssp_amd;
@@ -256,6 +272,19 @@ int lssp_amd_comm_init(lssp_amd_ctx *c, int nranks, int rank, const void *idp)
     LSSP_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
     LSSP_HIP(hipEventCreateWithFlags(&c->ev_pack, hipEventDisableTiming));
     LSSP_HIP(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
+    return LSSP_AMD_OK;
+}
+
+int lssp_amd_comm_nranks(lssp_amd_ctx *c, int *nranks)
+{
+    if (!c || !nranks) return LSSP_AMD_EINVAL;
+    if (!c->comm) {  // host transport, or no communicator (single rank)
+        *nranks = c->nranks;
+        return LSSP_AMD_OK;
+    }
+    int n = 0;
+    LSSP_NCCL(ncclCommCount((ncclComm_t)c->comm, &n));
+    *nranks = n;
     return LSSP_AMD_OK;
 }
 
@@ -344,14 +373,8 @@ int lssp_amd_comm_barrier(lssp_amd_ctx *c)
 // every rank's status -> the first non-zero one (rank order), identical on all ranks
 static int agree_status(lssp_amd_ctx *c, int st)
 {
-    DevMem d_mine, d_all;
-    LSSP_HIP(hipMalloc(&d_mine.p, sizeof(int)));
-    LSSP_HIP(hipMalloc(&d_all.p, sizeof(int) * c->nranks));
-    LSSP_HIP(hipMemcpy(d_mine.p, &st, sizeof(int), hipMemcpyHostToDevice));
-    LSSP_TRY(xfer_allgather(c, d_mine.p, d_all.p, (long)sizeof(int)));
-    std::vector<int> all(c->nranks);
-    LSSP_HIP(hipMemcpyAsync(all.data(), d_all.p, sizeof(int) * c->nranks, hipMemcpyDeviceToHost, c->stream));
-    LSSP_HIP(hipStreamSynchronize(c->stream));
+    std::vector<int> all;
+    LSSP_TRY(comm_gather_int(c, st, all));
     for (int s : all)
         if (s != LSSP_AMD_OK) return s;
     return LSSP_AMD_OK;

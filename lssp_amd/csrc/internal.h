@@ -126,6 +126,9 @@ struct lssp_amd_mat {
     double *s_ax = nullptr;
     uint32_t *s_col = nullptr, *s_row = nullptr;
     int *s_meta = nullptr;
+    // device bytes held beside the CSR arrays (offset ids + table, window spans,
+    // the sliced copy): lssp_amd_mat_bytes
+    long long aux_bytes = 0;
     // distributed layout
     int n_global = 0, row0 = 0, nhalo = 0;
     // halo exchange plan: for each peer, indices (local) to send and the count to receive
@@ -274,6 +277,7 @@ struct Ew {
 int launch_ew(lssp_amd_ctx *c, const Ew &e);
 // x = y (vector.cxx:73-83): 16-byte vector copy when both are 16-byte aligned
 int launch_copy(lssp_amd_ctx *c, double *x, const double *y, long n);
+int launch_stream_read(lssp_amd_ctx *c, const double *x, long n, double *sink);
 
 // finish a reduction whose level-1 partials (tree) or operands (serial) are set:
 // tree: level-2 over nslot partial rows of C entries; then the finalize program
@@ -374,6 +378,7 @@ int comm_allgather_sums(lssp_amd_ctx *c, int nslot);
 // recv (nranks * bytes, rank order) = every rank's send (bytes), through the
 // context's transport (RCCL or the host hooks)
 int comm_allgather(lssp_amd_ctx *c, const void *send, void *recv, long bytes);
+int comm_gather_int(lssp_amd_ctx *c, int v, std::vector<int> &all);  // collective, rank order
 // serial mode, P ranks: receive the running sums of rank-1 (zeros on rank 0)
 // into c->d_carry / pass this rank's on to rank+1
 int comm_carry_in(lssp_amd_ctx *c);

@@ -797,6 +797,45 @@ __global__ __launch_bounds__(256) void k_copy16(const line_dbl2v *__restrict__ s
     }
 }
 
+// Streaming read (the HBM read roofline the bench quotes beside the 8 TB/s
+// spec): every word read once with 16-byte non-temporal loads, 8 in flight
+// per lane, XOR-folded into *sink (64-bit, one atomic per workgroup) so the
+// loads cannot be dropped and the result is checkable.
+__global__ __launch_bounds__(256) void k_read16(const line_dbl2v *__restrict__ s2, long n2,
+                                               unsigned long long *sink)
+{
+    typedef unsigned long long u64;
+    const long stride = (long)gridDim.x * 256;
+    u64 acc = 0;
+    constexpr int U = 8;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n2; i += U * stride) {
+        line_dbl2v v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = i + u * stride < n2 ? __builtin_nontemporal_load(s2 + i + u * stride)
+                                                               : line_dbl2v{0, 0};
+#pragma unroll
+        for (int u = 0; u < U; u++) acc ^= (u64)__double_as_longlong(v[u][0]) ^ (u64)__double_as_longlong(v[u][1]);
+    }
+    for (int o = 32; o >= 1; o >>= 1) acc ^= __shfl_xor(acc, o);
+    __shared__ u64 w[4];
+    if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicXor(sink, w[0] ^ w[1] ^ w[2] ^ w[3]);
+}
+
+int launch_stream_read(lssp_amd_ctx *c, const double *x, long n, double *sink)
+{
+    LSSP_HIP(hipMemsetAsync(sink, 0, sizeof(double), c->stream));
+    const long n2 = n / 2;  // n even, x 16-byte aligned (lssp_amd_stream_read)
+    unsigned long long *s = reinterpret_cast<unsigned long long *>(sink);
+    if (n2 > 0) {
+        const long grid = std::min<long>((n2 + 2047) / 2048, 8L * c->num_cus);
+        k_read16<<<grid, 256, 0, c->stream>>>(reinterpret_cast<const line_dbl2v *>(x), n2, s);
+        LSSP_HIP(hipGetLastError());
+    }
+    return LSSP_AMD_OK;
+}
+
 int launch_copy(lssp_amd_ctx *c, double *x, const double *y, long n)
 {
     if (n <= 0) return LSSP_AMD_OK;

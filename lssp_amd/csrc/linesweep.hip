@@ -727,16 +727,21 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                         m &= kgm;
                         int vo = ll * 8;
                         asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(vo) : "v"(OOB), "v"(vo), "s"(m));
+                        if (q < 0) vo = OOB;  // (no row of plane np-1 exists before step np-1)
+                        // soffset is not range-checked: only voffset carries the drop
                         __builtin_amdgcn_raw_buffer_store_b64(split64((uint64_t)__double_as_longlong(v)), hko, vo,
-                                                              q >= 0 ? q * (NJ * 8) : OOB, 16);  // sc1
+                                                              max(q, 0) * (NJ * 8), 16);  // sc1
                     }
                     if (jout) {
                         // planes past the tile (p >= np) publish nothing: the two sweeps
                         // share the hand-off buffers, and the other sweep's tile of this
                         // index may have more planes, whose consumer would take a value
                         // left here for a ready one
+                        // steps q < 0 publish nothing: the drop goes in voffset (the
+                        // buffer range check covers voffset, not soffset)
                         const int q = s + 1 - nj;
-                        const int sof = q >= 0 ? (q * P + p0) * 8 : OOB;
+                        const int sof = (max(q, 0) * P + p0) * 8;
+                        const int jlq = q >= 0 ? jl_off : OOB;
                         if constexpr (PC == 2) {
                             const uint64_t b0 = (uint64_t)__double_as_longlong(xn[0]);
                             const uint64_t b1 = (uint64_t)__double_as_longlong(xn[1]);
@@ -745,15 +750,15 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
                             d4.y = (unsigned)(b0 >> 32);
                             d4.z = (unsigned)b1;
                             d4.w = (unsigned)(b1 >> 32);
-                            __builtin_amdgcn_raw_buffer_store_b128(d4, hjo, pg + 1 < np ? jl_off : OOB, sof, 16);
+                            __builtin_amdgcn_raw_buffer_store_b128(d4, hjo, pg + 1 < np ? jlq : OOB, sof, 16);
                             if (np & 1)  // uniform: the group whose second plane is past the tile
-                                __builtin_amdgcn_raw_buffer_store_b64(split64(b0), hjo, pg + 1 == np ? jl_off : OOB,
+                                __builtin_amdgcn_raw_buffer_store_b64(split64(b0), hjo, pg + 1 == np ? jlq : OOB,
                                                                       sof, 16);
                         } else {
 #pragma unroll
                             for (int u = 0; u < PC; u++)
                                 __builtin_amdgcn_raw_buffer_store_b64(split64((uint64_t)__double_as_longlong(xn[u])), hjo,
-                                                                      pg + u < np ? jl_off + 8 * u : OOB, sof, 16);
+                                                                      pg + u < np ? jlq + 8 * u : OOB, sof, 16);
                         }
                     }
                     if (trs && wave == 0 && s >= 0 && s < T) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();

@@ -2218,7 +2218,18 @@ extern "C" int lssp_amd_solve(lssp_amd_ctx *c, const lssp_amd_mat *A, const lssp
     // M: the rank's own rows (a block-Jacobi block on P ranks), or on P ranks
     // the factors of the whole matrix (the reference's global ILU)
     const bool gpc = M && c->nranks > 1 && M->n == A->n_global && M->n != A->nrows;
-    if (M && M->n != A->nrows && !gpc) return LSSP_AMD_EINVAL;
+    const bool bad_m = M && M->n != A->nrows && !gpc;
+    if (c->nranks > 1) {
+        // every rank must take the same preconditioner path (none / its own block /
+        // the global factors): the global path all-gathers in every apply, so a
+        // mixed choice would leave some ranks waiting there.  Agreed first, so a
+        // mismatch fails every rank with EINVAL instead of hanging the job.
+        std::vector<int> modes;
+        LSSP_TRY(comm_gather_int(c, bad_m ? -1 : !M ? 0 : gpc ? 2 : 1, modes));
+        for (int m : modes)
+            if (m < 0 || m != modes[0]) return LSSP_AMD_EINVAL;
+    }
+    if (bad_m) return LSSP_AMD_EINVAL;
     LSSP_HIP(hipSetDevice(c->device));
     Run R;
     R.c = c;

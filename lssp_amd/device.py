@@ -112,6 +112,12 @@ class Device:
     def barrier(self):
         _ck(self.L.lssp_amd_comm_barrier(self.h), "barrier")
 
+    def comm_nranks(self) -> int:
+        """the communicator's rank count (ncclCommCount on RCCL; the host transport's count)"""
+        v = ctypes.c_int()
+        _ck(self.L.lssp_amd_comm_nranks(self.h, ctypes.byref(v)), "comm_nranks")
+        return v.value
+
     def comm_selftest(self):
         """all-gather + grouped send/recv ring through the configured transport, checked"""
         _ck(self.L.lssp_amd_comm_selftest(self.h), "comm_selftest")
@@ -230,6 +236,13 @@ class DMat:
         v, w = ctypes.c_int(), ctypes.c_int()
         _ck(self.dev.L.lssp_amd_mat_layout(self.h, ctypes.byref(v), ctypes.byref(w)), "mat_layout")
         return bool(w.value)
+
+    @property
+    def device_bytes(self) -> tuple[int, int]:
+        """(resident CSR bytes, bytes of the SpMV layouts beside it)"""
+        c, a = ctypes.c_longlong(), ctypes.c_longlong()
+        _ck(self.dev.L.lssp_amd_mat_bytes(self.h, ctypes.byref(c), ctypes.byref(a)), "mat_bytes")
+        return c.value, a.value
 
     def close(self):
         if self.h:

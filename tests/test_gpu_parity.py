@@ -399,3 +399,28 @@ print("ok", r.nits)
         res = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,
                              timeout=150)
         assert res.returncode == 0 and "ok" in res.stdout, (env, res.stdout[-2000:], res.stderr[-2000:])
+
+
+def test_sliced_copy_footprint_and_cap_fallback(dev, monkeypatch):
+    """A windowed matrix reports the sliced copy it keeps beside the CSR
+    (lssp_amd_mat_bytes); one whose padded copy exceeds the slice-offset cap
+    is not windowed and runs on k_spmv3 with the same sums (the cap is lowered
+    through LSSP_AMD_SELL_CAP to reach that branch at a small size)."""
+    import lssp_amd
+    from lssp_amd.synthetic import thermal_like
+    Ap, Aj, Ax = thermal_like(m=150, window=512)
+    A = O.CSR(Ap.size - 1, Ap, Aj, Ax)
+    xh = uniform(0x5EED, A.n)
+    ref = O.spmv(0, A, xh)
+    M = lssp_amd.DMat(dev, A.Ap, A.Aj, A.Ax)
+    csr, aux = M.device_bytes
+    assert M.windowed and csr == 4 * (A.n + 1) + 12 * A.nnz
+    assert aux >= 12 * A.nnz  # f64 values + 16-bit column pairs, padded per slice
+    monkeypatch.setenv("LSSP_AMD_SELL_CAP", "1000")
+    F = lssp_amd.DMat(dev, A.Ap, A.Aj, A.Ax)
+    assert not F.windowed and F.device_bytes[1] == 0
+    x, z = dev.vec(A.n, xh), dev.vec(A.n)
+    F.mv_mxy(x, z)
+    assert np.array_equal(z.download(), ref)
+    M.mv_mxy(x, z)
+    assert np.array_equal(z.download(), ref)

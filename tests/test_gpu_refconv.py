@@ -1,0 +1,108 @@
+"""The TIMED mode against the reference at full size: complete solves.
+
+bench.py times the library's TREE reduction order: it is
+bitwise equal to the oracle's restatement of that order, and its iterates
+differ from the reference's sequential sums in the last bits, which BiCGSTAB
+amplifies.  These tests pin what the timed mode must still share
+with the reference (tests/golden/full.json, written by make_golden_full.py
+from oracle/_ref/libref.so -- the reference compiled from /root/reference)
+on the benchmark configurations, solved to the reference's defaults
+rtol = atol = rb = 1e-7 (lssp.cxx:11-13), b = 1, x0 = 0:
+
+  * the iteration count within 1 of the reference's (the stop test is
+    solver-bicgstab.cxx:141-157 / solver-gmres.cxx:206-217);
+  * the final residual within REL_RES (relative) of the reference's, and the
+    scalar history (every dot and norm the driver computed, in the
+    reference's call order) within HIST_TOL relative over the iterations both
+    runs share -- documented tolerances, measured values printed;
+  * the recomputed true residual ||b - A x|| at most TRUE_FACTOR times the
+    reference's own true residual and below the stop tolerance scale;
+
+and, at 512^3 (config 4's matrix, which the reference cannot run here: 134 M
+rows), convergence and the true residual as properties.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_path = os.path.join(HERE, "golden", "full.json")
+FULL = []
+if os.path.exists(_path):
+    with open(_path) as _f:
+        FULL = json.load(_f)["cases"]
+
+# documented tolerances of the timed (TREE) mode against the reference
+REL_RES = 0.5      # final residual: |res - ref| / ref
+HIST_TOL = 1e-2    # scalar history, max relative deviation over the shared iterations
+TRUE_FACTOR = 2.0  # true residual vs the reference's true residual
+
+
+def _fx(h):
+    return float.fromhex(h)
+
+
+def _solve_case(c):
+    import lssp_amd
+    dev = lssp_amd.Device(0, reduction=lssp_amd.TREE)
+    try:
+        Ap, Aj, Ax = lssp_amd.poisson(3, c["N"])
+        n = Ap.size - 1
+        A = lssp_amd.DMat(dev, Ap, Aj, Ax)
+        if c["pc"]["kind"] == "iluk":
+            M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=c["pc"]["level"])
+        else:
+            M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUT, tol=c["pc"]["tol"], p=c["pc"]["p"])
+        b = dev.vec(n, np.ones(n))
+        x = dev.vec(n, np.zeros(n))
+        r = lssp_amd.solve(dev, A, M, x, b, solver=c["solver"], tol_rel=c["rtol"], tol_abs=c["atol"],
+                           tol_rb=c["rbtol"], maxit=5000, restart=c["restart"], trace_cap=200000)
+        z = dev.vec(n)
+        A.mv_amxpbyz(-1.0, x, 1.0, b, z)
+        zh = z.download()
+        true_res = math.sqrt(float(np.dot(zh, zh)))
+        return r, true_res, n
+    finally:
+        dev.close()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("c", FULL, ids=[c["name"] for c in FULL])
+def test_tree_mode_full_solve_vs_reference(c):
+    r, true_res, n = _solve_case(c)
+    ref_nits, ref_res, ref_true = c["nits"], _fx(c["residual"]), _fx(c["true_residual"])
+    ref_tr = np.array([_fx(h) for h in c["trace"]])
+    k = min(len(ref_tr), len(r.trace))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        dev_hist = np.abs(r.trace[:k] - ref_tr[:k]) / np.maximum(np.abs(ref_tr[:k]), 1e-300)
+    hist = float(np.max(dev_hist)) if k else 0.0
+    rel = abs(r.residual - ref_res) / ref_res
+    print(f"\n{c['name']}: nits {r.nits} (reference {ref_nits}), residual {r.residual:.6e} "
+          f"(reference {ref_res:.6e}, rel {rel:.3e}), true residual {true_res:.6e} "
+          f"(reference {ref_true:.6e}), history max rel dev {hist:.3e} over {k} scalars")
+    assert abs(r.nits - ref_nits) <= 1
+    assert rel <= REL_RES
+    assert hist <= HIST_TOL
+    # the stop scale max(rtol ||r0||, atol, rb ||b||) with r0 = b (x0 = 0)
+    scale = max(c["rtol"] * math.sqrt(n), c["atol"], c["rbtol"] * math.sqrt(n))
+    assert true_res <= TRUE_FACTOR * max(ref_true, scale)
+
+
+@pytest.mark.timeout(900)
+def test_tree_mode_512_bicgstab_converges():
+    """config 4's matrix on one GPU (7-pt 512^3, n = 134,217,728): BiCGSTAB +
+    ILU(0) in the timed mode converges to the default tolerances and the
+    recomputed true residual is at that scale (the reference does not run at
+    this size here; round 2 measured 308 iterations)."""
+    c = {"N": 512, "pc": {"kind": "iluk", "level": 0}, "solver": 4, "rtol": 1e-7, "atol": 1e-7,
+         "rbtol": 1e-7, "restart": 30}
+    r, true_res, n = _solve_case(c)
+    scale = 1e-7 * math.sqrt(n)
+    print(f"\n512^3: nits {r.nits}, residual {r.residual:.6e} (stop scale {scale:.6e}), true {true_res:.6e}")
+    assert 0 < r.nits < 5000 and r.residual <= scale
+    assert true_res <= TRUE_FACTOR * scale
