@@ -185,7 +185,7 @@ struct LineGeom {
 struct LineTile {  // one workgroup's unit of work, in its sweep's coordinates
     int j0, nj, k0, np;
     int flags;        // LT_*
-    int T;            // steps
+    int T;            // levels (k_line2: padded to a whole number of two-level steps)
     int roff;         // (unused)
     int tk, tj;       // producer tiles of the k / j inputs (-1: none)
     int ut;           // L sweep: the mirror U tile (its rhs stream)
@@ -194,7 +194,9 @@ struct LineTile {  // one workgroup's unit of work, in its sweep's coordinates
 };
 struct LineSweep {
     int nx = 0, ny = 0, nz = 0, ntiles = 0, tmax = 0, NA = 3;
-    int P = 4;  // planes per tile (256 / P lines)
+    int P = 4;    // planes per tile
+    int NJ = 64;  // lines per tile (k_line: 256 / P; k_line2: 16)
+    int LV = 1;   // levels per workgroup step (k_line2: 2; its planes P/2.. run one level later)
     long rows_total = 0;
     LineTile *d_tiles = nullptr;
     double *d_coef = nullptr;
@@ -204,7 +206,7 @@ struct LineSweep {
 };
 struct LineILU {
     LineGeom g;
-    int P = 4, W = 0, S = 0, tmax = 0, ntiles = 0;
+    int P = 4, NJ = 64, LV = 1, W = 0, S = 0, tmax = 0, ntiles = 0;
     LineSweep L, U;
     double *d_ustream = nullptr;  // the U sweep's rhs, written by the L sweep
     double *d_lstream = nullptr;  // the L sweep's rhs in its stream layout (k_line_rhs)

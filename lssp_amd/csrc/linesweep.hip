@@ -125,16 +125,21 @@ static bool detect_grid(int n, const std::vector<int> &Lp, const std::vector<int
     return true;
 }
 
-// rows of a tile (nj lines, np planes) valid at step s, plane p: lanes [lo, hi]
-static inline void step_range(int nx, int nj, int np, int s, int p, int &lo, int &hi)
+// k_line2's plane skew: the planes of its second compute wave (p >= P/2) run
+// one level later, so the k-input of plane P/2 is one whole step old
+static inline int line_sigma(int LV, int P, int p) { return LV == 2 && p >= P / 2 ? 1 : 0; }
+
+// rows of a tile (nj lines, np planes) valid at level s, plane p: lanes [lo, hi]
+// (row i = s - l - p - sigma(p))
+static inline void step_range(int nx, int nj, int np, int s, int p, int sg, int &lo, int &hi)
 {
     if (p >= np) {
         lo = 0;
         hi = -1;
         return;
     }
-    lo = std::max(0, s - p - nx + 1);
-    hi = std::min(nj - 1, s - p);
+    lo = std::max(0, s - p - sg - nx + 1);
+    hi = std::min(nj - 1, s - p - sg);
 }
 
 // coefficients of one sweep in that sweep's row order (row r_sweep = r for L,
@@ -164,8 +169,9 @@ struct CoefSrc {
     double get(long r_sweep, int a) const { return c[(size_t)r_sweep * NA + a]; }
 };
 
-static int build_tiles(const LineGeom &g, int P, int W, std::vector<LineTile> &tiles, int &S)
+static int build_tiles(const LineGeom &g, int P, int NJ, int LV, int W, std::vector<LineTile> &tiles, int &S)
 {
+    (void)NJ;
     // plane segments between cuts, cut into tiles of <= P planes
     std::vector<std::pair<int, int>> kt;  // (k0, np)
     for (int k = 0; k < g.nz;) {
@@ -188,7 +194,8 @@ static int build_tiles(const LineGeom &g, int P, int W, std::vector<LineTile> &t
             t.np = kt[K].second;
             const bool kin = t.k0 > 0 && g.kin[t.k0];
             t.flags = (kin ? LT_KIN : 0) | (J > 0 ? LT_JIN : 0) | (J < W - 1 ? LT_JOUT : 0);
-            t.T = g.nx + t.nj + t.np - 2;
+            t.T = g.nx + t.nj + t.np - 2 + line_sigma(LV, P, t.np - 1);
+            t.T = (t.T + LV - 1) / LV * LV;
             t.tk = kin ? (K - 1) * W + J : -1;
             t.tj = J > 0 ? K * W + J - 1 : -1;
         }
@@ -206,7 +213,7 @@ static int build_tiles(const LineGeom &g, int P, int W, std::vector<LineTile> &t
 static int upload_sweep(lssp_amd_ctx *c, const LineGeom &g, const std::vector<LineTile> &tiles, const CoefSrc &src,
                         int NA, LineSweep &ls)
 {
-    const int nx = g.nx, P = ls.P;
+    const int nx = g.nx, P = ls.P, LV = ls.LV;
     std::vector<LineTile> tt = tiles;
     long rows_total = 0;
     int tmax = 0;
@@ -226,9 +233,10 @@ static int upload_sweep(lssp_amd_ctx *c, const LineGeom &g, const std::vector<Li
             double *blk = coef.data() + (size_t)(t.cbase + (long)s * P * t.nj) * NA;
             for (int p = 0; p < t.np; p++) {
                 int lo, hi;
-                step_range(nx, t.nj, t.np, s, p, lo, hi);
+                const int sg = line_sigma(LV, P, p);
+                step_range(nx, t.nj, t.np, s, p, sg, lo, hi);
                 for (int l = lo; l <= hi; l++) {
-                    const long i = s - l - p;
+                    const long i = s - l - p - sg;
                     const long r = ((long)(t.k0 + p) * g.ny + (t.j0 + l)) * nx + i;
                     for (int a = 0; a < NA; a++) blk[(size_t)(p * t.nj + l) * NA + a] = src.get(r, a);
                 }
@@ -278,6 +286,23 @@ static int line_choose_P(const LineGeom &g)
     return best;
 }
 
+// which kernel sweeps a factor: k_line2 (8 planes x 16 lines, two levels per
+// step; the default) or k_line (256 rows per step, one level per step; P from
+// line_choose_P).  LSSP_AMD_LINE_MODE=1 selects k_line (A/B runs, tests).
+static void line_plan(const LineGeom &g, int &P, int &NJ, int &LV)
+{
+    const char *e = getenv("LSSP_AMD_LINE_MODE");
+    if (e && atoi(e) == 1) {
+        P = line_choose_P(g);
+        NJ = 256 / P;
+        LV = 1;
+        return;
+    }
+    P = 8;
+    NJ = 16;
+    LV = 2;
+}
+
 int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std::vector<int> &Lj,
                      const std::vector<double> &Lx, const std::vector<int> &Up, const std::vector<int> &Uj,
                      const std::vector<double> &Ux, LineILU &li)
@@ -286,11 +311,12 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
     if (env && !atoi(env)) return LSSP_AMD_EUNSUPPORTED;
     LineGeom g;
     if (!detect_grid(n, Lp, Lj, Lx, Up, Uj, g)) return LSSP_AMD_EUNSUPPORTED;
-    const int P = line_choose_P(g);
-    const int W = (g.ny + 256 / P - 1) / (256 / P);
+    int P, NJ, LV;
+    line_plan(g, P, NJ, LV);
+    const int W = (g.ny + NJ - 1) / NJ;
     std::vector<LineTile> Lt;
     int S = 0;
-    LSSP_TRY(build_tiles(g, P, W, Lt, S));
+    LSSP_TRY(build_tiles(g, P, NJ, LV, W, Lt, S));
     // U tiles: exact mirrors of the L tiles (U tile (W-1-J, S-1-K) <-> L tile (J, K))
     std::vector<LineTile> Ut(Lt.size());
     for (int K = 0; K < S; K++)
@@ -314,6 +340,8 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
     cu.build(Up, Uj, Ux, true, n, g.nx, plane, 4);
     li.g = g;
     li.P = li.L.P = li.U.P = P;
+    li.NJ = li.L.NJ = li.U.NJ = NJ;
+    li.LV = li.L.LV = li.U.LV = LV;
     li.W = W;
     li.S = S;
     LSSP_TRY(upload_sweep(c, g, Lt, cl, g.unitL ? 3 : 4, li.L));
@@ -338,7 +366,7 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
     LSSP_HIP(hipMalloc(&li.d_lstream, sizeof(double) * (li.L.rows_total + 16 * 1024 / 8)));
     LSSP_HIP(hipMemset(li.d_lstream, 0, sizeof(double) * (li.L.rows_total + 16 * 1024 / 8)));
     li.tmax = std::max(li.L.tmax, li.U.tmax);
-    li.hk_stride = (long)li.tmax * (256 / P);
+    li.hk_stride = (long)li.tmax * NJ;
     li.hj_stride = (long)li.tmax * P;
     li.ntiles = (int)Lt.size();
     li.hk_n = li.hk_stride * li.ntiles;
