@@ -1063,6 +1063,462 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
 }
 
 // ---------------------------------------------------------------------------
+// k_line2: two levels per workgroup step (the default line sweep)
+// ---------------------------------------------------------------------------
+// A tile is nj <= 16 lines x np <= 8 planes, 128 rows per level.  Two compute
+// waves: wave w owns planes 4w .. 4w+3; lane (g, l) = 16 g + l owns line l of
+// plane 4w + g -- ONE row per level -- and a step advances TWO levels (v = 2s,
+// 2s+1).  The barrier, the loop, the poller's round trip and every role's
+// per-step work are paid once per two levels, and a tile moves half the
+// bytes per level of k_line's 256-row tiles (the loaders' LDS-DMA issue,
+// ~80 clk per 1 KB piece per CU, bounded k_line's level at ~800-950 clk).
+// Row (i, l, p) is computed at level v = i + l + p + sigma(p), sigma = 1 on
+// wave 1's planes (line_sigma).  The operands of a row at level v:
+//   (i-1): the lane's own value of level v-1 (a register);
+//   (j-1): line l-1's value of level v-1: DPP row_shr:1 (the 16-lane groups
+//          are the DPP rows); line 0 takes the poller's j-input;
+//   (k-1): plane p-1's value of level v-1: lane - 16 inside a wave (two
+//          permlane swaps); plane 4's k-neighbour (plane 3, wave 0) is, with
+//          the skew, level v-2 -- the previous step's result of the same
+//          sub-level, read from LDS after the barrier; plane 0 takes the
+//          poller's k-input.
+// The arithmetic is k_line's, operand for operand (rhs - c_k x_k - c_j x_j -
+// c_i x_i, then / diag), so every value is bitwise the same.
+// Roles, one barrier per step: 2 compute waves, NL loaders (LDS-DMA of a
+// step's two coefficient blocks and its rhs block D steps ahead), 1 poller
+// (LDS-DMA sc1 reads of the two levels' hand-off inputs DH steps ahead), SW
+// storers (OUT 2: the U sweep's rhs stream; OUT 1: natural-order x in 8-row
+// runs of a line).  The rhs always comes from a stream (k_line_rhs gathers it).
+namespace l2 {
+constexpr int P = 8, NJ = 16, CW = 2, LV = 2, ROWS = P * NJ;
+constexpr uint64_t GS = 0x0001000100010001ull;  // line 0 of each 16-lane group
+constexpr uint64_t G0M = 0xFFFFull;             // group 0 (the wave's first plane)
+template <int NA>
+struct Slot {
+    static constexpr int NPC = (LV * ROWS * NA * 8 + 1023) / 1024;  // 1 KB DMA pieces of the two coefficient blocks
+    static constexpr int NRP = (LV * ROWS * 8 + 1023) / 1024;       // ... of the two rhs blocks
+    static constexpr int COEF = 0;
+    static constexpr int RHS = NPC * 1024;
+    static constexpr int KFIN = RHS + NRP * 1024;    // double[LV][NJ]
+    static constexpr int JFIN = KFIN + LV * NJ * 8;  // double[LV][P]
+    static constexpr int BYTES = JFIN + LV * P * 8;
+    static_assert(BYTES % 16 == 0, "slot alignment");
+};
+// levels of results kept in LDS: the storers' source (OUT 1 writes 8-level
+// blocks as runs, so it keeps two) and wave 1's k-input
+template <int OUT>
+constexpr int rsl() { return OUT == 1 ? 16 : 4; }
+template <int NA, int OUT, int D>
+constexpr int lds_bytes() { return (D + 1) * Slot<NA>::BYTES + rsl<OUT>() * ROWS * 8 + 16 + 512; }
+constexpr int waves(int NL, int SW) { return CW + NL + 1 + SW; }
+}  // namespace l2
+
+// lane l <- lane l - 16 (rows R0..R3 of the wave -> [R0, R0, R1, R2]; row 0 is
+// not used): v_permlane16_swap gives [R0, R0, R2, R2] / [R1, R1, R3, R3],
+// v_permlane32_swap of those [R0, R0, R1, R1]; rows 1 and 3 from the first,
+// row 2 from the second (tools/probe/shfl_probe.hip checks it against ds_bpermute)
+// ds_bpermute is the default: 93 against 133 clk per dependent shuffle + f64
+// mul/add (profiles/r04/r04a_shfl_probe.txt); -DLINE2_PERMLANE selects the swaps
+__device__ __forceinline__ unsigned up16_u32(unsigned x)
+{
+#ifndef LINE2_PERMLANE
+    return (unsigned)__builtin_amdgcn_ds_bpermute((int)(((threadIdx.x & 63) - 16) & 63) * 4, (int)x);
+#else
+    auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    auto q = __builtin_amdgcn_permlane32_swap(r[0], r[1], false, false);
+    unsigned o;
+    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(o) : "v"(r[0]), "v"(q[0]), "s"(0x0000FFFF00000000ull));
+    return o;
+#endif
+}
+__device__ __forceinline__ double up16(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = up16_u32((unsigned)b), hi = up16_u32((unsigned)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | lo);
+}
+
+template <int NA, int OUT, int NL, int D, int DH, int SW, bool TRACE>
+__global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
+{
+    using namespace l2;
+    using SL = Slot<NA>;
+    constexpr int LA = 2;  // the loaders complete step s+LA's slot during step s
+    constexpr int R = D + 1;
+    constexpr int RSL = rsl<OUT>();
+    constexpr int NITEM = SL::NPC + SL::NRP;  // DMA instructions per step, shared by the loaders
+    constexpr int KPER = (NITEM + NL - 1) / NL;
+    constexpr int S0 = -2 * ((D + 2) / 2);  // first step of every role (even, <= -D-1)
+    static_assert(DH >= 2 && DH < D && (D - LA) * KPER <= 63 && 2 * (DH - 1) <= 63, "leads");
+    static_assert(OUT == 1 || OUT == 2, "out");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char *ring = smem;
+    double *res = reinterpret_cast<double *>(smem + R * SL::BYTES);  // [RSL][P][NJ]
+    int *s_tile = reinterpret_cast<int *>(res + RSL * ROWS);
+    const unsigned lds0 = (unsigned)(uintptr_t)smem;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int nx = a.nx;
+    if (a.guard && *a.guard != 0.0) {  // a batched iteration past the stop: consume the launch's tile claims
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.claim, (unsigned long long)a.ntiles + gridDim.x);
+        return;
+    }
+
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) *s_tile = (int)(atomicAdd(a.claim, 1ull) - a.base);
+        __syncthreads();
+        const int t = __builtin_amdgcn_readfirstlane(*s_tile);
+        if (t >= a.ntiles) break;
+        if (TRACE && threadIdx.x == 0) a.trace[8 * t] = __builtin_amdgcn_s_memrealtime();
+        const LineTile d = a.tiles[t];
+        const int T = d.T, TS = T / LV, nj = d.nj, np = d.np;
+        const long SB = (long)P * nj;  // rows per level block
+        const bool kin = d.flags & LT_KIN, jin = d.flags & LT_JIN, kout = d.flags & LT_KOUT,
+                   jout = d.flags & LT_JOUT;
+        const int ll = lane & (NJ - 1), gl = lane >> 4;
+        const int lc = min(ll, nj - 1);
+        auto nb = [&](int p, int l) {  // natural row of (i = 0, line l, plane p); + i (mirror: - i)
+            const long r = ((long)(d.k0 + p) * a.ny + (d.j0 + l)) * nx;
+            return a.mirror ? a.n - 1 - r : r;
+        };
+        auto sig = [](int p) { return p >= P / 2 ? 1 : 0; };
+        unsigned long long *ts = TRACE ? a.trace + 8 * (long)a.ntiles : nullptr;
+        const bool trs = TRACE && t == a.ttile && lane == 0;
+
+        if (wave < CW) {
+            // ---------------- compute: plane pw = 4 wave + g, line l ----------------
+            const int pw = wave * 4 + gl;
+            const int sg = wave;  // sigma of the wave's planes
+            struct In {
+                double ck[LV], cj[LV], ci[LV], dg[LV], rh[LV], jv[LV];
+            };
+            // the step's inputs, read from LDS one step ahead (their slot was
+            // completed before the barrier that ended the previous step)
+            auto load = [&](unsigned so, In &in) {
+                const char *slot = ring + so;
+#pragma unroll
+                for (int v = 0; v < LV; v++) {
+                    const long r = v * SB + pw * nj + lc;
+                    const double *b = reinterpret_cast<const double *>(slot + SL::COEF) + r * NA;
+                    in.ck[v] = b[0];
+                    in.cj[v] = b[1];
+                    in.ci[v] = b[2];
+                    if constexpr (NA == 4) in.dg[v] = b[3];
+                    in.rh[v] = reinterpret_cast<const double *>(slot + SL::RHS)[r];
+                    in.jv[v] = reinterpret_cast<const double *>(slot + SL::JFIN)[v * P + pw];
+                }
+            };
+            In A, B;
+            double xp = 0.0;  // the lane's value of the previous level
+            double xs = 0.0;  // lane - 16's value of the previous level (formed at the end of the previous step)
+            constexpr int OOB = 0x40000000;  // voffset that drops a buffer store (soffset is not range-checked)
+            const __amdgpu_buffer_rsrc_t hko =
+                __builtin_amdgcn_make_buffer_rsrc(a.hk + (long)t * a.hk_stride, 0, (int)(a.hk_stride * 8), 0x00020000);
+            const __amdgpu_buffer_rsrc_t hjo =
+                __builtin_amdgcn_make_buffer_rsrc(a.hj + (long)t * a.hj_stride, 0, (int)(a.hj_stride * 8), 0x00020000);
+            const uint64_t njm = (1ull << nj) - 1;
+            uint64_t pm = 0;  // lanes of the tile: line < nj, plane < np
+#pragma unroll
+            for (int g = 0; g < 4; g++)
+                if (wave * 4 + g < np) pm |= njm << (16 * g);
+            // plane np-1 feeds the next k-tile (group gk of the wave holding it): hk[q][l], q = v - (np-1) - sigma
+            const int gk = np - 1 - 4 * wave;
+            const bool kw = kout && gk >= 0 && gk < 4;
+            const uint64_t kgm = kw ? (0xFFFFull << (16 * (kw ? gk : 0))) : 0ull;
+            const int kq = -(np - 1) - sg;
+            // line nj-1 feeds the next j-tile: hj[q][p], q = v - (nj-1)
+            const uint64_t jgm = jout ? (GS << (nj - 1)) & pm : 0ull;
+            uint64_t hw = 0;  // lanes whose row exists at the previous level
+            // line 0 of group g has its row (i = v - p - sigma) at level v: 0 <= i < nx, in integer (SALU) ops
+            auto starts = [&](int v) {
+                uint64_t m = 0;
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const int y = v - (wave * 4 + g) - sg;
+                    m |= (uint64_t)(((unsigned)((y - nx) & ~y)) >> 31) << (16 * g);
+                }
+                return m;
+            };
+            auto publish = [&](int v, uint64_t h, double x) {
+                const uint64_t bx = (uint64_t)__double_as_longlong(x);
+                if (kw) {  // uniform
+                    const int q = v + kq;
+                    int vo = ll * 8;
+                    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(vo) : "v"(OOB), "v"(vo), "s"(h & kgm));
+                    if (q < 0) vo = OOB;
+                    __builtin_amdgcn_raw_buffer_store_b64(split64(bx), hko, vo, max(q, 0) * (NJ * 8), 16);  // sc1
+                }
+                if (jout) {
+                    const int q = v - (nj - 1);
+                    int vo = pw * 8;
+                    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(vo) : "v"(OOB), "v"(vo), "s"(h & jgm));
+                    if (q < 0) vo = OOB;
+                    __builtin_amdgcn_raw_buffer_store_b64(split64(bx), hjo, vo, max(q, 0) * (P * 8), 16);  // sc1
+                }
+            };
+            unsigned so = (unsigned)(((S0 % R) + R) % R) * SL::BYTES;  // slot of step s
+            constexpr unsigned RB = (unsigned)(R * SL::BYTES);
+            auto body = [&](int s, In &cur, In &nxt) {
+                if (TRACE && lane == 0 && wave == 0 && s == 0) a.trace[8 * t + 1] = __builtin_amdgcn_s_memrealtime();
+                if (trs && wave == 0 && s >= 0 && s < TS) ts[8 * s] = __builtin_amdgcn_s_memtime();
+                const unsigned sn = so + SL::BYTES == RB ? 0u : so + SL::BYTES;  // slot of step s+1
+                // k-inputs of group 0 (read first: LDS returns in order): wave 0 the
+                // poller's, wave 1 plane 3's results of the previous step
+                double kx0, kx1;
+                if (wave == 0) {
+                    kx0 = reinterpret_cast<const double *>(ring + so + SL::KFIN)[ll];
+                    kx1 = reinterpret_cast<const double *>(ring + so + SL::KFIN)[NJ + ll];
+                } else {
+                    kx0 = res[((2 * s - 2) & (RSL - 1)) * ROWS + 3 * NJ + ll];
+                    kx1 = res[((2 * s - 1) & (RSL - 1)) * ROWS + 3 * NJ + ll];
+                }
+                asm volatile("" ::: "memory");
+                load(sn, nxt);
+                const uint64_t h0 = (((hw << 1) & ~GS) | starts(2 * s)) & pm;
+                const uint64_t h1 = (((h0 << 1) & ~GS) | starts(2 * s + 1)) & pm;
+                hw = h1;
+                if (s >= 0 && s < TS) {
+                    // level 2s
+                    double xk = sel_lanes(G0M, kx0, xs);
+                    double xj = dpp_shr1g<4>(xp, cur.jv[0]);
+                    double v = cur.rh[0] - cur.ck[0] * xk;
+                    v = v - cur.cj[0] * xj;
+                    v = v - cur.ci[0] * xp;
+                    if constexpr (NA == 4) v = v / cur.dg[0];
+                    const double x0 = sel_lanes(h0, v, xp);
+                    // level 2s + 1
+                    xk = sel_lanes(G0M, kx1, up16(x0));
+                    xj = dpp_shr1g<4>(x0, cur.jv[1]);
+                    v = cur.rh[1] - cur.ck[1] * xk;
+                    v = v - cur.cj[1] * xj;
+                    v = v - cur.ci[1] * x0;
+                    if constexpr (NA == 4) v = v / cur.dg[1];
+                    const double x1 = sel_lanes(h1, v, x0);
+                    if (trs && wave == 0) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
+                    publish(2 * s, h0, x0);
+                    publish(2 * s + 1, h1, x1);
+                    res[((2 * s) & (RSL - 1)) * ROWS + pw * NJ + ll] = x0;
+                    res[((2 * s + 1) & (RSL - 1)) * ROWS + pw * NJ + ll] = x1;
+                    xp = x1;
+                    xs = up16(x1);  // the next step's first k-operand, off its critical path
+                }
+                so = sn;
+                if (trs && s >= 0 && s < TS) ts[8 * s + (wave == 0 ? 1 : 7)] = __builtin_amdgcn_s_memtime();
+                line_barrier();
+            };
+            for (int s = S0; s <= TS; s += 2) {
+                body(s, A, B);
+                if (s + 1 <= TS) body(s + 1, B, A);
+            }
+            if (TRACE && lane == 0 && wave == 0) {
+                a.trace[8 * t + 2] = __builtin_amdgcn_s_memrealtime();
+                unsigned xcc;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                a.trace[8 * t + 4] = xcc;
+            }
+        } else if (wave < CW + NL) {
+            // ---------------- loaders: a step's DMAs spread over the NL waves ----------------
+            const int w = wave - CW;
+            auto issue = [&](int q) {
+                const int qc = min(max(q, 0), TS - 1);
+                const unsigned sl = lds0 + (unsigned)(((q % R + R) % R) * SL::BYTES);
+                const long row = d.cbase + (long)qc * LV * SB;
+                const char *cb = reinterpret_cast<const char *>(a.coef) + row * (8L * NA);
+                const char *ub = reinterpret_cast<const char *>(a.rhs) + row * 8L;
+#pragma unroll
+                for (int k = 0; k < KPER; k++) {
+                    const int m = w + k * NL;
+                    if (m < SL::NPC) {
+                        dma16(cb + m * 1024 + lane * 16, sl + SL::COEF + m * 1024);
+                    } else if (m < NITEM) {
+                        const int r = m - SL::NPC;
+                        dma16(ub + r * 1024 + lane * 16, sl + SL::RHS + r * 1024);
+                    } else {
+                        dma16(cb + lane * 16, sl + SL::COEF);  // keeps the per-wave count fixed
+                    }
+                }
+            };
+            for (int s = S0; s <= TS; s++) {
+                const unsigned long long i0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
+                issue(s + D);  // dummies past TS keep the wait counts exact
+                const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
+                // steps s+LA+1 .. s+D were issued after step s+LA's
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - LA) * KPER) : "memory");
+                if (trs && w == 0 && s >= 0 && s < TS) {
+                    ts[8 * s + 4] = w0 - i0;
+                    ts[8 * s + 3] = __builtin_amdgcn_s_memtime() - w0;
+                }
+                line_barrier();
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (wave == CW + NL) {
+            // ---------------- poller ----------------
+            // At step s: LDS-DMA sc1 reads of step s+DH's k-inputs (two levels x NJ
+            // lines: 16 lanes x 16 B) and step s+DH+1's j-inputs (two levels x P
+            // planes: 8 lanes x 16 B); then the k-inputs of step s+1 and the
+            // j-inputs of step s+2 (issued DH-1 steps ago) are waited for and
+            // checked.  A tile without a k (j) input gets +0.0 there (its
+            // coefficient is +0.0 too).
+            const double *hk = a.hk + (long)max(d.tk, 0) * a.hk_stride;
+            const double *hj = a.hj + (long)max(d.tj, 0) * a.hj_stride;
+            const int qmax = (int)(a.hk_stride / (NJ * LV)) - 1;  // steps
+            const int kl = lane & (NJ - 1), kv = lane >> 4;      // k check: lanes 0..31 = (level, line)
+            const int jp = lane & (P - 1), jv = lane >> 3;       // j check: lanes 0..15 = (level, plane)
+            auto kval = [&](int q) {  // q: level
+                return lane < LV * NJ && q < T && kl < nj && (unsigned)(q - kl) < (unsigned)nx;
+            };
+            auto jval = [&](int q) {
+                return lane < LV * P && q < T && jp < np && (unsigned)(q - jp - sig(jp)) < (unsigned)nx;
+            };
+            const unsigned sink = lds0 + (unsigned)(R * SL::BYTES + RSL * ROWS * 8 + 16);
+            auto issue = [&](int q) {
+                const char *kp = reinterpret_cast<const char *>(hk + (long)min(max(q, 0), qmax) * LV * NJ) + lane * 16;
+                const char *jp2 = reinterpret_cast<const char *>(hj + (long)min(max(q + 1, 0), qmax) * LV * P) + lane * 16;
+                const unsigned ks = kin ? lds0 + (unsigned)((((q % R) + R) % R) * SL::BYTES + SL::KFIN) : sink;
+                const unsigned js = jin ? lds0 + (unsigned)(((((q + 1) % R) + R) % R) * SL::BYTES + SL::JFIN) : sink;
+                if (lane < LV * NJ / 2) dma16_sc1(kp, ks);
+                if (lane < LV * P / 2) dma16_sc1(jp2, js);
+            };
+            if (!kin || !jin) {
+                for (int q = 0; q < R; q++) {
+                    if (!kin && lane < LV * NJ) reinterpret_cast<double *>(ring + q * SL::BYTES + SL::KFIN)[lane] = 0.0;
+                    if (!jin && lane < LV * P) reinterpret_cast<double *>(ring + q * SL::BYTES + SL::JFIN)[lane] = 0.0;
+                }
+            }
+            __builtin_amdgcn_s_setprio(3);  // the polls enter the CU's memory queue ahead of the coefficient DMAs
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            unsigned polls = 0;
+            for (int s = S0; s <= TS; s++) {
+                const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
+                issue(s + DH);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (DH - 1)) : "memory");
+                if (s > TS) break;
+                const int qk = s + 1, qj = s + 2;  // steps
+                double *kslot = reinterpret_cast<double *>(ring + (qk % R) * SL::BYTES + SL::KFIN) + min(lane, LV * NJ - 1);
+                double *jslot = reinterpret_cast<double *>(ring + (qj % R) * SL::BYTES + SL::JFIN) + min(lane, LV * P - 1);
+                const int lk = LV * qk + kv, lj = LV * qj + jv;  // levels checked by this lane
+                const bool vk = kin && kval(lk), vj = jin && jval(lj);
+                const uint64_t kvb = vk ? (uint64_t)__double_as_longlong(*kslot) : 0;
+                const uint64_t jvb = vj ? (uint64_t)__double_as_longlong(*jslot) : 0;
+                const bool bk = vk && kvb == TRI_SENTINEL, bj = vj && jvb == TRI_SENTINEL;
+                if (__any(bk || bj)) {
+                    // resync episode (k_line's): drain, wait for these values and for
+                    // the furthest step in flight, re-issue
+                    polls++;
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    auto spin = [&](const double *src) {
+                        for (;;) {
+                            const uint64_t b = line_ld_agent(src);
+                            if (b != TRI_SENTINEL) return b;
+                            if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s
+                                atomicOr(a.err, 8);
+                                return (uint64_t)0x7FF8000000000000ull;
+                            }
+                            __builtin_amdgcn_s_sleep(1);
+                        }
+                    };
+                    if (bk) *kslot = __longlong_as_double((long long)spin(hk + (long)lk * NJ + kl));
+                    if (bj) *jslot = __longlong_as_double((long long)spin(hj + (long)lj * P + jp));
+                    const int fk = LV * (s + DH) + kv, fj = LV * (s + DH + 1) + jv;
+                    if (kin && kval(fk)) (void)spin(hk + (long)fk * NJ + kl);
+                    if (jin && jval(fj)) (void)spin(hj + (long)fj * P + jp);
+                    for (int k = 2; k <= DH; k++) issue(s + k);  // the polls issued at steps s+k-DH
+                }
+                if (trs && s >= 0 && s < TS) ts[8 * s + 2] = __builtin_amdgcn_s_memtime() - w0;
+                line_barrier();
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (TRACE) {
+                for (int o = 32; o >= 1; o >>= 1) polls += __shfl_xor(polls, o);
+                if (lane == 0) a.trace[8 * t + 3] = polls;
+            }
+        } else {
+            // ---------------- storers: results, re-arms ----------------
+            // Storer 0 re-arms the consumed j-inputs, storer SW-1 the k-inputs.
+            const int w = wave - (CW + NL + 1);
+            const int kl = lane & (NJ - 1), kv = lane >> 4, jp = lane & (P - 1), jv = lane >> 3;
+            uint64_t *hki = reinterpret_cast<uint64_t *>(a.hk + (long)max(d.tk, 0) * a.hk_stride) + kl;
+            uint64_t *hji = reinterpret_cast<uint64_t *>(a.hj + (long)max(d.tj, 0) * a.hj_stride) + jp;
+            const bool rk = w == SW - 1 && kin && lane < LV * NJ && kl < nj;
+            const bool rj = w == 0 && jin && lane < LV * P && jp < np;
+            auto rearm = [&](int q) {  // step q's entries
+                const int vk = LV * q + kv, vj = LV * q + jv;
+                if (rk && vk < T && (unsigned)(vk - kl) < (unsigned)nx) hki[(long)vk * NJ] = TRI_SENTINEL;
+                if (rj && vj < T && (unsigned)(vj - jp - (jp >= P / 2 ? 1 : 0)) < (unsigned)nx)
+                    hji[(long)vj * P] = TRI_SENTINEL;
+            };
+            if constexpr (OUT == 1) {
+                // block B (levels 8B .. 8B+7, steps 4B .. 4B+3) is written during
+                // steps 4B+4 .. 4B+7, a quarter per step: value k of the block is
+                // level 8B + (k & 7) of run k >> 3 = (plane, line), so 8 lanes store
+                // 8 consecutive rows of one line
+                static_assert(RSL == 16 && ROWS * 8 / 4 == 64 * 4, "runs");
+                auto slice = [&](int s) {
+                    const int B = (s >> 2) - 1, u = s & 3;
+                    if (B < 0) return;
+                    constexpr int PER = ROWS * 8 / 4 / 64 / SW;  // values per lane per step
+#pragma unroll
+                    for (int it = 0; it < PER; it++) {
+                        const int k = u * (ROWS * 2) + (w * PER + it) * 64 + lane;
+                        const int m = k & 7, r = k >> 3, p = r >> 4, l = r & (NJ - 1);
+                        const int q = 8 * B + m;
+                        const int i = q - l - p - (p >= P / 2 ? 1 : 0);
+                        const double x = res[(q & (RSL - 1)) * ROWS + p * NJ + l];
+                        if (!(a.diag & 1) && p < np && l < nj && (unsigned)i < (unsigned)nx)
+                            a.out[a.mirror ? nb(p, l) - i : nb(p, l) + i] = x;
+                    }
+                };
+                for (int s = S0; s <= TS; s++) {
+                    const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
+                    if (s >= 0) slice(s);
+                    if (s >= 1 && s <= TS) rearm(s - 1);
+                    if (trs && w == 0 && s >= 0 && s < TS) ts[8 * s + 5] = __builtin_amdgcn_s_memtime() - w0;
+                    line_barrier();
+                }
+                // the last blocks' remaining quarters (every result is in LDS)
+                for (int s = TS + 1; s < 4 * ((T - 1) / 8) + 8; s++) slice(s);
+            } else {
+                // step s-1's two levels: value k = 64 (w + SW it) + lane is level
+                // 2(s-1) + (k >> 7), plane (k >> 4) & 7, line k & 15; its place in the
+                // mirror U tile's rhs stream (same nj, np): level Cp - v with
+                // Cp = nx + nj + np - 3 + sigma(p) + sigma(np-1-p)
+                constexpr int PS = LV * ROWS / 64 / SW;
+                static_assert(LV * ROWS % (64 * SW) == 0, "chunks");
+                double *po[PS];
+                int vlo[PS], lvs[PS], roff[PS];
+#pragma unroll
+                for (int u = 0; u < PS; u++) {
+                    const int k = (w + u * SW) * 64 + lane;
+                    const int lv = k >> 7, p = (k >> 4) & (P - 1), l = k & (NJ - 1);
+                    const int pp = min(p, np - 1), lq = min(l, nj - 1);
+                    lvs[u] = lv;
+                    roff[u] = (lv * P + p) * NJ + l;
+                    vlo[u] = p < np && l < nj ? l + p + sig(p) : 1 << 30;  // valid iff 0 <= v - vlo < nx
+                    const long Cp = (long)nx + nj + np - 3 + sig(pp) + sig(np - 1 - pp);
+                    po[u] = a.out + d.ubase + Cp * SB + (long)(np - 1 - pp) * nj + (nj - 1 - lq);
+                }
+                for (int s = S0; s <= TS; s++) {
+                    const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
+                    const int q = s - 1;
+                    if (q >= 0 && q < TS) {
+#pragma unroll
+                        for (int u = 0; u < PS; u++) {
+                            const int v = LV * q + lvs[u];
+                            const double x = res[(v & (RSL - 1)) * ROWS + (roff[u] & (ROWS - 1))];
+                            if (!(a.diag & 33) && (unsigned)(v - vlo[u]) < (unsigned)nx) po[u][-SB * v] = x;
+                        }
+                        rearm(q);
+                    }
+                    if (trs && w == 0 && s >= 0 && s < TS) ts[8 * s + 5] = __builtin_amdgcn_s_memtime() - w0;
+                    line_barrier();
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // launch
 // ---------------------------------------------------------------------------
 // Leads (steps): loaders D, poller DH.  The apply's sweeps (rhs from a stream)
@@ -1168,10 +1624,12 @@ static int launch_line_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a
 // step, 8 lanes store 8 consecutive stream entries.  Block b runs on XCD b % 8
 // and the XCD's blocks walk whole tiles in step order.
 constexpr int LRHS_RUN = 8;
-template <int P>
+// P planes x NJ lines per tile; SKEW: k_line2's level map (planes >= P/2 one
+// level later); mirror: the tiles are a U sweep's (natural row n-1 - r)
+template <int P, int NJ, bool SKEW>
 __global__ __launch_bounds__(256) void k_line_rhs(const LineTile *__restrict__ tiles, int ntiles, int nq, int nx,
-                                                 int ny, const double *__restrict__ rhs, double *__restrict__ out,
-                                                 const double *guard)
+                                                 int ny, long n, int mirror, const double *__restrict__ rhs,
+                                                 double *__restrict__ out, const double *guard)
 {
     if (guard && *guard != 0.0) return;  // a batched iteration past the stop (lssp_amd_ctx::guard)
     const long b = blockIdx.x, j = b >> 3;
@@ -1179,23 +1637,132 @@ __global__ __launch_bounds__(256) void k_line_rhs(const LineTile *__restrict__ t
     if (t >= ntiles) return;
     const LineTile d = tiles[t];
     if (q0 >= d.T) return;
-    constexpr int NJ = 256 / P, NV = P * NJ * LRHS_RUN / 256;  // values per thread
+    constexpr int NV = P * NJ * LRHS_RUN / 256;  // values per thread
+    static_assert(NV >= 1 && P * NJ * LRHS_RUN % 256 == 0, "block");
     double v[NV];
 #pragma unroll
     for (int it = 0; it < NV; it++) {
         const int k = it * 256 + threadIdx.x, m = k & 7, l = (k >> 3) % NJ, p = (k >> 3) / NJ;
-        const int i = q0 + m - l - p;
+        const int i = q0 + m - l - p - (SKEW && p >= P / 2 ? 1 : 0);
         const bool ok = q0 + m < d.T && p < d.np && l < d.nj && (unsigned)i < (unsigned)nx;
-        v[it] = ok ? rhs[((long)(d.k0 + p) * ny + (d.j0 + l)) * nx + i] : 0.0;
+        const long r = ((long)(d.k0 + p) * ny + (d.j0 + l)) * nx + i;
+        v[it] = ok ? rhs[mirror ? n - 1 - r : r] : 0.0;
     }
     const long SB = (long)P * d.nj;
 #pragma unroll
     for (int it = 0; it < NV; it++) {
         const int k = it * 256 + threadIdx.x, m = k & 7, l = (k >> 3) % NJ, p = (k >> 3) / NJ;
-        const int i = q0 + m - l - p;
+        const int i = q0 + m - l - p - (SKEW && p >= P / 2 ? 1 : 0);
         if (q0 + m < d.T && p < d.np && l < d.nj && (unsigned)i < (unsigned)nx)
             out[d.cbase + (q0 + m) * SB + p * d.nj + l] = v[it];
     }
+}
+
+// the natural-order rhs into a sweep's stream layout (stream: li.d_lstream for
+// the L sweep, li.d_ustream for the U sweep)
+static int launch_line_gather(lssp_amd_ctx *c, const LineSweep &ls, int mirror, const double *rhs, double *stream)
+{
+    const int nq = (ls.tmax + LRHS_RUN - 1) / LRHS_RUN;
+    const long grid = 8L * ((ls.ntiles + 7) / 8) * nq;
+    auto kr = ls.LV == 2 ? k_line_rhs<8, 16, true>
+              : ls.P == 16 ? k_line_rhs<16, 16, false> : ls.P == 8 ? k_line_rhs<8, 32, false> : k_line_rhs<4, 64, false>;
+    if (ls.LV == 2 && (ls.P != 8 || ls.NJ != 16)) return LSSP_AMD_EUNSUPPORTED;
+    const long n = (long)ls.nx * ls.ny * ls.nz;
+    kr<<<grid, 256, 0, c->stream>>>(ls.d_tiles, ls.ntiles, nq, ls.nx, ls.ny, n, mirror, rhs, stream, c->guard);
+    LSSP_HIP(hipGetLastError());
+    return LSSP_AMD_OK;
+}
+
+// ---- k_line2 launches -------------------------------------------------------
+#ifndef LINE2_D
+#define LINE2_D 6  // loader lead (steps of two levels)
+#endif
+#ifndef LINE2_DH
+#define LINE2_DH 3  // poller lead (steps)
+#endif
+#ifndef LINE2_NL
+#define LINE2_NL 4
+#endif
+#ifndef LINE2_SW
+#define LINE2_SW 4
+#endif
+template <int NA, int OUT, bool TRACE>
+static int launch_line2_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)
+{
+    auto kern = k_line2<NA, OUT, LINE2_NL, LINE2_D, LINE2_DH, LINE2_SW, TRACE>;
+    static int attr = 0;
+    if (lds > attr) {
+        LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        attr = lds;
+    }
+    const int grid = std::min(ls.ntiles, c->num_cus);
+    kern<<<grid, 64 * l2::waves(LINE2_NL, LINE2_SW), lds, c->stream>>>(g);
+    ls.base += (unsigned long long)ls.ntiles + grid;
+    LSSP_HIP(hipGetLastError());
+    return LSSP_AMD_OK;
+}
+
+template <int NA, int OUT>
+static int launch_line2_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a)
+{
+    constexpr int lds = l2::lds_bytes<NA, OUT, LINE2_D>();
+    static_assert(lds <= 160 * 1024, "LDS");
+    // diagnostics only: LSSP_AMD_LINE_TRACE=path[:tile] appends one JSON line per sweep
+    static const char *trp = getenv("LSSP_AMD_LINE_TRACE");
+    if (!trp) return launch_line2_k<NA, OUT, false>(c, ls, a, lds);
+    LineArgs g = a;
+    const size_t tn = 8 * (size_t)ls.ntiles + 8 * (size_t)ls.tmax + 64;
+    const char *colon = strrchr(trp, ':');
+    g.ttile = colon ? atoi(colon + 1) : ls.ntiles / 2;
+    LSSP_HIP(hipMalloc(&g.trace, sizeof(unsigned long long) * tn));
+    LSSP_HIP(hipMemsetAsync(g.trace, 0, sizeof(unsigned long long) * tn, c->stream));
+    const int grid = std::min(ls.ntiles, c->num_cus);
+    LSSP_TRY((launch_line2_k<NA, OUT, true>(c, ls, g, lds)));
+    std::vector<unsigned long long> h(tn);
+    LSSP_HIP(hipMemcpyAsync(h.data(), g.trace, sizeof(unsigned long long) * tn, hipMemcpyDeviceToHost, c->stream));
+    LSSP_HIP(hipStreamSynchronize(c->stream));
+    (void)hipFree(g.trace);
+    std::string path(trp, colon ? colon - trp : strlen(trp));
+    FILE *f = fopen(path.c_str(), "a");
+    if (f) {
+        fprintf(f, "{\"mirror\": %d, \"ntiles\": %d, \"W\": %d, \"ttile\": %d, \"T\": %d, \"LV\": 2, \"grid\": %d, "
+                   "\"data\": [",
+                a.mirror, ls.ntiles, (ls.ny + ls.NJ - 1) / ls.NJ, g.ttile, ls.h_tiles[g.ttile].T / 2, grid);
+        for (size_t i = 0; i < tn; i++) fprintf(f, "%s%llu", i ? ", " : "", h[i]);
+        fprintf(f, "]}\n");
+        fclose(f);
+    }
+    return LSSP_AMD_OK;
+}
+
+// k_line2 sweep of ls: rhs from a stream; OUT 2: out = the U rhs stream, OUT 1: natural order
+static int launch_line2(lssp_amd_ctx *c, const LineILU &li, int which, const double *stream, double *out, int outk)
+{
+    const LineSweep &ls = which ? li.U : li.L;
+    LineArgs a{};
+    a.nx = ls.nx;
+    a.ny = ls.ny;
+    a.ntiles = ls.ntiles;
+    a.n = (long)ls.nx * ls.ny * ls.nz;
+    a.tiles = ls.d_tiles;
+    a.coef = ls.d_coef;
+    a.rhs = stream;
+    a.out = out;
+    a.hk = li.d_hk;
+    a.hj = li.d_hj;
+    a.hk_stride = li.hk_stride;
+    a.hj_stride = li.hj_stride;
+    a.claim = ls.d_claim;
+    a.base = ls.base;
+    a.mirror = which;
+    a.err = c->d_err;
+    a.guard = c->guard;
+    {
+        const char *dg = getenv("LSSP_AMD_LINE_DIAG");
+        a.diag = dg ? atoi(dg) : 0;
+    }
+    if (outk == 2) return ls.NA == 3 ? launch_line2_t<3, 2>(c, ls, a) : launch_line2_t<4, 2>(c, ls, a);
+    return ls.NA == 3 ? launch_line2_t<3, 1>(c, ls, a) : launch_line2_t<4, 1>(c, ls, a);
 }
 
 static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const double *rhs, bool u_in, double *out,
@@ -1232,22 +1799,27 @@ static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const doub
 
 int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs)
 {
+    if (li.LV == 2) {  // k_line2: gather, L sweep -> the U rhs stream, U sweep -> x
+        LSSP_TRY(launch_line_gather(c, li.L, 0, rhs, li.d_lstream));
+        LSSP_TRY(launch_line2(c, li, 0, li.d_lstream, li.d_ustream, 2));
+        return launch_line2(c, li, 1, li.d_ustream, x, 1);
+    }
 #ifdef LINE_APPLY_NAT  // tuning builds: the L sweep reads the natural-order rhs itself (rhs wave)
     LSSP_TRY(launch_line(c, li, 0, rhs, false, nullptr, true));
     return launch_line(c, li, 1, nullptr, true, x, false);
 #endif
-    const LineSweep &L = li.L;
-    const int nq = (L.tmax + LRHS_RUN - 1) / LRHS_RUN;
-    const long grid = 8L * ((L.ntiles + 7) / 8) * nq;
-    auto kr = L.P == 16 ? k_line_rhs<16> : L.P == 8 ? k_line_rhs<8> : k_line_rhs<4>;
-    kr<<<grid, 256, 0, c->stream>>>(L.d_tiles, L.ntiles, nq, L.nx, L.ny, rhs, li.d_lstream, c->guard);
-    LSSP_HIP(hipGetLastError());
+    LSSP_TRY(launch_line_gather(c, li.L, 0, rhs, li.d_lstream));
     LSSP_TRY(launch_line(c, li, 0, nullptr, false, nullptr, true, true));
     return launch_line(c, li, 1, nullptr, true, x, false);
 }
 
 int launch_line_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs)
 {
+    if (li.LV == 2) {  // one sweep: its rhs gathered into its own stream, natural-order output
+        double *st = which ? li.d_ustream : li.d_lstream;
+        LSSP_TRY(launch_line_gather(c, which ? li.U : li.L, which, rhs, st));
+        return launch_line2(c, li, which, st, x, 1);
+    }
     return launch_line(c, li, which, rhs, false, x, false);
 }
 

@@ -213,13 +213,20 @@ def _box7(nx, ny, nz, seed):
     return np.array(Ap, np.int32), np.array(Aj, np.int32), np.array(Ax)
 
 
-# boxes whose line-sweep tiles are 64 x 4 (planes per tile chosen by hop count:
-# (20, 100, 6)), 32 x 8 ((20, 60, 24)) and 16 x 16 ((20, 40, 40), (13, 37, 35)),
-# with partial tiles in j and k and an odd last plane count
-@pytest.mark.parametrize("nx,ny,nz,tile", [(20, 100, 6, (64, 4)), (20, 60, 24, (32, 8)), (20, 40, 40, (16, 16)),
-                                           (13, 37, 35, (16, 16))])
-def test_line_sweep_tile_shapes_bitwise_vs_oracle(dev, nx, ny, nz, tile):
+# boxes whose k_line tiles (LSSP_AMD_LINE_MODE=1, 256 rows per level) are 64 x 4
+# (planes per tile chosen by hop count: (20, 100, 6)), 32 x 8 ((20, 60, 24))
+# and 16 x 16 ((20, 40, 40), (13, 37, 35)); k_line2 (the default) always takes
+# 16 x 8 -- partial tiles in j and k, an odd last plane count, slabs with 1..3
+# planes in the second compute wave ((13, 37, 35): 35 = 4 x 8 + 3; (9, 21, 13):
+# 13 = 8 + 5, (20, 17, 6): one tile of 6 planes, (11, 16, 4): planes in wave 0 only)
+@pytest.mark.parametrize("nx,ny,nz,tile,mode", [(20, 100, 6, (64, 4), 1), (20, 60, 24, (32, 8), 1),
+                                                (20, 40, 40, (16, 16), 1), (13, 37, 35, (16, 16), 1),
+                                                (20, 100, 6, (16, 8), 2), (13, 37, 35, (16, 8), 2),
+                                                (9, 21, 13, (16, 8), 2), (20, 17, 6, (16, 8), 2),
+                                                (11, 16, 4, (16, 8), 2), (40, 33, 19, (16, 8), 2)])
+def test_line_sweep_tile_shapes_bitwise_vs_oracle(dev, monkeypatch, nx, ny, nz, tile, mode):
     import lssp_amd
+    monkeypatch.setenv("LSSP_AMD_LINE_MODE", str(mode))
     Ap, Aj, Ax = _box7(nx, ny, nz, nx + ny + nz)
     n = Ap.size - 1
     M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=1, level=0)
@@ -232,6 +239,15 @@ def test_line_sweep_tile_shapes_bitwise_vs_oracle(dev, nx, ny, nz, tile):
         rhs = uniform(200 + rep, n)
         M.apply(x, dev.vec(n, rhs))
         assert np.array_equal(x.download(), O.ilu_apply(L, U, rhs)), rep
+    # the single sweeps (lssp_pc_ilu_solve_lower/upper_matrix, solver-tri.cxx:4-46)
+    rhs = uniform(300, n)
+    z = dev.vec(n)
+    M.trisolve(0, z, dev.vec(n, rhs))
+    lo = O.ilu_apply(L, O.CSR(n, np.arange(n + 1, dtype=np.int32), np.arange(n, dtype=np.int32), np.ones(n)), rhs)
+    assert np.array_equal(z.download(), lo)
+    M.trisolve(1, z, dev.vec(n, rhs))
+    up = O.ilu_apply(O.CSR(n, np.arange(n + 1, dtype=np.int32), np.arange(n, dtype=np.int32), np.ones(n)), U, rhs)
+    assert np.array_equal(z.download(), up)
 
 
 @pytest.mark.parametrize("seed,n,per_row,missing,blk", [(11, 3000, 6, 0, 0), (12, 2500, 9, 7, 0),
@@ -415,7 +431,7 @@ def test_sliced_copy_footprint_and_cap_fallback(dev, monkeypatch):
     M = lssp_amd.DMat(dev, A.Ap, A.Aj, A.Ax)
     csr, aux = M.device_bytes
     assert M.windowed and csr == 4 * (A.n + 1) + 12 * A.nnz
-    assert aux >= 12 * A.nnz  # f64 values + 16-bit column pairs, padded per slice
+    assert aux >= 10 * A.nnz  # f64 values + 16-bit columns, padded per slice
     monkeypatch.setenv("LSSP_AMD_SELL_CAP", "1000")
     F = lssp_amd.DMat(dev, A.Ap, A.Aj, A.Ax)
     assert not F.windowed and F.device_bytes[1] == 0

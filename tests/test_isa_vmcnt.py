@@ -85,3 +85,16 @@ def test_line_instantiations_hazard_free_and_no_scratch(line_asm):
             continue
         m = re.search(r"\.amdhsa_kernel " + name + r"\n(.*?)\.end_amdhsa_kernel", text, re.S)
         assert int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", m.group(1)).group(1)) == 0, name
+
+
+def test_line2_instantiations_hazard_free_and_no_scratch(line_asm):
+    """k_line2 (two levels per step): every instantiation, TRACE included,
+    hazard-free on its loaders' / poller's asm-issued DMAs and without scratch."""
+    import check_vmcnt
+    names = sorted(set(re.findall(r"^(_ZN8lssp_amd7k_line2\w+):", open(line_asm).read(), re.M)))
+    assert len(names) >= 4, names
+    text = open(line_asm).read()
+    for name in names:
+        assert check_vmcnt.check_loader(line_asm, name) == 0, name
+        m = re.search(r"\.amdhsa_kernel " + name + r"\n(.*?)\.end_amdhsa_kernel", text, re.S)
+        assert int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", m.group(1)).group(1)) == 0, name
