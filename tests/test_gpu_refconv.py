@@ -9,14 +9,14 @@ from oracle/_ref/libref.so -- the reference compiled from /root/reference)
 on the benchmark configurations, solved to the reference's defaults
 rtol = atol = rb = 1e-7 (lssp.cxx:11-13), b = 1, x0 = 0:
 
-  * the iteration count within 1 of the reference's (the stop test is
+  * bitwise equality with the oracle's TREE restatement of the same driver
+    at full size (nits, residual, every scalar of the history, x), which
+    separates "the order of the sums differs" from "the code differs";
+  * the iteration count and final residual within the stated tolerances
+    NITS_REL / RES_REL of the reference's (the stop test is
     solver-bicgstab.cxx:141-157 / solver-gmres.cxx:206-217);
-  * the final residual within REL_RES (relative) of the reference's, and the
-    scalar history (every dot and norm the driver computed, in the
-    reference's call order) within HIST_TOL relative over the iterations both
-    runs share -- documented tolerances, measured values printed;
   * the recomputed true residual ||b - A x|| at most TRUE_FACTOR times the
-    reference's own true residual and below the stop tolerance scale;
+    reference's own true residual and the stop scale;
 
 and, at 512^3 (config 4's matrix, which the reference cannot run here: 134 M
 rows), convergence and the true residual as properties.
@@ -37,10 +37,16 @@ if os.path.exists(_path):
     with open(_path) as _f:
         FULL = json.load(_f)["cases"]
 
-# documented tolerances of the timed (TREE) mode against the reference
-REL_RES = 0.5      # final residual: |res - ref| / ref
-HIST_TOL = 1e-2    # scalar history, max relative deviation over the shared iterations
-TRUE_FACTOR = 2.0  # true residual vs the reference's true residual
+# documented tolerances of the timed (TREE) mode against the reference.  The
+# summation order alone moves BiCGSTAB's stop by a few iterations (the
+# oracle's TREE restatement of the same driver: 144 vs 145 at 216^3, 161 vs
+# 155 at 256^3 -- tests/golden/full.json "tree"): its residual history is
+# erratic near the tolerance, and the TREE and sequential scalar histories
+# part after ~12 iterations at 1e-6 (lead_agree_* in full.json).  GMRES's
+# restarted residual is smooth: its count and residual stay with the reference.
+NITS_REL = {4: 0.05, 0: 0.0}   # |nits - ref| <= max(1, ceil(NITS_REL * ref))
+RES_REL = {4: 0.5, 0: 1e-6}    # |res - ref| / ref
+TRUE_FACTOR = 2.0              # true residual vs max(reference's true residual, stop scale)
 
 
 def _fx(h):
@@ -49,6 +55,7 @@ def _fx(h):
 
 def _solve_case(c):
     import lssp_amd
+    from inputs import digest
     dev = lssp_amd.Device(0, reduction=lssp_amd.TREE)
     try:
         Ap, Aj, Ax = lssp_amd.poisson(3, c["N"])
@@ -58,6 +65,7 @@ def _solve_case(c):
             M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=c["pc"]["level"])
         else:
             M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUT, tol=c["pc"]["tol"], p=c["pc"]["p"])
+        del Aj, Ax
         b = dev.vec(n, np.ones(n))
         x = dev.vec(n, np.zeros(n))
         r = lssp_amd.solve(dev, A, M, x, b, solver=c["solver"], tol_rel=c["rtol"], tol_abs=c["atol"],
@@ -66,7 +74,7 @@ def _solve_case(c):
         A.mv_amxpbyz(-1.0, x, 1.0, b, z)
         zh = z.download()
         true_res = math.sqrt(float(np.dot(zh, zh)))
-        return r, true_res, n
+        return r, true_res, n, digest(x.download())
     finally:
         dev.close()
 
@@ -74,22 +82,24 @@ def _solve_case(c):
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("c", FULL, ids=[c["name"] for c in FULL])
 def test_tree_mode_full_solve_vs_reference(c):
-    r, true_res, n = _solve_case(c)
+    from inputs import digest
+    r, true_res, n, xsha = _solve_case(c)
     ref_nits, ref_res, ref_true = c["nits"], _fx(c["residual"]), _fx(c["true_residual"])
-    ref_tr = np.array([_fx(h) for h in c["trace"]])
-    k = min(len(ref_tr), len(r.trace))
-    with np.errstate(divide="ignore", invalid="ignore"):
-        dev_hist = np.abs(r.trace[:k] - ref_tr[:k]) / np.maximum(np.abs(ref_tr[:k]), 1e-300)
-    hist = float(np.max(dev_hist)) if k else 0.0
     rel = abs(r.residual - ref_res) / ref_res
-    print(f"\n{c['name']}: nits {r.nits} (reference {ref_nits}), residual {r.residual:.6e} "
-          f"(reference {ref_res:.6e}, rel {rel:.3e}), true residual {true_res:.6e} "
-          f"(reference {ref_true:.6e}), history max rel dev {hist:.3e} over {k} scalars")
-    assert abs(r.nits - ref_nits) <= 1
-    assert rel <= REL_RES
-    assert hist <= HIST_TOL
+    tr = c.get("tree")
+    print(f"\n{c['name']}: nits {r.nits} (reference {ref_nits}"
+          f"{', oracle TREE ' + str(tr['nits']) if tr else ''}), residual {r.residual:.6e} "
+          f"(reference {ref_res:.6e}, rel {rel:.3e}), true residual {true_res:.6e} (reference {ref_true:.6e})")
+    # the same algorithm in the same order as the oracle's TREE restatement: bit for bit
+    if tr:
+        assert r.nits == tr["nits"] and r.residual == _fx(tr["residual"])
+        assert digest(r.trace) == tr["trace_sha256"] and xsha == tr["x_sha256"]
+    # ... and within the stated tolerances of the reference's sequential order
+    assert abs(r.nits - ref_nits) <= max(1, math.ceil(NITS_REL[c["solver"]] * ref_nits))
+    assert rel <= RES_REL[c["solver"]]
     # the stop scale max(rtol ||r0||, atol, rb ||b||) with r0 = b (x0 = 0)
     scale = max(c["rtol"] * math.sqrt(n), c["atol"], c["rbtol"] * math.sqrt(n))
+    assert r.residual <= scale
     assert true_res <= TRUE_FACTOR * max(ref_true, scale)
 
 
@@ -101,7 +111,7 @@ def test_tree_mode_512_bicgstab_converges():
     this size here; round 2 measured 308 iterations)."""
     c = {"N": 512, "pc": {"kind": "iluk", "level": 0}, "solver": 4, "rtol": 1e-7, "atol": 1e-7,
          "rbtol": 1e-7, "restart": 30}
-    r, true_res, n = _solve_case(c)
+    r, true_res, n, _ = _solve_case(c)
     scale = 1e-7 * math.sqrt(n)
     print(f"\n512^3: nits {r.nits}, residual {r.residual:.6e} (stop scale {scale:.6e}), true {true_res:.6e}")
     assert 0 < r.nits < 5000 and r.residual <= scale
