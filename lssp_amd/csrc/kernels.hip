@@ -320,6 +320,7 @@ struct SpmvArgs {
     int ndiag;
     const double *guard;  // lssp_amd_ctx::guard
     long blk0;            // first chunk of this launch (spmv_halo splits a product)
+    int streams;          // concurrent block streams (a multiple of 8, spmv_streams)
 };
 
 // The 256-row blocks are dealt so that each of the 8 XCDs owns one contiguous
@@ -343,8 +344,8 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
     __shared__ int soff[CMP ? 256 : 1];
     __shared__ double lds[MAX_SLOTS][4];
     if (a.guard && *a.guard != 0.0) return;
-    const long per = gridDim.x / 8;
-    const long lb = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    const long per = gridDim.x / a.streams;
+    const long lb = (blockIdx.x % a.streams) * per + blockIdx.x / a.streams;
     if (lb >= nblk) return;
     const long blk = a.blk0 + lb;
     const int r0 = (int)(blk * 256);
@@ -570,10 +571,28 @@ static void spmv_sell_dispatch(const SpmvArgs &a, const lssp_amd_mat *A, int nre
     else k_spmv_sell<EPI, 2><<<g, WIN_ROWS, 0, s>>>(a, A->d_win, A->s_ax, A->s_col, A->s_row, A->s_meta, nb);
 }
 
+// Workgroup w of the product takes block (w % K) * (grid / K) + w / K: K
+// streams of consecutive blocks, stream q on XCD q % 8 (dispatch deals
+// workgroups round-robin over the 8 XCDs), so the x entries a block gathers
+// (+-1, +-N, +-N^2 rows away) are re-used by its stream's later blocks out of
+// that XCD's L2 / the MALL.  K = 8 walks each XCD's eighth as ONE window; more
+// streams spread the concurrent HBM reads over the address space (a streaming
+// read of contiguous per-workgroup chunks runs at 7.0 TB/s against 5.3-6.3
+// for one narrow window, tools/probe/read_probe.hip).  LSSP_AMD_SPMV_STREAMS.
+static int spmv_streams()
+{
+    static const int k = [] {
+        const char *e = getenv("LSSP_AMD_SPMV_STREAMS");
+        const int v = e ? atoi(e) : 8;
+        return v >= 8 && v % 8 == 0 && v <= 4096 ? v : 8;
+    }();
+    return k;
+}
+
 template <int EPI, bool CMP>
 static void spmv_dispatch(const SpmvArgs &a, int nred, long nblocks, hipStream_t s, long nnz_pad)
 {
-    const long g = (nblocks + 7) / 8 * 8;  // a multiple of 8: whole XCD shares
+    const long g = (nblocks + a.streams - 1) / a.streams * a.streams;  // a multiple of K: whole stream shares
     if (nred == 0) k_spmv3<EPI, 0, CMP><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
     else if (nred == 1) k_spmv3<EPI, 1, CMP><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
     else k_spmv3<EPI, 2, CMP><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
@@ -598,7 +617,7 @@ int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, c
     const long nb = ce - cb;
     if (nb == 0) return LSSP_AMD_OK;
     SpmvArgs a{A->nrows, A->Ap, A->Aj, A->Ax, x, y, z, alpha, beta, w0, w1, c->d_part, c->part_cap,
-               A->Ad, A->d_off, A->ndiag, c->guard, cb};
+               A->Ad, A->d_off, A->ndiag, c->guard, cb, spmv_streams()};
     if (A->d_win && nb == nall) {
         switch (epi) {
         case EPI_MXY: spmv_sell_dispatch<EPI_MXY>(a, A, nred, c->stream); break;
@@ -662,6 +681,7 @@ struct EwArgs {
     long pcap;
     long nchunks;
     const double *guard;
+    int chunked;  // 1: workgroup b takes chunks [b per, (b+1) per) in order; 0: grid-strided (ew_chunked)
 };
 
 template <int NRED>
@@ -669,7 +689,11 @@ __global__ __launch_bounds__(256) void k_ew(EwArgs g)
 {
     __shared__ double lds[MAX_SLOTS][4];
     if (g.guard && *g.guard != 0.0) return;
-    for (long c = blockIdx.x; c < g.nchunks; c += gridDim.x) {
+    const long per = g.chunked ? (g.nchunks + gridDim.x - 1) / gridDim.x : 1;
+    const long cbeg = g.chunked ? blockIdx.x * per : blockIdx.x;
+    const long cend = g.chunked ? min(cbeg + per, g.nchunks) : g.nchunks;
+    const long cstep = g.chunked ? 1 : gridDim.x;
+    for (long c = cbeg; c < cend; c += cstep) {
         const long i = c * 256 + threadIdx.x;
         const bool in = i < g.n;
         // the reduction operands: an output of this pass is read as the value just
@@ -868,10 +892,14 @@ int launch_ew(lssp_amd_ctx *c, const Ew &e)
     if (e.n <= 0) return LSSP_AMD_OK;
     long C = num_chunks(e.n);
     LSSP_TRY(ensure_part(c, C));
+    static const int chunked = [] {  // LSSP_AMD_EW_CHUNKED (A/B)
+        const char *v = getenv("LSSP_AMD_EW_CHUNKED");
+        return v ? atoi(v) : 0;
+    }();
     EwArgs g{e.kind, e.n, e.a, e.b, e.x, e.y, e.u, e.v, e.out0, e.out1, e.scal,
              e.r0a, e.r0b, e.r1a, e.r1b, e.r2a, e.r2b, e.r3a, e.r3b, e.vbase, e.k, e.sidx,
              c->d_part + (long)e.pslot * c->part_cap, c->part_cap, C,
-             c->guard};
+             c->guard, chunked};
     // one chunk per block up to a cap; the cap keeps >= 8 blocks per CU resident
     long grid = C < 8L * c->num_cus * 4 ? C : 8L * c->num_cus * 4;
     if (e.nred == 0) k_ew<0><<<grid, 256, 0, c->stream>>>(g);

@@ -1089,6 +1089,32 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
 // (LDS-DMA sc1 reads of the two levels' hand-off inputs DH steps ahead), SW
 // storers (OUT 2: the U sweep's rhs stream; OUT 1: natural-order x in 8-row
 // runs of a line).  The rhs always comes from a stream (k_line_rhs gathers it).
+// The U sweep's division x / d (solver-tri.cxx:44) in 3 dependent operations
+// instead of IEEE division's ~10 (the divisor is a coefficient, known a step
+// ahead): with y = RN(1 / d) formed early, q0 = RN(x y), e = x - q0 d (exact,
+// FMA) and q = RN(q0 + e y) IS the correctly rounded quotient when nothing
+// under- or overflows (Markstein's theorem) -- guaranteed here by |x|, |d| in
+// [2^-400, 2^400] (line2_div_range; zeros, denormals, infinities and NaNs
+// fail it); a row outside takes the IEEE division.  Checked bit for bit
+// against IEEE division on 4e8 random operand pairs with exponents over that
+// whole range and all-ones / near-power-of-two significands
+// (tools/probe/div_check.c), and by every U-sweep parity test.
+// -DLINE2_DIV=0 selects the plain division.
+#ifndef LINE2_DIV
+#define LINE2_DIV 1
+#endif
+__device__ __forceinline__ bool line2_div_range(double x)
+{
+    const unsigned e = ((unsigned)(__double_as_longlong(x) >> 52)) & 0x7FF;
+    return e - (1023u - 400u) <= 800u;
+}
+__device__ __forceinline__ double line2_div(double x, double d, double y)
+{
+    const double q0 = x * y;
+    const double e = __builtin_fma(-q0, d, x);
+    return __builtin_fma(e, y, q0);
+}
+
 namespace l2 {
 constexpr int P = 8, NJ = 16, CW = 2, LV = 2, ROWS = P * NJ;
 constexpr uint64_t GS = 0x0001000100010001ull;  // line 0 of each 16-lane group
@@ -1101,7 +1127,9 @@ struct Slot {
     static constexpr int RHS = NPC * 1024;
     static constexpr int KFIN = RHS + NRP * 1024;    // double[LV][NJ]
     static constexpr int JFIN = KFIN + LV * NJ * 8;  // double[LV][P]
-    static constexpr int BYTES = JFIN + LV * P * 8;
+    static constexpr bool RCP_ON = NA == 4 && LINE2_DIV;
+    static constexpr int RCP = JFIN + LV * P * 8;    // double[LV * ROWS]: 1 / diag of each row (the loaders')
+    static constexpr int BYTES = RCP + (RCP_ON ? LV * ROWS * 8 : 0);
     static_assert(BYTES % 16 == 0, "slot alignment");
 };
 // levels of results kept in LDS: the storers' source (OUT 1 writes 8-level
@@ -1192,6 +1220,8 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
             const int sg = wave;  // sigma of the wave's planes
             struct In {
                 double ck[LV], cj[LV], ci[LV], dg[LV], rh[LV], jv[LV];
+                double rc[LV];  // LINE2_DIV: 1 / diag, correctly rounded (formed one step early)
+                bool dok[LV];   // ... diag in the safe range of line2_div
             };
             // the step's inputs, read from LDS one step ahead (their slot was
             // completed before the barrier that ended the previous step)
@@ -1204,10 +1234,27 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
                     in.ck[v] = b[0];
                     in.cj[v] = b[1];
                     in.ci[v] = b[2];
-                    if constexpr (NA == 4) in.dg[v] = b[3];
+                    if constexpr (NA == 4) {
+                        in.dg[v] = b[3];
+                        if constexpr (SL::RCP_ON) {
+                            in.rc[v] = reinterpret_cast<const double *>(slot + SL::RCP)[r];
+                            in.dok[v] = line2_div_range(in.dg[v]);
+                        }
+                    }
                     in.rh[v] = reinterpret_cast<const double *>(slot + SL::RHS)[r];
                     in.jv[v] = reinterpret_cast<const double *>(slot + SL::JFIN)[v * P + pw];
                 }
+            };
+            // x / diag of level v on the rows of mask h (bitwise IEEE division)
+            auto divide = [&](double x, const In &in, int v, uint64_t h) {
+#if LINE2_DIV
+                const double q = line2_div(x, in.dg[v], in.rc[v]);
+                const uint64_t bad = __ballot(!(in.dok[v] && line2_div_range(x))) & h;
+                return bad ? ((bad >> lane) & 1 ? x / in.dg[v] : q) : q;
+#else
+                (void)h;
+                return x / in.dg[v];
+#endif
             };
             In A, B;
             double xp = 0.0;  // the lane's value of the previous level
@@ -1285,20 +1332,20 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
                     double v = cur.rh[0] - cur.ck[0] * xk;
                     v = v - cur.cj[0] * xj;
                     v = v - cur.ci[0] * xp;
-                    if constexpr (NA == 4) v = v / cur.dg[0];
+                    if constexpr (NA == 4) v = divide(v, cur, 0, h0);
                     const double x0 = sel_lanes(h0, v, xp);
+                    publish(2 * s, h0, x0);  // its store issues under level 2s+1's arithmetic
+                    res[((2 * s) & (RSL - 1)) * ROWS + pw * NJ + ll] = x0;
                     // level 2s + 1
                     xk = sel_lanes(G0M, kx1, up16(x0));
                     xj = dpp_shr1g<4>(x0, cur.jv[1]);
                     v = cur.rh[1] - cur.ck[1] * xk;
                     v = v - cur.cj[1] * xj;
                     v = v - cur.ci[1] * x0;
-                    if constexpr (NA == 4) v = v / cur.dg[1];
+                    if constexpr (NA == 4) v = divide(v, cur, 1, h1);
                     const double x1 = sel_lanes(h1, v, x0);
                     if (trs && wave == 0) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
-                    publish(2 * s, h0, x0);
                     publish(2 * s + 1, h1, x1);
-                    res[((2 * s) & (RSL - 1)) * ROWS + pw * NJ + ll] = x0;
                     res[((2 * s + 1) & (RSL - 1)) * ROWS + pw * NJ + ll] = x1;
                     xp = x1;
                     xs = up16(x1);  // the next step's first k-operand, off its critical path
@@ -1345,6 +1392,21 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
                 const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
                 // steps s+LA+1 .. s+D were issued after step s+LA's
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - LA) * KPER) : "memory");
+                if constexpr (SL::RCP_ON) {
+                    // 1 / diag of the rows in this wave's own landed pieces of step
+                    // s+LA's block (a 1 KB piece holds 32 rows of {c_k, c_j, c_i, d}):
+                    // off the compute waves' dependent chain (line2_div)
+                    const char *sl = ring + ((s + LA) % R + R) % R * SL::BYTES;
+#pragma unroll
+                    for (int k = 0; k < KPER; k++) {
+                        const int m = w + k * NL;
+                        if (m < SL::NPC && (lane >> 5) == (k & 1)) {
+                            const int row = 32 * m + (lane & 31);
+                            const double dg = reinterpret_cast<const double *>(sl + SL::COEF)[row * 4 + 3];
+                            reinterpret_cast<double *>(const_cast<char *>(sl) + SL::RCP)[row] = 1.0 / dg;
+                        }
+                    }
+                }
                 if (trs && w == 0 && s >= 0 && s < TS) {
                     ts[8 * s + 4] = w0 - i0;
                     ts[8 * s + 3] = __builtin_amdgcn_s_memtime() - w0;
