@@ -578,7 +578,10 @@ static void spmv_sell_dispatch(const SpmvArgs &a, const lssp_amd_mat *A, int nre
 // that XCD's L2 / the MALL.  K = 8 walks each XCD's eighth as ONE window; more
 // streams spread the concurrent HBM reads over the address space (a streaming
 // read of contiguous per-workgroup chunks runs at 7.0 TB/s against 5.3-6.3
-// for one narrow window, tools/probe/read_probe.hip).  LSSP_AMD_SPMV_STREAMS.
+// for one narrow window, tools/probe/read_probe.hip) -- but for this product
+// K = 8 measured fastest: 143.7 us at 216^3 against 148-159 us for K = 16 ..
+// 256 (profiles/r04/r04c_stream_order.txt; the x re-use out of L2 is worth
+// more).  LSSP_AMD_SPMV_STREAMS overrides it (A/B runs).
 static int spmv_streams()
 {
     static const int k = [] {
@@ -681,7 +684,6 @@ struct EwArgs {
     long pcap;
     long nchunks;
     const double *guard;
-    int chunked;  // 1: workgroup b takes chunks [b per, (b+1) per) in order; 0: grid-strided (ew_chunked)
 };
 
 template <int NRED>
@@ -689,11 +691,9 @@ __global__ __launch_bounds__(256) void k_ew(EwArgs g)
 {
     __shared__ double lds[MAX_SLOTS][4];
     if (g.guard && *g.guard != 0.0) return;
-    const long per = g.chunked ? (g.nchunks + gridDim.x - 1) / gridDim.x : 1;
-    const long cbeg = g.chunked ? blockIdx.x * per : blockIdx.x;
-    const long cend = g.chunked ? min(cbeg + per, g.nchunks) : g.nchunks;
-    const long cstep = g.chunked ? 1 : gridDim.x;
-    for (long c = cbeg; c < cend; c += cstep) {
+    // grid-strided chunks (a contiguous range of chunks per workgroup measured
+    // the same or slower: profiles/r04/r04c_stream_order.txt)
+    for (long c = blockIdx.x; c < g.nchunks; c += gridDim.x) {
         const long i = c * 256 + threadIdx.x;
         const bool in = i < g.n;
         // the reduction operands: an output of this pass is read as the value just
@@ -892,14 +892,10 @@ int launch_ew(lssp_amd_ctx *c, const Ew &e)
     if (e.n <= 0) return LSSP_AMD_OK;
     long C = num_chunks(e.n);
     LSSP_TRY(ensure_part(c, C));
-    static const int chunked = [] {  // LSSP_AMD_EW_CHUNKED (A/B)
-        const char *v = getenv("LSSP_AMD_EW_CHUNKED");
-        return v ? atoi(v) : 0;
-    }();
     EwArgs g{e.kind, e.n, e.a, e.b, e.x, e.y, e.u, e.v, e.out0, e.out1, e.scal,
              e.r0a, e.r0b, e.r1a, e.r1b, e.r2a, e.r2b, e.r3a, e.r3b, e.vbase, e.k, e.sidx,
              c->d_part + (long)e.pslot * c->part_cap, c->part_cap, C,
-             c->guard, chunked};
+             c->guard};
     // one chunk per block up to a cap; the cap keeps >= 8 blocks per CU resident
     long grid = C < 8L * c->num_cus * 4 ? C : 8L * c->num_cus * 4;
     if (e.nred == 0) k_ew<0><<<grid, 256, 0, c->stream>>>(g);

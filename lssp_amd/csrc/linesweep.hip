@@ -1248,9 +1248,13 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
             // x / diag of level v on the rows of mask h (bitwise IEEE division)
             auto divide = [&](double x, const In &in, int v, uint64_t h) {
 #if LINE2_DIV
-                const double q = line2_div(x, in.dg[v], in.rc[v]);
+                double q = line2_div(x, in.dg[v], in.rc[v]);
                 const uint64_t bad = __ballot(!(in.dok[v] && line2_div_range(x))) & h;
-                return bad ? ((bad >> lane) & 1 ? x / in.dg[v] : q) : q;
+                if (__builtin_expect(bad != 0, 0)) {  // uniform branch, never taken on sane data
+                    asm volatile("" ::: "memory");    // (keeps the division out of the common path)
+                    if ((bad >> lane) & 1) q = x / in.dg[v];
+                }
+                return q;
 #else
                 (void)h;
                 return x / in.dg[v];

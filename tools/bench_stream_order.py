@@ -59,7 +59,7 @@ d.close()
 
 def main():
     N = int(sys.argv[1]) if len(sys.argv) > 1 else 216
-    configs = [(8, 0), (16, 0), (32, 0), (64, 0), (128, 0), (256, 0), (8, 1), (64, 1), (8, 0)]
+    configs = [(8, 0), (16, 0), (32, 0), (64, 0), (128, 0), (256, 0), (8, 0)]
     for K, C in configs:
         env = dict(os.environ, LSSP_AMD_SPMV_STREAMS=str(K), LSSP_AMD_EW_CHUNKED=str(C))
         code = CHILD.format(root=ROOT, N=N, K=K, C=C)
