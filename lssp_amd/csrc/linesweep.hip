@@ -1099,9 +1099,12 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
 // against IEEE division on 4e8 random operand pairs with exponents over that
 // whole range and all-ones / near-power-of-two significands
 // (tools/probe/div_check.c), and by every U-sweep parity test.
-// -DLINE2_DIV=0 selects the plain division.
+// Measured SLOWER and off by default (-DLINE2_DIV=1 enables it): the loaders'
+// reciprocals cost the compute waves more than the shorter chain saves --
+// 216^3 U sweep 394 us against 355 us with the IEEE division
+// (profiles/r04/r04d_line2_div_lead_variants.txt).
 #ifndef LINE2_DIV
-#define LINE2_DIV 1
+#define LINE2_DIV 0
 #endif
 __device__ __forceinline__ bool line2_div_range(double x)
 {

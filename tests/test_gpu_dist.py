@@ -240,3 +240,22 @@ def test_global_ilu_on_p_ranks(world, N, mode):
     assert np.array_equal(x, o.x)
     if mode == O.SERIAL and N == 32:  # the reference takes 21 iterations at 32^3
         assert nits == 21
+
+
+def test_bench_gpus_2_launches_two_ranks():
+    """`python bench.py --gpus 2` run plainly starts two ranks itself (here on
+    one device over the host transport, --share-gpu) and reports n_gpus 2 and a
+    2-rank communicator -- the driver's multi-GPU scaling run cannot silently
+    measure one rank."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--share-gpu", "--grid", "32",
+                        "--steps", "5", "--warmup", "1", "--no-cpu", "--spmv-reps", "3", "--apply-reps", "2"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["comm_ranks"] == 2 and line["steps"] == 5
