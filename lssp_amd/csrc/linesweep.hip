@@ -1141,8 +1141,50 @@ template <int OUT>
 constexpr int rsl() { return OUT == 1 ? 16 : 4; }
 template <int NA, int OUT, int D>
 constexpr int lds_bytes() { return (D + 1) * Slot<NA>::BYTES + rsl<OUT>() * ROWS * 8 + 16 + 512; }
-constexpr int waves(int NL, int SW) { return CW + NL + 1 + SW; }
+// LINE2_SPOLL: the hand-off inputs are polled with scalar (SMEM, glc) loads
+// by two poller waves (k and j) instead of one wave's LDS-DMA vector loads,
+// off the CU's vector memory queue that the coefficient DMAs fill
+#ifndef LINE2_SPOLL
+#define LINE2_SPOLL 0
+#endif
+constexpr int NPW = LINE2_SPOLL ? 2 : 1;  // poller waves
+constexpr int waves(int NL, int SW) { return CW + NL + NPW + SW; }
 }  // namespace l2
+
+typedef unsigned int line_u32x16 __attribute__((ext_vector_type(16)));
+// N (1..4) x 64 bytes from a uniform address, bypassing the scalar cache (glc),
+// then lane i of lo / hi gets dwords 2i / 2i+1 (doubles 0 .. 8N-1 on lanes 0 .. 8N-1)
+template <int N>
+__device__ __forceinline__ double spoll_load(const double *p)
+{
+    line_u32x16 a0, a1, a2, a3;
+    if constexpr (N == 2) {
+        asm volatile("s_load_dwordx16 %0, %2, 0x0 glc\n\ts_load_dwordx16 %1, %2, 0x40 glc\n\ts_waitcnt lgkmcnt(0)"
+                     : "=s"(a0), "=s"(a1) : "s"(p) : "memory");
+    } else {
+        static_assert(N == 4, "N");
+        asm volatile("s_load_dwordx16 %0, %4, 0x0 glc\n\ts_load_dwordx16 %1, %4, 0x40 glc\n\t"
+                     "s_load_dwordx16 %2, %4, 0x80 glc\n\ts_load_dwordx16 %3, %4, 0xc0 glc\n\ts_waitcnt lgkmcnt(0)"
+                     : "=s"(a0), "=s"(a1), "=s"(a2), "=s"(a3) : "s"(p) : "memory");
+    }
+    unsigned lo = 0, hi = 0;
+    // lane selects as inline constants (two SGPR operands break the constant-bus limit)
+#define SPOLL_WL(A, I, L)                                                           \
+    asm("v_writelane_b32 %0, %1, " #L : "+v"(lo) : "s"(A[2 * (I)]));             \
+    asm("v_writelane_b32 %0, %1, " #L : "+v"(hi) : "s"(A[2 * (I) + 1]));
+    SPOLL_WL(a0, 0, 0) SPOLL_WL(a0, 1, 1) SPOLL_WL(a0, 2, 2) SPOLL_WL(a0, 3, 3)
+    SPOLL_WL(a0, 4, 4) SPOLL_WL(a0, 5, 5) SPOLL_WL(a0, 6, 6) SPOLL_WL(a0, 7, 7)
+    SPOLL_WL(a1, 0, 8) SPOLL_WL(a1, 1, 9) SPOLL_WL(a1, 2, 10) SPOLL_WL(a1, 3, 11)
+    SPOLL_WL(a1, 4, 12) SPOLL_WL(a1, 5, 13) SPOLL_WL(a1, 6, 14) SPOLL_WL(a1, 7, 15)
+    if constexpr (N == 4) {
+        SPOLL_WL(a2, 0, 16) SPOLL_WL(a2, 1, 17) SPOLL_WL(a2, 2, 18) SPOLL_WL(a2, 3, 19)
+        SPOLL_WL(a2, 4, 20) SPOLL_WL(a2, 5, 21) SPOLL_WL(a2, 6, 22) SPOLL_WL(a2, 7, 23)
+        SPOLL_WL(a3, 0, 24) SPOLL_WL(a3, 1, 25) SPOLL_WL(a3, 2, 26) SPOLL_WL(a3, 3, 27)
+        SPOLL_WL(a3, 4, 28) SPOLL_WL(a3, 5, 29) SPOLL_WL(a3, 6, 30) SPOLL_WL(a3, 7, 31)
+    }
+#undef SPOLL_WL
+    return __longlong_as_double(((long long)hi << 32) | lo);
+}
 
 // lane l <- lane l - 16 (rows R0..R3 of the wave -> [R0, R0, R1, R2]; row 0 is
 // not used): v_permlane16_swap gives [R0, R0, R2, R2] / [R1, R1, R3, R3],
@@ -1421,6 +1463,53 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
                 line_barrier();
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (LINE2_SPOLL && wave < CW + NL + NPW) {
+            // ---------------- scalar pollers (LINE2_SPOLL) ----------------
+            // wave CW+NL: at step s the k-inputs of step s+1 (2 levels x NJ lines =
+            // 256 B), wave CW+NL+1: the j-inputs of step s+2 (2 x P planes = 128 B),
+            // re-read until every existing entry is published, into the slot.
+            const bool isk = wave == CW + NL;
+            const bool has = isk ? kin : jin;
+            const int cnt = isk ? LV * NJ : LV * P;
+            const double *src = isk ? a.hk + (long)max(d.tk, 0) * a.hk_stride : a.hj + (long)max(d.tj, 0) * a.hj_stride;
+            const int qmax = (int)(a.hk_stride / (NJ * LV)) - 1;  // steps
+            const int kl = lane & (NJ - 1), kv = lane >> 4, jp = lane & (P - 1), jv = lane >> 3;
+            const unsigned foff = isk ? SL::KFIN : SL::JFIN;
+            if (!has) {
+                for (int q = 0; q < R; q++)
+                    if (lane < cnt) reinterpret_cast<double *>(ring + q * SL::BYTES + foff)[lane] = 0.0;
+            }
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            unsigned polls = 0;
+            for (int s = S0; s <= TS; s++) {
+                const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
+                const int q = isk ? s + 1 : s + 2;  // step
+                if (has && q >= 0 && q < TS) {
+                    const double *p = src + (long)min(q, qmax) * cnt;
+                    const int lv = LV * q + (isk ? kv : jv);
+                    const bool val = lane < cnt && lv < T &&
+                                     (isk ? kl < nj && (unsigned)(lv - kl) < (unsigned)nx
+                                          : jp < np && (unsigned)(lv - jp - sig(jp)) < (unsigned)nx);
+                    double x;
+                    for (;;) {
+                        x = isk ? spoll_load<4>(p) : spoll_load<2>(p);
+                        if (!__any(val && (uint64_t)__double_as_longlong(x) == TRI_SENTINEL)) break;
+                        polls++;
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s
+                            atomicOr(a.err, 8);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    if (lane < cnt) reinterpret_cast<double *>(ring + (q % R) * SL::BYTES + foff)[lane] = x;
+                }
+                if (trs && isk && s >= 0 && s < TS) ts[8 * s + 2] = __builtin_amdgcn_s_memtime() - w0;
+                line_barrier();
+            }
+            if (TRACE) {
+                for (int o = 32; o >= 1; o >>= 1) polls += __shfl_xor(polls, o);
+                if (lane == 0 && isk) a.trace[8 * t + 3] = polls / 64;
+            }
         } else if (wave == CW + NL) {
             // ---------------- poller ----------------
             // At step s: LDS-DMA sc1 reads of step s+DH's k-inputs (two levels x NJ
@@ -1505,7 +1594,7 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
         } else {
             // ---------------- storers: results, re-arms ----------------
             // Storer 0 re-arms the consumed j-inputs, storer SW-1 the k-inputs.
-            const int w = wave - (CW + NL + 1);
+            const int w = wave - (CW + NL + NPW);
             const int kl = lane & (NJ - 1), kv = lane >> 4, jp = lane & (P - 1), jv = lane >> 3;
             uint64_t *hki = reinterpret_cast<uint64_t *>(a.hk + (long)max(d.tk, 0) * a.hk_stride) + kl;
             uint64_t *hji = reinterpret_cast<uint64_t *>(a.hj + (long)max(d.tj, 0) * a.hj_stride) + jp;
