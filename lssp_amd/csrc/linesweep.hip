@@ -1130,7 +1130,7 @@ struct Slot {
     static constexpr int RHS = NPC * 1024;
     static constexpr int KFIN = RHS + NRP * 1024;    // double[LV][NJ]
     static constexpr int JFIN = KFIN + LV * NJ * 8;  // double[LV][P]
-    static constexpr bool RCP_ON = NA == 4 && LINE2_DIV;
+    static constexpr bool RCP_ON = NA == 4 && LINE2_DIV == 1;  // the loaders form 1/d into the slot
     static constexpr int RCP = JFIN + LV * P * 8;    // double[LV * ROWS]: 1 / diag of each row (the loaders')
     static constexpr int BYTES = RCP + (RCP_ON ? LV * ROWS * 8 : 0);
     static_assert(BYTES % 16 == 0, "slot alignment");
@@ -1381,6 +1381,10 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
                     double v = cur.rh[0] - cur.ck[0] * xk;
                     v = v - cur.cj[0] * xj;
                     v = v - cur.ci[0] * xp;
+#if LINE2_DIV == 2
+                    // the next step's reciprocals, interleaved into this step's chains
+                    if constexpr (NA == 4) nxt.rc[0] = 1.0 / nxt.dg[0], nxt.dok[0] = line2_div_range(nxt.dg[0]);
+#endif
                     if constexpr (NA == 4) v = divide(v, cur, 0, h0);
                     const double x0 = sel_lanes(h0, v, xp);
                     publish(2 * s, h0, x0);  // its store issues under level 2s+1's arithmetic
@@ -1391,6 +1395,9 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
                     v = cur.rh[1] - cur.ck[1] * xk;
                     v = v - cur.cj[1] * xj;
                     v = v - cur.ci[1] * x0;
+#if LINE2_DIV == 2
+                    if constexpr (NA == 4) nxt.rc[1] = 1.0 / nxt.dg[1], nxt.dok[1] = line2_div_range(nxt.dg[1]);
+#endif
                     if constexpr (NA == 4) v = divide(v, cur, 1, h1);
                     const double x1 = sel_lanes(h1, v, x0);
                     if (trs && wave == 0) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
@@ -1399,6 +1406,12 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
                     xp = x1;
                     xs = up16(x1);  // the next step's first k-operand, off its critical path
                 }
+#if LINE2_DIV == 2
+                else if constexpr (NA == 4) {
+#pragma unroll
+                    for (int v = 0; v < LV; v++) nxt.rc[v] = 1.0 / nxt.dg[v], nxt.dok[v] = line2_div_range(nxt.dg[v]);
+                }
+#endif
                 so = sn;
                 if (trs && s >= 0 && s < TS) ts[8 * s + (wave == 0 ? 1 : 7)] = __builtin_amdgcn_s_memtime();
                 line_barrier();
