@@ -125,9 +125,9 @@ static bool detect_grid(int n, const std::vector<int> &Lp, const std::vector<int
     return true;
 }
 
-// k_line2's plane skew: the planes of its second compute wave (p >= P/2) run
-// one level later, so the k-input of plane P/2 is one whole step old
-static inline int line_sigma(int LV, int P, int p) { return LV == 2 && p >= P / 2 ? 1 : 0; }
+// k_line2's plane skew: compute wave w owns planes 4w .. 4w+3 and runs w
+// levels later, so the k-input of a wave's first plane is one whole step old
+static inline int line_sigma(int LV, int P, int p) { return LV == 2 ? p / 4 : 0; }
 
 // rows of a tile (nj lines, np planes) valid at level s, plane p: lanes [lo, hi]
 // (row i = s - l - p - sigma(p))
@@ -298,7 +298,9 @@ static void line_plan(const LineGeom &g, int &P, int &NJ, int &LV)
         LV = 1;
         return;
     }
-    P = 8;
+    // LSSP_AMD_LINE2_P=16: 16-plane tiles (4 compute waves, 256 rows per level)
+    const char *ep = getenv("LSSP_AMD_LINE2_P");
+    P = ep && atoi(ep) == 16 ? 16 : 8;
     NJ = 16;
     LV = 2;
 }
@@ -1119,11 +1121,12 @@ __device__ __forceinline__ double line2_div(double x, double d, double y)
 }
 
 namespace l2 {
-constexpr int P = 8, NJ = 16, CW = 2, LV = 2, ROWS = P * NJ;
+constexpr int NJ = 16, LV = 2;  // lines per tile, levels per step; P (8 or 16) planes per tile: 2 or 4 compute waves
 constexpr uint64_t GS = 0x0001000100010001ull;  // line 0 of each 16-lane group
 constexpr uint64_t G0M = 0xFFFFull;             // group 0 (the wave's first plane)
-template <int NA>
+template <int NA, int P>
 struct Slot {
+    static constexpr int ROWS = P * NJ;
     static constexpr int NPC = (LV * ROWS * NA * 8 + 1023) / 1024;  // 1 KB DMA pieces of the two coefficient blocks
     static constexpr int NRP = (LV * ROWS * 8 + 1023) / 1024;       // ... of the two rhs blocks
     static constexpr int COEF = 0;
@@ -1139,8 +1142,8 @@ struct Slot {
 // blocks as runs, so it keeps two) and wave 1's k-input
 template <int OUT>
 constexpr int rsl() { return OUT == 1 ? 16 : 4; }
-template <int NA, int OUT, int D>
-constexpr int lds_bytes() { return (D + 1) * Slot<NA>::BYTES + rsl<OUT>() * ROWS * 8 + 16 + 512; }
+template <int NA, int OUT, int D, int P>
+constexpr int lds_bytes() { return (D + 1) * Slot<NA, P>::BYTES + rsl<OUT>() * P * NJ * 8 + 16 + 512; }
 // LINE2_SPOLL: the hand-off inputs are polled with scalar (SMEM, glc) loads
 // by two poller waves (k and j) instead of one wave's LDS-DMA vector loads,
 // off the CU's vector memory queue that the coefficient DMAs fill
@@ -1148,7 +1151,7 @@ constexpr int lds_bytes() { return (D + 1) * Slot<NA>::BYTES + rsl<OUT>() * ROWS
 #define LINE2_SPOLL 0
 #endif
 constexpr int NPW = LINE2_SPOLL ? 2 : 1;  // poller waves
-constexpr int waves(int NL, int SW) { return CW + NL + NPW + SW; }
+constexpr int waves(int P, int NL, int SW) { return P / 4 + NL + NPW + SW; }
 }  // namespace l2
 
 typedef unsigned int line_u32x16 __attribute__((ext_vector_type(16)));
@@ -1211,11 +1214,12 @@ __device__ __forceinline__ double up16(double v)
     return __longlong_as_double(((long long)hi << 32) | lo);
 }
 
-template <int NA, int OUT, int NL, int D, int DH, int SW, bool TRACE>
-__global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
+template <int P, int NA, int OUT, int NL, int D, int DH, int SW, bool TRACE>
+__global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
 {
     using namespace l2;
-    using SL = Slot<NA>;
+    using SL = Slot<NA, P>;
+    constexpr int CW = P / 4, ROWS = P * NJ;
     constexpr int LA = 2;  // the loaders complete step s+LA's slot during step s
     constexpr int R = D + 1;
     constexpr int RSL = rsl<OUT>();
@@ -1255,7 +1259,7 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
             const long r = ((long)(d.k0 + p) * a.ny + (d.j0 + l)) * nx;
             return a.mirror ? a.n - 1 - r : r;
         };
-        auto sig = [](int p) { return p >= P / 2 ? 1 : 0; };
+        auto sig = [](int p) { return p >> 2; };
         unsigned long long *ts = TRACE ? a.trace + 8 * (long)a.ntiles : nullptr;
         const bool trs = TRACE && t == a.ttile && lane == 0;
 
@@ -1366,8 +1370,8 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
                     kx0 = reinterpret_cast<const double *>(ring + so + SL::KFIN)[ll];
                     kx1 = reinterpret_cast<const double *>(ring + so + SL::KFIN)[NJ + ll];
                 } else {
-                    kx0 = res[((2 * s - 2) & (RSL - 1)) * ROWS + 3 * NJ + ll];
-                    kx1 = res[((2 * s - 1) & (RSL - 1)) * ROWS + 3 * NJ + ll];
+                    kx0 = res[((2 * s - 2) & (RSL - 1)) * ROWS + (4 * wave - 1) * NJ + ll];
+                    kx1 = res[((2 * s - 1) & (RSL - 1)) * ROWS + (4 * wave - 1) * NJ + ll];
                 }
                 asm volatile("" ::: "memory");
                 load(sn, nxt);
@@ -1486,7 +1490,7 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
             const int cnt = isk ? LV * NJ : LV * P;
             const double *src = isk ? a.hk + (long)max(d.tk, 0) * a.hk_stride : a.hj + (long)max(d.tj, 0) * a.hj_stride;
             const int qmax = (int)(a.hk_stride / (NJ * LV)) - 1;  // steps
-            const int kl = lane & (NJ - 1), kv = lane >> 4, jp = lane & (P - 1), jv = lane >> 3;
+            const int kl = lane & (NJ - 1), kv = lane >> 4, jp = lane & (P - 1), jv = lane / P;
             const unsigned foff = isk ? SL::KFIN : SL::JFIN;
             if (!has) {
                 for (int q = 0; q < R; q++)
@@ -1505,7 +1509,7 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
                                           : jp < np && (unsigned)(lv - jp - sig(jp)) < (unsigned)nx);
                     double x;
                     for (;;) {
-                        x = isk ? spoll_load<4>(p) : spoll_load<2>(p);
+                        x = (isk || P == 16) ? spoll_load<4>(p) : spoll_load<2>(p);
                         if (!__any(val && (uint64_t)__double_as_longlong(x) == TRI_SENTINEL)) break;
                         polls++;
                         if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s
@@ -1535,7 +1539,7 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
             const double *hj = a.hj + (long)max(d.tj, 0) * a.hj_stride;
             const int qmax = (int)(a.hk_stride / (NJ * LV)) - 1;  // steps
             const int kl = lane & (NJ - 1), kv = lane >> 4;      // k check: lanes 0..31 = (level, line)
-            const int jp = lane & (P - 1), jv = lane >> 3;       // j check: lanes 0..15 = (level, plane)
+            const int jp = lane & (P - 1), jv = lane / P;        // j check: lanes 0..2P-1 = (level, plane)
             auto kval = [&](int q) {  // q: level
                 return lane < LV * NJ && q < T && kl < nj && (unsigned)(q - kl) < (unsigned)nx;
             };
@@ -1608,7 +1612,7 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
             // ---------------- storers: results, re-arms ----------------
             // Storer 0 re-arms the consumed j-inputs, storer SW-1 the k-inputs.
             const int w = wave - (CW + NL + NPW);
-            const int kl = lane & (NJ - 1), kv = lane >> 4, jp = lane & (P - 1), jv = lane >> 3;
+            const int kl = lane & (NJ - 1), kv = lane >> 4, jp = lane & (P - 1), jv = lane / P;
             uint64_t *hki = reinterpret_cast<uint64_t *>(a.hk + (long)max(d.tk, 0) * a.hk_stride) + kl;
             uint64_t *hji = reinterpret_cast<uint64_t *>(a.hj + (long)max(d.tj, 0) * a.hj_stride) + jp;
             const bool rk = w == SW - 1 && kin && lane < LV * NJ && kl < nj;
@@ -1616,7 +1620,7 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
             auto rearm = [&](int q) {  // step q's entries
                 const int vk = LV * q + kv, vj = LV * q + jv;
                 if (rk && vk < T && (unsigned)(vk - kl) < (unsigned)nx) hki[(long)vk * NJ] = TRI_SENTINEL;
-                if (rj && vj < T && (unsigned)(vj - jp - (jp >= P / 2 ? 1 : 0)) < (unsigned)nx)
+                if (rj && vj < T && (unsigned)(vj - jp - sig(jp)) < (unsigned)nx)
                     hji[(long)vj * P] = TRI_SENTINEL;
             };
             if constexpr (OUT == 1) {
@@ -1624,7 +1628,7 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
                 // steps 4B+4 .. 4B+7, a quarter per step: value k of the block is
                 // level 8B + (k & 7) of run k >> 3 = (plane, line), so 8 lanes store
                 // 8 consecutive rows of one line
-                static_assert(RSL == 16 && ROWS * 8 / 4 == 64 * 4, "runs");
+                static_assert(RSL == 16 && (2 * ROWS) % (64 * SW) == 0, "runs");
                 auto slice = [&](int s) {
                     const int B = (s >> 2) - 1, u = s & 3;
                     if (B < 0) return;
@@ -1634,7 +1638,7 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
                         const int k = u * (ROWS * 2) + (w * PER + it) * 64 + lane;
                         const int m = k & 7, r = k >> 3, p = r >> 4, l = r & (NJ - 1);
                         const int q = 8 * B + m;
-                        const int i = q - l - p - (p >= P / 2 ? 1 : 0);
+                        const int i = q - l - p - sig(p);
                         const double x = res[(q & (RSL - 1)) * ROWS + p * NJ + l];
                         if (!(a.diag & 1) && p < np && l < nj && (unsigned)i < (unsigned)nx)
                             a.out[a.mirror ? nb(p, l) - i : nb(p, l) + i] = x;
@@ -1661,7 +1665,7 @@ __global__ __launch_bounds__(64 * l2::waves(NL, SW)) void k_line2(LineArgs a)
 #pragma unroll
                 for (int u = 0; u < PS; u++) {
                     const int k = (w + u * SW) * 64 + lane;
-                    const int lv = k >> 7, p = (k >> 4) & (P - 1), l = k & (NJ - 1);
+                    const int lv = k / ROWS, p = (k >> 4) & (P - 1), l = k & (NJ - 1);
                     const int pp = min(p, np - 1), lq = min(l, nj - 1);
                     lvs[u] = lv;
                     roff[u] = (lv * P + p) * NJ + l;
@@ -1814,7 +1818,7 @@ __global__ __launch_bounds__(256) void k_line_rhs(const LineTile *__restrict__ t
 #pragma unroll
     for (int it = 0; it < NV; it++) {
         const int k = it * 256 + threadIdx.x, m = k & 7, l = (k >> 3) % NJ, p = (k >> 3) / NJ;
-        const int i = q0 + m - l - p - (SKEW && p >= P / 2 ? 1 : 0);
+        const int i = q0 + m - l - p - (SKEW ? p / 4 : 0);
         const bool ok = q0 + m < d.T && p < d.np && l < d.nj && (unsigned)i < (unsigned)nx;
         const long r = ((long)(d.k0 + p) * ny + (d.j0 + l)) * nx + i;
         v[it] = ok ? rhs[mirror ? n - 1 - r : r] : 0.0;
@@ -1823,7 +1827,7 @@ __global__ __launch_bounds__(256) void k_line_rhs(const LineTile *__restrict__ t
 #pragma unroll
     for (int it = 0; it < NV; it++) {
         const int k = it * 256 + threadIdx.x, m = k & 7, l = (k >> 3) % NJ, p = (k >> 3) / NJ;
-        const int i = q0 + m - l - p - (SKEW && p >= P / 2 ? 1 : 0);
+        const int i = q0 + m - l - p - (SKEW ? p / 4 : 0);
         if (q0 + m < d.T && p < d.np && l < d.nj && (unsigned)i < (unsigned)nx)
             out[d.cbase + (q0 + m) * SB + p * d.nj + l] = v[it];
     }
@@ -1835,9 +1839,9 @@ static int launch_line_gather(lssp_amd_ctx *c, const LineSweep &ls, int mirror, 
 {
     const int nq = (ls.tmax + LRHS_RUN - 1) / LRHS_RUN;
     const long grid = 8L * ((ls.ntiles + 7) / 8) * nq;
-    auto kr = ls.LV == 2 ? k_line_rhs<8, 16, true>
+    auto kr = ls.LV == 2 ? (ls.P == 16 ? k_line_rhs<16, 16, true> : k_line_rhs<8, 16, true>)
               : ls.P == 16 ? k_line_rhs<16, 16, false> : ls.P == 8 ? k_line_rhs<8, 32, false> : k_line_rhs<4, 64, false>;
-    if (ls.LV == 2 && (ls.P != 8 || ls.NJ != 16)) return LSSP_AMD_EUNSUPPORTED;
+    if (ls.LV == 2 && ((ls.P != 8 && ls.P != 16) || ls.NJ != 16)) return LSSP_AMD_EUNSUPPORTED;
     const long n = (long)ls.nx * ls.ny * ls.nz;
     kr<<<grid, 256, 0, c->stream>>>(ls.d_tiles, ls.ntiles, nq, ls.nx, ls.ny, n, mirror, rhs, stream, c->guard);
     LSSP_HIP(hipGetLastError());
@@ -1857,30 +1861,35 @@ static int launch_line_gather(lssp_amd_ctx *c, const LineSweep &ls, int mirror, 
 #ifndef LINE2_SW
 #define LINE2_SW 4
 #endif
-template <int NA, int OUT, bool TRACE>
+#ifndef LINE2_D16
+#define LINE2_D16 4  // loader lead of the 16-plane tiles (their slots are twice as large)
+#endif
+template <int P>
+constexpr int line2_d() { return P == 16 ? LINE2_D16 : LINE2_D; }
+template <int P, int NA, int OUT, bool TRACE>
 static int launch_line2_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)
 {
-    auto kern = k_line2<NA, OUT, LINE2_NL, LINE2_D, LINE2_DH, LINE2_SW, TRACE>;
+    auto kern = k_line2<P, NA, OUT, LINE2_NL, line2_d<P>(), LINE2_DH, LINE2_SW, TRACE>;
     static int attr = 0;
     if (lds > attr) {
         LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
         attr = lds;
     }
     const int grid = std::min(ls.ntiles, c->num_cus);
-    kern<<<grid, 64 * l2::waves(LINE2_NL, LINE2_SW), lds, c->stream>>>(g);
+    kern<<<grid, 64 * l2::waves(P, LINE2_NL, LINE2_SW), lds, c->stream>>>(g);
     ls.base += (unsigned long long)ls.ntiles + grid;
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;
 }
 
-template <int NA, int OUT>
+template <int P, int NA, int OUT>
 static int launch_line2_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a)
 {
-    constexpr int lds = l2::lds_bytes<NA, OUT, LINE2_D>();
+    constexpr int lds = l2::lds_bytes<NA, OUT, line2_d<P>(), P>();
     static_assert(lds <= 160 * 1024, "LDS");
     // diagnostics only: LSSP_AMD_LINE_TRACE=path[:tile] appends one JSON line per sweep
     static const char *trp = getenv("LSSP_AMD_LINE_TRACE");
-    if (!trp) return launch_line2_k<NA, OUT, false>(c, ls, a, lds);
+    if (!trp) return launch_line2_k<P, NA, OUT, false>(c, ls, a, lds);
     LineArgs g = a;
     const size_t tn = 8 * (size_t)ls.ntiles + 8 * (size_t)ls.tmax + 64;
     const char *colon = strrchr(trp, ':');
@@ -1888,7 +1897,7 @@ static int launch_line2_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &
     LSSP_HIP(hipMalloc(&g.trace, sizeof(unsigned long long) * tn));
     LSSP_HIP(hipMemsetAsync(g.trace, 0, sizeof(unsigned long long) * tn, c->stream));
     const int grid = std::min(ls.ntiles, c->num_cus);
-    LSSP_TRY((launch_line2_k<NA, OUT, true>(c, ls, g, lds)));
+    LSSP_TRY((launch_line2_k<P, NA, OUT, true>(c, ls, g, lds)));
     std::vector<unsigned long long> h(tn);
     LSSP_HIP(hipMemcpyAsync(h.data(), g.trace, sizeof(unsigned long long) * tn, hipMemcpyDeviceToHost, c->stream));
     LSSP_HIP(hipStreamSynchronize(c->stream));
@@ -1932,8 +1941,12 @@ static int launch_line2(lssp_amd_ctx *c, const LineILU &li, int which, const dou
         const char *dg = getenv("LSSP_AMD_LINE_DIAG");
         a.diag = dg ? atoi(dg) : 0;
     }
-    if (outk == 2) return ls.NA == 3 ? launch_line2_t<3, 2>(c, ls, a) : launch_line2_t<4, 2>(c, ls, a);
-    return ls.NA == 3 ? launch_line2_t<3, 1>(c, ls, a) : launch_line2_t<4, 1>(c, ls, a);
+    if (ls.P == 16) {
+        if (outk == 2) return ls.NA == 3 ? launch_line2_t<16, 3, 2>(c, ls, a) : launch_line2_t<16, 4, 2>(c, ls, a);
+        return ls.NA == 3 ? launch_line2_t<16, 3, 1>(c, ls, a) : launch_line2_t<16, 4, 1>(c, ls, a);
+    }
+    if (outk == 2) return ls.NA == 3 ? launch_line2_t<8, 3, 2>(c, ls, a) : launch_line2_t<8, 4, 2>(c, ls, a);
+    return ls.NA == 3 ? launch_line2_t<8, 3, 1>(c, ls, a) : launch_line2_t<8, 4, 1>(c, ls, a);
 }
 
 static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const double *rhs, bool u_in, double *out,

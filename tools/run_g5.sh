@@ -9,11 +9,17 @@ timeout -k 10 120 python -u tools/line_trace.py 216 150 2>&1 | grep -v amdgpu > 
 timeout -k 10 1100 python -u -m pytest tests -m gpu -q --timeout 600 --timeout-method thread > $O/pytest.log 2>&1
 tail -4 $O/pytest.log
 export LINE_DIAG_NOCHECK=1
-for v in default v_d5 v_d4 v_dh2_d5 v_nl3 v_nl3_d5 v_div2 default v_spoll v_spoll_d5; do
+for v in default v_d5 v_d4 v_dh2_d5 v_nl3 v_div2 default v_spoll v_spoll_d5; do
   if [ "$v" = default ]; then unset LSSP_AMD_LIB; else export LSSP_AMD_LIB=$PWD/build/$v.so; fi
   echo "== $v"; timeout -k 10 120 python tools/line_diag.py 216 0 || { echo "variant $v failed"; exit 1; }
 done 2>&1 | grep -v amdgpu.ids | tee $O/variants.txt
 unset LINE_DIAG_NOCHECK
+unset LSSP_AMD_LIB
+export LSSP_AMD_LINE2_P=16
+echo "== P16 (default lib)"; timeout -k 10 120 python -u tools/line_diag.py 216 0 2>&1 | grep -v amdgpu | tee $O/check_p16.txt
+export LSSP_AMD_LIB=$PWD/build/v_p16d5.so
+echo "== P16 D5"; timeout -k 10 120 python -u tools/line_diag.py 216 0 2>&1 | grep -v amdgpu | tee $O/check_p16d5.txt
+unset LSSP_AMD_LIB LSSP_AMD_LINE2_P
 for v in v_div2 v_spoll; do export LSSP_AMD_LIB=$PWD/build/$v.so
 timeout -k 10 120 python -u tools/line_diag.py 216 0 2>&1 | grep -v amdgpu | tee $O/check_$v.txt; done
 export LSSP_AMD_LIB=$PWD/build/v_spoll.so
