@@ -1105,6 +1105,9 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
 // reciprocals cost the compute waves more than the shorter chain saves --
 // 216^3 U sweep 394 us against 355 us with the IEEE division
 // (profiles/r04/r04d_line2_div_lead_variants.txt).
+#ifndef LINE2_LOAD_SLEEP
+#define LINE2_LOAD_SLEEP 0  // tuning builds: loaders' s_sleep (x 64 clk) before each step's DMAs
+#endif
 #ifndef LINE2_DIV
 #define LINE2_DIV 0
 #endif
@@ -1454,6 +1457,9 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
             };
             for (int s = S0; s <= TS; s++) {
                 const unsigned long long i0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
+#if LINE2_LOAD_SLEEP
+                __builtin_amdgcn_s_sleep(LINE2_LOAD_SLEEP);  // tuning: let the step's polls enter the memory queue first
+#endif
                 issue(s + D);  // dummies past TS keep the wait counts exact
                 const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
                 // steps s+LA+1 .. s+D were issued after step s+LA's

@@ -9,7 +9,7 @@ timeout -k 10 120 python -u tools/line_trace.py 216 150 2>&1 | grep -v amdgpu > 
 timeout -k 10 1100 python -u -m pytest tests -m gpu -q --timeout 600 --timeout-method thread > $O/pytest.log 2>&1
 tail -4 $O/pytest.log
 export LINE_DIAG_NOCHECK=1
-for v in default v_d5 v_d4 v_dh2_d5 v_nl3 v_div2 default v_spoll v_spoll_d5; do
+for v in default v_d5 v_d4 v_dh2_d5 v_nl3 v_div2 v_ls6 v_ls3d4 default v_spoll v_spoll_d5; do
   if [ "$v" = default ]; then unset LSSP_AMD_LIB; else export LSSP_AMD_LIB=$PWD/build/$v.so; fi
   echo "== $v"; timeout -k 10 120 python tools/line_diag.py 216 0 || { echo "variant $v failed"; exit 1; }
 done 2>&1 | grep -v amdgpu.ids | tee $O/variants.txt
