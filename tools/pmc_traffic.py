@@ -34,7 +34,7 @@ def main(fetch_dir, write_dir, out):
     res = {}
     for k in find("k_spmv3<0, 0"):  # y = A x (any column coding)
         res["k_spmv3"] = int(2 * fe[k] + wr.get(k, 0))
-    line = find("k_line<") + find("k_line_rhs")  # line sweeps: rhs gather + one L and one U launch
+    line = find("k_line<") + find("k_line2<") + find("k_line_rhs")  # line sweeps: rhs gather + one L and one U launch
     if line:
         res["ilu_apply"] = int(sum(2 * fe[k] + wr.get(k, 0) for k in line))
     tri = find("k_tri_pk6")
