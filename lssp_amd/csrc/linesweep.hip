@@ -157,7 +157,8 @@ struct CoefSrc {
         for (long r = r0; r < r1; r++) {
             double *row = c.data() + (size_t)(upper ? n - 1 - r : r) * NA;
             const int b = Tp[r], e = Tp[r + 1];
-            if (NA == 4) row[3] = upper ? Tx[b] : Tx[e - 1];
+            if (NA >= 4) row[3] = upper ? Tx[b] : Tx[e - 1];
+            if (NA == 5) row[4] = 1.0 / row[3];  // k_line2's division (line2_div)
             for (int q = upper ? b + 1 : b; q < (upper ? e : e - 1); q++) {
                 const long off = upper ? Tj[q] - r : r - Tj[q];
                 const int a = off == plane ? 0 : off == nx ? 1 : 2;  // detect_grid: off is one of 1, nx, plane
@@ -337,19 +338,25 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
             u.tj = Jp > 0 ? Kp * W + Jp - 1 : -1;
         }
     const long plane = (long)g.nx * g.ny;
+    // coefficients per row: c_k, c_j, c_i (unit L), + diag, + 1 / diag for
+    // k_line2's three-operation division (line2_div; LSSP_AMD_LINE2_RCP=0: the
+    // IEEE division from the diagonal alone)
+    const char *er = getenv("LSSP_AMD_LINE2_RCP");
+    const int NAD = LV == 2 && !(er && atoi(er) == 0) ? 5 : 4;
+    const int NAL = g.unitL ? 3 : NAD;
     CoefSrc cl, cu;
-    cl.build(Lp, Lj, Lx, false, n, g.nx, plane, g.unitL ? 3 : 4);
-    cu.build(Up, Uj, Ux, true, n, g.nx, plane, 4);
+    cl.build(Lp, Lj, Lx, false, n, g.nx, plane, NAL);
+    cu.build(Up, Uj, Ux, true, n, g.nx, plane, NAD);
     li.g = g;
     li.P = li.L.P = li.U.P = P;
     li.NJ = li.L.NJ = li.U.NJ = NJ;
     li.LV = li.L.LV = li.U.LV = LV;
     li.W = W;
     li.S = S;
-    LSSP_TRY(upload_sweep(c, g, Lt, cl, g.unitL ? 3 : 4, li.L));
+    LSSP_TRY(upload_sweep(c, g, Lt, cl, NAL, li.L));
     LineGeom gu = g;
     for (int k = 0; k < g.nz; k++) gu.kin[k] = k > 0 ? g.kin[g.nz - k] : 0;
-    LSSP_TRY(upload_sweep(c, gu, Ut, cu, 4, li.U));
+    LSSP_TRY(upload_sweep(c, gu, Ut, cu, NAD, li.U));
     // the L sweep writes its output into the U sweep's rhs stream: per L tile
     // the base row of its mirror U tile
     for (int K = 0; K < S; K++)
@@ -1092,25 +1099,20 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
 // storers (OUT 2: the U sweep's rhs stream; OUT 1: natural-order x in 8-row
 // runs of a line).  The rhs always comes from a stream (k_line_rhs gathers it).
 // The U sweep's division x / d (solver-tri.cxx:44) in 3 dependent operations
-// instead of IEEE division's ~10 (the divisor is a coefficient, known a step
-// ahead): with y = RN(1 / d) formed early, q0 = RN(x y), e = x - q0 d (exact,
-// FMA) and q = RN(q0 + e y) IS the correctly rounded quotient when nothing
-// under- or overflows (Markstein's theorem) -- guaranteed here by |x|, |d| in
-// [2^-400, 2^400] (line2_div_range; zeros, denormals, infinities and NaNs
-// fail it); a row outside takes the IEEE division.  Checked bit for bit
-// against IEEE division on 4e8 random operand pairs with exponents over that
-// whole range and all-ones / near-power-of-two significands
-// (tools/probe/div_check.c), and by every U-sweep parity test.
-// Measured SLOWER and off by default (-DLINE2_DIV=1 enables it): the loaders'
-// reciprocals cost the compute waves more than the shorter chain saves --
-// 216^3 U sweep 394 us against 355 us with the IEEE division
-// (profiles/r04/r04d_line2_div_lead_variants.txt).
-#ifndef LINE2_LOAD_SLEEP
-#define LINE2_LOAD_SLEEP 0  // tuning builds: loaders' s_sleep (x 64 clk) before each step's DMAs
-#endif
-#ifndef LINE2_DIV
-#define LINE2_DIV 0
-#endif
+// instead of IEEE division's ~10: with y = RN(1 / d) stored in the
+// coefficient stream beside d (NA = 5, formed at setup by the same IEEE
+// division), q0 = RN(x y), e = x - q0 d (exact, FMA) and q = RN(q0 + e y) IS
+// the correctly rounded quotient when nothing under- or overflows
+// (Markstein's theorem) -- guaranteed here by |x|, |d| in [2^-400, 2^400]
+// (line2_div_range; zeros, denormals, infinities and NaNs fail it); a row
+// outside takes the IEEE division in a uniform branch sane data never enters.
+// Checked bit for bit against IEEE division on 4e8 random operand pairs with
+// exponents over that whole range and all-ones / near-power-of-two
+// significands (tools/probe/div_check.c), and by every U-sweep parity test.
+// (Forming y in the kernel instead -- by the loader waves into the slot, or
+// by the compute waves a step early -- cost more than the shorter chain saved:
+// U sweep 394 / 396 us against 355 us with the IEEE division,
+// profiles/r04/r04d_*, r04e_*.)
 __device__ __forceinline__ bool line2_div_range(double x)
 {
     const unsigned e = ((unsigned)(__double_as_longlong(x) >> 52)) & 0x7FF;
@@ -1136,9 +1138,7 @@ struct Slot {
     static constexpr int RHS = NPC * 1024;
     static constexpr int KFIN = RHS + NRP * 1024;    // double[LV][NJ]
     static constexpr int JFIN = KFIN + LV * NJ * 8;  // double[LV][P]
-    static constexpr bool RCP_ON = NA == 4 && LINE2_DIV == 1;  // the loaders form 1/d into the slot
-    static constexpr int RCP = JFIN + LV * P * 8;    // double[LV * ROWS]: 1 / diag of each row (the loaders')
-    static constexpr int BYTES = RCP + (RCP_ON ? LV * ROWS * 8 : 0);
+    static constexpr int BYTES = JFIN + LV * P * 8;
     static_assert(BYTES % 16 == 0, "slot alignment");
 };
 // levels of results kept in LDS: the storers' source (OUT 1 writes 8-level
@@ -1147,50 +1147,8 @@ template <int OUT>
 constexpr int rsl() { return OUT == 1 ? 16 : 4; }
 template <int NA, int OUT, int D, int P>
 constexpr int lds_bytes() { return (D + 1) * Slot<NA, P>::BYTES + rsl<OUT>() * P * NJ * 8 + 16 + 512; }
-// LINE2_SPOLL: the hand-off inputs are polled with scalar (SMEM, glc) loads
-// by two poller waves (k and j) instead of one wave's LDS-DMA vector loads,
-// off the CU's vector memory queue that the coefficient DMAs fill
-#ifndef LINE2_SPOLL
-#define LINE2_SPOLL 0
-#endif
-constexpr int NPW = LINE2_SPOLL ? 2 : 1;  // poller waves
-constexpr int waves(int P, int NL, int SW) { return P / 4 + NL + NPW + SW; }
+constexpr int waves(int P, int NL, int SW) { return P / 4 + NL + 1 + SW; }
 }  // namespace l2
-
-typedef unsigned int line_u32x16 __attribute__((ext_vector_type(16)));
-// N (1..4) x 64 bytes from a uniform address, bypassing the scalar cache (glc),
-// then lane i of lo / hi gets dwords 2i / 2i+1 (doubles 0 .. 8N-1 on lanes 0 .. 8N-1)
-template <int N>
-__device__ __forceinline__ double spoll_load(const double *p)
-{
-    line_u32x16 a0, a1, a2, a3;
-    if constexpr (N == 2) {
-        asm volatile("s_load_dwordx16 %0, %2, 0x0 glc\n\ts_load_dwordx16 %1, %2, 0x40 glc\n\ts_waitcnt lgkmcnt(0)"
-                     : "=s"(a0), "=s"(a1) : "s"(p) : "memory");
-    } else {
-        static_assert(N == 4, "N");
-        asm volatile("s_load_dwordx16 %0, %4, 0x0 glc\n\ts_load_dwordx16 %1, %4, 0x40 glc\n\t"
-                     "s_load_dwordx16 %2, %4, 0x80 glc\n\ts_load_dwordx16 %3, %4, 0xc0 glc\n\ts_waitcnt lgkmcnt(0)"
-                     : "=s"(a0), "=s"(a1), "=s"(a2), "=s"(a3) : "s"(p) : "memory");
-    }
-    unsigned lo = 0, hi = 0;
-    // lane selects as inline constants (two SGPR operands break the constant-bus limit)
-#define SPOLL_WL(A, I, L)                                                           \
-    asm("v_writelane_b32 %0, %1, " #L : "+v"(lo) : "s"(A[2 * (I)]));             \
-    asm("v_writelane_b32 %0, %1, " #L : "+v"(hi) : "s"(A[2 * (I) + 1]));
-    SPOLL_WL(a0, 0, 0) SPOLL_WL(a0, 1, 1) SPOLL_WL(a0, 2, 2) SPOLL_WL(a0, 3, 3)
-    SPOLL_WL(a0, 4, 4) SPOLL_WL(a0, 5, 5) SPOLL_WL(a0, 6, 6) SPOLL_WL(a0, 7, 7)
-    SPOLL_WL(a1, 0, 8) SPOLL_WL(a1, 1, 9) SPOLL_WL(a1, 2, 10) SPOLL_WL(a1, 3, 11)
-    SPOLL_WL(a1, 4, 12) SPOLL_WL(a1, 5, 13) SPOLL_WL(a1, 6, 14) SPOLL_WL(a1, 7, 15)
-    if constexpr (N == 4) {
-        SPOLL_WL(a2, 0, 16) SPOLL_WL(a2, 1, 17) SPOLL_WL(a2, 2, 18) SPOLL_WL(a2, 3, 19)
-        SPOLL_WL(a2, 4, 20) SPOLL_WL(a2, 5, 21) SPOLL_WL(a2, 6, 22) SPOLL_WL(a2, 7, 23)
-        SPOLL_WL(a3, 0, 24) SPOLL_WL(a3, 1, 25) SPOLL_WL(a3, 2, 26) SPOLL_WL(a3, 3, 27)
-        SPOLL_WL(a3, 4, 28) SPOLL_WL(a3, 5, 29) SPOLL_WL(a3, 6, 30) SPOLL_WL(a3, 7, 31)
-    }
-#undef SPOLL_WL
-    return __longlong_as_double(((long long)hi << 32) | lo);
-}
 
 // lane l <- lane l - 16 (rows R0..R3 of the wave -> [R0, R0, R1, R2]; row 0 is
 // not used): v_permlane16_swap gives [R0, R0, R2, R2] / [R1, R1, R3, R3],
@@ -1272,7 +1230,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
             const int sg = wave;  // sigma of the wave's planes
             struct In {
                 double ck[LV], cj[LV], ci[LV], dg[LV], rh[LV], jv[LV];
-                double rc[LV];  // LINE2_DIV: 1 / diag, correctly rounded (formed one step early)
+                double rc[LV];  // NA 5: 1 / diag, correctly rounded (the stream's fifth component)
                 bool dok[LV];   // ... diag in the safe range of line2_div
             };
             // the step's inputs, read from LDS one step ahead (their slot was
@@ -1286,31 +1244,29 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     in.ck[v] = b[0];
                     in.cj[v] = b[1];
                     in.ci[v] = b[2];
-                    if constexpr (NA == 4) {
-                        in.dg[v] = b[3];
-                        if constexpr (SL::RCP_ON) {
-                            in.rc[v] = reinterpret_cast<const double *>(slot + SL::RCP)[r];
-                            in.dok[v] = line2_div_range(in.dg[v]);
-                        }
+                    if constexpr (NA >= 4) in.dg[v] = b[3];
+                    if constexpr (NA == 5) {
+                        in.rc[v] = b[4];
+                        in.dok[v] = line2_div_range(in.dg[v]);
                     }
                     in.rh[v] = reinterpret_cast<const double *>(slot + SL::RHS)[r];
                     in.jv[v] = reinterpret_cast<const double *>(slot + SL::JFIN)[v * P + pw];
                 }
             };
-            // x / diag of level v on the rows of mask h (bitwise IEEE division)
+            // x / diag of level v on the rows of mask h (bitwise the IEEE division)
             auto divide = [&](double x, const In &in, int v, uint64_t h) {
-#if LINE2_DIV
-                double q = line2_div(x, in.dg[v], in.rc[v]);
-                const uint64_t bad = __ballot(!(in.dok[v] && line2_div_range(x))) & h;
-                if (__builtin_expect(bad != 0, 0)) {  // uniform branch, never taken on sane data
-                    asm volatile("" ::: "memory");    // (keeps the division out of the common path)
-                    if ((bad >> lane) & 1) q = x / in.dg[v];
+                if constexpr (NA == 5) {
+                    double q = line2_div(x, in.dg[v], in.rc[v]);
+                    const uint64_t bad = __ballot(!(in.dok[v] && line2_div_range(x))) & h;
+                    if (__builtin_expect(bad != 0, 0)) {  // uniform branch, never taken on sane data
+                        asm volatile("" ::: "memory");    // (keeps the division out of the common path)
+                        if ((bad >> lane) & 1) q = x / in.dg[v];
+                    }
+                    return q;
+                } else {
+                    (void)h;
+                    return x / in.dg[v];
                 }
-                return q;
-#else
-                (void)h;
-                return x / in.dg[v];
-#endif
             };
             In A, B;
             double xp = 0.0;  // the lane's value of the previous level
@@ -1388,11 +1344,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     double v = cur.rh[0] - cur.ck[0] * xk;
                     v = v - cur.cj[0] * xj;
                     v = v - cur.ci[0] * xp;
-#if LINE2_DIV == 2
-                    // the next step's reciprocals, interleaved into this step's chains
-                    if constexpr (NA == 4) nxt.rc[0] = 1.0 / nxt.dg[0], nxt.dok[0] = line2_div_range(nxt.dg[0]);
-#endif
-                    if constexpr (NA == 4) v = divide(v, cur, 0, h0);
+                    if constexpr (NA >= 4) v = divide(v, cur, 0, h0);
                     const double x0 = sel_lanes(h0, v, xp);
                     publish(2 * s, h0, x0);  // its store issues under level 2s+1's arithmetic
                     res[((2 * s) & (RSL - 1)) * ROWS + pw * NJ + ll] = x0;
@@ -1402,10 +1354,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     v = cur.rh[1] - cur.ck[1] * xk;
                     v = v - cur.cj[1] * xj;
                     v = v - cur.ci[1] * x0;
-#if LINE2_DIV == 2
-                    if constexpr (NA == 4) nxt.rc[1] = 1.0 / nxt.dg[1], nxt.dok[1] = line2_div_range(nxt.dg[1]);
-#endif
-                    if constexpr (NA == 4) v = divide(v, cur, 1, h1);
+                    if constexpr (NA >= 4) v = divide(v, cur, 1, h1);
                     const double x1 = sel_lanes(h1, v, x0);
                     if (trs && wave == 0) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
                     publish(2 * s + 1, h1, x1);
@@ -1413,12 +1362,6 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     xp = x1;
                     xs = up16(x1);  // the next step's first k-operand, off its critical path
                 }
-#if LINE2_DIV == 2
-                else if constexpr (NA == 4) {
-#pragma unroll
-                    for (int v = 0; v < LV; v++) nxt.rc[v] = 1.0 / nxt.dg[v], nxt.dok[v] = line2_div_range(nxt.dg[v]);
-                }
-#endif
                 so = sn;
                 if (trs && s >= 0 && s < TS) ts[8 * s + (wave == 0 ? 1 : 7)] = __builtin_amdgcn_s_memtime();
                 line_barrier();
@@ -1464,21 +1407,6 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                 const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
                 // steps s+LA+1 .. s+D were issued after step s+LA's
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - LA) * KPER) : "memory");
-                if constexpr (SL::RCP_ON) {
-                    // 1 / diag of the rows in this wave's own landed pieces of step
-                    // s+LA's block (a 1 KB piece holds 32 rows of {c_k, c_j, c_i, d}):
-                    // off the compute waves' dependent chain (line2_div)
-                    const char *sl = ring + ((s + LA) % R + R) % R * SL::BYTES;
-#pragma unroll
-                    for (int k = 0; k < KPER; k++) {
-                        const int m = w + k * NL;
-                        if (m < SL::NPC && (lane >> 5) == (k & 1)) {
-                            const int row = 32 * m + (lane & 31);
-                            const double dg = reinterpret_cast<const double *>(sl + SL::COEF)[row * 4 + 3];
-                            reinterpret_cast<double *>(const_cast<char *>(sl) + SL::RCP)[row] = 1.0 / dg;
-                        }
-                    }
-                }
                 if (trs && w == 0 && s >= 0 && s < TS) {
                     ts[8 * s + 4] = w0 - i0;
                     ts[8 * s + 3] = __builtin_amdgcn_s_memtime() - w0;
@@ -1486,53 +1414,6 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                 line_barrier();
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else if (LINE2_SPOLL && wave < CW + NL + NPW) {
-            // ---------------- scalar pollers (LINE2_SPOLL) ----------------
-            // wave CW+NL: at step s the k-inputs of step s+1 (2 levels x NJ lines =
-            // 256 B), wave CW+NL+1: the j-inputs of step s+2 (2 x P planes = 128 B),
-            // re-read until every existing entry is published, into the slot.
-            const bool isk = wave == CW + NL;
-            const bool has = isk ? kin : jin;
-            const int cnt = isk ? LV * NJ : LV * P;
-            const double *src = isk ? a.hk + (long)max(d.tk, 0) * a.hk_stride : a.hj + (long)max(d.tj, 0) * a.hj_stride;
-            const int qmax = (int)(a.hk_stride / (NJ * LV)) - 1;  // steps
-            const int kl = lane & (NJ - 1), kv = lane >> 4, jp = lane & (P - 1), jv = lane / P;
-            const unsigned foff = isk ? SL::KFIN : SL::JFIN;
-            if (!has) {
-                for (int q = 0; q < R; q++)
-                    if (lane < cnt) reinterpret_cast<double *>(ring + q * SL::BYTES + foff)[lane] = 0.0;
-            }
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            unsigned polls = 0;
-            for (int s = S0; s <= TS; s++) {
-                const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
-                const int q = isk ? s + 1 : s + 2;  // step
-                if (has && q >= 0 && q < TS) {
-                    const double *p = src + (long)min(q, qmax) * cnt;
-                    const int lv = LV * q + (isk ? kv : jv);
-                    const bool val = lane < cnt && lv < T &&
-                                     (isk ? kl < nj && (unsigned)(lv - kl) < (unsigned)nx
-                                          : jp < np && (unsigned)(lv - jp - sig(jp)) < (unsigned)nx);
-                    double x;
-                    for (;;) {
-                        x = (isk || P == 16) ? spoll_load<4>(p) : spoll_load<2>(p);
-                        if (!__any(val && (uint64_t)__double_as_longlong(x) == TRI_SENTINEL)) break;
-                        polls++;
-                        if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s
-                            atomicOr(a.err, 8);
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                    if (lane < cnt) reinterpret_cast<double *>(ring + (q % R) * SL::BYTES + foff)[lane] = x;
-                }
-                if (trs && isk && s >= 0 && s < TS) ts[8 * s + 2] = __builtin_amdgcn_s_memtime() - w0;
-                line_barrier();
-            }
-            if (TRACE) {
-                for (int o = 32; o >= 1; o >>= 1) polls += __shfl_xor(polls, o);
-                if (lane == 0 && isk) a.trace[8 * t + 3] = polls / 64;
-            }
         } else if (wave == CW + NL) {
             // ---------------- poller ----------------
             // At step s: LDS-DMA sc1 reads of step s+DH's k-inputs (two levels x NJ
@@ -1617,7 +1498,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
         } else {
             // ---------------- storers: results, re-arms ----------------
             // Storer 0 re-arms the consumed j-inputs, storer SW-1 the k-inputs.
-            const int w = wave - (CW + NL + NPW);
+            const int w = wave - (CW + NL + 1);
             const int kl = lane & (NJ - 1), kv = lane >> 4, jp = lane & (P - 1), jv = lane / P;
             uint64_t *hki = reinterpret_cast<uint64_t *>(a.hk + (long)max(d.tk, 0) * a.hk_stride) + kl;
             uint64_t *hji = reinterpret_cast<uint64_t *>(a.hj + (long)max(d.tj, 0) * a.hj_stride) + jp;
@@ -1947,12 +1828,15 @@ static int launch_line2(lssp_amd_ctx *c, const LineILU &li, int which, const dou
         const char *dg = getenv("LSSP_AMD_LINE_DIAG");
         a.diag = dg ? atoi(dg) : 0;
     }
-    if (ls.P == 16) {
-        if (outk == 2) return ls.NA == 3 ? launch_line2_t<16, 3, 2>(c, ls, a) : launch_line2_t<16, 4, 2>(c, ls, a);
-        return ls.NA == 3 ? launch_line2_t<16, 3, 1>(c, ls, a) : launch_line2_t<16, 4, 1>(c, ls, a);
-    }
-    if (outk == 2) return ls.NA == 3 ? launch_line2_t<8, 3, 2>(c, ls, a) : launch_line2_t<8, 4, 2>(c, ls, a);
-    return ls.NA == 3 ? launch_line2_t<8, 3, 1>(c, ls, a) : launch_line2_t<8, 4, 1>(c, ls, a);
+    auto go = [&](auto PP) {
+        constexpr int P = decltype(PP)::value;
+        if (outk == 2)
+            return ls.NA == 3 ? launch_line2_t<P, 3, 2>(c, ls, a)
+                   : ls.NA == 4 ? launch_line2_t<P, 4, 2>(c, ls, a) : launch_line2_t<P, 5, 2>(c, ls, a);
+        return ls.NA == 3 ? launch_line2_t<P, 3, 1>(c, ls, a)
+               : ls.NA == 4 ? launch_line2_t<P, 4, 1>(c, ls, a) : launch_line2_t<P, 5, 1>(c, ls, a);
+    };
+    return ls.P == 16 ? go(std::integral_constant<int, 16>()) : go(std::integral_constant<int, 8>());
 }
 
 static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const double *rhs, bool u_in, double *out,
