@@ -157,8 +157,7 @@ struct CoefSrc {
         for (long r = r0; r < r1; r++) {
             double *row = c.data() + (size_t)(upper ? n - 1 - r : r) * NA;
             const int b = Tp[r], e = Tp[r + 1];
-            if (NA >= 4) row[3] = upper ? Tx[b] : Tx[e - 1];
-            if (NA == 5) row[4] = 1.0 / row[3];  // k_line2's division (line2_div)
+            if (NA == 4) row[3] = upper ? Tx[b] : Tx[e - 1];
             for (int q = upper ? b + 1 : b; q < (upper ? e : e - 1); q++) {
                 const long off = upper ? Tj[q] - r : r - Tj[q];
                 const int a = off == plane ? 0 : off == nx ? 1 : 2;  // detect_grid: off is one of 1, nx, plane
@@ -299,9 +298,10 @@ static void line_plan(const LineGeom &g, int &P, int &NJ, int &LV)
         LV = 1;
         return;
     }
-    // LSSP_AMD_LINE2_P=16: 16-plane tiles (4 compute waves, 256 rows per level)
-    const char *ep = getenv("LSSP_AMD_LINE2_P");
-    P = ep && atoi(ep) == 16 ? 16 : 8;
+    // (the kernel is generic in P = 4 x compute waves; 16-plane tiles measured
+    // slower: 216^3 apply 666 against 593 us, 512^3 4.72 against 4.59 ms,
+    // profiles/r04/r04e_*, r04f_line2_512_p8_p16.txt)
+    P = 8;
     NJ = 16;
     LV = 2;
 }
@@ -338,11 +338,8 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
             u.tj = Jp > 0 ? Kp * W + Jp - 1 : -1;
         }
     const long plane = (long)g.nx * g.ny;
-    // coefficients per row: c_k, c_j, c_i (unit L), + diag, + 1 / diag for
-    // k_line2's three-operation division (line2_div; LSSP_AMD_LINE2_RCP=0: the
-    // IEEE division from the diagonal alone)
-    const char *er = getenv("LSSP_AMD_LINE2_RCP");
-    const int NAD = LV == 2 && !(er && atoi(er) == 0) ? 5 : 4;
+    // coefficients per row: c_k, c_j, c_i (unit L), + diag
+    const int NAD = 4;
     const int NAL = g.unitL ? 3 : NAD;
     CoefSrc cl, cu;
     cl.build(Lp, Lj, Lx, false, n, g.nx, plane, NAL);
@@ -1098,32 +1095,15 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
 // (LDS-DMA sc1 reads of the two levels' hand-off inputs DH steps ahead), SW
 // storers (OUT 2: the U sweep's rhs stream; OUT 1: natural-order x in 8-row
 // runs of a line).  The rhs always comes from a stream (k_line_rhs gathers it).
-// The U sweep's division x / d (solver-tri.cxx:44) in 3 dependent operations
-// instead of IEEE division's ~10: with y = RN(1 / d) stored in the
-// coefficient stream beside d (NA = 5, formed at setup by the same IEEE
-// division), q0 = RN(x y), e = x - q0 d (exact, FMA) and q = RN(q0 + e y) IS
-// the correctly rounded quotient when nothing under- or overflows
-// (Markstein's theorem) -- guaranteed here by |x|, |d| in [2^-400, 2^400]
-// (line2_div_range; zeros, denormals, infinities and NaNs fail it); a row
-// outside takes the IEEE division in a uniform branch sane data never enters.
-// Checked bit for bit against IEEE division on 4e8 random operand pairs with
-// exponents over that whole range and all-ones / near-power-of-two
-// significands (tools/probe/div_check.c), and by every U-sweep parity test.
-// (Forming y in the kernel instead -- by the loader waves into the slot, or
-// by the compute waves a step early -- cost more than the shorter chain saved:
-// U sweep 394 / 396 us against 355 us with the IEEE division,
-// profiles/r04/r04d_*, r04e_*.)
-__device__ __forceinline__ bool line2_div_range(double x)
-{
-    const unsigned e = ((unsigned)(__double_as_longlong(x) >> 52)) & 0x7FF;
-    return e - (1023u - 400u) <= 800u;
-}
-__device__ __forceinline__ double line2_div(double x, double d, double y)
-{
-    const double q0 = x * y;
-    const double e = __builtin_fma(-q0, d, x);
-    return __builtin_fma(e, y, q0);
-}
+// The U sweep's division stays the IEEE division x / d (solver-tri.cxx:44).
+// Markstein's three-operation form from y = RN(1/d) (q0 = x y, e = fma(-q0,
+// d, x), q = fma(e, y, q0): bitwise IEEE when |x|, |d| lie in [2^-400,
+// 2^400], checked on 4e8 operand pairs by tools/probe/div_check.c) measured
+// SLOWER in every placement of y: formed by the loader waves into the slot
+// (U sweep 394 us), by the compute waves a step early (396 us), stored in the
+// coefficient stream at setup (372-376 us) -- against 352-357 us with the
+// plain division (profiles/r04/r04d_*, r04e_*, r04f_*): its range checks and
+// the extra operand cost as much as the shorter chain saves.
 
 namespace l2 {
 constexpr int NJ = 16, LV = 2;  // lines per tile, levels per step; P (8 or 16) planes per tile: 2 or 4 compute waves
@@ -1230,8 +1210,6 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
             const int sg = wave;  // sigma of the wave's planes
             struct In {
                 double ck[LV], cj[LV], ci[LV], dg[LV], rh[LV], jv[LV];
-                double rc[LV];  // NA 5: 1 / diag, correctly rounded (the stream's fifth component)
-                bool dok[LV];   // ... diag in the safe range of line2_div
             };
             // the step's inputs, read from LDS one step ahead (their slot was
             // completed before the barrier that ended the previous step)
@@ -1244,28 +1222,9 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     in.ck[v] = b[0];
                     in.cj[v] = b[1];
                     in.ci[v] = b[2];
-                    if constexpr (NA >= 4) in.dg[v] = b[3];
-                    if constexpr (NA == 5) {
-                        in.rc[v] = b[4];
-                        in.dok[v] = line2_div_range(in.dg[v]);
-                    }
+                    if constexpr (NA == 4) in.dg[v] = b[3];
                     in.rh[v] = reinterpret_cast<const double *>(slot + SL::RHS)[r];
                     in.jv[v] = reinterpret_cast<const double *>(slot + SL::JFIN)[v * P + pw];
-                }
-            };
-            // x / diag of level v on the rows of mask h (bitwise the IEEE division)
-            auto divide = [&](double x, const In &in, int v, uint64_t h) {
-                if constexpr (NA == 5) {
-                    double q = line2_div(x, in.dg[v], in.rc[v]);
-                    const uint64_t bad = __ballot(!(in.dok[v] && line2_div_range(x))) & h;
-                    if (__builtin_expect(bad != 0, 0)) {  // uniform branch, never taken on sane data
-                        asm volatile("" ::: "memory");    // (keeps the division out of the common path)
-                        if ((bad >> lane) & 1) q = x / in.dg[v];
-                    }
-                    return q;
-                } else {
-                    (void)h;
-                    return x / in.dg[v];
                 }
             };
             In A, B;
@@ -1344,7 +1303,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     double v = cur.rh[0] - cur.ck[0] * xk;
                     v = v - cur.cj[0] * xj;
                     v = v - cur.ci[0] * xp;
-                    if constexpr (NA >= 4) v = divide(v, cur, 0, h0);
+                    if constexpr (NA == 4) v = v / cur.dg[0];
                     const double x0 = sel_lanes(h0, v, xp);
                     publish(2 * s, h0, x0);  // its store issues under level 2s+1's arithmetic
                     res[((2 * s) & (RSL - 1)) * ROWS + pw * NJ + ll] = x0;
@@ -1354,7 +1313,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     v = cur.rh[1] - cur.ck[1] * xk;
                     v = v - cur.cj[1] * xj;
                     v = v - cur.ci[1] * x0;
-                    if constexpr (NA >= 4) v = divide(v, cur, 1, h1);
+                    if constexpr (NA == 4) v = v / cur.dg[1];
                     const double x1 = sel_lanes(h1, v, x0);
                     if (trs && wave == 0) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
                     publish(2 * s + 1, h1, x1);
@@ -1726,9 +1685,9 @@ static int launch_line_gather(lssp_amd_ctx *c, const LineSweep &ls, int mirror, 
 {
     const int nq = (ls.tmax + LRHS_RUN - 1) / LRHS_RUN;
     const long grid = 8L * ((ls.ntiles + 7) / 8) * nq;
-    auto kr = ls.LV == 2 ? (ls.P == 16 ? k_line_rhs<16, 16, true> : k_line_rhs<8, 16, true>)
+    auto kr = ls.LV == 2 ? k_line_rhs<8, 16, true>
               : ls.P == 16 ? k_line_rhs<16, 16, false> : ls.P == 8 ? k_line_rhs<8, 32, false> : k_line_rhs<4, 64, false>;
-    if (ls.LV == 2 && ((ls.P != 8 && ls.P != 16) || ls.NJ != 16)) return LSSP_AMD_EUNSUPPORTED;
+    if (ls.LV == 2 && (ls.P != 8 || ls.NJ != 16)) return LSSP_AMD_EUNSUPPORTED;
     const long n = (long)ls.nx * ls.ny * ls.nz;
     kr<<<grid, 256, 0, c->stream>>>(ls.d_tiles, ls.ntiles, nq, ls.nx, ls.ny, n, mirror, rhs, stream, c->guard);
     LSSP_HIP(hipGetLastError());
@@ -1748,11 +1707,8 @@ static int launch_line_gather(lssp_amd_ctx *c, const LineSweep &ls, int mirror, 
 #ifndef LINE2_SW
 #define LINE2_SW 4
 #endif
-#ifndef LINE2_D16
-#define LINE2_D16 4  // loader lead of the 16-plane tiles (their slots are twice as large)
-#endif
 template <int P>
-constexpr int line2_d() { return P == 16 ? LINE2_D16 : LINE2_D; }
+constexpr int line2_d() { return LINE2_D; }
 template <int P, int NA, int OUT, bool TRACE>
 static int launch_line2_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)
 {
@@ -1830,13 +1786,10 @@ static int launch_line2(lssp_amd_ctx *c, const LineILU &li, int which, const dou
     }
     auto go = [&](auto PP) {
         constexpr int P = decltype(PP)::value;
-        if (outk == 2)
-            return ls.NA == 3 ? launch_line2_t<P, 3, 2>(c, ls, a)
-                   : ls.NA == 4 ? launch_line2_t<P, 4, 2>(c, ls, a) : launch_line2_t<P, 5, 2>(c, ls, a);
-        return ls.NA == 3 ? launch_line2_t<P, 3, 1>(c, ls, a)
-               : ls.NA == 4 ? launch_line2_t<P, 4, 1>(c, ls, a) : launch_line2_t<P, 5, 1>(c, ls, a);
+        if (outk == 2) return ls.NA == 3 ? launch_line2_t<P, 3, 2>(c, ls, a) : launch_line2_t<P, 4, 2>(c, ls, a);
+        return ls.NA == 3 ? launch_line2_t<P, 3, 1>(c, ls, a) : launch_line2_t<P, 4, 1>(c, ls, a);
     };
-    return ls.P == 16 ? go(std::integral_constant<int, 16>()) : go(std::integral_constant<int, 8>());
+    return go(std::integral_constant<int, 8>());
 }
 
 static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const double *rhs, bool u_in, double *out,
