@@ -201,6 +201,7 @@ struct LineSweep {
     LineTile *d_tiles = nullptr;
     double *d_coef = nullptr;
     unsigned long long *d_claim = nullptr;
+    int *d_order = nullptr;  // k_line2: the tile of each claim (anti-diagonal order)
     mutable unsigned long long base = 0;
     std::vector<LineTile> h_tiles;
 };

@@ -257,6 +257,25 @@ static int upload_sweep(lssp_amd_ctx *c, const LineGeom &g, const std::vector<Li
     LSSP_HIP(hipMemcpy(ls.d_coef, coef.data(), sizeof(double) * coef.size(), hipMemcpyHostToDevice));
     LSSP_HIP(hipMalloc(&ls.d_claim, sizeof(unsigned long long)));
     LSSP_HIP(hipMemset(ls.d_claim, 0, sizeof(unsigned long long)));
+    if (LV == 2) {
+        // k_line2 claims tiles by anti-diagonal J + K (then K): a claimed tile's
+        // producers (J-1, K) and (J, K-1) were claimed before it, and the
+        // workgroups hold tiles of the advancing wavefront instead of tiles
+        // many hops ahead of it (row order: the first 256 claims of a 216^3 sweep
+        // reach K = 18, whose tiles wait ~30 hops before they can start).
+        // LSSP_AMD_LINE2_ROWORDER=1: row order (A/B).
+        const int W = (g.ny + ls.NJ - 1) / ls.NJ, nt = (int)tt.size();
+        std::vector<int> ord(nt);
+        for (int q = 0; q < nt; q++) ord[q] = q;
+        const char *ro = getenv("LSSP_AMD_LINE2_ROWORDER");
+        if (!(ro && atoi(ro)))
+            std::stable_sort(ord.begin(), ord.end(), [W](int x, int y) {
+                const int dx = x % W + x / W, dy = y % W + y / W;
+                return dx != dy ? dx < dy : x < y;
+            });
+        LSSP_HIP(hipMalloc(&ls.d_order, sizeof(int) * nt));
+        LSSP_HIP(hipMemcpy(ls.d_order, ord.data(), sizeof(int) * nt, hipMemcpyHostToDevice));
+    }
     ls.h_tiles = std::move(tt);
     return LSSP_AMD_OK;
 }
@@ -396,6 +415,7 @@ void free_line_sweep(LineILU &li)
         if (s->d_tiles) (void)hipFree(s->d_tiles);
         if (s->d_coef) (void)hipFree(s->d_coef);
         if (s->d_claim) (void)hipFree(s->d_claim);
+        if (s->d_order) (void)hipFree(s->d_order);
         *s = LineSweep{};
     }
     if (li.d_ustream) (void)hipFree(li.d_ustream);
@@ -420,6 +440,7 @@ struct LineArgs {
     long hk_stride, hj_stride;
     unsigned long long *claim;
     unsigned long long base;
+    const int *order;       // k_line2: tile of each claim (wavefront order), nullptr: claim order
     int mirror;             // U sweep: natural row = n-1 - sweep row
     int *err;
     // diagnostics (LSSP_AMD_LINE_TRACE): per tile {claim, step 0, end, re-polls,
@@ -1184,7 +1205,12 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
 
     for (;;) {
         __syncthreads();
-        if (threadIdx.x == 0) *s_tile = (int)(atomicAdd(a.claim, 1ull) - a.base);
+        if (threadIdx.x == 0) {
+            // claims in wavefront order (LineSweep::d_order): every tile's producers
+            // have a smaller anti-diagonal J + K and were claimed before it
+            const int c = (int)(atomicAdd(a.claim, 1ull) - a.base);
+            *s_tile = c < a.ntiles ? (a.order ? a.order[c] : c) : a.ntiles;
+        }
         __syncthreads();
         const int t = __builtin_amdgcn_readfirstlane(*s_tile);
         if (t >= a.ntiles) break;
@@ -1777,6 +1803,7 @@ static int launch_line2(lssp_amd_ctx *c, const LineILU &li, int which, const dou
     a.hj_stride = li.hj_stride;
     a.claim = ls.d_claim;
     a.base = ls.base;
+    a.order = ls.d_order;
     a.mirror = which;
     a.err = c->d_err;
     a.guard = c->guard;
