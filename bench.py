@@ -19,8 +19,9 @@ send/recv and dots with an RCCL all-gather; the preconditioner becomes
 block-Jacobi ILU(0) per slab (the reference's blk_size path).
 
 The roofline object describes the dominant operator, the ILU(0) apply
-(pc.solve: the two line sweeps k_line, L then U -- rocprof attributes ~75% of
-a step to them); roofline_spmv describes the metric's SpMV kernel, y = A x
+(pc.solve: the rhs gather and the two line sweeps k_line2, L then U --
+rocprof attributes ~65% of a step to them); roofline_spmv describes the
+metric's SpMV kernel, y = A x
 (lssp_mv_mxy).  Both are timed live with HIP events on the library's stream.
 traffic: HBM bytes per launch from rocprofv3 PMC counters (FETCH_SIZE x 2 on
 gfx950, + WRITE_SIZE), read from profiles/pmc_traffic.json when present.
@@ -343,9 +344,9 @@ def main():
                      "csr_int32_equivalent_gbps": round(csr_equiv_gbs, 1)},
             "roofline": {"bound": "hbm", "achieved": round(apply_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(apply_gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("ilu_apply"),
-                         "kernel": "ILU(0) apply = k_line_rhs (rhs -> the L sweep's stream) + k_line (L sweep "
-                                   "-> the U sweep's rhs stream) + k_line (U sweep -> x in natural order); "
-                                   "latency-bound: 2 x 646 dependent levels",
+                         "kernel": "ILU(0) apply = k_line_rhs (rhs -> the L sweep's stream) + k_line2 (L sweep "
+                                   "-> the U sweep's rhs stream) + k_line2 (U sweep -> x in natural order); "
+                                   f"latency-bound: 2 x {M.levelsL} dependent levels, two per workgroup step",
                          "bytes_per_launch": apply_b, "ms_per_launch": round(apply_ms, 5),
                          "peak_measured": peak_measured, "peak_measured_detail": peak_detail,
                          "frac_of_measured_peak": round(apply_gbs / peak_measured, 4) if peak_measured else None},
