@@ -153,6 +153,13 @@ int lssp_amd_ilu_from_factors(lssp_amd_ctx *ctx, int n, const int *Lp, const int
                               lssp_amd_ilu **M);
 int lssp_amd_ilu_destroy(lssp_amd_ilu *M);
 int lssp_amd_ilu_apply(lssp_amd_ctx *ctx, const lssp_amd_ilu *M, double *x, const double *rhs);
+/* The apply enqueued on the context's stream without waiting for it (the
+ * synchronous lssp_amd_ilu_apply returns when x is written, like the
+ * reference's pc.solve); lssp_amd_ilu_check then waits for the stream and
+ * reports a hand-off timeout (LSSP_AMD_ETIMEOUT) of any apply since the last
+ * check, re-arming the factor's hand-off buffers. */
+int lssp_amd_ilu_apply_async(lssp_amd_ctx *ctx, const lssp_amd_ilu *M, double *x, const double *rhs);
+int lssp_amd_ilu_check(lssp_amd_ctx *ctx, const lssp_amd_ilu *M);
 /* one triangular sweep: which = 0 lower (solver-tri.cxx:4-24), 1 upper (:26-46) */
 int lssp_amd_ilu_trisolve(lssp_amd_ctx *ctx, const lssp_amd_ilu *M, int which, double *x,
                           const double *rhs);

@@ -71,6 +71,8 @@ SIGNATURES = {
     "lssp_amd_ilu_from_factors": (_ci, [_vp, _ci, _vp, _vp, _vp, _vp, _vp, _vp, _pvp]),
     "lssp_amd_ilu_destroy": (_ci, [_vp]),
     "lssp_amd_ilu_apply": (_ci, [_vp, _vp, _vp, _vp]),
+    "lssp_amd_ilu_apply_async": (_ci, [_vp, _vp, _vp, _vp]),
+    "lssp_amd_ilu_check": (_ci, [_vp, _vp]),
     "lssp_amd_ilu_trisolve": (_ci, [_vp, _vp, _ci, _vp, _vp]),
     "lssp_amd_ilu_info": (_ci, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "lssp_amd_ilu_get_factors": (_ci, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),

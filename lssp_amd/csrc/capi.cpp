@@ -876,6 +876,21 @@ int lssp_amd_ilu_apply(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const 
     return check_err(c, M);
 }
 
+// The same apply, only enqueued on the context's stream (no host round trip):
+// for callers that pipeline applies with other work; a hand-off timeout of an
+// enqueued apply is reported by lssp_amd_ilu_check.
+int lssp_amd_ilu_apply_async(lssp_amd_ctx *c, const lssp_amd_ilu *M, double *x, const double *rhs)
+{
+    if (!c || !M || !x || !rhs) return LSSP_AMD_EINVAL;
+    return launch_ilu_apply(c, M, x, rhs);
+}
+
+int lssp_amd_ilu_check(lssp_amd_ctx *c, const lssp_amd_ilu *M)
+{
+    if (!c || !M) return LSSP_AMD_EINVAL;
+    return check_err(c, M);
+}
+
 int lssp_amd_ilu_trisolve(lssp_amd_ctx *c, const lssp_amd_ilu *M, int which, double *x, const double *rhs)
 {
     if (!c || !M || !x || !rhs || x == rhs) return LSSP_AMD_EINVAL;

@@ -318,6 +318,13 @@ class DILU:
         """x = U^-1 L^-1 rhs (lssp_pc_ilu_solve, solver-tri.cxx:57-60)"""
         _ck(self.dev.L.lssp_amd_ilu_apply(self.dev.h, self.h, x.ptr, rhs.ptr), "ilu_apply")
 
+    def apply_async(self, x: DVec, rhs: DVec):
+        """the apply enqueued without waiting (lssp_amd_ilu_apply_async); check() reports timeouts"""
+        _ck(self.dev.L.lssp_amd_ilu_apply_async(self.dev.h, self.h, x.ptr, rhs.ptr), "ilu_apply_async")
+
+    def check(self):
+        _ck(self.dev.L.lssp_amd_ilu_check(self.dev.h, self.h), "ilu_check")
+
     def trisolve(self, which: int, x: DVec, rhs: DVec):
         _ck(self.dev.L.lssp_amd_ilu_trisolve(self.dev.h, self.h, which, x.ptr, rhs.ptr), "ilu_trisolve")
 
