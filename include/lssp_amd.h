@@ -170,8 +170,10 @@ int lssp_amd_ilu_get_factors(const lssp_amd_ilu *M, int *Lp, int *Lj, double *Lx
 /* How an apply sweeps M's factors (no reference counterpart: a query like
  * lssp_amd_mat_layout).  *line = 1 when the factors are a natural-ordered 5-/7-
  * point grid's ILU(0) and run as line sweeps, with tiles of *lines lines x
- * *planes planes (chosen per factor); 0 (and 0 x 0) for the general packet
- * sweeps.  Any pointer may be NULL. */
+ * *planes planes (chosen per factor); 2 when they are a 7-point grid's ILU(1)
+ * (fill offsets nx-1, nx*ny-nx, nx*ny-1) and run as skewed line sweeps
+ * (*lines = 16 lines of j + k, *planes = 8); 0 (and 0 x 0) for the general
+ * packet sweeps.  Any pointer may be NULL. */
 int lssp_amd_ilu_sweep_layout(const lssp_amd_ilu *M, int *line, int *lines, int *planes);
 
 /* ---- Krylov solve: lssp_solver_solve (lssp.cxx:250-414) for BiCGSTAB

@@ -921,7 +921,7 @@ int lssp_amd_ilu_sweep_layout(const lssp_amd_ilu *M, int *line, int *lines, int 
 {
     if (!M) return LSSP_AMD_EINVAL;
     const bool ls = M->line.ntiles > 0;
-    if (line) *line = ls ? 1 : 0;
+    if (line) *line = ls ? 1 + M->line.kind : 0;
     if (lines) *lines = ls ? M->line.NJ : 0;
     if (planes) *planes = ls ? M->line.P : 0;
     return LSSP_AMD_OK;

@@ -208,6 +208,7 @@ struct LineSweep {
 struct LineILU {
     LineGeom g;
     int P = 4, NJ = 64, LV = 1, W = 0, S = 0, tmax = 0, ntiles = 0;
+    int kind = 0;  // 0: 7-point ILU(0) (linesweep.hip); 1: 7-point ILU(1) pattern (linefill.hip)
     LineSweep L, U;
     double *d_ustream = nullptr;  // the U sweep's rhs, written by the L sweep
     double *d_lstream = nullptr;  // the L sweep's rhs in its stream layout (k_line_rhs)
@@ -366,6 +367,12 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
                      const std::vector<double> &Lx, const std::vector<int> &Up, const std::vector<int> &Uj,
                      const std::vector<double> &Ux, LineILU &li);
 int line_rearm(lssp_amd_ctx *c, LineILU &li);
+// linefill.hip: the 7-point ILU(1) pattern (EUNSUPPORTED when the factor is not it)
+int build_linefill(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std::vector<int> &Lj,
+                   const std::vector<double> &Lx, const std::vector<int> &Up, const std::vector<int> &Uj,
+                   const std::vector<double> &Ux, LineILU &li);
+int launch_linefill_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs);
+int launch_linefill_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs);
 void free_line_sweep(LineILU &li);
 int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs);
 int launch_line_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs);

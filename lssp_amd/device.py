@@ -283,11 +283,12 @@ class DILU:
         self.levelsL, self.levelsU, self.setup_seconds = ll.value, lu.value, ts.value
 
     def sweep_layout(self):
-        """(line sweeps?, tile lines, tile planes) -- lssp_amd_ilu_sweep_layout."""
+        """(line sweeps: 0 none, 1 ILU(0) grid, 2 ILU(1) grid; tile lines, tile planes)
+        -- lssp_amd_ilu_sweep_layout."""
         a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _ck(self.dev.L.lssp_amd_ilu_sweep_layout(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
             "ilu_sweep_layout")
-        return bool(a.value), b.value, c.value
+        return a.value, b.value, c.value
 
     @classmethod
     def create(cls, dev: Device, Ap, Aj, Ax, kind=ILUK, level=0, tol=1e-3, p=-1, blk=0):

@@ -251,6 +251,39 @@ def test_line_sweep_tile_shapes_bitwise_vs_oracle(dev, monkeypatch, nx, ny, nz, 
     assert np.array_equal(z.download(), up)
 
 
+# ILU(1) of a 7-point box: skewed line sweeps (linefill.hip).  Boxes with one
+# or several j' columns and k-tiles, partial 8-plane tiles (6, 13 = 8 + 5,
+# 35 = 4 x 8 + 3, 2), thin lines (nx = 3) and few lines per plane (ny = 3, 4).
+@pytest.mark.parametrize("nx,ny,nz", [(20, 17, 6), (13, 37, 35), (9, 21, 13), (40, 33, 19), (3, 3, 2),
+                                      (11, 16, 4), (5, 40, 9), (33, 4, 17), (24, 24, 24), (30, 27, 1),
+                                      (100, 100, 1)])
+def test_line_sweep_ilu1_bitwise_vs_oracle(dev, nx, ny, nz):
+    import lssp_amd
+    Ap, Aj, Ax = _box7(nx, ny, nz, 7 * nx + ny + nz)
+    n = Ap.size - 1
+    M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=1, level=1)
+    assert M.sweep_layout() == (2, 16, 8)
+    L, U = O.ilu(O.CSR(n, Ap, Aj, Ax), "iluk", level=1)
+    (Lp, Lj, Lx), (Up, Uj, Ux) = M.factors()
+    assert np.array_equal(Lj, L.Aj) and np.array_equal(Lx, L.Ax) and np.array_equal(Ux, U.Ax)
+    x = dev.vec(n)
+    for rep in range(4):  # repeated applies: the shared hand-off buffers must be re-armed exactly
+        rhs = uniform(400 + rep, n)
+        M.apply(x, dev.vec(n, rhs))
+        assert np.array_equal(x.download(), O.ilu_apply(L, U, rhs)), rep
+    rhs = uniform(500, n)
+    z = dev.vec(n)
+    one = O.CSR(n, np.arange(n + 1, dtype=np.int32), np.arange(n, dtype=np.int32), np.ones(n))
+    M.trisolve(0, z, dev.vec(n, rhs))
+    assert np.array_equal(z.download(), O.ilu_apply(L, one, rhs))
+    M.trisolve(1, z, dev.vec(n, rhs))
+    assert np.array_equal(z.download(), O.ilu_apply(one, U, rhs))
+    # x aliasing rhs (lssp_pc_ilu_solve may be called in place)
+    y = dev.vec(n, rhs)
+    M.apply(y, y)
+    assert np.array_equal(y.download(), O.ilu_apply(L, U, rhs))
+
+
 @pytest.mark.parametrize("seed,n,per_row,missing,blk", [(11, 3000, 6, 0, 0), (12, 2500, 9, 7, 0),
                                                         (13, 4000, 5, 0, 1000), (14, 1999, 4, 5, 333)])
 def test_gpu_ilu0_factorization_bitwise_vs_oracle(dev, seed, n, per_row, missing, blk):

@@ -98,3 +98,21 @@ def test_line2_instantiations_hazard_free_and_no_scratch(line_asm):
         assert check_vmcnt.check_loader(line_asm, name) == 0, name
         m = re.search(r"\.amdhsa_kernel " + name + r"\n(.*?)\.end_amdhsa_kernel", text, re.S)
         assert int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", m.group(1)).group(1)) == 0, name
+
+
+@pytest.fixture(scope="module")
+def fill_asm(tmp_path_factory):
+    return _compile(tmp_path_factory, "linefill.hip")
+
+
+def test_linefill_instantiations_hazard_free_and_no_scratch(fill_asm):
+    """k_linef (the 7-point ILU(1) line sweep): every instantiation hazard-free
+    on its loaders' / poller's asm-issued DMAs and without scratch."""
+    import check_vmcnt
+    names = sorted(set(re.findall(r"^(_ZN8lssp_amd7k_linef\w+):", open(fill_asm).read(), re.M)))
+    assert len(names) >= 4, names
+    text = open(fill_asm).read()
+    for name in names:
+        assert check_vmcnt.check_loader(fill_asm, name) == 0, name
+        m = re.search(r"\.amdhsa_kernel " + name + r"\n(.*?)\.end_amdhsa_kernel", text, re.S)
+        assert int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", m.group(1)).group(1)) == 0, name
