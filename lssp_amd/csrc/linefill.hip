@@ -381,7 +381,11 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
     constexpr int LA = 2;  // the loaders complete step s+LA's slot during step s
     constexpr int R = D + 1;
     constexpr int RSL = rsl<OUT>();
+#ifndef LINEF_NITEM
     constexpr int NITEM = SL::NPC + SL::NRP;
+#else
+    constexpr int NITEM = LINEF_NITEM;  // timing experiments only: a step's later DMA pieces are not loaded
+#endif
     constexpr int KPER = (NITEM + NL - 1) / NL;
     constexpr int S0 = -2 * ((D + 2) / 2);  // first step of every role (even, <= -D-1)
     constexpr int SC = -1;                  // first computed step: levels -2, -1 prime S, B
@@ -516,7 +520,11 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
                         r = r - cur.c[3][lv] * sep;
                         r = r - cur.c[4][lv] * se;
                         r = r - cur.c[5][lv] * xp;
+#ifndef LINEF_NODIV
                         if constexpr (NA == 7) r = r / cur.c[6][lv];
+#else
+                        if constexpr (NA == 7) r = r * cur.c[6][lv];  // timing experiments only
+#endif
                         const bool ok = lane_ok && (unsigned)(v - off) < (unsigned)nx;
                         const double x = sel_lanes(__builtin_amdgcn_ballot_w64(ok), r, 0.0);
                         publish(v, x, se);

@@ -130,3 +130,35 @@ def test_ilut_128_factors_apply_and_gmres_tree_bitwise():
         assert _bits_equal(xs.download(), o.x)
     finally:
         dev.close()
+
+
+def test_ilu1_line_sweeps_128_and_exam_matrix_bitwise():
+    """ILU(1) -- the reference's default level (pc.cxx:3) -- on the skewed line
+    sweeps (linefill.hip): 7-pt 128^3 (2 x 763 levels, 144 x 2 tiles) and the
+    5-pt 100^2 Laplacian of exam.cxx: factors equal the oracle's, one apply and
+    both single sweeps bitwise."""
+    import lssp_amd
+    dev = lssp_amd.Device(0)
+    try:
+        for dim, N in ((3, 128), (2, 100)):
+            Ap, Aj, Ax = lssp_amd.poisson(dim, N)
+            n = Ap.size - 1
+            M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=1)
+            assert M.sweep_layout() == (2, 16, 8)
+            if dim == 3:
+                assert M.levelsL == 6 * N - 5
+            L, U = O.ilu(O.CSR(n, Ap, Aj, Ax), "iluk", level=1)
+            (Lp, Lj, Lx), (Up, Uj, Ux) = M.factors()
+            assert _bits_equal(Lx, L.Ax) and _bits_equal(Ux, U.Ax)
+            rhs = uniform(777 + dim, n)
+            y = dev.vec(n)
+            M.apply(y, dev.vec(n, rhs))
+            assert _bits_equal(y.download(), O.ilu_apply(L, U, rhs))
+            one = O.CSR(n, np.arange(n + 1, dtype=np.int32), np.arange(n, dtype=np.int32), np.ones(n))
+            M.trisolve(0, y, dev.vec(n, rhs))
+            assert _bits_equal(y.download(), O.ilu_apply(L, one, rhs))
+            M.trisolve(1, y, dev.vec(n, rhs))
+            assert _bits_equal(y.download(), O.ilu_apply(one, U, rhs))
+            M.close()
+    finally:
+        dev.close()

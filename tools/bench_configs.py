@@ -69,10 +69,11 @@ def apply_leg(dev, M, n, reps=5):
     M.apply(z, x)
     s, e0, e1 = _events(dev)
     e0.record(s)
-    for _ in range(reps):
-        M.apply(z, x)
+    for _ in range(reps):  # queued back to back (the synchronous apply adds a host round trip per call)
+        M.apply_async(z, x)
     e1.record(s)
     e1.synchronize()
+    M.check()
     ms = e0.elapsed_time(e1) / reps
     b = 12 * (M.nnzL + M.nnzU) + 8 * (n + 1) + 32 * n
     return {"ms": round(ms, 4), "GBps": round(b / ms / 1e6, 1), "bytes": b, "levels_L": M.levelsL,
@@ -231,8 +232,8 @@ def general_ilu(args):
         A = lssp_amd.DMat(dev, Ap, Aj, Ax)
         out = {"case": name, "rows": n, "nnz": nnz, "ilu": {"level": level, "nnzL": M.nnzL, "nnzU": M.nnzU,
                                                             "setup_s": round(t_pc, 2),
-                                                            "sweeps": "line" if line and "7-pt" in name and level == 0
-                                                            else "packet"},
+                                                            "sweeps": ["packet", "line ILU(0)", "line ILU(1)"][
+                                                                M.sweep_layout()[0]]},
                "ilu_apply": apply_leg(dev, M, n, reps=10)}
         timed_solve(dev, A, M, n, lssp_amd.BICGSTAB, 5)
         r, t = timed_solve(dev, A, M, n, lssp_amd.BICGSTAB, args.iters)
@@ -249,7 +250,11 @@ def general_ilu(args):
     Ap, Aj, Ax = thermal_like()
     case("thermal-like ILU(0)", Ap, Aj, Ax, 0, True, ref_iters=args.ref_iters)
     Ap, Aj, Ax = lssp_amd.poisson(3, 128)
-    case("7-pt 128^3 ILU(1)", Ap, Aj, Ax, 1, True)
+    case("7-pt 128^3 ILU(1), line sweeps", Ap, Aj, Ax, 1, True)
+    case("7-pt 128^3 ILU(1), packet sweeps", Ap, Aj, Ax, 1, False)
+    Ap, Aj, Ax = lssp_amd.poisson(2, 100)
+    case("5-pt 100^2 ILU(1) (exam.cxx's matrix), line sweeps", Ap, Aj, Ax, 1, True)
+    case("5-pt 100^2 ILU(1) (exam.cxx's matrix), packet sweeps", Ap, Aj, Ax, 1, False)
     Ap, Aj, Ax = lssp_amd.poisson(3, args.grid)
     case(f"7-pt {args.grid}^3 ILU(0), packet sweeps", Ap, Aj, Ax, 0, False)
     case(f"7-pt {args.grid}^3 ILU(0), line sweeps", Ap, Aj, Ax, 0, True)

@@ -3,6 +3,7 @@
 
     python tools/line_diag.py [N] [diag,diag,...]
 
+LINE_DIAG_LEVEL=1 times the ILU(1) factor's sweeps instead of ILU(0)'s.
 For each LSSP_AMD_LINE_DIAG value (linesweep.hip; results are WRONG when it is
 non-zero: 1 storers skip the output stores, 2 loaders skip their DMAs,
 4 multiply instead of divide, 8 the poller does not wait for producers,
@@ -26,7 +27,8 @@ def main():
     dev = lssp_amd.Device(0)
     Ap, Aj, Ax = lssp_amd.poisson(3, N)
     n = Ap.size - 1
-    M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=0)
+    level = int(os.environ.get("LINE_DIAG_LEVEL", "0"))  # 1: the ILU(1) line sweeps (linefill.hip)
+    M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=level)
     r = dev.vec(n, np.random.default_rng(0).uniform(-1, 1, n))
     x, y = dev.vec(n), dev.vec(n)
     s = torch.cuda.ExternalStream(dev.stream)
@@ -48,7 +50,7 @@ def main():
     M.apply(x, r)
     got = x.download()
     os.environ["LSSP_AMD_LINE"] = "0"
-    Mp = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=0)
+    Mp = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=level)
     os.environ.pop("LSSP_AMD_LINE")
     Mp.apply(x, r)
     ref = x.download()
@@ -72,7 +74,8 @@ def timings(M, r, x, y, diags, timeit, N, dev):
         out = {"N": N, "diag": d,
                "L_us": t(lambda: M.trisolve(0, y, r)),
                "U_us": t(lambda: M.trisolve(1, x, y)),
-               "apply_us": t(lambda: M.apply(x, r))}
+               "apply_us": t(lambda: M.apply(x, r)),
+               "apply_async_us": t(lambda: M.apply_async(x, r))}
         print(json.dumps(out), flush=True)
     os.environ["LSSP_AMD_LINE_DIAG"] = "0"
     dev.close()
