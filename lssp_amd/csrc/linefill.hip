@@ -767,7 +767,11 @@ namespace {
 #define LINEF_D 6  // loader lead (steps of two levels)
 #endif
 #ifndef LINEF_DH
-#define LINEF_DH 3  // poller lead (steps)
+// poller lead (steps): 2 measured faster than 3 on both sweeps (128^3 ILU(1):
+// L 382 / U 410 against 409 / 436 us; loading only 4 of the step's 16 KB
+// changed little, so the sweeps are bound by their chain and hops, not by the
+// loaders; profiles/r04/r04k_linef_variants_128.txt)
+#define LINEF_DH 2
 #endif
 constexpr int LF_NL = 4, LF_SW = 4;
 
