@@ -955,8 +955,21 @@ __global__ __launch_bounds__(1024) void k_cg_fused(CgFusedArgs a)
         return;
     }
     {
+        // lane t adds partials t, t+1024, ... in order; the loads of 8 of them
+        // are issued before the adds (k_reduce2m's form), so the prologue waits
+        // for one L2 round trip instead of one per partial
         double acc = 0.0;
-        for (long k = tid; k < a.C; k += L2_LANES) acc += a.pin[k];
+        for (long k0 = tid; k0 < a.C; k0 += 8L * L2_LANES) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const long k = k0 + (long)u * L2_LANES;
+                v[u] = k < a.C ? a.pin[k] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (k0 + (long)u * L2_LANES < a.C) acc += v[u];
+        }
         acc = wave_sum(acc);
         if (lane == 0) wl[wave] = acc;
         __syncthreads();

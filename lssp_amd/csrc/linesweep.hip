@@ -126,9 +126,10 @@ static bool detect_grid(int n, const std::vector<int> &Lp, const std::vector<int
     return true;
 }
 
-// k_line2's plane skew: compute wave w owns planes 4w .. 4w+3 and runs w
-// levels later, so the k-input of a wave's first plane is one whole step old
-static inline int line_sigma(int LV, int P, int p) { return LV == 2 ? p / 4 : 0; }
+// k_line2's plane skew: compute wave w owns planes 4w .. 4w+3 and runs
+// (LV-1) w levels later, so the k-input of a wave's first plane is one whole
+// step (LV levels) old
+static inline int line_sigma(int LV, int P, int p) { return LV >= 2 ? (LV - 1) * (p / 4) : 0; }
 
 // rows of a tile (nj lines, np planes) valid at level s, plane p: lanes [lo, hi]
 // (row i = s - l - p - sigma(p))
@@ -258,7 +259,7 @@ static int upload_sweep(lssp_amd_ctx *c, const LineGeom &g, const std::vector<Li
     LSSP_HIP(hipMemcpy(ls.d_coef, coef.data(), sizeof(double) * coef.size(), hipMemcpyHostToDevice));
     LSSP_HIP(hipMalloc(&ls.d_claim, sizeof(unsigned long long)));
     LSSP_HIP(hipMemset(ls.d_claim, 0, sizeof(unsigned long long)));
-    if (LV == 2) {
+    if (LV >= 2) {
         // k_line2 claims tiles by anti-diagonal J + K (then K): a claimed tile's
         // producers (J-1, K) and (J, K-1) were claimed before it, and the
         // workgroups hold tiles of the advancing wavefront instead of tiles
@@ -323,7 +324,8 @@ static void line_plan(const LineGeom &g, int &P, int &NJ, int &LV)
     // profiles/r04/r04e_*, r04f_line2_512_p8_p16.txt)
     P = 8;
     NJ = 16;
-    LV = 2;
+    const char *lv = getenv("LSSP_AMD_LINE_LV");  // 2 or 4 levels per workgroup step (4: unit L only)
+    LV = lv && atoi(lv) == 4 && g.unitL ? 4 : 2;
 }
 
 int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std::vector<int> &Lj,
@@ -1042,10 +1044,10 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
 // the extra operand cost as much as the shorter chain saves.
 
 namespace l2 {
-constexpr int NJ = 16, LV = 2;  // lines per tile, levels per step; P (8 or 16) planes per tile: 2 or 4 compute waves
+constexpr int NJ = 16;  // lines per tile; LV (2 or 4) levels per step; P (8 or 16) planes per tile: 2 or 4 compute waves
 constexpr uint64_t GS = 0x0001000100010001ull;  // line 0 of each 16-lane group
 constexpr uint64_t G0M = 0xFFFFull;             // group 0 (the wave's first plane)
-template <int NA, int P>
+template <int NA, int P, int LV>
 struct Slot {
     static constexpr int ROWS = P * NJ;
     static constexpr int NPC = (LV * ROWS * NA * 8 + 1023) / 1024;  // 1 KB DMA pieces of the two coefficient blocks
@@ -1058,23 +1060,24 @@ struct Slot {
     static_assert(BYTES % 16 == 0, "slot alignment");
 };
 // levels of results kept in LDS: the storers' source (OUT 1 writes 8-level
-// blocks as runs, so it keeps two) and wave 1's k-input
-template <int OUT>
-constexpr int rsl() { return OUT == 1 ? 16 : 4; }
-template <int NA, int OUT, int D, int P>
-constexpr int lds_bytes() { return (D + 1) * Slot<NA, P>::BYTES + rsl<OUT>() * P * NJ * 8 + 16 + 512; }
+// blocks as runs, so it keeps two) and wave 1's k-input (LV levels back)
+template <int OUT, int LV>
+constexpr int rsl() { return OUT == 1 ? 16 : 2 * LV; }
+template <int NA, int OUT, int D, int P, int LV>
+constexpr int lds_bytes() { return (D + 1) * Slot<NA, P, LV>::BYTES + rsl<OUT, LV>() * P * NJ * 8 + 16 + 512; }
 constexpr int waves(int P, int NL, int SW) { return P / 4 + NL + 1 + SW; }
 }  // namespace l2
 
-template <int P, int NA, int OUT, int NL, int D, int DH, int SW, bool TRACE>
+template <int P, int LV, int NA, int OUT, int NL, int D, int DH, int SW, bool TRACE>
 __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
 {
     using namespace l2;
-    using SL = Slot<NA, P>;
+    using SL = Slot<NA, P, LV>;
+    static_assert(LV == 2 || LV == 4, "levels per step");
     constexpr int CW = P / 4, ROWS = P * NJ;
     constexpr int LA = 2;  // the loaders complete step s+LA's slot during step s
     constexpr int R = D + 1;
-    constexpr int RSL = rsl<OUT>();
+    constexpr int RSL = rsl<OUT, LV>();
     constexpr int NITEM = SL::NPC + SL::NRP;  // DMA instructions per step, shared by the loaders
     constexpr int KPER = (NITEM + NL - 1) / NL;
     constexpr int S0 = -2 * ((D + 2) / 2);  // first step of every role (even, <= -D-1)
@@ -1116,14 +1119,14 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
             const long r = ((long)(d.k0 + p) * a.ny + (d.j0 + l)) * nx;
             return a.mirror ? a.n - 1 - r : r;
         };
-        auto sig = [](int p) { return p >> 2; };
+        auto sig = [](int p) { return (LV - 1) * (p >> 2); };
         unsigned long long *ts = TRACE ? a.trace + 8 * (long)a.ntiles : nullptr;
         const bool trs = TRACE && t == a.ttile && lane == 0;
 
         if (wave < CW) {
             // ---------------- compute: plane pw = 4 wave + g, line l ----------------
             const int pw = wave * 4 + gl;
-            const int sg = wave;  // sigma of the wave's planes
+            const int sg = (LV - 1) * wave;  // sigma of the wave's planes
             struct In {
                 double ck[LV], cj[LV], ci[LV], dg[LV], rh[LV], jv[LV];
             };
@@ -1199,43 +1202,37 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                 const unsigned sn = so + SL::BYTES == RB ? 0u : so + SL::BYTES;  // slot of step s+1
                 // k-inputs of group 0 (read first: LDS returns in order): wave 0 the
                 // poller's, wave 1 plane 3's results of the previous step
-                double kx0, kx1;
-                if (wave == 0) {
-                    kx0 = reinterpret_cast<const double *>(ring + so + SL::KFIN)[ll];
-                    kx1 = reinterpret_cast<const double *>(ring + so + SL::KFIN)[NJ + ll];
-                } else {
-                    kx0 = res[((2 * s - 2) & (RSL - 1)) * ROWS + (4 * wave - 1) * NJ + ll];
-                    kx1 = res[((2 * s - 1) & (RSL - 1)) * ROWS + (4 * wave - 1) * NJ + ll];
-                }
+                double kx[LV];
+#pragma unroll
+                for (int lv = 0; lv < LV; lv++)
+                    kx[lv] = wave == 0 ? reinterpret_cast<const double *>(ring + so + SL::KFIN)[lv * NJ + ll]
+                                       : res[((LV * s - LV + lv) & (RSL - 1)) * ROWS + (4 * wave - 1) * NJ + ll];
                 asm volatile("" ::: "memory");
                 load(sn, nxt);
-                const uint64_t h0 = (((hw << 1) & ~GS) | starts(2 * s)) & pm;
-                const uint64_t h1 = (((h0 << 1) & ~GS) | starts(2 * s + 1)) & pm;
-                hw = h1;
+                uint64_t h[LV];
+#pragma unroll
+                for (int lv = 0; lv < LV; lv++)
+                    h[lv] = ((((lv ? h[lv - 1] : hw) << 1) & ~GS) | starts(LV * s + lv)) & pm;
+                hw = h[LV - 1];
                 if (s >= 0 && s < TS) {
-                    // level 2s
-                    double xk = sel_lanes(G0M, kx0, xs);
-                    double xj = dpp_shr1g<4>(xp, cur.jv[0]);
-                    double v = cur.rh[0] - cur.ck[0] * xk;
-                    v = v - cur.cj[0] * xj;
-                    v = v - cur.ci[0] * xp;
-                    if constexpr (NA == 4) v = v / cur.dg[0];
-                    const double x0 = sel_lanes(h0, v, xp);
-                    publish(2 * s, h0, x0);  // its store issues under level 2s+1's arithmetic
-                    res[((2 * s) & (RSL - 1)) * ROWS + pw * NJ + ll] = x0;
-                    // level 2s + 1
-                    xk = sel_lanes(G0M, kx1, up16(x0));
-                    xj = dpp_shr1g<4>(x0, cur.jv[1]);
-                    v = cur.rh[1] - cur.ck[1] * xk;
-                    v = v - cur.cj[1] * xj;
-                    v = v - cur.ci[1] * x0;
-                    if constexpr (NA == 4) v = v / cur.dg[1];
-                    const double x1 = sel_lanes(h1, v, x0);
-                    if (trs && wave == 0) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
-                    publish(2 * s + 1, h1, x1);
-                    res[((2 * s + 1) & (RSL - 1)) * ROWS + pw * NJ + ll] = x1;
-                    xp = x1;
-                    xs = up16(x1);  // the next step's first k-operand, off its critical path
+                    double xq = xp;  // the previous level's value
+#pragma unroll
+                    for (int lv = 0; lv < LV; lv++) {
+                        // level LV s + lv
+                        const double xk = sel_lanes(G0M, kx[lv], lv == 0 ? xs : up16(xq));
+                        const double xj = dpp_shr1g<4>(xq, cur.jv[lv]);
+                        double v = cur.rh[lv] - cur.ck[lv] * xk;
+                        v = v - cur.cj[lv] * xj;
+                        v = v - cur.ci[lv] * xq;
+                        if constexpr (NA == 4) v = v / cur.dg[lv];
+                        const double x = sel_lanes(h[lv], v, xq);
+                        if (trs && wave == 0 && lv == LV - 1) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
+                        publish(LV * s + lv, h[lv], x);  // its store issues under the next level's arithmetic
+                        res[((LV * s + lv) & (RSL - 1)) * ROWS + pw * NJ + ll] = x;
+                        xq = x;
+                    }
+                    xp = xq;
+                    xs = up16(xq);  // the next step's first k-operand, off its critical path
                 }
                 so = sn;
                 if (trs && s >= 0 && s < TS) ts[8 * s + (wave == 0 ? 1 : 7)] = __builtin_amdgcn_s_memtime();
@@ -1386,18 +1383,19 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     hji[(long)vj * P] = TRI_SENTINEL;
             };
             if constexpr (OUT == 1) {
-                // block B (levels 8B .. 8B+7, steps 4B .. 4B+3) is written during
-                // steps 4B+4 .. 4B+7, a quarter per step: value k of the block is
-                // level 8B + (k & 7) of run k >> 3 = (plane, line), so 8 lanes store
-                // 8 consecutive rows of one line
-                static_assert(RSL == 16 && (2 * ROWS) % (64 * SW) == 0, "runs");
+                // block B (levels 8B .. 8B+7, steps SPB B .. SPB B + SPB-1, SPB =
+                // 8 / LV) is written during the next SPB steps, 1 / SPB of it per
+                // step: value k of the block is level 8B + (k & 7) of run k >> 3 =
+                // (plane, line), so 8 lanes store 8 consecutive rows of one line
+                constexpr int SPB = 8 / LV;
+                static_assert(RSL == 16 && (ROWS * 8 / SPB) % (64 * SW) == 0, "runs");
                 auto slice = [&](int s) {
-                    const int B = (s >> 2) - 1, u = s & 3;
+                    const int B = s / SPB - 1, u = s % SPB;
                     if (B < 0) return;
-                    constexpr int PER = ROWS * 8 / 4 / 64 / SW;  // values per lane per step
+                    constexpr int PER = ROWS * 8 / SPB / 64 / SW;  // values per lane per step
 #pragma unroll
                     for (int it = 0; it < PER; it++) {
-                        const int k = u * (ROWS * 2) + (w * PER + it) * 64 + lane;
+                        const int k = u * (ROWS * 8 / SPB) + (w * PER + it) * 64 + lane;
                         const int m = k & 7, r = k >> 3, p = r >> 4, l = r & (NJ - 1);
                         const int q = 8 * B + m;
                         const int i = q - l - p - sig(p);
@@ -1414,10 +1412,10 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     line_barrier();
                 }
                 // the last blocks' remaining quarters (every result is in LDS)
-                for (int s = TS + 1; s < 4 * ((T - 1) / 8) + 8; s++) slice(s);
+                for (int s = TS + 1; s < SPB * ((T - 1) / 8 + 2); s++) slice(s);
             } else {
-                // step s-1's two levels: value k = 64 (w + SW it) + lane is level
-                // 2(s-1) + (k >> 7), plane (k >> 4) & 7, line k & 15; its place in the
+                // step s-1's LV levels: value k = 64 (w + SW it) + lane is level
+                // LV(s-1) + k / ROWS, plane (k >> 4) & (P-1), line k & 15; its place in the
                 // mirror U tile's rhs stream (same nj, np): level Cp - v with
                 // Cp = nx + nj + np - 3 + sigma(p) + sigma(np-1-p)
                 constexpr int PS = LV * ROWS / 64 / SW;
@@ -1561,9 +1559,9 @@ static int launch_line_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a
 // step, 8 lanes store 8 consecutive stream entries.  Block b runs on XCD b % 8
 // and the XCD's blocks walk whole tiles in step order.
 constexpr int LRHS_RUN = 8;
-// P planes x NJ lines per tile; SKEW: k_line2's level map (planes >= P/2 one
-// level later); mirror: the tiles are a U sweep's (natural row n-1 - r)
-template <int P, int NJ, bool SKEW>
+// P planes x NJ lines per tile; SKEW: k_line2's level map (compute wave w's
+// planes SKEW w levels later); mirror: the tiles are a U sweep's (natural row n-1 - r)
+template <int P, int NJ, int SKEW>
 __global__ __launch_bounds__(256) void k_line_rhs(const LineTile *__restrict__ tiles, int ntiles, int nq, int nx,
                                                  int ny, long n, int mirror, const double *__restrict__ rhs,
                                                  double *__restrict__ out, const double *guard)
@@ -1580,7 +1578,7 @@ __global__ __launch_bounds__(256) void k_line_rhs(const LineTile *__restrict__ t
 #pragma unroll
     for (int it = 0; it < NV; it++) {
         const int k = it * 256 + threadIdx.x, m = k & 7, l = (k >> 3) % NJ, p = (k >> 3) / NJ;
-        const int i = q0 + m - l - p - (SKEW ? p / 4 : 0);
+        const int i = q0 + m - l - p - SKEW * (p / 4);
         const bool ok = q0 + m < d.T && p < d.np && l < d.nj && (unsigned)i < (unsigned)nx;
         const long r = ((long)(d.k0 + p) * ny + (d.j0 + l)) * nx + i;
         v[it] = ok ? rhs[mirror ? n - 1 - r : r] : 0.0;
@@ -1589,7 +1587,7 @@ __global__ __launch_bounds__(256) void k_line_rhs(const LineTile *__restrict__ t
 #pragma unroll
     for (int it = 0; it < NV; it++) {
         const int k = it * 256 + threadIdx.x, m = k & 7, l = (k >> 3) % NJ, p = (k >> 3) / NJ;
-        const int i = q0 + m - l - p - (SKEW ? p / 4 : 0);
+        const int i = q0 + m - l - p - SKEW * (p / 4);
         if (q0 + m < d.T && p < d.np && l < d.nj && (unsigned)i < (unsigned)nx)
             out[d.cbase + (q0 + m) * SB + p * d.nj + l] = v[it];
     }
@@ -1601,9 +1599,9 @@ static int launch_line_gather(lssp_amd_ctx *c, const LineSweep &ls, int mirror, 
 {
     const int nq = (ls.tmax + LRHS_RUN - 1) / LRHS_RUN;
     const long grid = 8L * ((ls.ntiles + 7) / 8) * nq;
-    auto kr = ls.LV == 2 ? k_line_rhs<8, 16, true>
-              : ls.P == 16 ? k_line_rhs<16, 16, false> : ls.P == 8 ? k_line_rhs<8, 32, false> : k_line_rhs<4, 64, false>;
-    if (ls.LV == 2 && (ls.P != 8 || ls.NJ != 16)) return LSSP_AMD_EUNSUPPORTED;
+    auto kr = ls.LV == 4 ? k_line_rhs<8, 16, 3> : ls.LV == 2 ? k_line_rhs<8, 16, 1>
+              : ls.P == 16 ? k_line_rhs<16, 16, 0> : ls.P == 8 ? k_line_rhs<8, 32, 0> : k_line_rhs<4, 64, 0>;
+    if (ls.LV >= 2 && (ls.P != 8 || ls.NJ != 16)) return LSSP_AMD_EUNSUPPORTED;
     const long n = (long)ls.nx * ls.ny * ls.nz;
     kr<<<grid, 256, 0, c->stream>>>(ls.d_tiles, ls.ntiles, nq, ls.nx, ls.ny, n, mirror, rhs, stream, c->guard);
     LSSP_HIP(hipGetLastError());
@@ -1623,12 +1621,21 @@ static int launch_line_gather(lssp_amd_ctx *c, const LineSweep &ls, int mirror, 
 #ifndef LINE2_SW
 #define LINE2_SW 4
 #endif
-template <int P>
-constexpr int line2_d() { return LINE2_D; }
-template <int P, int NA, int OUT, bool TRACE>
+// four levels per step: leads in (twice as long) steps
+#ifndef LINE4_D
+#define LINE4_D 4
+#endif
+#ifndef LINE4_DH
+#define LINE4_DH 2
+#endif
+template <int LV>
+constexpr int line2_d() { return LV == 4 ? LINE4_D : LINE2_D; }
+template <int LV>
+constexpr int line2_dh() { return LV == 4 ? LINE4_DH : LINE2_DH; }
+template <int P, int LV, int NA, int OUT, bool TRACE>
 static int launch_line2_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)
 {
-    auto kern = k_line2<P, NA, OUT, LINE2_NL, line2_d<P>(), LINE2_DH, LINE2_SW, TRACE>;
+    auto kern = k_line2<P, LV, NA, OUT, LINE2_NL, line2_d<LV>(), line2_dh<LV>(), LINE2_SW, TRACE>;
     static int attr = 0;
     if (lds > attr) {
         LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -1641,14 +1648,14 @@ static int launch_line2_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &
     return LSSP_AMD_OK;
 }
 
-template <int P, int NA, int OUT>
+template <int P, int LV, int NA, int OUT>
 static int launch_line2_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a)
 {
-    constexpr int lds = l2::lds_bytes<NA, OUT, line2_d<P>(), P>();
+    constexpr int lds = l2::lds_bytes<NA, OUT, line2_d<LV>(), P, LV>();
     static_assert(lds <= 160 * 1024, "LDS");
     // diagnostics only: LSSP_AMD_LINE_TRACE=path[:tile] appends one JSON line per sweep
     static const char *trp = getenv("LSSP_AMD_LINE_TRACE");
-    if (!trp) return launch_line2_k<P, NA, OUT, false>(c, ls, a, lds);
+    if (!trp) return launch_line2_k<P, LV, NA, OUT, false>(c, ls, a, lds);
     LineArgs g = a;
     const size_t tn = 8 * (size_t)ls.ntiles + 8 * (size_t)ls.tmax + 64;
     const char *colon = strrchr(trp, ':');
@@ -1656,7 +1663,7 @@ static int launch_line2_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &
     LSSP_HIP(hipMalloc(&g.trace, sizeof(unsigned long long) * tn));
     LSSP_HIP(hipMemsetAsync(g.trace, 0, sizeof(unsigned long long) * tn, c->stream));
     const int grid = std::min(ls.ntiles, c->num_cus);
-    LSSP_TRY((launch_line2_k<P, NA, OUT, true>(c, ls, g, lds)));
+    LSSP_TRY((launch_line2_k<P, LV, NA, OUT, true>(c, ls, g, lds)));
     std::vector<unsigned long long> h(tn);
     LSSP_HIP(hipMemcpyAsync(h.data(), g.trace, sizeof(unsigned long long) * tn, hipMemcpyDeviceToHost, c->stream));
     LSSP_HIP(hipStreamSynchronize(c->stream));
@@ -1664,9 +1671,9 @@ static int launch_line2_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &
     std::string path(trp, colon ? colon - trp : strlen(trp));
     FILE *f = fopen(path.c_str(), "a");
     if (f) {
-        fprintf(f, "{\"mirror\": %d, \"ntiles\": %d, \"W\": %d, \"ttile\": %d, \"T\": %d, \"LV\": 2, \"grid\": %d, "
+        fprintf(f, "{\"mirror\": %d, \"ntiles\": %d, \"W\": %d, \"ttile\": %d, \"T\": %d, \"LV\": %d, \"grid\": %d, "
                    "\"data\": [",
-                a.mirror, ls.ntiles, (ls.ny + ls.NJ - 1) / ls.NJ, g.ttile, ls.h_tiles[g.ttile].T / 2, grid);
+                a.mirror, ls.ntiles, (ls.ny + ls.NJ - 1) / ls.NJ, g.ttile, ls.h_tiles[g.ttile].T / LV, LV, grid);
         for (size_t i = 0; i < tn; i++) fprintf(f, "%s%llu", i ? ", " : "", h[i]);
         fprintf(f, "]}\n");
         fclose(f);
@@ -1701,12 +1708,12 @@ static int launch_line2(lssp_amd_ctx *c, const LineILU &li, int which, const dou
         const char *dg = getenv("LSSP_AMD_LINE_DIAG");
         a.diag = dg ? atoi(dg) : 0;
     }
-    auto go = [&](auto PP) {
-        constexpr int P = decltype(PP)::value;
-        if (outk == 2) return ls.NA == 3 ? launch_line2_t<P, 3, 2>(c, ls, a) : launch_line2_t<P, 4, 2>(c, ls, a);
-        return ls.NA == 3 ? launch_line2_t<P, 3, 1>(c, ls, a) : launch_line2_t<P, 4, 1>(c, ls, a);
-    };
-    return go(std::integral_constant<int, 8>());
+    if (ls.LV == 4) {  // unit L only (line_plan): the non-unit L sweep into the U stream would spill
+        if (outk == 2) return ls.NA == 3 ? launch_line2_t<8, 4, 3, 2>(c, ls, a) : LSSP_AMD_EUNSUPPORTED;
+        return ls.NA == 3 ? launch_line2_t<8, 4, 3, 1>(c, ls, a) : launch_line2_t<8, 4, 4, 1>(c, ls, a);
+    }
+    if (outk == 2) return ls.NA == 3 ? launch_line2_t<8, 2, 3, 2>(c, ls, a) : launch_line2_t<8, 2, 4, 2>(c, ls, a);
+    return ls.NA == 3 ? launch_line2_t<8, 2, 3, 1>(c, ls, a) : launch_line2_t<8, 2, 4, 1>(c, ls, a);
 }
 
 static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const double *rhs, bool u_in, double *out,
@@ -1744,7 +1751,7 @@ static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const doub
 int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs)
 {
     if (li.kind == 1) return launch_linefill_apply(c, li, x, rhs);
-    if (li.LV == 2) {  // k_line2: gather, L sweep -> the U rhs stream, U sweep -> x
+    if (li.LV >= 2) {  // k_line2: gather, L sweep -> the U rhs stream, U sweep -> x
         LSSP_TRY(launch_line_gather(c, li.L, 0, rhs, li.d_lstream));
         LSSP_TRY(launch_line2(c, li, 0, li.d_lstream, li.d_ustream, 2));
         return launch_line2(c, li, 1, li.d_ustream, x, 1);
@@ -1761,7 +1768,7 @@ int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const doubl
 int launch_line_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs)
 {
     if (li.kind == 1) return launch_linefill_sweep(c, li, which, x, rhs);
-    if (li.LV == 2) {  // one sweep: its rhs gathered into its own stream, natural-order output
+    if (li.LV >= 2) {  // one sweep: its rhs gathered into its own stream, natural-order output
         double *st = which ? li.d_ustream : li.d_lstream;
         LSSP_TRY(launch_line_gather(c, which ? li.U : li.L, which, rhs, st));
         return launch_line2(c, li, which, st, x, 1);
