@@ -1167,6 +1167,8 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
             // line nj-1 feeds the next j-tile: hj[q][p], q = v - (nj-1)
             const uint64_t jgm = jout ? (GS << (nj - 1)) & pm : 0ull;
             uint64_t hw = 0;  // lanes whose row exists at the previous level
+            const bool lane_in = (pm >> lane) & 1;  // LINE2_VMASK: row i = v - loff
+            const int loff = ll + pw + sg;
             // line 0 of group g has its row (i = v - p - sigma) at level v: 0 <= i < nx, in integer (SALU) ops
             auto starts = [&](int v) {
                 uint64_t m = 0;
@@ -1210,20 +1212,35 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                 asm volatile("" ::: "memory");
                 load(sn, nxt);
                 uint64_t h[LV];
+#ifndef LINE2_VMASK
 #pragma unroll
                 for (int lv = 0; lv < LV; lv++)
                     h[lv] = ((((lv ? h[lv - 1] : hw) << 1) & ~GS) | starts(LV * s + lv)) & pm;
                 hw = h[LV - 1];
+#else  // tuning: the row masks from one per-lane compare each (VALU) instead of the SALU shift chain
+#pragma unroll
+                for (int lv = 0; lv < LV; lv++)
+                    h[lv] = __builtin_amdgcn_ballot_w64(lane_in && (unsigned)(LV * s + lv - loff) < (unsigned)nx);
+#endif
                 if (s >= 0 && s < TS) {
                     double xq = xp;  // the previous level's value
 #pragma unroll
                     for (int lv = 0; lv < LV; lv++) {
                         // level LV s + lv
+#ifndef LINE2_HOIST
                         const double xk = sel_lanes(G0M, kx[lv], lv == 0 ? xs : up16(xq));
                         const double xj = dpp_shr1g<4>(xq, cur.jv[lv]);
                         double v = cur.rh[lv] - cur.ck[lv] * xk;
                         v = v - cur.cj[lv] * xj;
                         v = v - cur.ci[lv] * xq;
+#else  // tuning: the j and i products formed before the k operand's shuffle returns (same roundings)
+                        const double xj = dpp_shr1g<4>(xq, cur.jv[lv]);
+                        const double pj = cur.cj[lv] * xj, pi = cur.ci[lv] * xq;
+                        const double xk = sel_lanes(G0M, kx[lv], lv == 0 ? xs : up16(xq));
+                        double v = cur.rh[lv] - cur.ck[lv] * xk;
+                        v = v - pj;
+                        v = v - pi;
+#endif
                         if constexpr (NA == 4) v = v / cur.dg[lv];
                         const double x = sel_lanes(h[lv], v, xq);
                         if (trs && wave == 0 && lv == LV - 1) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
