@@ -324,8 +324,7 @@ static void line_plan(const LineGeom &g, int &P, int &NJ, int &LV)
     // profiles/r04/r04e_*, r04f_line2_512_p8_p16.txt)
     P = 8;
     NJ = 16;
-    const char *lv = getenv("LSSP_AMD_LINE_LV");  // 2 or 4 levels per workgroup step (4: unit L only)
-    LV = lv && atoi(lv) == 4 && g.unitL ? 4 : 2;
+    LV = 2;  // levels per workgroup step (4 measured slower)
 }
 
 int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std::vector<int> &Lj,
@@ -1166,19 +1165,8 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
             const int kq = -(np - 1) - sg;
             // line nj-1 feeds the next j-tile: hj[q][p], q = v - (nj-1)
             const uint64_t jgm = jout ? (GS << (nj - 1)) & pm : 0ull;
-            uint64_t hw = 0;  // lanes whose row exists at the previous level
-            const bool lane_in = (pm >> lane) & 1;  // LINE2_VMASK: row i = v - loff
-            const int loff = ll + pw + sg;
-            // line 0 of group g has its row (i = v - p - sigma) at level v: 0 <= i < nx, in integer (SALU) ops
-            auto starts = [&](int v) {
-                uint64_t m = 0;
-#pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const int y = v - (wave * 4 + g) - sg;
-                    m |= (uint64_t)(((unsigned)((y - nx) & ~y)) >> 31) << (16 * g);
-                }
-                return m;
-            };
+            const bool lane_in = (pm >> lane) & 1;  // a row of the tile: line < nj, plane < np
+            const int loff = ll + pw + sg;           // its row at level v: i = v - loff
             auto publish = [&](int v, uint64_t h, double x) {
                 const uint64_t bx = (uint64_t)__double_as_longlong(x);
                 if (kw) {  // uniform
@@ -1211,36 +1199,23 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                                        : res[((LV * s - LV + lv) & (RSL - 1)) * ROWS + (4 * wave - 1) * NJ + ll];
                 asm volatile("" ::: "memory");
                 load(sn, nxt);
+                // lanes whose row exists at each level: one per-lane compare each
+                // (a SALU chain of shifts and per-group start tests measured 3 %
+                // slower per apply, profiles/r04/r04n_line2_compute_variants.txt)
                 uint64_t h[LV];
-#ifndef LINE2_VMASK
-#pragma unroll
-                for (int lv = 0; lv < LV; lv++)
-                    h[lv] = ((((lv ? h[lv - 1] : hw) << 1) & ~GS) | starts(LV * s + lv)) & pm;
-                hw = h[LV - 1];
-#else  // tuning: the row masks from one per-lane compare each (VALU) instead of the SALU shift chain
 #pragma unroll
                 for (int lv = 0; lv < LV; lv++)
                     h[lv] = __builtin_amdgcn_ballot_w64(lane_in && (unsigned)(LV * s + lv - loff) < (unsigned)nx);
-#endif
                 if (s >= 0 && s < TS) {
                     double xq = xp;  // the previous level's value
 #pragma unroll
                     for (int lv = 0; lv < LV; lv++) {
                         // level LV s + lv
-#ifndef LINE2_HOIST
                         const double xk = sel_lanes(G0M, kx[lv], lv == 0 ? xs : up16(xq));
                         const double xj = dpp_shr1g<4>(xq, cur.jv[lv]);
                         double v = cur.rh[lv] - cur.ck[lv] * xk;
                         v = v - cur.cj[lv] * xj;
                         v = v - cur.ci[lv] * xq;
-#else  // tuning: the j and i products formed before the k operand's shuffle returns (same roundings)
-                        const double xj = dpp_shr1g<4>(xq, cur.jv[lv]);
-                        const double pj = cur.cj[lv] * xj, pi = cur.ci[lv] * xq;
-                        const double xk = sel_lanes(G0M, kx[lv], lv == 0 ? xs : up16(xq));
-                        double v = cur.rh[lv] - cur.ck[lv] * xk;
-                        v = v - pj;
-                        v = v - pi;
-#endif
                         if constexpr (NA == 4) v = v / cur.dg[lv];
                         const double x = sel_lanes(h[lv], v, xq);
                         if (trs && wave == 0 && lv == LV - 1) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
@@ -1638,17 +1613,11 @@ static int launch_line_gather(lssp_amd_ctx *c, const LineSweep &ls, int mirror, 
 #ifndef LINE2_SW
 #define LINE2_SW 4
 #endif
-// four levels per step: leads in (twice as long) steps
-#ifndef LINE4_D
-#define LINE4_D 4
-#endif
-#ifndef LINE4_DH
-#define LINE4_DH 2
-#endif
+// four levels per step (measured with leads 4 / 2 steps) are not instantiated
 template <int LV>
-constexpr int line2_d() { return LV == 4 ? LINE4_D : LINE2_D; }
+constexpr int line2_d() { return LV == 4 ? 4 : LINE2_D; }
 template <int LV>
-constexpr int line2_dh() { return LV == 4 ? LINE4_DH : LINE2_DH; }
+constexpr int line2_dh() { return LV == 4 ? 2 : LINE2_DH; }
 template <int P, int LV, int NA, int OUT, bool TRACE>
 static int launch_line2_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)
 {
@@ -1725,10 +1694,7 @@ static int launch_line2(lssp_amd_ctx *c, const LineILU &li, int which, const dou
         const char *dg = getenv("LSSP_AMD_LINE_DIAG");
         a.diag = dg ? atoi(dg) : 0;
     }
-    if (ls.LV == 4) {  // unit L only (line_plan): the non-unit L sweep into the U stream would spill
-        if (outk == 2) return ls.NA == 3 ? launch_line2_t<8, 4, 3, 2>(c, ls, a) : LSSP_AMD_EUNSUPPORTED;
-        return ls.NA == 3 ? launch_line2_t<8, 4, 3, 1>(c, ls, a) : launch_line2_t<8, 4, 4, 1>(c, ls, a);
-    }
+    // (the kernel is generic in LV; four levels per step measured slower)
     if (outk == 2) return ls.NA == 3 ? launch_line2_t<8, 2, 3, 2>(c, ls, a) : launch_line2_t<8, 2, 4, 2>(c, ls, a);
     return ls.NA == 3 ? launch_line2_t<8, 2, 3, 1>(c, ls, a) : launch_line2_t<8, 2, 4, 1>(c, ls, a);
 }

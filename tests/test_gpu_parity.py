@@ -223,16 +223,11 @@ def _box7(nx, ny, nz, seed):
                                                 (20, 40, 40, (16, 16), 1), (13, 37, 35, (16, 16), 1),
                                                 (20, 100, 6, (16, 8), 2), (13, 37, 35, (16, 8), 2),
                                                 (9, 21, 13, (16, 8), 2), (20, 17, 6, (16, 8), 2),
-                                                (11, 16, 4, (16, 8), 2), (40, 33, 19, (16, 8), 2),
-                                                (20, 100, 6, (16, 8), 4), (13, 37, 35, (16, 8), 4),
-                                                (9, 21, 13, (16, 8), 4), (20, 17, 6, (16, 8), 4),
-                                                (11, 16, 4, (16, 8), 4), (40, 33, 19, (16, 8), 4)])
+                                                (11, 16, 4, (16, 8), 2), (40, 33, 19, (16, 8), 2)])
 def test_line_sweep_tile_shapes_bitwise_vs_oracle(dev, monkeypatch, nx, ny, nz, tile, mode):
-    """mode 1: k_line; 2: k_line2, two levels per step (the default); 4: k_line2,
-    four levels per step (LSSP_AMD_LINE_LV=4)"""
+    """mode 1: k_line; 2: k_line2 (the default)"""
     import lssp_amd
-    monkeypatch.setenv("LSSP_AMD_LINE_MODE", str(min(mode, 2)))
-    monkeypatch.setenv("LSSP_AMD_LINE_LV", "4" if mode == 4 else "2")
+    monkeypatch.setenv("LSSP_AMD_LINE_MODE", str(mode))
     Ap, Aj, Ax = _box7(nx, ny, nz, nx + ny + nz)
     n = Ap.size - 1
     M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=1, level=0)
