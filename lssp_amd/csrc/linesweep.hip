@@ -1616,12 +1616,15 @@ static int launch_line_gather(lssp_amd_ctx *c, const LineSweep &ls, int mirror, 
 // four levels per step (measured with leads 4 / 2 steps) are not instantiated
 template <int LV>
 constexpr int line2_d() { return LV == 4 ? 4 : LINE2_D; }
-template <int LV>
-constexpr int line2_dh() { return LV == 4 ? 2 : LINE2_DH; }
+#ifndef LINE2_DH_U
+#define LINE2_DH_U LINE2_DH  // the poller lead of the sweeps with natural-order output (OUT 1)
+#endif
+template <int LV, int OUT>
+constexpr int line2_dh() { return LV == 4 ? 2 : OUT == 1 ? LINE2_DH_U : LINE2_DH; }
 template <int P, int LV, int NA, int OUT, bool TRACE>
 static int launch_line2_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)
 {
-    auto kern = k_line2<P, LV, NA, OUT, LINE2_NL, line2_d<LV>(), line2_dh<LV>(), LINE2_SW, TRACE>;
+    auto kern = k_line2<P, LV, NA, OUT, LINE2_NL, line2_d<LV>(), line2_dh<LV, OUT>(), LINE2_SW, TRACE>;
     static int attr = 0;
     if (lds > attr) {
         LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
