@@ -743,23 +743,36 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
 // ---------------------------------------------------------------------------
 // rhs gather and launches
 // ---------------------------------------------------------------------------
-// the natural-order rhs into a sweep's stream: block = (tile, step), thread =
-// (level, plane, line); rows off the grid stay +0.0 (the stream was zeroed)
-__global__ __launch_bounds__(256) void k_linef_rhs(const LineTile *__restrict__ tiles, int nts, int nx, int ny, long n,
+// the natural-order rhs into a sweep's stream: block = (tile, 16 consecutive
+// levels); value k of the block is level q0 + (k & 15) of line (k >> 4) & 15 of
+// plane k >> 8, so 16 neighbouring lanes read one 128-byte run of a grid line
+// (consecutive levels are consecutive rows i); rows off the grid stay +0.0 (the
+// stream was zeroed).  All loads are issued before the stores.
+constexpr int LF_RUN = 16;
+__global__ __launch_bounds__(256) void k_linef_rhs(const LineTile *__restrict__ tiles, int nq, int nx, int ny, long n,
                                                   int mirror, const double *__restrict__ rhs,
                                                   double *__restrict__ out, const double *guard)
 {
     using namespace lf;
     if (guard && *guard != 0.0) return;  // a batched iteration past the stop (lssp_amd_ctx::guard)
-    const int t = blockIdx.x / nts, s = blockIdx.x % nts;
+    const int t = blockIdx.x / nq, q0 = (blockIdx.x % nq) * LF_RUN;
     const LineTile d = tiles[t];
-    if (2 * s >= d.T) return;
-    const int lv = threadIdx.x >> 7, p = (threadIdx.x >> 4) & 7, l = threadIdx.x & 15;
-    const int v = 2 * s + lv, i = v - 2 * l - p - sig(p), j = d.j0 + l - d.k0 - p;
-    if (p < d.np && l < d.nj && (unsigned)j < (unsigned)ny && (unsigned)i < (unsigned)nx) {
+    if (q0 >= d.T) return;
+    constexpr int NV = P * NJ * LF_RUN / 256;
+    double v[NV];
+    long o[NV];
+#pragma unroll
+    for (int it = 0; it < NV; it++) {
+        const int k = it * 256 + threadIdx.x, m = k & (LF_RUN - 1), l = (k >> 4) & (NJ - 1), p = k >> 8;
+        const int lv = q0 + m, i = lv - 2 * l - p - sig(p), j = d.j0 + l - d.k0 - p;
+        const bool ok = lv < d.T && p < d.np && l < d.nj && (unsigned)j < (unsigned)ny && (unsigned)i < (unsigned)nx;
         const long r = ((long)(d.k0 + p) * ny + j) * nx + i;
-        out[d.cbase + (long)v * P * d.nj + p * d.nj + l] = rhs[mirror ? n - 1 - r : r];
+        v[it] = ok ? rhs[mirror ? n - 1 - r : r] : 0.0;
+        o[it] = ok ? d.cbase + (long)lv * P * d.nj + p * d.nj + l : -1;
     }
+#pragma unroll
+    for (int it = 0; it < NV; it++)
+        if (o[it] >= 0) out[o[it]] = v[it];
 }
 
 namespace {
@@ -777,10 +790,10 @@ constexpr int LF_NL = 4, LF_SW = 4;
 
 int linef_gather(lssp_amd_ctx *c, const LineSweep &ls, int mirror, const double *rhs, double *stream)
 {
-    const int nts = (ls.tmax + 1) / 2;
-    const long grid = (long)ls.ntiles * nts;
+    const int nq = (ls.tmax + LF_RUN - 1) / LF_RUN;
+    const long grid = (long)ls.ntiles * nq;
     const long n = (long)ls.nx * ls.ny * ls.nz;
-    k_linef_rhs<<<grid, 256, 0, c->stream>>>(ls.d_tiles, nts, ls.nx, ls.ny, n, mirror, rhs, stream, c->guard);
+    k_linef_rhs<<<grid, 256, 0, c->stream>>>(ls.d_tiles, nq, ls.nx, ls.ny, n, mirror, rhs, stream, c->guard);
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;
 }

@@ -29,7 +29,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, N, maxit, seed, out, solver="bicgstab", mode=1, pc="bj"):
+def _worker(rank, world, port, N, maxit, seed, out, solver="bicgstab", mode=1, pc="bj", level=0):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -52,7 +52,9 @@ def _worker(rank, world, port, N, maxit, seed, out, solver="bicgstab", mode=1, p
             M = lssp_amd.DILU.create(dev, gp, gj, gx, kind=lssp_amd.ILUK, level=0)
         else:
             bp, bj, bx = local_block(Ap, Aj, Ax, r0, nl)
-            M = lssp_amd.DILU.create(dev, bp, bj, bx, kind=lssp_amd.ILUK, level=0)
+            M = lssp_amd.DILU.create(dev, bp, bj, bx, kind=lssp_amd.ILUK, level=level)
+            if level == 1 and nl % (N * N) == 0:  # a whole-plane slab: the ILU(1) line sweeps
+                assert M.sweep_layout()[0] == 2
         # SpMV with a halo: y = A x for a seeded global x
         xg = uniform(seed, n)
         xv = dev.vec(A.nx, np.concatenate([xg[r0:r0 + nl], np.zeros(A.nhalo)]))
@@ -78,12 +80,12 @@ def _worker(rank, world, port, N, maxit, seed, out, solver="bicgstab", mode=1, p
         dist.destroy_process_group()
 
 
-def _run(world, N, solver, mode, maxit=500, pc="bj"):
+def _run(world, N, solver, mode, maxit=500, pc="bj", level=0):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, N, maxit, 0x5EED, q, solver, mode, pc))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, maxit, 0x5EED, q, solver, mode, pc, level))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -139,6 +141,21 @@ def test_multirank_on_one_gpu_equals_oracle_prank_mode(world, N, solver):
     sol = {"bicgstab": O.BICGSTAB, "gmres": O.GMRES, "cg": O.CG, "idrs": O.IDRS, "bicgstabl": O.BICGSTABL}[solver]
     o = O.solve(sol, A, np.ones(A.n), L=L, U=U, mode=O.TREE, nranks=world, maxit=500,
                 restart=4 if solver in ("idrs", "bicgstabl") else 30)  # l / s = 4, the library default
+    assert nits == o.nits
+    assert res == o.residual
+    assert np.array_equal(trace, o.trace)
+    assert np.array_equal(x, o.x)
+
+
+@pytest.mark.parametrize("world,N", [(2, 16), (4, 16)])
+def test_multirank_ilu1_line_sweeps_equal_oracle_prank_mode(world, N):
+    """block-Jacobi ILU(1) (the reference's default level) per rank: each whole-plane
+    slab's factor runs on the skewed line sweeps; BiCGSTAB in tree order equals the
+    oracle's P-rank mode bit for bit"""
+    nits, res, trace, y, x = _run(world, N, "bicgstab", O.TREE, level=1)
+    A = O.poisson(3, N)
+    L, U = O.ilu(A, "iluk", level=1, blk=(A.n + world - 1) // world)
+    o = O.solve(O.BICGSTAB, A, np.ones(A.n), L=L, U=U, mode=O.TREE, nranks=world, maxit=500, restart=30)
     assert nits == o.nits
     assert res == o.residual
     assert np.array_equal(trace, o.trace)
