@@ -1253,10 +1253,13 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                 for (int k = 0; k < KPER; k++) {
                     const int m = w + k * NL;
                     if (m < SL::NPC) {
-                        dma16(cb + m * 1024 + lane * 16, sl + SL::COEF + m * 1024);
+                        // non-temporal streams (read once): 216^3 apply 539 against
+                        // 547 us, bench 597 against 588 it/s; 512^3 unchanged
+                        // (profiles/r04/r04s_line2_nt_dma_ab.txt)
+                        dma16_nt(cb + m * 1024 + lane * 16, sl + SL::COEF + m * 1024);
                     } else if (m < NITEM) {
                         const int r = m - SL::NPC;
-                        dma16(ub + r * 1024 + lane * 16, sl + SL::RHS + r * 1024);
+                        dma16_nt(ub + r * 1024 + lane * 16, sl + SL::RHS + r * 1024);
                     } else {
                         dma16(cb + lane * 16, sl + SL::COEF);  // keeps the per-wave count fixed
                     }

@@ -16,6 +16,10 @@ __device__ __forceinline__ void dma16(const void *g, unsigned lds)
 {
     asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
 }
+__device__ __forceinline__ void dma16_nt(const void *g, unsigned lds)
+{
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(g), "s"(lds) : "memory", "m0");
+}
 __device__ __forceinline__ void dma16_sc1(const void *g, unsigned lds)
 {
     asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off sc1" ::"v"(g), "s"(__builtin_amdgcn_readfirstlane(lds))
