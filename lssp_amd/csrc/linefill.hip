@@ -556,18 +556,12 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
                 for (int k = 0; k < KPER; k++) {
                     const int m = w + k * NL;
                     if (m < SL::NPC) {
-#ifndef LINEF_DMA_NT
+                        // (non-temporal streams changed nothing here, unlike k_line2:
+                        // profiles/r04/r04t_linef_nt_ab_dropped.txt)
                         dma16(cb + m * 1024 + lane * 16, sl + SL::COEF + m * 1024);
-#else  // tuning: non-temporal streams
-                        dma16_nt(cb + m * 1024 + lane * 16, sl + SL::COEF + m * 1024);
-#endif
                     } else if (m < NITEM) {
                         const int r = m - SL::NPC;
-#ifndef LINEF_DMA_NT
                         dma16(ub + r * 1024 + lane * 16, sl + SL::RHS + r * 1024);
-#else
-                        dma16_nt(ub + r * 1024 + lane * 16, sl + SL::RHS + r * 1024);
-#endif
                     } else {
                         dma16(cb + lane * 16, sl + SL::COEF);  // keeps the per-wave count fixed
                     }
