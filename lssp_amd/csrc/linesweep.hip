@@ -1436,8 +1436,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                         for (int u = 0; u < PS; u++) {
                             const int v = LV * q + lvs[u];
                             const double x = res[(v & (RSL - 1)) * ROWS + (roff[u] & (ROWS - 1))];
-                            if (!(a.diag & 33) && (unsigned)(v - vlo[u]) < (unsigned)nx)
-                                __builtin_nontemporal_store(x, &po[u][-SB * v]);  // non-temporal (k_line_rhs)
+                            if (!(a.diag & 33) && (unsigned)(v - vlo[u]) < (unsigned)nx) po[u][-SB * v] = x;
                         }
                         rearm(q);
                     }
@@ -1585,9 +1584,7 @@ __global__ __launch_bounds__(256) void k_line_rhs(const LineTile *__restrict__ t
         const int k = it * 256 + threadIdx.x, m = k & 7, l = (k >> 3) % NJ, p = (k >> 3) / NJ;
         const int i = q0 + m - l - p - SKEW * (p / 4);
         if (q0 + m < d.T && p < d.np && l < d.nj && (unsigned)i < (unsigned)nx)
-            // non-temporal stream stores (with the U-stream stores: 512^3 apply
-            // 3.53 against 3.69 ms, 216^3 unchanged; profiles/r04/r04u_nt_stores_ab.txt)
-            __builtin_nontemporal_store(v[it], &out[d.cbase + (q0 + m) * SB + p * d.nj + l]);
+            out[d.cbase + (q0 + m) * SB + p * d.nj + l] = v[it];
     }
 }
 
