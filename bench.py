@@ -25,6 +25,12 @@ metric's SpMV kernel, y = A x
 (lssp_mv_mxy).  Both are timed live with HIP events on the library's stream.
 traffic: HBM bytes per launch from rocprofv3 PMC counters (FETCH_SIZE x 2 on
 gfx950, + WRITE_SIZE), read from profiles/pmc_traffic.json when present.
+config4: the same BiCGSTAB + ILU(0) step on config 4's 7-pt 512^3 matrix
+(134 M rows) over the same N ranks -- z-slabs, block-Jacobi ILU(0) per rank
+on N > 1 -- timed the same way (>= 10 iterations, barrier + sync, max over
+ranks), so the driver's N = 1, 2, 4, 8 runs record BASELINE.md 3's curve on
+the matrix it names; --config4-steps 0 skips it.  The headline value stays on
+216^3.
 cpu_baseline is the REFERENCE itself (oracle/_ref/libref.so, compiled from
 /root/reference, g++ -O2, 1 core) on a bounded sample of the same workload.
 """
@@ -162,11 +168,73 @@ def measure_hbm_peak(dev, stream, gpu, e0, e1):
         want = int(np.bitwise_xor.reduce(w.cpu().numpy()))
         got = int(sink.view(torch.int64)[0].item())
         best["read_checked"] = got == want
-        peak_measured = best["read"]
+        # the read kernel's number only when its fold checked out; else the copy peak
+        peak_measured = best["read"] if best["read_checked"] else best["copy"]
         del src, dst
         return peak_measured, best
     except Exception as ex:  # noqa: BLE001
         return None, {"error": repr(ex)[:200]}
+
+
+def config4_leg(dev, rank: int, world: int, steps: int, warmup: int = 2):
+    """Config 4 (BASELINE.json configs[3]): 7-pt Poisson 512^3 (n = 134,217,728),
+    BiCGSTAB + ILU(0), row-partitioned over the same N ranks as the headline
+    (z-slabs, block-Jacobi ILU(0) per rank -- the reference's blk_size path,
+    pc-iluk.cxx:411-552 -- halos and dots over RCCL; one rank: the global
+    ILU(0)).  Timed like the headline: barrier + device sync on both sides, the
+    max over ranks.  Its it/s at N = 1, 2, 4, 8 is the curve BASELINE.md 3 asks
+    for; the headline value stays on 216^3."""
+    import torch
+    import torch.distributed as dist
+    import lssp_amd
+    N = 512
+    t0 = time.perf_counter()
+    n, row0, nl, Ap, Aj, Ax = build_local(N, rank, world)
+    if world > 1:
+        A = lssp_amd.DMat(dev, Ap, Aj, Ax, dist=(n, row0))
+        bp, bj, bx = local_block(Ap, Aj, Ax, row0, nl)
+        del Ap, Aj, Ax
+        M = lssp_amd.DILU.create(dev, bp, bj, bx, kind=lssp_amd.ILUK, level=0)
+        del bp, bj, bx
+    else:
+        A = lssp_amd.DMat(dev, Ap, Aj, Ax)
+        M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=0)
+        del Ap, Aj, Ax
+    x = dev.vec(A.nx, np.zeros(A.nx))
+    b = dev.vec(A.nx, np.ones(A.nx))
+    setup_s = time.perf_counter() - t0
+
+    def run(iters):
+        return lssp_amd.solve(dev, A, M, x, b, solver=lssp_amd.BICGSTAB, tol_rel=0.0, tol_abs=0.0, tol_rb=0.0,
+                              maxit=iters)
+
+    if warmup > 0:
+        run(warmup)
+    if world > 1:
+        dist.barrier()
+    dev.sync()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    res = run(steps)
+    dev.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t1
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    assert res.nits == steps, f"config4: expected {steps} iterations, got {res.nits}"
+    out = {"workload": f"7-pt Poisson {N}^3 (n={n}, nnz={7 * N ** 3 - 6 * N ** 2}), BiCGSTAB + ILUK(0)"
+                       f"{' block-Jacobi per rank' if world > 1 else ''}, b=1, x0=0, fp64",
+           "value": round(steps / el, 3), "unit": "iters/s", "ms_per_step": round(el / steps * 1e3, 4),
+           "steps": steps, "warmup": warmup, "n_gpus": world, "rows_per_rank": nl,
+           "partition": f"{world} z-slab row blocks", "levels_per_sweep": M.levelsL,
+           "comm_ranks": dev.comm_nranks() if world > 1 else 1, "setup_s": round(setup_s, 2)}
+    for o in (x, b, M, A):
+        o.close()
+    return out
 
 
 def free_port() -> int:
@@ -198,6 +266,8 @@ def main():
     ap.add_argument("--apply-reps", type=int, default=10)
     ap.add_argument("--cpu-iters", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--config4-steps", type=int, default=10,
+                    help="BiCGSTAB iterations timed on config 4's 512^3 matrix over the same N ranks (0: skip)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal: every rank on device 0, collectives over the host-staged gloo transport "
                          "(RCCL refuses two ranks on one GPU); not a scaling measurement")
@@ -362,6 +432,16 @@ def main():
             "ilu": {"levels_L": M.levelsL, "levels_U": M.levelsU, "setup_s": round(M.setup_seconds, 3)},
             "setup_s": round(t_setup, 2),
         }
+    # ---- config 4 (512^3 over the same ranks): the scaling curve's matrix ----
+    if N == 512:
+        args.config4_steps = 0  # the headline is config 4's matrix already
+    if args.config4_steps > 0:
+        for o in (x, b, y, xs, zs, M, A):
+            o.close()
+        c4 = config4_leg(dev, rank, world, args.config4_steps)
+    if rank == 0:
+        if args.config4_steps > 0:
+            out["config4"] = c4
         if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline(N, args.cpu_iters)
         print(json.dumps(out), flush=True)

@@ -15,6 +15,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstring>
 #include <map>
 
@@ -195,6 +196,10 @@ int comm_destroy(lssp_amd_ctx *c)
         (void)hipFree(c->d_carry);
         c->d_carry = nullptr;
     }
+    if (c->d_igather) {
+        (void)hipFree(c->d_igather);
+        c->d_igather = nullptr;
+    }
     if (c->ev_pack) (void)hipEventDestroy(c->ev_pack);
     if (c->ev_halo) (void)hipEventDestroy(c->ev_halo);
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
@@ -206,19 +211,29 @@ int comm_destroy(lssp_amd_ctx *c)
     return LSSP_AMD_OK;
 }
 
-// one int per rank, all-gathered in rank order (collective)
+// one int per rank, all-gathered in rank order (collective).  The scratch is
+// the context's (allocated with the communicator), so nothing here can fail on
+// one rank before the all-gather and leave the others waiting in it; a failed
+// copy-in on this rank is sent as INT_MIN, which every caller treats as an error.
 int comm_gather_int(lssp_amd_ctx *c, int v, std::vector<int> &all)
 {
-    int *d = nullptr;  // [mine | all ranks]
-    LSSP_HIP(hipMalloc(&d, sizeof(int) * (1 + c->nranks)));
-    int st = hipMemcpy(d, &v, sizeof(int), hipMemcpyHostToDevice) == hipSuccess ? LSSP_AMD_OK : LSSP_AMD_EHIP;
-    if (st == LSSP_AMD_OK) st = xfer_allgather(c, d, d + 1, (long)sizeof(int));
-    all.assign(c->nranks, 0);
+    all.assign(c->nranks, INT_MIN);
+    if (c->nranks <= 1 || !c->d_igather) {
+        all.assign(c->nranks, v);
+        return LSSP_AMD_OK;
+    }
+    (void)hipSetDevice(c->device);
+    int *d = c->d_igather;  // [mine | all ranks]
+    if (hipMemcpyAsync(d, &v, sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+        const int bad = INT_MIN;  // still join the gather, with an error code
+        (void)hipGetLastError();
+        (void)hipMemcpy(d, &bad, sizeof(int), hipMemcpyHostToDevice);
+    }
+    int st = xfer_allgather(c, d, d + 1, (long)sizeof(int));
     if (st == LSSP_AMD_OK &&
         (hipMemcpyAsync(all.data(), d + 1, sizeof(int) * c->nranks, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
          hipStreamSynchronize(c->stream) != hipSuccess))
         st = LSSP_AMD_EHIP;
-    (void)hipFree(d);
     return st;
 }
 
@@ -269,6 +284,7 @@ int lssp_amd_comm_init(lssp_amd_ctx *c, int nranks, int rank, const void *idp)
     c->rank = rank;
     LSSP_HIP(hipMalloc(&c->d_gather, sizeof(double) * MAX_SLOTS * nranks));
     LSSP_HIP(hipMalloc(&c->d_carry, sizeof(double) * MAX_SLOTS));
+    LSSP_HIP(hipMalloc(&c->d_igather, sizeof(int) * (1 + nranks)));
     LSSP_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
     LSSP_HIP(hipEventCreateWithFlags(&c->ev_pack, hipEventDisableTiming));
     LSSP_HIP(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
@@ -349,6 +365,7 @@ int lssp_amd_comm_init_host(lssp_amd_ctx *c, int nranks, int rank, const lssp_am
     c->rank = rank;
     LSSP_HIP(hipMalloc(&c->d_gather, sizeof(double) * MAX_SLOTS * nranks));
     LSSP_HIP(hipMalloc(&c->d_carry, sizeof(double) * MAX_SLOTS));
+    LSSP_HIP(hipMalloc(&c->d_igather, sizeof(int) * (1 + nranks)));
     return LSSP_AMD_OK;
 }
 
@@ -376,7 +393,7 @@ static int agree_status(lssp_amd_ctx *c, int st)
     std::vector<int> all;
     LSSP_TRY(comm_gather_int(c, st, all));
     for (int s : all)
-        if (s != LSSP_AMD_OK) return s;
+        if (s != LSSP_AMD_OK) return s == INT_MIN ? LSSP_AMD_EHIP : s;
     return LSSP_AMD_OK;
 }
 

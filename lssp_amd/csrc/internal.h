@@ -86,6 +86,7 @@ struct lssp_amd_ctx {
     lssp_amd_host_transport host{};  // host-staged transport (comm == nullptr, nranks > 1)
     double *d_gather = nullptr;  // [nranks][MAX_SLOTS]
     double *d_carry = nullptr;   // [MAX_SLOTS] serial mode: running sums of the ranks before this one
+    int *d_igather = nullptr;    // [1 + nranks] comm_gather_int scratch (allocated with the communicator)
     // RCCL mode: the halo round runs on comm_stream while the interior rows'
     // product runs on stream (ev_pack: send buffer packed; ev_halo: halo landed)
     hipStream_t comm_stream = nullptr;

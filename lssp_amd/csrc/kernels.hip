@@ -223,11 +223,26 @@ struct SerialArgs {
 };
 
 // SERIAL reduction mode: sum += x[i]*y[i] for i = 0 .. n-1 from 0.0, exactly
-// vector.cxx:123-133.  The additions are one dependent chain per slot, run by
-// lane 0 of wave 0 out of LDS; waves 1..15 stream the products (each rounded
-// as the reference rounds it) of the next 2048-element chunk into the other
-// LDS buffer meanwhile, so the chain never waits on HBM latency.
-constexpr int SER_C = 2048;
+// vector.cxx:123-133.  The additions are ONE dependent chain per slot, so the
+// kernel's speed is the f64 add's dependent latency times n; everything else
+// is kept off that chain:
+//   * wave 0 runs the chains, lane s the chain of slot s (up to MAX_SLOTS dots
+//     of one round cost the same as one), with SIMD 0 to itself: the product
+//     waves are the 12 waves on SIMDs 1-3 (wave % 4 != 0; waves 4, 8, 12 only
+//     take part in the barriers), so no other wave's VALU issue interleaves
+//     with the chain;
+//   * the products (each rounded as the reference rounds it: -ffp-contract=off)
+//     of the next 2048-element chunk are written to the other LDS buffer while
+//     the chain adds the current one, slot-major so lane s reads its own two
+//     consecutive products with one ds_read_b128;
+//   * the chain reads its operands 16 at a time, one batch ahead in registers,
+//     so the LDS latency is hidden behind the previous batch's 16 adds.
+// A chunk's tail is padded with +0.0: a running sum that starts at +0.0 (or a
+// previous rank's running sum, itself such a sum) is never -0.0, and s + 0.0
+// == s for every other s, so the padding never changes a bit.
+constexpr int SER_C = 2048;  // elements per LDS chunk
+constexpr int SER_B = 16;    // elements per register batch of the chain
+static_assert(SER_C % SER_B == 0, "whole batches per chunk");
 // carry (multi-rank): the running sums of the ranks before this one, so the
 // chain continues theirs and the P ranks add in global index order.
 __global__ __launch_bounds__(1024) void k_dot_serial(SerialArgs g, long n, int nslot, double *sums, double *scal,
@@ -236,42 +251,67 @@ __global__ __launch_bounds__(1024) void k_dot_serial(SerialArgs g, long n, int n
 {
     if (guard && *guard != 0.0) return;
     __shared__ double buf[2][MAX_SLOTS][SER_C];
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const long nch = (n + SER_C - 1) / SER_C;
-    auto fill = [&](long k, int b) {
-        if (tid < 64) return;
+    const bool producer = (wave & 3) != 0;
+    const int pid = (wave - 1 - (wave >> 2)) * 64 + lane;  // 0 .. 767 over the 12 product waves
+    auto fill = [&](long k, int bsel) {
         for (int s = 0; s < nslot; s++) {
             const double *x = g.a[s], *y = g.b[s];
-            for (int i = tid - 64; i < SER_C; i += 1024 - 64) {
+            for (int i = pid; i < SER_C; i += 768) {
                 const long e = k * SER_C + i;
-                if (e < n) buf[b][s][i] = x[e] * y[e];
+                buf[bsel][s][i] = e < n ? x[e] * y[e] : 0.0;
             }
         }
     };
-    double acc[MAX_SLOTS] = {0, 0, 0, 0};
-    if (carry)
-        for (int s = 0; s < MAX_SLOTS; s++) acc[s] = carry[s];
-    if (nch > 0) fill(0, 0);
+    const int sl = lane < nslot ? lane : 0;
+    double acc = carry ? carry[sl] : 0.0;
+    if (producer && nch > 0) fill(0, 0);
     __syncthreads();
     for (long k = 0; k < nch; k++) {
-        if (k + 1 < nch) fill(k + 1, (k + 1) & 1);
-        if (tid == 0) {
-            const int m = (int)min((long)SER_C, n - k * SER_C);
-            const double(*B)[SER_C] = buf[k & 1];
-            if (nslot == 1) {
-                for (int i = 0; i < m; i++) acc[0] += B[0][i];
-            } else {
-                for (int i = 0; i < m; i++)
+        if (producer) {
+            if (k + 1 < nch) fill(k + 1, (k + 1) & 1);
+        } else if (wave == 0) {
+            const long m = min((long)SER_C, n - k * SER_C);
+            const int nb = (int)((m + SER_B - 1) / SER_B);
+            const double2 *B = reinterpret_cast<const double2 *>(&buf[k & 1][sl][0]);
+            // two register sets, a batch's reads issued before the previous
+            // batch's adds (the empty asm with a memory clobber keeps the reads
+            // ahead of them); a read past the chunk's last batch re-reads batch 0
+            double2 va[SER_B / 2], vb[SER_B / 2];
+            auto rd = [&](double2 (&v)[SER_B / 2], int q) {
+                const int qq = q < SER_C / SER_B ? q : 0;
 #pragma unroll
-                    for (int s = 0; s < MAX_SLOTS; s++)
-                        if (s < nslot) acc[s] += B[s][i];
+                for (int u = 0; u < SER_B / 2; u++) v[u] = B[qq * (SER_B / 2) + u];
+            };
+            auto add = [&](const double2 (&v)[SER_B / 2]) {
+#pragma unroll
+                for (int u = 0; u < SER_B / 2; u++) {
+                    acc = acc + v[u].x;
+                    acc = acc + v[u].y;
+                }
+            };
+            rd(va, 0);
+            for (int q = 0; q < nb; q += 2) {
+                rd(vb, q + 1);
+                asm volatile("" ::: "memory");
+                add(va);
+                if (q + 1 >= nb) break;
+                rd(va, q + 2);
+                asm volatile("" ::: "memory");
+                add(vb);
             }
         }
         __syncthreads();
     }
-    if (tid == 0) {
-        for (int s = 0; s < nslot; s++) sums[s] = acc[s];
-        if (do_fin) finalize(f, acc, scal, trace);
+    if (wave == 0) {
+        double r[MAX_SLOTS];
+#pragma unroll
+        for (int s = 0; s < MAX_SLOTS; s++) r[s] = __shfl(acc, s, 64);
+        if (lane == 0) {
+            for (int s = 0; s < nslot; s++) sums[s] = r[s];
+            if (do_fin) finalize(f, r, scal, trace);
+        }
     }
 }
 

@@ -2213,12 +2213,15 @@ extern "C" int lssp_amd_solve(lssp_amd_ctx *c, const lssp_amd_mat *A, const lssp
                               const lssp_amd_solve_params *prm, double *x, const double *b, int *nits,
                               double *residual, double *trace, int trace_cap, int *trace_len)
 {
-    if (!c || !A || !prm || !x || !b) return LSSP_AMD_EINVAL;
-    if (A->nrows != A->ncols - A->nhalo) return LSSP_AMD_EINVAL;  // square (lssp.cxx:152)
+    if (!c) return LSSP_AMD_EINVAL;
+    LSSP_HIP(hipSetDevice(c->device));  // before the agreement below: its scratch and stream are this device's
+    // a rank-local argument error still joins the agreement (as -1), so no peer
+    // is left waiting in it
+    const bool bad_args = !A || !prm || !x || !b || A->nrows != A->ncols - A->nhalo;  // square (lssp.cxx:152)
     // M: the rank's own rows (a block-Jacobi block on P ranks), or on P ranks
     // the factors of the whole matrix (the reference's global ILU)
-    const bool gpc = M && c->nranks > 1 && M->n == A->n_global && M->n != A->nrows;
-    const bool bad_m = M && M->n != A->nrows && !gpc;
+    const bool gpc = !bad_args && M && c->nranks > 1 && M->n == A->n_global && M->n != A->nrows;
+    const bool bad_m = bad_args || (M && M->n != A->nrows && !gpc);
     if (c->nranks > 1) {
         // every rank must take the same preconditioner path (none / its own block /
         // the global factors): the global path all-gathers in every apply, so a
@@ -2230,7 +2233,6 @@ extern "C" int lssp_amd_solve(lssp_amd_ctx *c, const lssp_amd_mat *A, const lssp
             if (m < 0 || m != modes[0]) return LSSP_AMD_EINVAL;
     }
     if (bad_m) return LSSP_AMD_EINVAL;
-    LSSP_HIP(hipSetDevice(c->device));
     Run R;
     R.c = c;
     R.A = A;

@@ -132,3 +132,18 @@ def test_multirank_bicgstab_equals_oracle_prank_mode(world, N):
     assert res == o.residual
     assert np.array_equal(trace, o.trace)
     assert np.array_equal(x, o.x)
+
+
+def test_threaded_block_factors_equal_oracle_blk_mode():
+    """tests/test_gpu_dist.py builds config 4's block-Jacobi oracle factors one
+    block per thread; they must be O.ilu(A, blk=ceil(n/P)) bit for bit"""
+    import numpy as np
+    import oracle as O
+    from test_gpu_dist import _bj_factors_threaded
+    A = O.poisson(3, 20)
+    for P in (3, 8):
+        L, U = O.ilu(A, "iluk", level=0, blk=(A.n + P - 1) // P)
+        L2, U2 = _bj_factors_threaded(A, P)
+        for a, b in ((L, L2), (U, U2)):
+            assert np.array_equal(a.Ap, b.Ap) and np.array_equal(a.Aj, b.Aj)
+            assert np.array_equal(a.Ax.view(np.int64), b.Ax.view(np.int64))

@@ -126,6 +126,135 @@ def test_config4_partition_8_ranks(mode):
         assert digest(x) == g["x_sha256"]
 
 
+def _c4_worker(rank, world, port, out):
+    """one rank of config 4 at full size: its 512^3 / 8 z-slab, block-Jacobi ILU(0)"""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import lssp_amd
+        from bench import local_block
+        from inputs import digest
+        from lssp_amd.dist import GlooTransport
+        dev = lssp_amd.Device(0, reduction=lssp_amd.TREE)
+        dev.comm_init_host(world, rank, GlooTransport())
+        N = 512
+        n = N ** 3
+        blk = (n + world - 1) // world
+        r0 = min(rank * blk, n)
+        nl = min(blk, n - r0)
+        Ap, Aj, Ax = lssp_amd.poisson(3, N, r0, nl)
+        A = lssp_amd.DMat(dev, Ap, Aj, Ax, dist=(n, r0))
+        bp, bj, bx = local_block(Ap, Aj, Ax, r0, nl)
+        del Ap, Aj, Ax
+        M = lssp_amd.DILU.create(dev, bp, bj, bx, kind=lssp_amd.ILUK, level=0)
+        del bp, bj, bx
+        layout = M.sweep_layout()
+        b = dev.vec(A.nx, np.ones(A.nx))
+        x = dev.vec(A.nx, np.zeros(A.nx))
+        # (1) the first three iterations, zero tolerances: trace and x
+        r3 = lssp_amd.solve(dev, A, M, x, b, solver=lssp_amd.BICGSTAB, tol_rel=0.0, tol_abs=0.0, tol_rb=0.0,
+                            maxit=3, trace_cap=64)
+        x3 = digest(x.download(nl))
+        # (2) converged at the reference's default tolerances
+        x.upload(np.zeros(A.nx))
+        rc = lssp_amd.solve(dev, A, M, x, b, solver=lssp_amd.BICGSTAB, maxit=5000)
+        z = dev.vec(A.nx)
+        A.mv_amxpbyz(-1.0, x, 1.0, b, z)  # b - A x with this rank's halo
+        zh = z.download(nl)
+        ss = float(np.dot(zh, zh))
+        dev.barrier()
+        parts = [None] * world
+        dist.all_gather_object(parts, (x3, ss, layout))
+        if rank == 0:
+            out.put((r3.nits, r3.residual, r3.trace, [p[0] for p in parts], rc.nits, rc.residual,
+                     sum(p[1] for p in parts), [p[2] for p in parts]))
+        dev.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def _bj_factors_threaded(A, nblk):
+    """the oracle's block-Jacobi ILU(0) factors (O.ilu(A, blk=ceil(n/nblk))) built
+    block by block on nblk threads (ctypes drops the GIL): each block's factor is
+    the ILU(0) of its diagonal block (pc-iluk.cxx:441-535), columns shifted back"""
+    from concurrent.futures import ThreadPoolExecutor
+    from bench import local_block
+    n = A.n
+    blk = (n + nblk - 1) // nblk
+
+    def one(q):
+        r0 = q * blk
+        nl = min(blk, n - r0)
+        e0, e1 = int(A.Ap[r0]), int(A.Ap[r0 + nl])
+        bp, bj, bx = local_block(A.Ap[r0:r0 + nl + 1] - e0, A.Aj[e0:e1], A.Ax[e0:e1], r0, nl)
+        return O.ilu(O.CSR(nl, bp, bj, bx), "iluk", level=0)
+
+    with ThreadPoolExecutor(nblk) as ex:
+        parts = list(ex.map(one, range((n + blk - 1) // blk)))
+
+    def cat(fs):
+        ap, off = [np.zeros(1, np.int64)], 0
+        for f in fs:
+            ap.append(f.Ap[1:].astype(np.int64) + off)
+            off += int(f.Ap[-1])
+        return O.CSR(n, np.concatenate(ap).astype(np.int32),
+                     np.concatenate([f.Aj + q * blk for q, f in enumerate(fs)]).astype(np.int32),
+                     np.concatenate([f.Ax for f in fs]))
+
+    return cat([p[0] for p in parts]), cat([p[1] for p in parts])
+
+
+@pytest.mark.timeout(900)
+def test_config4_full_size_8_ranks_on_one_gpu():
+    """Config 4 at its FULL size: 7-pt 512^3 (n = 134,217,728) over 8 ranks --
+    8 z-slabs of 64 planes, block-Jacobi ILU(0) per rank on the line sweeps
+    (pc-iluk.cxx:411-552 with blk = n / 8), halo planes and rank-combined dots
+    over the host transport, all 8 ranks on this one GPU.  The first three
+    BiCGSTAB iterations (every traced scalar, each rank's x) are bitwise the
+    oracle's 8-rank TREE mode on the whole 512^3 system, computed here while
+    the ranks run; then the solve converges at the reference's default
+    tolerances (lssp.cxx:11-13) below the stop scale, and the recomputed global
+    true residual ||b - A x|| is within 2x that scale."""
+    import math
+    import torch.multiprocessing as mp
+    from inputs import digest
+    world, N = 8, 512
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c4_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        # the oracle's 8-rank mode on the whole system, concurrently with the ranks
+        A = O.poisson(3, N)
+        n = A.n
+        blk = (n + world - 1) // world
+        L, U = _bj_factors_threaded(A, world)  # == O.ilu(A, "iluk", level=0, blk=blk), one block per thread
+        o = O.solve(O.BICGSTAB, A, np.ones(n), L=L, U=U, rtol=0.0, atol=0.0, rbtol=0.0, maxit=3, mode=O.TREE,
+                    nranks=world, trace_cap=64)
+        del L, U, A
+        want_x = [digest(o.x[q0:q0 + blk]) for q0 in range(0, n, blk)]
+        nits3, res3, trace3, x3, nits, res, ss, layouts = q.get(timeout=800)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(lay[0] == 1 for lay in layouts), layouts  # every slab on the ILU(0) line sweeps
+    assert nits3 == o.nits == 3
+    assert res3 == o.residual
+    assert np.array_equal(trace3.view(np.int64), o.trace.view(np.int64))
+    assert x3 == want_x
+    scale = 1e-7 * math.sqrt(n)  # max(rtol ||r0||, atol, rb ||b||), r0 = b = 1
+    true_res = math.sqrt(ss)
+    print(f"\nconfig 4, 8 ranks: {nits} iterations, residual {res:.6e}, true residual {true_res:.6e}, "
+          f"stop scale {scale:.6e}")
+    assert 0 < nits < 5000 and res <= scale
+    assert true_res <= 2.0 * scale
+
+
 @pytest.mark.parametrize("world,N,solver", [(2, 12, "bicgstab"), (3, 10, "bicgstab"), (4, 16, "bicgstab"),
                                              (2, 12, "gmres"), (3, 11, "gmres"), (2, 12, "cg"), (4, 13, "cg"),
                                              # IDR(4): each rank keeps its rows of the global rand() shadow space
@@ -271,7 +400,8 @@ def test_bench_gpus_2_launches_two_ranks():
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--share-gpu", "--grid", "32",
-                        "--steps", "5", "--warmup", "1", "--no-cpu", "--spmv-reps", "3", "--apply-reps", "2"],
+                        "--steps", "5", "--warmup", "1", "--no-cpu", "--spmv-reps", "3", "--apply-reps", "2",
+                        "--config4-steps", "0"],
                        env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])

@@ -116,3 +116,40 @@ def test_tree_mode_512_bicgstab_converges():
     print(f"\n512^3: nits {r.nits}, residual {r.residual:.6e} (stop scale {scale:.6e}), true {true_res:.6e}")
     assert 0 < r.nits < 5000 and r.residual <= scale
     assert true_res <= TRUE_FACTOR * scale
+
+
+SERIAL_CASES = [c for c in FULL if c["solver"] == 4 and c["N"] == 216]
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("c", SERIAL_CASES, ids=[c["name"] for c in SERIAL_CASES])
+def test_serial_mode_full_solve_bitwise_reference(c):
+    """The reference-exact mode at the benchmark size, to convergence: SERIAL
+    reductions (k_dot_serial, the sequential sum of vector.cxx:123-131) make
+    the 216^3 BiCGSTAB + ILU(0) solve bit for bit the reference's own complete
+    run (tests/golden/full.json from oracle/_ref/libref.so): the iteration count
+    (145), the final residual, every one of the 872 dots and norms the driver
+    computed (solver-bicgstab.cxx:73-157) and the sha256 of x."""
+    import time
+    import lssp_amd
+    from inputs import digest
+    dev = lssp_amd.Device(0, reduction=lssp_amd.SERIAL)
+    try:
+        Ap, Aj, Ax = lssp_amd.poisson(3, c["N"])
+        n = Ap.size - 1
+        A = lssp_amd.DMat(dev, Ap, Aj, Ax)
+        M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=c["pc"]["level"])
+        del Aj, Ax
+        b = dev.vec(n, np.ones(n))
+        x = dev.vec(n, np.zeros(n))
+        t0 = time.perf_counter()
+        r = lssp_amd.solve(dev, A, M, x, b, solver=c["solver"], tol_rel=c["rtol"], tol_abs=c["atol"],
+                           tol_rb=c["rbtol"], maxit=5000, restart=c["restart"], trace_cap=200000)
+        dt = time.perf_counter() - t0
+        print(f"\n{c['name']} SERIAL: {r.nits} iterations in {dt:.2f} s = {r.nits / dt:.2f} it/s")
+        assert r.nits == c["nits"]
+        assert r.residual.hex() == float.fromhex(c["residual"]).hex()
+        assert [v.hex() for v in r.trace] == [float.fromhex(h).hex() for h in c["trace"]]
+        assert digest(x.download()) == c["x_sha256"]
+    finally:
+        dev.close()
