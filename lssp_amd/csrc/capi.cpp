@@ -7,6 +7,7 @@
 #include <climits>
 #include <cstdarg>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <mutex>
@@ -219,6 +220,8 @@ int build_diag_ids(lssp_amd_mat *M, const int *Ap, const int *Aj)
     LSSP_HIP(hipMemcpy(M->d_off, off.data(), sizeof(int) * off.size(), hipMemcpyHostToDevice));
     M->aux_bytes += (long long)ad.size() + (long long)sizeof(int) * (long long)off.size();
     M->ndiag = (int)off.size();
+    M->max_off = 0;
+    for (int o : off) M->max_off = std::max(M->max_off, std::abs(o));
     return LSSP_AMD_OK;
 }
 

@@ -112,6 +112,7 @@ struct lssp_amd_mat {
     uint8_t *Ad = nullptr;
     int *d_off = nullptr;
     int ndiag = 0;
+    int max_off = 0;  // max |col - row| of the coded offsets
     // windowed x (k_spmv_sell): when every 1024-row block's columns fall in a
     // span of at most WIN_CAP entries, d_win[2b], d_win[2b+1] = that span
     // [lo, hi) and the product stages x[lo, hi) in LDS; nullptr: not windowed
@@ -215,6 +216,13 @@ struct LineILU {
     double *d_lstream = nullptr;  // the L sweep's rhs in its stream layout (k_line_rhs)
     double *d_hk = nullptr, *d_hj = nullptr;  // hand-off buffers (armed with TRI_SENTINEL)
     long hk_stride = 0, hj_stride = 0, hk_n = 0, hj_n = 0;
+    // the U sweep's tail product (launch_line_apply_spmv): U tiles finished per
+    // tile row (monotonic), natural plane -> L tile row, chunk claims
+    unsigned *d_kdone = nullptr;
+    int *d_kof = nullptr;
+    unsigned long long *d_tclaim = nullptr;
+    mutable unsigned long long tbase = 0;
+    mutable unsigned kepoch = 0;
 };
 
 }  // namespace lssp_amd
@@ -376,6 +384,13 @@ int launch_linefill_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const d
 int launch_linefill_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs);
 void free_line_sweep(LineILU &li);
 int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs);
+// the apply followed by z = op(A x) (+ fused dots), the product run by the U
+// sweep's workgroups as planes of x become final (k_line2 tail); results are
+// bitwise launch_line_apply + launch_spmv.  EUNSUPPORTED when A is not a coded
+// single-rank stencil of the factor's grid (the caller then runs the two)
+int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs, const lssp_amd_mat *A,
+                           int epi, double alpha, double beta, const double *y, double *z, int nred,
+                           const double *w0, const double *w1);
 int launch_line_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs);
 void free_trisched(TriSched &t);
 

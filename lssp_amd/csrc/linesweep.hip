@@ -424,6 +424,12 @@ void free_line_sweep(LineILU &li)
     if (li.d_lstream) (void)hipFree(li.d_lstream);
     if (li.d_hk) (void)hipFree(li.d_hk);
     if (li.d_hj) (void)hipFree(li.d_hj);
+    if (li.d_kdone) (void)hipFree(li.d_kdone);
+    if (li.d_kof) (void)hipFree(li.d_kof);
+    if (li.d_tclaim) (void)hipFree(li.d_tclaim);
+    li.d_kdone = nullptr;
+    li.d_kof = nullptr;
+    li.d_tclaim = nullptr;
     li.d_ustream = li.d_lstream = li.d_hk = li.d_hj = nullptr;
     li.ntiles = 0;
 }
@@ -431,6 +437,41 @@ void free_line_sweep(LineILU &li)
 // ---------------------------------------------------------------------------
 // device
 // ---------------------------------------------------------------------------
+// The product z = op(A x) on the output x of a U sweep, run by the sweep's
+// own workgroups once the tile claims are exhausted (launch_line_apply_spmv):
+// a workgroup that finds no tile left turns its 11 waves into product waves,
+// each claiming whole 256-row reduction chunks from the top of the matrix down
+// (the U sweep completes planes in that order) and starting a chunk once every
+// plane its rows read (k-1 .. k+1, a 5-/7-point stencil of the sweep's grid)
+// is final: the U tiles count their completion per tile row (kdone, agent-
+// scope atomics after the storers' write-through stores drained).  Lane l of
+// a wave owns rows 64q + l (q = 0..3) of its chunk, forms each row's sum in
+// CSR order from 0.0 and the epilogue of k_spmv3, and the chunk's fused-dot
+// partials are (w0 + w1) + (w2 + w3) of the four 64-row wave sums -- exactly
+// chunk_reduce's order -- so every output and partial is bitwise k_spmv3's.
+// Only CUs whose sweep work is over run product waves: the hand-off polls of
+// the tiles still running do not queue behind product loads.
+struct LineTail {
+    const int *Ap;
+    const double *Ax;
+    const uint8_t *Ad;  // diagonal-id coding (lssp_amd_mat::Ad)
+    const int *off;
+    int ndiag, nrows, epi, nred;
+    const double *y;
+    double *z;
+    double alpha, beta;
+    const double *w0, *w1;
+    double *part;
+    long pcap, nblk;
+    unsigned long long *claim;  // chunk claims (monotonic)
+    unsigned long long base;
+    unsigned *kdone;            // U tiles finished per tile row (monotonic)
+    unsigned ktarget;           // this launch's count per row (W x launches)
+    const int *kof;             // natural plane -> L tile row
+    int S, W, nz;
+    long pl;                    // rows per plane
+};
+
 struct LineArgs {
     int nx, ny, ntiles;
     long n;
@@ -452,7 +493,100 @@ struct LineArgs {
     int ttile;
     int diag;  // LSSP_AMD_LINE_DIAG timing experiments (wrong results when != 0)
     const double *guard;  // lssp_amd_ctx::guard
+    int tail;     // k_line2 OUT 1: run the product tl after the tiles (write-through output, tile counts)
+    LineTail tl;
 };
+
+__device__ __forceinline__ double ld_sc1d(const double *p)
+{
+    return __longlong_as_double(
+        (long long)__hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1d(double *p, double v)
+{
+    __hip_atomic_store(reinterpret_cast<uint64_t *>(p), (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one wave's share of the tail product (see LineTail); soff: the offset table in LDS
+__device__ void line_tail_waves(const LineTail &T, const double *x, int *err, const int *soff)
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        unsigned long long c = 0;
+        if (lane == 0) c = atomicAdd(T.claim, 1ull) - T.base;
+        const unsigned clo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)c);
+        const unsigned chi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(c >> 32));
+        const unsigned long long cl = ((unsigned long long)chi << 32) | clo;
+        if (cl >= (unsigned long long)T.nblk) break;
+        const long blk = T.nblk - 1 - (long)cl;
+        const int r0 = (int)(blk * 256), r1 = min(r0 + 256, T.nrows);
+        // the planes the chunk's rows read: k-1 .. k+1 of its first / last row
+        if (lane == 0) {
+            const int ka = max(r0 / (int)T.pl - 1, 0), kb = min((r1 - 1) / (int)T.pl + 1, T.nz - 1);
+            const int K0 = T.kof[ka], K1 = T.kof[kb];
+            for (int K = K0; K <= K1; K++) {
+                const unsigned *cnt = T.kdone + (T.S - 1 - K);  // U tile row of L tile row K
+                for (;;) {
+                    // (an atomic read: coherent with the tiles' atomic increments on every XCD)
+                    if (__hip_atomic_fetch_add(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - T.ktarget <
+                        0x80000000u)
+                        break;
+                    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+                        __builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s: the sweep gave up
+                        atomicOr(err, 8);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        double v0[4], v1[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int r = r0 + 64 * q + lane;
+            const int rr = min(r, T.nrows - 1);
+            const int rb = T.Ap[rr], re = T.Ap[rr + 1];
+            double pr[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int k = max(min(rb + u, re - 1), 0);
+                pr[u] = ld_sc1d(x + rr + soff[T.Ad[k]]) * T.Ax[k];
+            }
+            double sum = 0;
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (u < re - rb) sum += pr[u];
+            for (int k = rb + 8; k < re; k++) sum += ld_sc1d(x + rr + soff[T.Ad[k]]) * T.Ax[k];
+            double zv = 0.0;
+            v0[q] = v1[q] = 0.0;
+            if (r < T.nrows) {
+                if (T.epi == EPI_MXY) zv = sum;
+                else if (T.epi == EPI_AMXY) zv = sum * T.alpha;
+                else if (T.epi == EPI_AXPBY) zv = ld_sc1d(T.y + r) * T.beta + T.alpha * sum;
+                else zv = T.alpha * sum;
+                T.z[r] = zv;
+                if (T.nred > 0) v0[q] = zv * (T.w0 == T.z ? zv : ld_sc1d(T.w0 + r));
+                if (T.nred > 1) v1[q] = zv * (T.w1 && T.w1 != T.z ? ld_sc1d(T.w1 + r) : zv);
+            }
+        }
+        // chunk_reduce's order: the four 64-row groups' halving trees, (w0 + w1) + (w2 + w3)
+        if (T.nred > 0) {
+            double w[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) w[q] = wave_sum_d(v0[q]);
+            if (lane == 0) T.part[blk] = (w[0] + w[1]) + (w[2] + w[3]);
+        }
+        if (T.nred > 1) {
+            double w[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) w[q] = wave_sum_d(v1[q]);
+            if (lane == 0) T.part[T.pcap + blk] = (w[0] + w[1]) + (w[2] + w[3]);
+        }
+    }
+}
 
 // slot layout (bytes): the step's coefficient block, its rhs, the hand-off inputs
 template <int P, int NA, bool RHS_NAT>
@@ -1042,6 +1176,10 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
 // plain division (profiles/r04/r04d_*, r04e_*, r04f_*): its range checks and
 // the extra operand cost as much as the shorter chain saves.
 
+#ifndef LINE2_EARLY_SHFL
+#define LINE2_EARLY_SHFL 1  // k-operand shuffle issued before the level's stores (k_line2 compute)
+#endif
+
 namespace l2 {
 constexpr int NJ = 16;  // lines per tile; LV (2 or 4) levels per step; P (8 or 16) planes per tile: 2 or 4 compute waves
 constexpr uint64_t GS = 0x0001000100010001ull;  // line 0 of each 16-lane group
@@ -1091,13 +1229,22 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
     const int lane = threadIdx.x & 63;
     const int nx = a.nx;
     if (a.guard && *a.guard != 0.0) {  // a batched iteration past the stop: consume the launch's tile claims
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.claim, (unsigned long long)a.ntiles + gridDim.x);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            atomicAdd(a.claim, (unsigned long long)a.ntiles + gridDim.x);
+            if (OUT == 1 && a.tail) {  // ... and the tail's chunk claims and tile counts
+                atomicAdd(a.tl.claim, (unsigned long long)a.tl.nblk + gridDim.x * l2::waves(P, NL, SW));
+                for (int K = 0; K < a.tl.S; K++) atomicAdd(a.tl.kdone + K, (unsigned)a.tl.W);
+            }
+        }
         return;
     }
 
+    int done_tile = -1;  // the tile this workgroup finished last (its completion is counted at the next claim)
     for (;;) {
         __syncthreads();
         if (threadIdx.x == 0) {
+            if (OUT == 1 && a.tail && done_tile >= 0)  // its storers' write-through stores drained before the barrier
+                __hip_atomic_fetch_add(a.tl.kdone + done_tile / a.tl.W, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // claims in wavefront order (LineSweep::d_order): every tile's producers
             // have a smaller anti-diagonal J + K and were claimed before it
             const int c = (int)(atomicAdd(a.claim, 1ull) - a.base);
@@ -1106,6 +1253,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
         __syncthreads();
         const int t = __builtin_amdgcn_readfirstlane(*s_tile);
         if (t >= a.ntiles) break;
+        done_tile = t;
         if (TRACE && threadIdx.x == 0) a.trace[8 * t] = __builtin_amdgcn_s_memrealtime();
         const LineTile d = a.tiles[t];
         const int T = d.T, TS = T / LV, nj = d.nj, np = d.np;
@@ -1208,10 +1356,11 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     h[lv] = __builtin_amdgcn_ballot_w64(lane_in && (unsigned)(LV * s + lv - loff) < (unsigned)nx);
                 if (s >= 0 && s < TS) {
                     double xq = xp;  // the previous level's value
+                    double xu = xs;  // lane - 16's value of the previous level
 #pragma unroll
                     for (int lv = 0; lv < LV; lv++) {
                         // level LV s + lv
-                        const double xk = sel_lanes(G0M, kx[lv], lv == 0 ? xs : up16(xq));
+                        const double xk = sel_lanes(G0M, kx[lv], xu);
                         const double xj = dpp_shr1g<4>(xq, cur.jv[lv]);
                         double v = cur.rh[lv] - cur.ck[lv] * xk;
                         v = v - cur.cj[lv] * xj;
@@ -1219,12 +1368,23 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                         if constexpr (NA == 4) v = v / cur.dg[lv];
                         const double x = sel_lanes(h[lv], v, xq);
                         if (trs && wave == 0 && lv == LV - 1) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
+#if LINE2_EARLY_SHFL
+                        // the next level's k operand (the next step's first, for the
+                        // last level) is shuffled BEFORE this level's hand-off and
+                        // LDS stores: its ds_bpermute round trip runs under them
+                        // instead of after them
+                        xu = up16(x);
+                        __builtin_amdgcn_sched_barrier(0);
+#endif
                         publish(LV * s + lv, h[lv], x);  // its store issues under the next level's arithmetic
                         res[((LV * s + lv) & (RSL - 1)) * ROWS + pw * NJ + ll] = x;
+#if !LINE2_EARLY_SHFL
+                        xu = up16(x);
+#endif
                         xq = x;
                     }
                     xp = xq;
-                    xs = up16(xq);  // the next step's first k-operand, off its critical path
+                    xs = xu;  // the next step's first k-operand, off its critical path
                 }
                 so = sn;
                 if (trs && s >= 0 && s < TS) ts[8 * s + (wave == 0 ? 1 : 7)] = __builtin_amdgcn_s_memtime();
@@ -1395,8 +1555,11 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                         const int q = 8 * B + m;
                         const int i = q - l - p - sig(p);
                         const double x = res[(q & (RSL - 1)) * ROWS + p * NJ + l];
-                        if (!(a.diag & 1) && p < np && l < nj && (unsigned)i < (unsigned)nx)
-                            a.out[a.mirror ? nb(p, l) - i : nb(p, l) + i] = x;
+                        if (!(a.diag & 1) && p < np && l < nj && (unsigned)i < (unsigned)nx) {
+                            double *o = a.out + (a.mirror ? nb(p, l) - i : nb(p, l) + i);
+                            if (a.tail) st_sc1d(o, x);  // read by the tail product on other CUs
+                            else *o = x;
+                        }
                     }
                 };
                 for (int s = S0; s <= TS; s++) {
@@ -1408,6 +1571,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                 }
                 // the last blocks' remaining quarters (every result is in LDS)
                 for (int s = TS + 1; s < SPB * ((T - 1) / 8 + 2); s++) slice(s);
+                if (a.tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // before the tile is counted
             } else {
                 // step s-1's LV levels: value k = 64 (w + SW it) + lane is level
                 // LV(s-1) + k / ROWS, plane (k >> 4) & (P-1), line k & 15; its place in the
@@ -1444,6 +1608,15 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     line_barrier();
                 }
             }
+        }
+    }
+    if constexpr (OUT == 1) {
+        if (a.tail) {  // no tile left for this workgroup: its waves run the tail product
+            int *soff = reinterpret_cast<int *>(smem);
+            __syncthreads();  // (the loop's last barrier already passed; the ring is free)
+            if (threadIdx.x < a.tl.ndiag) soff[threadIdx.x] = a.tl.off[threadIdx.x];
+            __syncthreads();
+            line_tail_waves(a.tl, a.out, a.err, soff);
         }
     }
 }
@@ -1674,7 +1847,9 @@ static int launch_line2_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &
 }
 
 // k_line2 sweep of ls: rhs from a stream; OUT 2: out = the U rhs stream, OUT 1: natural order
-static int launch_line2(lssp_amd_ctx *c, const LineILU &li, int which, const double *stream, double *out, int outk)
+// (tail: the product run by the sweep's workgroups after its tiles, OUT 1 only)
+static int launch_line2(lssp_amd_ctx *c, const LineILU &li, int which, const double *stream, double *out, int outk,
+                        const LineTail *tail = nullptr)
 {
     const LineSweep &ls = which ? li.U : li.L;
     LineArgs a{};
@@ -1700,6 +1875,8 @@ static int launch_line2(lssp_amd_ctx *c, const LineILU &li, int which, const dou
         const char *dg = getenv("LSSP_AMD_LINE_DIAG");
         a.diag = dg ? atoi(dg) : 0;
     }
+    a.tail = tail != nullptr && outk == 1;
+    if (a.tail) a.tl = *tail;
     // (the kernel is generic in LV; four levels per step measured slower)
     if (outk == 2) return ls.NA == 3 ? launch_line2_t<8, 2, 3, 2>(c, ls, a) : launch_line2_t<8, 2, 4, 2>(c, ls, a);
     return ls.NA == 3 ? launch_line2_t<8, 2, 3, 1>(c, ls, a) : launch_line2_t<8, 2, 4, 1>(c, ls, a);
@@ -1752,6 +1929,76 @@ int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const doubl
     LSSP_TRY(launch_line_gather(c, li.L, 0, rhs, li.d_lstream));
     LSSP_TRY(launch_line(c, li, 0, nullptr, false, nullptr, true, true));
     return launch_line(c, li, 1, nullptr, true, x, false);
+}
+
+int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs, const lssp_amd_mat *A,
+                           int epi, double alpha, double beta, const double *y, double *z, int nred,
+                           const double *w0, const double *w1)
+{
+    // LSSP_AMD_TAIL=0: the apply and the product as two separate steps (A/B runs,
+    // tests); =2: an ineligible call fails (EINVAL) instead of falling back (tests)
+    const char *te = getenv("LSSP_AMD_TAIL");
+    const int on = te ? atoi(te) : 1;
+    const long pl = (long)li.g.nx * li.g.ny, n = pl * li.g.nz;
+    if (!on || li.kind != 0 || li.LV < 2 || li.ntiles == 0 || !A || c->nranks > 1 || A->nhalo != 0 ||
+        A->ndiag == 0 || (long)A->nrows != n || A->max_off > pl || nred < 0 || nred > 2 || x == z || !A->Ad)
+        return on == 2 ? LSSP_AMD_EINVAL : LSSP_AMD_EUNSUPPORTED;
+    const int S = li.S, W = li.W, nz = li.g.nz;
+    if (!li.d_kdone) {
+        // every tile row holds W tiles (build_tiles); natural plane -> its L tile row
+        std::vector<int> kof(nz, 0);
+        for (int K = 0; K < S; K++) {
+            const LineTile &t = li.L.h_tiles[(size_t)K * W];
+            for (int k = t.k0; k < t.k0 + t.np; k++) kof[k] = K;
+        }
+        LineILU &m = const_cast<LineILU &>(li);
+        LSSP_HIP(hipMalloc(&m.d_kdone, sizeof(unsigned) * S));
+        LSSP_HIP(hipMalloc(&m.d_kof, sizeof(int) * nz));
+        LSSP_HIP(hipMalloc(&m.d_tclaim, sizeof(unsigned long long)));
+        LSSP_HIP(hipMemsetAsync(m.d_kdone, 0, sizeof(unsigned) * S, c->stream));
+        LSSP_HIP(hipMemsetAsync(m.d_tclaim, 0, sizeof(unsigned long long), c->stream));
+        LSSP_HIP(hipMemcpyAsync(m.d_kof, kof.data(), sizeof(int) * nz, hipMemcpyHostToDevice, c->stream));
+        LSSP_HIP(hipStreamSynchronize(c->stream));
+        m.tbase = 0;
+        m.kepoch = 0;
+    }
+    const long nblk = num_chunks(n);
+    LSSP_TRY(ensure_part(c, nblk));
+    LineTail T{};
+    T.Ap = A->Ap;
+    T.Ax = A->Ax;
+    T.Ad = A->Ad;
+    T.off = A->d_off;
+    T.ndiag = A->ndiag;
+    T.nrows = A->nrows;
+    T.epi = epi;
+    T.nred = nred;
+    T.y = y;
+    T.z = z;
+    T.alpha = alpha;
+    T.beta = beta;
+    T.w0 = w0;
+    T.w1 = w1;
+    T.part = c->d_part;
+    T.pcap = c->part_cap;
+    T.nblk = nblk;
+    T.claim = li.d_tclaim;
+    T.base = li.tbase;
+    T.kdone = li.d_kdone;
+    T.ktarget = (li.kepoch + 1) * (unsigned)W;
+    T.kof = li.d_kof;
+    T.S = S;
+    T.W = W;
+    T.nz = nz;
+    T.pl = pl;
+    LSSP_TRY(launch_line_gather(c, li.L, 0, rhs, li.d_lstream));
+    LSSP_TRY(launch_line2(c, li, 0, li.d_lstream, li.d_ustream, 2));
+    LSSP_TRY(launch_line2(c, li, 1, li.d_ustream, x, 1, &T));
+    // every wave of the grid ends on one failed chunk claim; every U tile counted once
+    li.tbase += (unsigned long long)nblk + (unsigned long long)std::min(li.U.ntiles, c->num_cus) *
+                                               l2::waves(8, LINE2_NL, LINE2_SW);
+    li.kepoch++;
+    return LSSP_AMD_OK;
 }
 
 int launch_line_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs)

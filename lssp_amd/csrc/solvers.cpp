@@ -124,6 +124,20 @@ struct Run {
         e.out0 = x;
         return ew(e);
     }
+    // x = M^-1 rhs, then z = op(A x) (+ fused dots): one rank with a line-swept
+    // ILU(0) runs the product in the U sweep's tail, as planes of x become
+    // final (launch_line_apply_spmv; bitwise the two steps)
+    int pc_spmv(double *x, const double *rhs, int epi, double alpha, double beta, const double *y, double *z,
+                int nred = 0, const double *w0 = nullptr, const double *w1 = nullptr)
+    {
+        if (M && !gpc && M->line.ntiles > 0 && c->nranks == 1) {
+            const int st = launch_line_apply_spmv(c, M->line, x, rhs, A, epi, alpha, beta, y, z, tree ? nred : 0,
+                                                  w0, w1);
+            if (st != LSSP_AMD_EUNSUPPORTED) return st;
+        }
+        LSSP_TRY(pc(x, rhs));
+        return spmv(epi, alpha, x, beta, y, z, nred, w0, w1);
+    }
     int sync(int first, int count)
     {
         LSSP_HIP(hipMemcpyAsync(c->h_scal + first, c->d_scal + first, sizeof(double) * count,
@@ -244,8 +258,7 @@ int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
             e.out0 = p;
         }
         LSSP_TRY(R.ew(e));
-        LSSP_TRY(R.pc(ph, p));                                   // :107-108
-        LSSP_TRY(R.spmv(EPI_AMX, 1, ph, 0, p, v, 1, rh));         // :110
+        LSSP_TRY(R.pc_spmv(ph, p, EPI_AMX, 1, 0, p, v, 1, rh));  // :107-108, :110
         LSSP_TRY(R.fin1(rh, v, R.fin(FIN_BICG_ALPHA, 1, R.T())));  // :112
         e = Ew();
         e.kind = K_BICG_S;  // :113-115
@@ -265,8 +278,7 @@ int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
         *pos_s = R.tl;
         const Fin fs = R.fin(FIN_BICG_S, 1, R.T());          // :117
         if (!merge_s) LSSP_TRY(R.fin1(s, s, fs));
-        LSSP_TRY(R.pc(sh, s));                                 // :130-131
-        LSSP_TRY(R.spmv(EPI_AMX, 1, sh, 0, p, t, 2, s, nullptr));  // :133
+        LSSP_TRY(R.pc_spmv(sh, s, EPI_AMX, 1, 0, p, t, 2, s, nullptr));  // :130-131, :133
         {
             int t0 = R.T(), t1 = R.T();
             if (merge_s) {

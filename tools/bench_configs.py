@@ -258,6 +258,7 @@ def general_ilu(args):
     Ap, Aj, Ax = lssp_amd.poisson(3, args.grid)
     case(f"7-pt {args.grid}^3 ILU(0), packet sweeps", Ap, Aj, Ax, 0, False)
     case(f"7-pt {args.grid}^3 ILU(0), line sweeps", Ap, Aj, Ax, 0, True)
+    case(f"7-pt {args.grid}^3 ILU(1) (the reference's default level), line sweeps", Ap, Aj, Ax, 1, True)
     dev.close()
 
 
