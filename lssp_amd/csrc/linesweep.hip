@@ -527,7 +527,7 @@ __device__ void line_tail_waves(const LineTail &T, const double *x, int *err, co
             const int ka = max(r0 / (int)T.pl - 1, 0), kb = min((r1 - 1) / (int)T.pl + 1, T.nz - 1);
             const int K0 = T.kof[ka], K1 = T.kof[kb];
             for (int K = K0; K <= K1; K++) {
-                const unsigned *cnt = T.kdone + (T.S - 1 - K);  // U tile row of L tile row K
+                unsigned *cnt = T.kdone + (T.S - 1 - K);  // U tile row of L tile row K
                 for (;;) {
                     // (an atomic read: coherent with the tiles' atomic increments on every XCD)
                     if (__hip_atomic_fetch_add(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - T.ktarget <
