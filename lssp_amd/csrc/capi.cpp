@@ -222,6 +222,7 @@ int build_diag_ids(lssp_amd_mat *M, const int *Ap, const int *Aj)
     M->ndiag = (int)off.size();
     M->max_off = 0;
     for (int o : off) M->max_off = std::max(M->max_off, std::abs(o));
+    if (M->nhalo == 0) M->max_off_int = M->max_off;  // (distributed: set over the halo-free chunks at upload)
     return LSSP_AMD_OK;
 }
 

@@ -182,6 +182,17 @@ int spmv_halo(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, dou
     return launch_spmv(c, A, epi, alpha, x, beta, y, z, nred, w0, w1, A->ich1, nall);
 }
 
+// after a product of the halo-free chunks [ich0, ich1) ran elsewhere (the U
+// sweep's tail): the halo round, then the boundary chunks
+int spmv_boundary(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, double *x, double beta,
+                  const double *y, double *z, int nred, const double *w0, const double *w1)
+{
+    const long nall = num_chunks(A->nrows);
+    LSSP_TRY(halo_exchange(A, x));
+    LSSP_TRY(launch_spmv(c, A, epi, alpha, x, beta, y, z, nred, w0, w1, 0, A->ich0));
+    return launch_spmv(c, A, epi, alpha, x, beta, y, z, nred, w0, w1, A->ich1, nall);
+}
+
 int comm_destroy(lssp_amd_ctx *c)
 {
     if (c->comm) {
@@ -456,6 +467,10 @@ int lssp_amd_mat_upload_dist(lssp_amd_ctx *c, int n_global, int row0, int nlocal
         }
         M->ich0 = best0;
         M->ich1 = best1;
+        int mo = 0;  // the halo-free rows' widest reach (the U sweep's tail product, linesweep.hip)
+        for (long i = best0 * 256; i < std::min<long>(best1 * 256, nlocal); i++)
+            for (int k = Ap[i]; k < Ap[i + 1]; k++) mo = std::max(mo, std::abs(lj[k] - (int)i));
+        M->max_off_int = mo;
     }
     // receive plan (per owner)
     std::vector<int> need(P, 0);

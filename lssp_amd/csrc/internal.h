@@ -113,6 +113,9 @@ struct lssp_amd_mat {
     int *d_off = nullptr;
     int ndiag = 0;
     int max_off = 0;  // max |col - row| of the coded offsets
+    // max |col - row| over the rows of the halo-free chunks [ich0, ich1) of a
+    // distributed matrix (its whole row range on one rank: max_off)
+    int max_off_int = 0;
     // windowed x (k_spmv_sell): when every 1024-row block's columns fall in a
     // span of at most WIN_CAP entries, d_win[2b], d_win[2b+1] = that span
     // [lo, hi) and the product stages x[lo, hi) in LDS; nullptr: not windowed
@@ -391,6 +394,10 @@ int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const doubl
 int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs, const lssp_amd_mat *A,
                            int epi, double alpha, double beta, const double *y, double *z, int nred,
                            const double *w0, const double *w1);
+// the same on P ranks: the tail computes the halo-free chunks [ich0, ich1)
+// only; the halo round and the boundary chunks follow it (spmv_boundary)
+int spmv_boundary(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, double *x, double beta,
+                  const double *y, double *z, int nred, const double *w0, const double *w1);
 int launch_line_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs);
 void free_trisched(TriSched &t);
 

@@ -462,7 +462,7 @@ struct LineTail {
     double alpha, beta;
     const double *w0, *w1;
     double *part;
-    long pcap, nblk;
+    long pcap, nblk, cend;      // chunks [cend - nblk, cend)
     unsigned long long *claim;  // chunk claims (monotonic)
     unsigned long long base;
     unsigned *kdone;            // U tiles finished per tile row (monotonic)
@@ -520,7 +520,7 @@ __device__ void line_tail_waves(const LineTail &T, const double *x, int *err, co
         const unsigned chi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(c >> 32));
         const unsigned long long cl = ((unsigned long long)chi << 32) | clo;
         if (cl >= (unsigned long long)T.nblk) break;
-        const long blk = T.nblk - 1 - (long)cl;
+        const long blk = T.cend - 1 - (long)cl;
         const int r0 = (int)(blk * 256), r1 = min(r0 + 256, T.nrows);
         // the planes the chunk's rows read: k-1 .. k+1 of its first / last row
         if (lane == 0) {
@@ -1940,8 +1940,12 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
     const char *te = getenv("LSSP_AMD_TAIL");
     const int on = te ? atoi(te) : 1;
     const long pl = (long)li.g.nx * li.g.ny, n = pl * li.g.nz;
-    if (!on || li.kind != 0 || li.LV < 2 || li.ntiles == 0 || !A || c->nranks > 1 || A->nhalo != 0 ||
-        A->ndiag == 0 || (long)A->nrows != n || A->max_off > pl || nred < 0 || nred > 2 || x == z || !A->Ad)
+    // one rank: every chunk; P ranks: the halo-free chunks (the caller runs the rest)
+    const bool dist = A && A->nhalo > 0;
+    const long nall = num_chunks(n);
+    const long cb = dist ? A->ich0 : 0, ce = dist ? A->ich1 : nall;
+    if (!on || li.kind != 0 || li.LV < 2 || li.ntiles == 0 || !A || (long)A->nrows != n || ce <= cb ||
+        (c->nranks > 1) != dist || A->ndiag == 0 || A->max_off_int > pl || nred < 0 || nred > 2 || x == z || !A->Ad)
         return on == 2 ? LSSP_AMD_EINVAL : LSSP_AMD_EUNSUPPORTED;
     const int S = li.S, W = li.W, nz = li.g.nz;
     if (!li.d_kdone) {
@@ -1962,8 +1966,8 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
         m.tbase = 0;
         m.kepoch = 0;
     }
-    const long nblk = num_chunks(n);
-    LSSP_TRY(ensure_part(c, nblk));
+    const long nblk = ce - cb;
+    LSSP_TRY(ensure_part(c, nall));
     LineTail T{};
     T.Ap = A->Ap;
     T.Ax = A->Ax;
@@ -1982,6 +1986,7 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
     T.part = c->d_part;
     T.pcap = c->part_cap;
     T.nblk = nblk;
+    T.cend = ce;
     T.claim = li.d_tclaim;
     T.base = li.tbase;
     T.kdone = li.d_kdone;

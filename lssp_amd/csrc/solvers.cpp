@@ -130,9 +130,11 @@ struct Run {
     int pc_spmv(double *x, const double *rhs, int epi, double alpha, double beta, const double *y, double *z,
                 int nred = 0, const double *w0 = nullptr, const double *w1 = nullptr)
     {
-        if (M && !gpc && M->line.ntiles > 0 && c->nranks == 1) {
-            const int st = launch_line_apply_spmv(c, M->line, x, rhs, A, epi, alpha, beta, y, z, tree ? nred : 0,
-                                                  w0, w1);
+        if (M && !gpc && M->line.ntiles > 0) {
+            const int nr = tree ? nred : 0;
+            const int st = launch_line_apply_spmv(c, M->line, x, rhs, A, epi, alpha, beta, y, z, nr, w0, w1);
+            if (st == LSSP_AMD_OK && c->nranks > 1)  // the halo round and the chunks that read it
+                return spmv_boundary(c, A, epi, alpha, x, beta, y, z, nr, w0, w1);
             if (st != LSSP_AMD_EUNSUPPORTED) return st;
         }
         LSSP_TRY(pc(x, rhs));

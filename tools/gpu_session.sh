@@ -12,6 +12,7 @@
 #   pmc              two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) -> pmc_traffic.json
 #   tests[=EXPR]     pytest -m gpu (optionally -k EXPR) -> pytest.log
 #   file=PATH        pytest -m gpu on one test file -> pytest_<name>.log
+#   quick=PATH       the same with a 120 s per-test limit and -x (new kernels)
 #   project512       tools/project_ranks.py --grid 512 --ranks 1,8 -> project_ranks_512.jsonl
 #   project216       tools/project_ranks.py --grid 216 --ranks 1,2,4,8 -> project_ranks_216.jsonl
 #   config3 / config5 / general   tools/bench_configs.py gmres-ilut / cg-thermal / general-ilu
@@ -50,6 +51,11 @@ for step in "$@"; do
   file=*)
     F=${step#file=}; B=$(basename "$F" .py)
     timeout -k 10 1200 python -u -m pytest "$F" -m gpu -v -s --timeout 900 --timeout-method thread > $O/pytest_$B.log 2>&1 || { tail -40 $O/pytest_$B.log; fail $step $?; }
+    tail -3 $O/pytest_$B.log
+    ;;
+  quick=*)
+    F=${step#quick=}; B=$(basename "$F" .py)
+    timeout -k 10 400 python -u -m pytest "$F" -m gpu -v -s -x --timeout 120 --timeout-method thread > $O/pytest_$B.log 2>&1 || { tail -40 $O/pytest_$B.log; fail $step $?; }
     tail -3 $O/pytest_$B.log
     ;;
   project512)
