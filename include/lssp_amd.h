@@ -157,7 +157,10 @@ int lssp_amd_ilu_apply(lssp_amd_ctx *ctx, const lssp_amd_ilu *M, double *x, cons
  * synchronous lssp_amd_ilu_apply returns when x is written, like the
  * reference's pc.solve); lssp_amd_ilu_check then waits for the stream and
  * reports a hand-off timeout (LSSP_AMD_ETIMEOUT) of any apply since the last
- * check, re-arming the factor's hand-off buffers. */
+ * check, re-arming the factor's hand-off buffers.  After an ETIMEOUT, the x of
+ * EVERY apply enqueued since the last successful check is invalid (an apply
+ * queued behind the one that timed out reads its un-armed hand-off buffers):
+ * re-run them. */
 int lssp_amd_ilu_apply_async(lssp_amd_ctx *ctx, const lssp_amd_ilu *M, double *x, const double *rhs);
 int lssp_amd_ilu_check(lssp_amd_ctx *ctx, const lssp_amd_ilu *M);
 /* one triangular sweep: which = 0 lower (solver-tri.cxx:4-24), 1 upper (:26-46) */

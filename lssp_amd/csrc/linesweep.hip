@@ -470,6 +470,7 @@ struct LineTail {
     const int *kof;             // natural plane -> L tile row
     int S, W, nz;
     long pl;                    // rows per plane
+    unsigned *dbg;              // LSSP_AMD_TAIL_DIAG: progress words in mapped host memory (diagnostics)
 };
 
 struct LineArgs {
@@ -519,7 +520,15 @@ __device__ void line_tail_waves(const LineTail &T, const double *x, int *err, co
         const unsigned clo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)c);
         const unsigned chi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(c >> 32));
         const unsigned long long cl = ((unsigned long long)chi << 32) | clo;
-        if (cl >= (unsigned long long)T.nblk) break;
+        unsigned *dw = T.dbg ? T.dbg + 1024 + 4 * (blockIdx.x * 16 + (threadIdx.x >> 6)) : nullptr;
+        if (dw && lane == 0) {
+            dw[0] = 1;
+            dw[1] = (unsigned)cl;
+        }
+        if (cl >= (unsigned long long)T.nblk) {
+            if (dw && lane == 0) dw[0] = 9;
+            break;
+        }
         const long blk = T.cend - 1 - (long)cl;
         const int r0 = (int)(blk * 256), r1 = min(r0 + 256, T.nrows);
         // the planes the chunk's rows read: k-1 .. k+1 of its first / last row
@@ -530,9 +539,12 @@ __device__ void line_tail_waves(const LineTail &T, const double *x, int *err, co
                 unsigned *cnt = T.kdone + (T.S - 1 - K);  // U tile row of L tile row K
                 for (;;) {
                     // (an atomic read: coherent with the tiles' atomic increments on every XCD)
-                    if (__hip_atomic_fetch_add(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - T.ktarget <
-                        0x80000000u)
-                        break;
+                    const unsigned seen = __hip_atomic_fetch_add(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (dw) {
+                        dw[2] = (unsigned)K;
+                        dw[3] = seen;
+                    }
+                    if (seen - T.ktarget < 0x80000000u) break;
                     if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
                         __builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s: the sweep gave up
                         atomicOr(err, 8);
@@ -543,6 +555,7 @@ __device__ void line_tail_waves(const LineTail &T, const double *x, int *err, co
             }
         }
         __builtin_amdgcn_wave_barrier();
+        if (dw && lane == 0) dw[0] = 2;
         double v0[4], v1[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -1243,8 +1256,10 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
     for (;;) {
         __syncthreads();
         if (threadIdx.x == 0) {
-            if (OUT == 1 && a.tail && done_tile >= 0)  // its storers' write-through stores drained before the barrier
+            if (OUT == 1 && a.tail && done_tile >= 0) {  // its storers' write-through stores drained before the barrier
                 __hip_atomic_fetch_add(a.tl.kdone + done_tile / a.tl.W, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (a.tl.dbg) a.tl.dbg[blockIdx.x] += 1;
+            }
             // claims in wavefront order (LineSweep::d_order): every tile's producers
             // have a smaller anti-diagonal J + K and were claimed before it
             const int c = (int)(atomicAdd(a.claim, 1ull) - a.base);
@@ -1931,6 +1946,8 @@ int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const doubl
     return launch_line(c, li, 1, nullptr, true, x, false);
 }
 
+unsigned *tail_dbg_host = nullptr;  // LSSP_AMD_TAIL_DIAG (lssp_amd_debug_words)
+
 int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs, const lssp_amd_mat *A,
                            int epi, double alpha, double beta, const double *y, double *z, int nred,
                            const double *w0, const double *w1)
@@ -1996,6 +2013,16 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
     T.W = W;
     T.nz = nz;
     T.pl = pl;
+    static unsigned *dbg_h = nullptr, *dbg_d = nullptr;
+    if (getenv("LSSP_AMD_TAIL_DIAG")) {
+        if (!dbg_h) {
+            LSSP_HIP(hipHostMalloc(&dbg_h, sizeof(unsigned) * 32768, hipHostMallocMapped));
+            LSSP_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&dbg_d), dbg_h, 0));
+        }
+        memset(dbg_h, 0, sizeof(unsigned) * 32768);
+        tail_dbg_host = dbg_h;
+        T.dbg = dbg_d;
+    }
     LSSP_TRY(launch_line_gather(c, li.L, 0, rhs, li.d_lstream));
     LSSP_TRY(launch_line2(c, li, 0, li.d_lstream, li.d_ustream, 2));
     LSSP_TRY(launch_line2(c, li, 1, li.d_ustream, x, 1, &T));
@@ -2018,3 +2045,11 @@ int launch_line_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, 
 }
 
 }  // namespace lssp_amd
+
+// diagnostics (LSSP_AMD_TAIL_DIAG): the tail's progress words, readable while a kernel runs
+extern "C" int lssp_amd_debug_words(unsigned *out, int n)
+{
+    if (!lssp_amd::tail_dbg_host || !out) return LSSP_AMD_EINVAL;
+    memcpy(out, lssp_amd::tail_dbg_host, sizeof(unsigned) * std::min(n, 32768));
+    return LSSP_AMD_OK;
+}
