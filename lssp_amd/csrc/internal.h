@@ -384,6 +384,9 @@ int build_linefill(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std
                    const std::vector<double> &Lx, const std::vector<int> &Up, const std::vector<int> &Uj,
                    const std::vector<double> &Ux, LineILU &li);
 int launch_linefill_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs);
+struct LineTail;  // linesweep_dev.h
+int launch_linefill_apply_tail(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs, const LineTail &T,
+                               long *tail_waves);
 int launch_linefill_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs);
 void free_line_sweep(LineILU &li);
 int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs);

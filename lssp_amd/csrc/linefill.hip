@@ -371,6 +371,8 @@ struct FillArgs {
     int mirror;        // U sweep: natural row = n-1 - sweep row
     int *err;
     const double *guard;  // lssp_amd_ctx::guard
+    int tail;     // OUT 1: run the product tl after the tiles (linesweep_dev.h LineTail)
+    LineTail tl;
 };
 
 template <int NA, int OUT, int NL, int D, int DH, int SW>
@@ -401,19 +403,29 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
     const int lane = threadIdx.x & 63;
     const int nx = a.nx;
     if (a.guard && *a.guard != 0.0) {  // a batched iteration past the stop: consume the launch's tile claims
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.claim, (unsigned long long)a.ntiles + gridDim.x);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            atomicAdd(a.claim, (unsigned long long)a.ntiles + gridDim.x);
+            if (OUT == 1 && a.tail) {  // ... and the tail's chunk claims and tile counts
+                atomicAdd(a.tl.claim, (unsigned long long)a.tl.nblk + gridDim.x * waves(NL, SW));
+                for (int K = 0; K < a.tl.S; K++) atomicAdd(a.tl.kdone + K, (unsigned)a.tl.W);
+            }
+        }
         return;
     }
 
+    int done_tile = -1;  // the tile this workgroup finished last (counted at the next claim)
     for (;;) {
         __syncthreads();
         if (threadIdx.x == 0) {
+            if (OUT == 1 && a.tail && done_tile >= 0)  // its storers' write-through stores drained before the barrier
+                __hip_atomic_fetch_add(a.tl.kdone + done_tile / a.tl.W, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int c = (int)(atomicAdd(a.claim, 1ull) - a.base);
             *s_tile = c < a.ntiles ? a.order[c] : a.ntiles;
         }
         __syncthreads();
         const int t = __builtin_amdgcn_readfirstlane(*s_tile);
         if (t >= a.ntiles) break;
+        done_tile = t;
         const LineTile d = a.tiles[t];
         const int T = d.T, TS = T / LV, nj = d.nj, np = d.np;
         const long SB = (long)P * nj;  // rows per level block
@@ -691,8 +703,10 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
                         const int i = q - 2 * l - p - sig(p);
                         const int j = d.j0 + l - d.k0 - p;
                         const double x = res[(q & (RSL - 1)) * ROWS + p * NJ + l];
-                        if (p < np && l < nj && (unsigned)j < (unsigned)a.ny && (unsigned)i < (unsigned)nx)
-                            a.out[nat(p, l, i)] = x;
+                        if (p < np && l < nj && (unsigned)j < (unsigned)a.ny && (unsigned)i < (unsigned)nx) {
+                            if (a.tail) st_sc1d(a.out + nat(p, l, i), x);  // read by the tail product on other CUs
+                            else a.out[nat(p, l, i)] = x;
+                        }
                     }
                 };
                 for (int s = S0; s <= TS; s++) {
@@ -703,6 +717,7 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
                 rearm(-1);  // step -1's entries (levels -2, -1)
                 // the last blocks' remaining quarters (every result is in LDS)
                 for (int s = TS + 1; s < 4 * ((T - 1) / 8) + 8; s++) slice(s);
+                if (a.tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // before the tile is counted
             } else {
                 // step s-1's two levels: value k = 64 (w + SW u) + lane is level
                 // 2(s-1) + (k >> 7), plane (k >> 4) & 7, line k & 15; its place in the
@@ -738,6 +753,15 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
                     line_barrier();
                 }
             }
+        }
+    }
+    if constexpr (OUT == 1) {
+        if (a.tail) {  // no tile left for this workgroup: its waves run the tail product
+            int *soff = reinterpret_cast<int *>(smem);  // (the ring's LDS is free now: TAIL_LDS_BYTES fit in it)
+            __syncthreads();
+            if (threadIdx.x < a.tl.ndiag) soff[threadIdx.x] = a.tl.off[threadIdx.x];
+            __syncthreads();
+            line_tail_waves(a.tl, a.out, a.err, smem);
         }
     }
 }
@@ -805,6 +829,7 @@ int linef_launch_t(lssp_amd_ctx *c, const LineSweep &ls, const FillArgs &a)
 {
     constexpr int lds = lf::lds_bytes<NA, OUT, LINEF_D>();
     static_assert(lds <= 160 * 1024, "LDS");
+    static_assert(OUT != 1 || lds >= TAIL_LDS_BYTES(lf::waves(LF_NL, LF_SW)), "the tail product's LDS");
     auto kern = k_linef<NA, OUT, LF_NL, LINEF_D, LINEF_DH, LF_SW>;
     static bool attr = false;
     if (!attr) {
@@ -819,8 +844,9 @@ int linef_launch_t(lssp_amd_ctx *c, const LineSweep &ls, const FillArgs &a)
 }
 
 // one sweep of li (which: 0 L, 1 U) from its rhs stream; OUT 2: out = the U
-// rhs stream, OUT 1: natural order
-int linef_sweep(lssp_amd_ctx *c, const LineILU &li, int which, const double *stream, double *out, int outk)
+// rhs stream, OUT 1: natural order (tail: the product after the tiles)
+int linef_sweep(lssp_amd_ctx *c, const LineILU &li, int which, const double *stream, double *out, int outk,
+                const LineTail *tail = nullptr)
 {
     const LineSweep &ls = which ? li.U : li.L;
     FillArgs a{};
@@ -842,6 +868,8 @@ int linef_sweep(lssp_amd_ctx *c, const LineILU &li, int which, const double *str
     a.mirror = which;
     a.err = c->d_err;
     a.guard = c->guard;
+    a.tail = tail != nullptr && outk == 1;
+    if (a.tail) a.tl = *tail;
     if (outk == 2) return ls.NA == 6 ? linef_launch_t<6, 2>(c, ls, a) : linef_launch_t<7, 2>(c, ls, a);
     return ls.NA == 6 ? linef_launch_t<6, 1>(c, ls, a) : linef_launch_t<7, 1>(c, ls, a);
 }
@@ -852,6 +880,18 @@ int launch_linefill_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const d
     LSSP_TRY(linef_gather(c, li.L, 0, rhs, li.d_lstream));
     LSSP_TRY(linef_sweep(c, li, 0, li.d_lstream, li.d_ustream, 2));
     return linef_sweep(c, li, 1, li.d_ustream, x, 1);
+}
+
+// the apply with the U sweep's tail product (launch_line_apply_spmv prepared T);
+// returns the tail waves of the launch (each ends on one failed chunk claim)
+int launch_linefill_apply_tail(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs, const LineTail &T,
+                               long *tail_waves)
+{
+    LSSP_TRY(linef_gather(c, li.L, 0, rhs, li.d_lstream));
+    LSSP_TRY(linef_sweep(c, li, 0, li.d_lstream, li.d_ustream, 2));
+    LSSP_TRY(linef_sweep(c, li, 1, li.d_ustream, x, 1, &T));
+    *tail_waves = (long)std::min(li.U.ntiles, c->num_cus) * lf::waves(LF_NL, LF_SW);
+    return LSSP_AMD_OK;
 }
 
 int launch_linefill_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs)

@@ -437,42 +437,6 @@ void free_line_sweep(LineILU &li)
 // ---------------------------------------------------------------------------
 // device
 // ---------------------------------------------------------------------------
-// The product z = op(A x) on the output x of a U sweep, run by the sweep's
-// own workgroups once the tile claims are exhausted (launch_line_apply_spmv):
-// a workgroup that finds no tile left turns its 11 waves into product waves,
-// each claiming whole 256-row reduction chunks from the top of the matrix down
-// (the U sweep completes planes in that order) and starting a chunk once every
-// plane its rows read (k-1 .. k+1, a 5-/7-point stencil of the sweep's grid)
-// is final: the U tiles count their completion per tile row (kdone, agent-
-// scope atomics after the storers' write-through stores drained).  Lane l of
-// a wave owns rows 64q + l (q = 0..3) of its chunk, forms each row's sum in
-// CSR order from 0.0 and the epilogue of k_spmv3, and the chunk's fused-dot
-// partials are (w0 + w1) + (w2 + w3) of the four 64-row wave sums -- exactly
-// chunk_reduce's order -- so every output and partial is bitwise k_spmv3's.
-// Only CUs whose sweep work is over run product waves: the hand-off polls of
-// the tiles still running do not queue behind product loads.
-struct LineTail {
-    const int *Ap;
-    const double *Ax;
-    const uint8_t *Ad;  // diagonal-id coding (lssp_amd_mat::Ad)
-    const int *off;
-    int ndiag, nrows, epi, nred;
-    const double *y;
-    double *z;
-    double alpha, beta;
-    const double *w0, *w1;
-    double *part;
-    long pcap, nblk, cend;      // chunks [cend - nblk, cend)
-    unsigned long long *claim;  // chunk claims (monotonic)
-    unsigned long long base;
-    unsigned *kdone;            // U tiles finished per tile row (monotonic)
-    unsigned ktarget;           // this launch's count per row (W x launches)
-    const int *kof;             // natural plane -> L tile row
-    int S, W, nz;
-    long pl;                    // rows per plane
-    unsigned *dbg;              // LSSP_AMD_TAIL_DIAG: progress words in mapped host memory (diagnostics)
-};
-
 struct LineArgs {
     int nx, ny, ntiles;
     long n;
@@ -497,109 +461,6 @@ struct LineArgs {
     int tail;     // k_line2 OUT 1: run the product tl after the tiles (write-through output, tile counts)
     LineTail tl;
 };
-
-__device__ __forceinline__ double ld_sc1d(const double *p)
-{
-    return __longlong_as_double(
-        (long long)__hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void st_sc1d(double *p, double v)
-{
-    __hip_atomic_store(reinterpret_cast<uint64_t *>(p), (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// one wave's share of the tail product (see LineTail); soff: the offset table in LDS
-__device__ void line_tail_waves(const LineTail &T, const double *x, int *err, const int *soff)
-{
-    const int lane = threadIdx.x & 63;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        unsigned long long c = 0;
-        if (lane == 0) c = atomicAdd(T.claim, 1ull) - T.base;
-        const unsigned clo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)c);
-        const unsigned chi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(c >> 32));
-        const unsigned long long cl = ((unsigned long long)chi << 32) | clo;
-        unsigned *dw = T.dbg ? T.dbg + 1024 + 4 * (blockIdx.x * 16 + (threadIdx.x >> 6)) : nullptr;
-        if (dw && lane == 0) {
-            dw[0] = 1;
-            dw[1] = (unsigned)cl;
-        }
-        if (cl >= (unsigned long long)T.nblk) {
-            if (dw && lane == 0) dw[0] = 9;
-            break;
-        }
-        const long blk = T.cend - 1 - (long)cl;
-        const int r0 = (int)(blk * 256), r1 = min(r0 + 256, T.nrows);
-        // the planes the chunk's rows read: k-1 .. k+1 of its first / last row
-        if (lane == 0) {
-            const int ka = max(r0 / (int)T.pl - 1, 0), kb = min((r1 - 1) / (int)T.pl + 1, T.nz - 1);
-            const int K0 = T.kof[ka], K1 = T.kof[kb];
-            for (int K = K0; K <= K1; K++) {
-                unsigned *cnt = T.kdone + (T.S - 1 - K);  // U tile row of L tile row K
-                for (;;) {
-                    // (an atomic read: coherent with the tiles' atomic increments on every XCD)
-                    const unsigned seen = __hip_atomic_fetch_add(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (dw) {
-                        dw[2] = (unsigned)K;
-                        dw[3] = seen;
-                    }
-                    if (seen - T.ktarget < 0x80000000u) break;
-                    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
-                        __builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s: the sweep gave up
-                        atomicOr(err, 8);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (dw && lane == 0) dw[0] = 2;
-        double v0[4], v1[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int r = r0 + 64 * q + lane;
-            const int rr = min(r, T.nrows - 1);
-            const int rb = T.Ap[rr], re = T.Ap[rr + 1];
-            double pr[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int k = max(min(rb + u, re - 1), 0);
-                pr[u] = ld_sc1d(x + rr + soff[T.Ad[k]]) * T.Ax[k];
-            }
-            double sum = 0;
-#pragma unroll
-            for (int u = 0; u < 8; u++)
-                if (u < re - rb) sum += pr[u];
-            for (int k = rb + 8; k < re; k++) sum += ld_sc1d(x + rr + soff[T.Ad[k]]) * T.Ax[k];
-            double zv = 0.0;
-            v0[q] = v1[q] = 0.0;
-            if (r < T.nrows) {
-                if (T.epi == EPI_MXY) zv = sum;
-                else if (T.epi == EPI_AMXY) zv = sum * T.alpha;
-                else if (T.epi == EPI_AXPBY) zv = ld_sc1d(T.y + r) * T.beta + T.alpha * sum;
-                else zv = T.alpha * sum;
-                T.z[r] = zv;
-                if (T.nred > 0) v0[q] = zv * (T.w0 == T.z ? zv : ld_sc1d(T.w0 + r));
-                if (T.nred > 1) v1[q] = zv * (T.w1 && T.w1 != T.z ? ld_sc1d(T.w1 + r) : zv);
-            }
-        }
-        // chunk_reduce's order: the four 64-row groups' halving trees, (w0 + w1) + (w2 + w3)
-        if (T.nred > 0) {
-            double w[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) w[q] = wave_sum_d(v0[q]);
-            if (lane == 0) T.part[blk] = (w[0] + w[1]) + (w[2] + w[3]);
-        }
-        if (T.nred > 1) {
-            double w[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) w[q] = wave_sum_d(v1[q]);
-            if (lane == 0) T.part[T.pcap + blk] = (w[0] + w[1]) + (w[2] + w[3]);
-        }
-    }
-}
 
 // slot layout (bytes): the step's coefficient block, its rhs, the hand-off inputs
 template <int P, int NA, bool RHS_NAT>
@@ -1627,11 +1488,11 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
     }
     if constexpr (OUT == 1) {
         if (a.tail) {  // no tile left for this workgroup: its waves run the tail product
-            int *soff = reinterpret_cast<int *>(smem);
+            int *soff = reinterpret_cast<int *>(smem);  // (the ring's LDS is free now: TAIL_LDS_BYTES fit in it)
             __syncthreads();  // (the loop's last barrier already passed; the ring is free)
             if (threadIdx.x < a.tl.ndiag) soff[threadIdx.x] = a.tl.off[threadIdx.x];
             __syncthreads();
-            line_tail_waves(a.tl, a.out, a.err, soff);
+            line_tail_waves(a.tl, a.out, a.err, smem);
         }
     }
 }
@@ -1833,6 +1694,7 @@ static int launch_line2_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &
 {
     constexpr int lds = l2::lds_bytes<NA, OUT, line2_d<LV>(), P, LV>();
     static_assert(lds <= 160 * 1024, "LDS");
+    static_assert(OUT != 1 || lds >= TAIL_LDS_BYTES(l2::waves(P, LINE2_NL, LINE2_SW)), "the tail product's LDS");
     // diagnostics only: LSSP_AMD_LINE_TRACE=path[:tile] appends one JSON line per sweep
     static const char *trp = getenv("LSSP_AMD_LINE_TRACE");
     if (!trp) return launch_line2_k<P, LV, NA, OUT, false>(c, ls, a, lds);
@@ -1961,7 +1823,7 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
     const bool dist = A && A->nhalo > 0;
     const long nall = num_chunks(n);
     const long cb = dist ? A->ich0 : 0, ce = dist ? A->ich1 : nall;
-    if (!on || li.kind != 0 || li.LV < 2 || li.ntiles == 0 || !A || (long)A->nrows != n || ce <= cb ||
+    if (!on || li.kind > 1 || li.LV < 2 || li.ntiles == 0 || !A || (long)A->nrows != n || ce <= cb ||
         (c->nranks > 1) != dist || A->ndiag == 0 || A->max_off_int > pl || nred < 0 || nred > 2 || x == z || !A->Ad)
         return on == 2 ? LSSP_AMD_EINVAL : LSSP_AMD_EUNSUPPORTED;
     const int S = li.S, W = li.W, nz = li.g.nz;
@@ -2023,12 +1885,16 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
         tail_dbg_host = dbg_h;
         T.dbg = dbg_d;
     }
-    LSSP_TRY(launch_line_gather(c, li.L, 0, rhs, li.d_lstream));
-    LSSP_TRY(launch_line2(c, li, 0, li.d_lstream, li.d_ustream, 2));
-    LSSP_TRY(launch_line2(c, li, 1, li.d_ustream, x, 1, &T));
+    long tail_waves = (long)std::min(li.U.ntiles, c->num_cus) * l2::waves(8, LINE2_NL, LINE2_SW);
+    if (li.kind == 1) {  // the 7-/5-point ILU(1) line sweeps (linefill.hip)
+        LSSP_TRY(launch_linefill_apply_tail(c, li, x, rhs, T, &tail_waves));
+    } else {
+        LSSP_TRY(launch_line_gather(c, li.L, 0, rhs, li.d_lstream));
+        LSSP_TRY(launch_line2(c, li, 0, li.d_lstream, li.d_ustream, 2));
+        LSSP_TRY(launch_line2(c, li, 1, li.d_ustream, x, 1, &T));
+    }
     // every wave of the grid ends on one failed chunk claim; every U tile counted once
-    li.tbase += (unsigned long long)nblk + (unsigned long long)std::min(li.U.ntiles, c->num_cus) *
-                                               l2::waves(8, LINE2_NL, LINE2_SW);
+    li.tbase += (unsigned long long)nblk + (unsigned long long)tail_waves;
     li.kepoch++;
     return LSSP_AMD_OK;
 }

@@ -6,7 +6,8 @@ fused dots) and the oracle's TREE-order restatement of the driver.
 
 LSSP_AMD_TAIL=2 makes an ineligible call fail instead of falling back, so a
 passing run here proves the tail path ran; LSSP_AMD_TAIL=0 is the two-step
-path.  Cases: cubes with partial tiles in j and k (N = 24, 40), a 2-D 5-point
+path.  Cases (ILU(0), k_line2, and ILU(1), the skewed k_linef sweeps): cubes
+with partial tiles in j and k (N = 24, 40), a 2-D 5-point
 grid (one plane: every chunk waits for the whole sweep), a block-Jacobi
 factor on one rank (plane cuts between tile rows), and a run that converges
 mid-batch (the guard skips queued sweeps and tails: the tile counts and chunk
@@ -22,15 +23,15 @@ import oracle as O
 pytestmark = pytest.mark.gpu
 
 
-def _solve(dev, Ap, Aj, Ax, mode, maxit, blk=0, tol=0.0):
+def _solve(dev, Ap, Aj, Ax, mode, maxit, blk=0, tol=0.0, level=0):
     import lssp_amd
     n = Ap.size - 1
     old = os.environ.get("LSSP_AMD_TAIL")
     os.environ["LSSP_AMD_TAIL"] = mode
     try:
         A = lssp_amd.DMat(dev, Ap, Aj, Ax)
-        M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=0, blk=blk)
-        assert M.sweep_layout()[0] == 1  # the ILU(0) line sweeps
+        M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=level, blk=blk)
+        assert M.sweep_layout()[0] == 1 + level  # the ILU(0) / ILU(1) line sweeps
         out = []
         for _ in range(2):  # twice: the counters and claims carry over between solves
             x = dev.vec(n, np.zeros(n))
@@ -48,21 +49,24 @@ def _solve(dev, Ap, Aj, Ax, mode, maxit, blk=0, tol=0.0):
             os.environ["LSSP_AMD_TAIL"] = old
 
 
-@pytest.mark.parametrize("dim,N,blk,maxit,tol", [(3, 24, 0, 30, 0.0), (3, 40, 0, 25, 0.0), (2, 100, 0, 40, 0.0),
-                                                 (3, 32, 32 * 32 * 11, 30, 0.0), (3, 32, 0, 500, 1e-7)],
-                         ids=["cube24", "cube40", "square100", "blockjacobi32", "converges32"])
-def test_tail_product_bitwise_two_step_and_oracle(dim, N, blk, maxit, tol):
+@pytest.mark.parametrize("dim,N,blk,maxit,tol,level", [(3, 24, 0, 30, 0.0, 0), (3, 40, 0, 25, 0.0, 0),
+                                                       (2, 100, 0, 40, 0.0, 0), (3, 32, 32 * 32 * 11, 30, 0.0, 0),
+                                                       (3, 32, 0, 500, 1e-7, 0), (3, 24, 0, 30, 0.0, 1),
+                                                       (3, 40, 0, 500, 1e-7, 1), (2, 100, 0, 40, 0.0, 1)],
+                         ids=["cube24", "cube40", "square100", "blockjacobi32", "converges32", "ilu1-cube24",
+                              "ilu1-converges40", "ilu1-square100"])
+def test_tail_product_bitwise_two_step_and_oracle(dim, N, blk, maxit, tol, level):
     import lssp_amd
     Ap, Aj, Ax = lssp_amd.poisson(dim, N)
     n = Ap.size - 1
     dev = lssp_amd.Device(0, reduction=lssp_amd.TREE)
     try:
-        fused = _solve(dev, Ap, Aj, Ax, "2", maxit, blk, tol)
-        plain = _solve(dev, Ap, Aj, Ax, "0", maxit, blk, tol)
+        fused = _solve(dev, Ap, Aj, Ax, "2", maxit, blk, tol, level)
+        plain = _solve(dev, Ap, Aj, Ax, "0", maxit, blk, tol, level)
     finally:
         dev.close()
     Ao = O.CSR(n, Ap, Aj, Ax)
-    L, U = O.ilu(Ao, "iluk", level=0, blk=blk)
+    L, U = O.ilu(Ao, "iluk", level=level, blk=blk)
     o = O.solve(O.BICGSTAB, Ao, np.ones(n), L=L, U=U, rtol=tol, atol=tol, rbtol=tol, maxit=maxit, mode=O.TREE)
     for f, p in zip(fused, plain):
         assert f[0] == p[0] == o.nits
