@@ -64,6 +64,10 @@
 
 namespace lssp_amd {
 
+#ifndef LINE2_EARLY_SHFL
+#define LINE2_EARLY_SHFL 1  // the BN shuffle issued before the level's stores (linesweep.hip k_line2)
+#endif
+
 namespace lf {
 constexpr int P = 8, NJ = 16, LV = 2, HKS = 18, ROWS = P * NJ;
 constexpr int HJ0 = 2;  // hj row of q = -2 (the compute runs from level -2)
@@ -406,7 +410,7 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             atomicAdd(a.claim, (unsigned long long)a.ntiles + gridDim.x);
             if (OUT == 1 && a.tail) {  // ... and the tail's chunk claims and tile counts
-                atomicAdd(a.tl.claim, (unsigned long long)a.tl.nblk + gridDim.x * waves(NL, SW));
+                atomicAdd(a.tl.claim, 2ull * ((a.tl.nblk + 1) / 2) + 2ull * gridDim.x);
                 for (int K = 0; K < a.tl.S; K++) atomicAdd(a.tl.kdone + K, (unsigned)a.tl.W);
             }
         }
@@ -519,10 +523,11 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
                 asm volatile("" ::: "memory");
                 load(sn, so, nxt);
                 if (s >= SC && s < TS) {
+                    double xu = xs;  // lane - 16's x of the previous level
 #pragma unroll
                     for (int lv = 0; lv < LV; lv++) {
                         const int v = 2 * s + lv;
-                        const double bn = sel_lanes(G0M, lv == 0 ? kx0 : kx1, lv == 0 ? xs : up16(xp));
+                        const double bn = sel_lanes(G0M, lv == 0 ? kx0 : kx1, xu);
                         const double be0 = wave == 0 ? sel_lanes(G0M, lv == 0 ? kb0 : kb1, cur.be0[lv]) : cur.be0[lv];
                         const double be = dpp_shr1g<4>(bnp, be0);
                         const double se = dpp_shr1g<4>(xp, cur.se0[lv]);
@@ -539,14 +544,22 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
 #endif
                         const bool ok = lane_ok && (unsigned)(v - off) < (unsigned)nx;
                         const double x = sel_lanes(__builtin_amdgcn_ballot_w64(ok), r, 0.0);
+#if LINE2_EARLY_SHFL
+                        // the next level's BN shuffle before this level's stores (as k_line2)
+                        xu = up16(x);
+                        __builtin_amdgcn_sched_barrier(0);
+#endif
                         publish(v, x, se);
                         res[(v & (RSL - 1)) * ROWS + pw * NJ + ll] = x;
+#if !LINE2_EARLY_SHFL
+                        xu = up16(x);
+#endif
                         bep = be;
                         sep = se;
                         bnp = bn;
                         xp = x;
                     }
-                    xs = up16(xp);  // the next step's first BN, off its critical path
+                    xs = xu;  // the next step's first BN, off its critical path
                 }
                 so = sn;
                 line_barrier();
@@ -761,7 +774,7 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
             __syncthreads();
             if (threadIdx.x < a.tl.ndiag) soff[threadIdx.x] = a.tl.off[threadIdx.x];
             __syncthreads();
-            line_tail_waves(a.tl, a.out, a.err, smem);
+            line_tail_wg(a.tl, a.out, a.err, smem);
         }
     }
 }
@@ -890,7 +903,7 @@ int launch_linefill_apply_tail(lssp_amd_ctx *c, const LineILU &li, double *x, co
     LSSP_TRY(linef_gather(c, li.L, 0, rhs, li.d_lstream));
     LSSP_TRY(linef_sweep(c, li, 0, li.d_lstream, li.d_ustream, 2));
     LSSP_TRY(linef_sweep(c, li, 1, li.d_ustream, x, 1, &T));
-    *tail_waves = (long)std::min(li.U.ntiles, c->num_cus) * lf::waves(LF_NL, LF_SW);
+    *tail_waves = (long)std::min(li.U.ntiles, c->num_cus);  // (the tail's claimants: workgroups)
     return LSSP_AMD_OK;
 }
 

@@ -1106,7 +1106,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             atomicAdd(a.claim, (unsigned long long)a.ntiles + gridDim.x);
             if (OUT == 1 && a.tail) {  // ... and the tail's chunk claims and tile counts
-                atomicAdd(a.tl.claim, (unsigned long long)a.tl.nblk + gridDim.x * l2::waves(P, NL, SW));
+                atomicAdd(a.tl.claim, 2ull * ((a.tl.nblk + 1) / 2) + 2ull * gridDim.x);
                 for (int K = 0; K < a.tl.S; K++) atomicAdd(a.tl.kdone + K, (unsigned)a.tl.W);
             }
         }
@@ -1492,7 +1492,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
             __syncthreads();  // (the loop's last barrier already passed; the ring is free)
             if (threadIdx.x < a.tl.ndiag) soff[threadIdx.x] = a.tl.off[threadIdx.x];
             __syncthreads();
-            line_tail_waves(a.tl, a.out, a.err, smem);
+            line_tail_wg(a.tl, a.out, a.err, smem);
         }
     }
 }
@@ -1854,6 +1854,8 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
     LSSP_TRY(ensure_part(c, nall));
     LineTail T{};
     T.Ap = A->Ap;
+    T.Aj = A->Aj;
+    T.nnz_pad = A->nnz + 4L;
     T.Ax = A->Ax;
     T.Ad = A->Ad;
     T.off = A->d_off;
@@ -1890,7 +1892,7 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
         tail_dbg_host = dbg_h;
         T.dbg = dbg_d;
     }
-    long tail_waves = (long)std::min(li.U.ntiles, c->num_cus) * l2::waves(8, LINE2_NL, LINE2_SW);
+    long tail_waves = (long)std::min(li.U.ntiles, c->num_cus);  // (the tail's claimants: workgroups)
     if (li.kind == 1) {  // the 7-/5-point ILU(1) line sweeps (linefill.hip)
         LSSP_TRY(launch_linefill_apply_tail(c, li, x, rhs, T, &tail_waves));
     } else {
@@ -1898,8 +1900,9 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
         LSSP_TRY(launch_line2(c, li, 0, li.d_lstream, li.d_ustream, 2));
         LSSP_TRY(launch_line2(c, li, 1, li.d_ustream, x, 1, &T));
     }
-    // every wave of the grid ends on one failed chunk claim; every U tile counted once
-    li.tbase += (unsigned long long)nblk + (unsigned long long)tail_waves;
+    // chunks are claimed in pairs and every workgroup of the grid ends on one
+    // failed pair claim; every U tile counted once
+    li.tbase += 2ull * (unsigned long long)((nblk + 1) / 2) + 2ull * (unsigned long long)tail_waves;
     li.kepoch++;
     return LSSP_AMD_OK;
 }

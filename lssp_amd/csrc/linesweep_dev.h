@@ -162,6 +162,8 @@ struct LineTail {
     const double *w0, *w1;
     double *part;
     long pcap, nblk, cend;      // chunks [cend - nblk, cend)
+    const int *Aj;              // int32 columns (rows past the staging cap)
+    long nnz_pad;               // Ax / Aj padded length (launch_spmv: nnz + 4)
     unsigned long long *claim;  // chunk claims (monotonic)
     unsigned long long base;
     unsigned *kdone;            // U tiles finished per tile row (monotonic)
@@ -183,132 +185,179 @@ __device__ __forceinline__ void st_sc1d(double *p, double v)
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// one wave's share of the tail product (see LineTail); soff: the offset table in LDS
-// LDS of the tail: the offset table (<= 255 ints) in the first 1 KB, then
-// per wave a TAIL_LDS-byte region: a 64-row group's values (TAIL_CAP + 2
-// doubles) and diagonal ids (TAIL_CAP + 32 bytes), staged with coalesced
-// 16-byte loads (per-lane row loads cost the texture unit one cache line per
-// lane per entry: the first version of this tail took 400 us per product)
-constexpr int TAIL_CAP = 448;  // entries of a 64-row group staged (7 per row)
-constexpr int TAIL_LDS = 4096;
-constexpr int TAIL_LDS_BYTES(int nwaves) { return 1024 + nwaves * TAIL_LDS; }
-static __device__ void line_tail_waves(const LineTail &T, const double *x, int *err, char *smem)
+// The tail product, workgroup-wide: every round the workgroup claims a PAIR of
+// 256-row chunks (threads 0..255 and 256..511 each run one as k_spmv3 runs a
+// block; the other waves only take part in the barriers).  The next pair's
+// staging loads (row bounds, the chunk's value and id ranges as 16-byte
+// vectors, the fused dots' operands -- none of them written by the sweep) are
+// in flight while the current pair's x gathers run, so a round costs about one
+// memory round trip; only the x gathers wait for the planes to be final.  LDS:
+// the offset table (1 KB), two sync words, then two buffers x two chunks of
+// TAIL_CH bytes.  (A first version with one 64-row group per wave and three
+// dependent round trips per group moved ~80 rows/us per CU and made the
+// product slower than k_spmv3: profiles/r05/r05c_tail_ab.txt.)
+constexpr int TAIL_CAP = 2048;                                   // staged entries per chunk (k_spmv3's SPMV_CAP)
+constexpr int TAIL_SX = 8 * (TAIL_CAP + 2);                      // values
+constexpr int TAIL_SD = 4 * (TAIL_CAP / 4 + 8);                  // diagonal ids
+constexpr int TAIL_CH = (TAIL_SX + TAIL_SD + 8 * 4 * 4 + 15) / 16 * 16;
+constexpr int TAIL_LDS_BYTES(int) { return 1024 + 64 + 4 * TAIL_CH; }
+static __device__ void line_tail_wg(const LineTail &T, const double *x, int *err, char *smem)
 {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int *soff = reinterpret_cast<const int *>(smem);
-    double *sx = reinterpret_cast<double *>(smem + 1024 + wave * TAIL_LDS);
-    uint8_t *sd = reinterpret_cast<uint8_t *>(smem + 1024 + wave * TAIL_LDS + 8 * (TAIL_CAP + 2));
     typedef double d2_t __attribute__((ext_vector_type(2)));
     typedef int i4_t __attribute__((ext_vector_type(4)));
+    constexpr int NX2 = (TAIL_CAP / 2 + 1 + 255) / 256;  // 16-byte value loads per thread
+    const int tid = threadIdx.x, c = tid >> 8, t = tid & 255;
+    const bool act = tid < 512;
+    const int *soff = reinterpret_cast<const int *>(smem);
+    unsigned *sync = reinterpret_cast<unsigned *>(smem + 1024);
+    auto buf = [&](int b) { return smem + 1088 + (2 * b + c) * TAIL_CH; };
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    // the staged state of one chunk (registers)
+    struct St {
+        long blk;
+        int r, rr, rb, re, base, cnt;
+        long xb, jb;
+        d2_t vx[NX2];
+        i4_t vj;
+        double w0p, w1p;
+    };
+    auto claim = [&]() {  // thread 0: the next pair's first chunk index (relative to base)
+        const unsigned long long cl = atomicAdd(T.claim, 2ull) - T.base;
+        sync[0] = (unsigned)cl;
+        sync[1] = (unsigned)(cl >> 32);
+    };
+    auto read_claim = [&]() { return ((unsigned long long)sync[1] << 32) | sync[0]; };
+    auto stage = [&](unsigned long long cl, St &S) {  // loads only; nothing here waits for the sweep
+        S.blk = cl + c < (unsigned long long)T.nblk ? T.cend - 1 - (long)(cl + c) : -1;
+        if (!act || S.blk < 0) return;
+        const int r0 = (int)(S.blk * 256);
+        S.r = r0 + t;
+        const int rend = min(r0 + 256, T.nrows);
+        S.base = T.Ap[r0];
+        S.cnt = T.Ap[rend] - S.base;
+        S.rr = min(S.r, T.nrows - 1);
+        S.rb = T.Ap[S.rr];
+        S.re = T.Ap[S.rr + 1];
+        S.w0p = S.w1p = 0.0;
+        if (T.nred > 0 && T.w0 != T.z) S.w0p = ld_sc1d(T.w0 + S.rr);
+        if (T.nred > 1 && T.w1 && T.w1 != T.z) S.w1p = ld_sc1d(T.w1 + S.rr);
+        if (S.cnt <= TAIL_CAP) {
+            S.xb = S.base & ~1L;
+            S.jb = S.base & ~15L;
+            const long last = S.cnt > 0 ? (long)S.base + S.cnt - 1 : (long)S.base;
+            const long xmax = min(last >> 1, (T.nnz_pad >> 1) - 1);
+            const long jmax = min(last >> 4, ((T.nnz_pad - 4 + 32) >> 4) - 1);
+            const d2_t *X2 = reinterpret_cast<const d2_t *>(T.Ax);
+            const i4_t *J4 = reinterpret_cast<const i4_t *>(T.Ad);
+#pragma unroll
+            for (int u = 0; u < NX2; u++) S.vx[u] = __builtin_nontemporal_load(X2 + min((S.xb >> 1) + t + 256 * u, xmax));
+            S.vj = __builtin_nontemporal_load(J4 + min((S.jb >> 4) + t, jmax));
+        }
+    };
+    auto land = [&](const St &S, int b) {  // the staged vectors into this chunk's LDS buffer
+        if (!act || S.blk < 0 || S.cnt > TAIL_CAP) return;
+        char *B = buf(b);
+        const long last = S.cnt > 0 ? (long)S.base + S.cnt - 1 : (long)S.base;
+        const int xn = (int)(min(last >> 1, (T.nnz_pad >> 1) - 1) - (S.xb >> 1)) + 1;
+        const int jn = (int)(min(last >> 4, ((T.nnz_pad - 4 + 32) >> 4) - 1) - (S.jb >> 4)) + 1;
+#pragma unroll
+        for (int u = 0; u < NX2; u++)
+            if (t + 256 * u < xn) reinterpret_cast<d2_t *>(B)[t + 256 * u] = S.vx[u];
+        if (t < jn) reinterpret_cast<i4_t *>(B + TAIL_SX)[t] = S.vj;
+    };
+    auto wait_planes = [&](unsigned long long cl) {  // thread 0: the pair's rows read final planes only
+        if (cl >= (unsigned long long)T.nblk) return;
+        const long hi = T.cend - 1 - (long)cl;                                   // upper chunk
+        const long lo = T.cend - 1 - (long)min(cl + 1, (unsigned long long)T.nblk - 1);
+        const int r0 = (int)(lo * 256), r1 = min((int)(hi * 256) + 256, T.nrows);
+        const int ka = max(r0 / (int)T.pl - 1, 0), kb = min((r1 - 1) / (int)T.pl + 1, T.nz - 1);
+        for (int K = T.kof[ka]; K <= T.kof[kb]; K++) {
+            unsigned *cnt = T.kdone + (T.S - 1 - K);  // U tile row of L tile row K
+            for (;;) {
+                // (an atomic read: coherent with the tiles' atomic increments on every XCD)
+                const unsigned seen = __hip_atomic_fetch_add(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (seen - T.ktarget < 0x80000000u) break;
+                if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+                    __builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s: the sweep gave up
+                    atomicOr(err, 8);
+                    return;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+    };
+    St A, Bs;
+    if (tid == 0) claim();
+    __syncthreads();
+    unsigned long long cur = read_claim();
+    __syncthreads();  // (sync is rewritten below)
+    if (cur >= (unsigned long long)T.nblk) return;  // uniform
+    stage(cur, A);
+    int b = 0;
     for (;;) {
-        unsigned long long c = 0;
-        if (lane == 0) c = atomicAdd(T.claim, 1ull) - T.base;
-        const unsigned clo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)c);
-        const unsigned chi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(c >> 32));
-        const unsigned long long cl = ((unsigned long long)chi << 32) | clo;
-        unsigned *dw = T.dbg ? T.dbg + 1024 + 4 * (blockIdx.x * 16 + wave) : nullptr;
-        if (dw && lane == 0) {
-            dw[0] = 1;
-            dw[1] = (unsigned)cl;
+        land(A, b);
+        if (tid == 0) {
+            wait_planes(cur);
+            claim();
         }
-        if (cl >= (unsigned long long)T.nblk) {
-            if (dw && lane == 0) dw[0] = 9;
-            break;
-        }
-        const long blk = T.cend - 1 - (long)cl;
-        const int r0 = (int)(blk * 256), r1 = min(r0 + 256, T.nrows);
-        // the planes the chunk's rows read: k-1 .. k+1 of its first / last row
-        if (lane == 0) {
-            const int ka = max(r0 / (int)T.pl - 1, 0), kb = min((r1 - 1) / (int)T.pl + 1, T.nz - 1);
-            const int K0 = T.kof[ka], K1 = T.kof[kb];
-            for (int K = K0; K <= K1; K++) {
-                unsigned *cnt = T.kdone + (T.S - 1 - K);  // U tile row of L tile row K
-                for (;;) {
-                    // (an atomic read: coherent with the tiles' atomic increments on every XCD)
-                    const unsigned seen = __hip_atomic_fetch_add(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (dw) {
-                        dw[2] = (unsigned)K;
-                        dw[3] = seen;
+        __syncthreads();  // the pair's data in LDS, its planes final, the next pair claimed
+        const unsigned long long nxt = read_claim();
+        stage(nxt, Bs);  // in flight while this pair's gathers run
+        double zv = 0.0, v0 = 0.0, v1 = 0.0;
+        if (act && A.blk >= 0) {
+            const char *B = buf(b);
+            const double *sx = reinterpret_cast<const double *>(B);
+            const unsigned char *sd = reinterpret_cast<const unsigned char *>(B + TAIL_SX);
+            double sum = 0.0;
+            if (A.r < T.nrows) {
+                if (A.cnt <= TAIL_CAP) {
+                    const int ox = (int)(A.base - A.xb) - A.base, oj = (int)(A.base - A.jb) - A.base;
+                    const int len = A.re - A.rb;
+                    if (len > 0 && len <= 8) {
+                        double pr[8];
+#pragma unroll
+                        for (int u = 0; u < 8; u++) {
+                            const int k = min(A.rb + u, A.re - 1);
+                            pr[u] = ld_sc1d(x + A.r + soff[sd[k + oj]]) * sx[k + ox];
+                        }
+#pragma unroll
+                        for (int u = 0; u < 8; u++)
+                            if (u < len) sum += pr[u];
+                    } else {
+                        for (int k = A.rb; k < A.re; k++) sum += ld_sc1d(x + A.r + soff[sd[k + oj]]) * sx[k + ox];
                     }
-                    if (seen - T.ktarget < 0x80000000u) break;
-                    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
-                        __builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s: the sweep gave up
-                        atomicOr(err, 8);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
+                } else {
+                    for (int k = A.rb; k < A.re; k++) sum += ld_sc1d(x + T.Aj[k]) * T.Ax[k];
                 }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (dw && lane == 0) dw[0] = 2;
-        double v0[4], v1[4];
-        for (int q = 0; q < 4; q++) {
-            const int rg = r0 + 64 * q;  // the group's first row
-            v0[q] = v1[q] = 0.0;
-            if (rg >= T.nrows) continue;  // (uniform)
-            const int r = rg + lane, rr = min(r, T.nrows - 1);
-            const int rb = T.Ap[rr], re = T.Ap[rr + 1];
-            const int e0 = __builtin_amdgcn_readfirstlane(rb);
-            const int e1 = __shfl(re, 63, 64);  // the group's last entry + 1
-            double sum = 0;
-            if (e1 - e0 <= TAIL_CAP) {  // (uniform) stage the group's values and ids
-                const int xb = e0 & ~1, db = e0 & ~15;
-                const int nv = (e1 - xb + 1) >> 1, nd = (e1 - db + 15) >> 4;
-                const d2_t *X2 = reinterpret_cast<const d2_t *>(T.Ax) + (xb >> 1);
-                const i4_t *D4 = reinterpret_cast<const i4_t *>(T.Ad) + (db >> 4);
-                d2_t vx[4];
-                i4_t vd;
-#pragma unroll
-                for (int u = 0; u < 4; u++) vx[u] = __builtin_nontemporal_load(X2 + min(lane + 64 * u, nv - 1));
-                vd = __builtin_nontemporal_load(D4 + min(lane, nd - 1));
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    if (lane + 64 * u < nv) reinterpret_cast<d2_t *>(sx)[lane + 64 * u] = vx[u];
-                if (lane < nd) reinterpret_cast<i4_t *>(sd)[lane] = vd;
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                double pr[8];
-#pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const int k = max(min(rb + u, re - 1), 0);
-                    pr[u] = ld_sc1d(x + rr + soff[sd[k - db]]) * sx[k - xb];
-                }
-#pragma unroll
-                for (int u = 0; u < 8; u++)
-                    if (u < re - rb) sum += pr[u];
-                for (int k = rb + 8; k < re; k++) sum += ld_sc1d(x + rr + soff[sd[k - db]]) * sx[k - xb];
-                __builtin_amdgcn_wave_barrier();  // the region is rewritten by the next group
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            } else {
-                for (int k = rb; k < re; k++) sum += ld_sc1d(x + rr + soff[T.Ad[k]]) * T.Ax[k];
-            }
-            if (r < T.nrows) {
-                double zv;
                 if (T.epi == EPI_MXY) zv = sum;
                 else if (T.epi == EPI_AMXY) zv = sum * T.alpha;
-                else if (T.epi == EPI_AXPBY) zv = ld_sc1d(T.y + r) * T.beta + T.alpha * sum;
+                else if (T.epi == EPI_AXPBY) zv = ld_sc1d(T.y + A.r) * T.beta + T.alpha * sum;
                 else zv = T.alpha * sum;
-                T.z[r] = zv;
-                if (T.nred > 0) v0[q] = zv * (T.w0 == T.z ? zv : ld_sc1d(T.w0 + r));
-                if (T.nred > 1) v1[q] = zv * (T.w1 && T.w1 != T.z ? ld_sc1d(T.w1 + r) : zv);
+                T.z[A.r] = zv;
+                if (T.nred > 0) v0 = zv * (T.w0 == T.z ? zv : A.w0p);
+                if (T.nred > 1) v1 = zv * (T.w1 && T.w1 != T.z ? A.w1p : zv);
             }
         }
-        // chunk_reduce's order: the four 64-row groups' halving trees, (w0 + w1) + (w2 + w3)
+        // chunk_reduce's order: the chunk's four wave halving trees, (w0 + w1) + (w2 + w3)
+        double *red = reinterpret_cast<double *>(buf(b) + TAIL_SX + TAIL_SD);  // [slot][wave]
+        const int wq = (tid >> 6) & 3;
         if (T.nred > 0) {
-            double w[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) w[q] = wave_sum_d(v0[q]);
-            if (lane == 0) T.part[blk] = (w[0] + w[1]) + (w[2] + w[3]);
+            const double s0 = wave_sum_d(v0);
+            const double s1 = T.nred > 1 ? wave_sum_d(v1) : 0.0;
+            if (act && (tid & 63) == 0) {
+                red[wq] = s0;
+                red[4 + wq] = s1;
+            }
         }
-        if (T.nred > 1) {
-            double w[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) w[q] = wave_sum_d(v1[q]);
-            if (lane == 0) T.part[T.pcap + blk] = (w[0] + w[1]) + (w[2] + w[3]);
+        __syncthreads();  // the pair's LDS is read (it is rewritten two rounds later) and reduced
+        if (T.nred > 0 && act && t == 0 && A.blk >= 0) {
+            T.part[A.blk] = (red[0] + red[1]) + (red[2] + red[3]);
+            if (T.nred > 1) T.part[T.pcap + A.blk] = (red[4] + red[5]) + (red[6] + red[7]);
         }
+        if (nxt >= (unsigned long long)T.nblk) break;  // uniform
+        A = Bs;
+        cur = nxt;
+        b ^= 1;
     }
 }
 
