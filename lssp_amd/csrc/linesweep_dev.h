@@ -265,14 +265,20 @@ static __device__ void line_tail_wg(const LineTail &T, const double *x, int *err
             if (t + 256 * u < xn) reinterpret_cast<d2_t *>(B)[t + 256 * u] = S.vx[u];
         if (t < jn) reinterpret_cast<i4_t *>(B + TAIL_SX)[t] = S.vj;
     };
-    auto wait_planes = [&](unsigned long long cl) {  // thread 0: the pair's rows read final planes only
+    // thread 0: the pair's rows read final planes only.  U tile rows Kp = S-1-K
+    // complete (nearly) in increasing Kp, and the pairs come from the top down,
+    // so thread 0 keeps the prefix of rows it has seen complete (kp_done) and
+    // asks the counters only about rows past it
+    int kp_done = -1;
+    auto wait_planes = [&](unsigned long long cl) {
         if (cl >= (unsigned long long)T.nblk) return;
         const long hi = T.cend - 1 - (long)cl;                                   // upper chunk
         const long lo = T.cend - 1 - (long)min(cl + 1, (unsigned long long)T.nblk - 1);
         const int r0 = (int)(lo * 256), r1 = min((int)(hi * 256) + 256, T.nrows);
         const int ka = max(r0 / (int)T.pl - 1, 0), kb = min((r1 - 1) / (int)T.pl + 1, T.nz - 1);
-        for (int K = T.kof[ka]; K <= T.kof[kb]; K++) {
-            unsigned *cnt = T.kdone + (T.S - 1 - K);  // U tile row of L tile row K
+        const int kpb = T.S - 1 - T.kof[ka];  // the highest U tile row needed
+        for (int Kp = kp_done + 1; Kp <= kpb; Kp++) {
+            unsigned *cnt = T.kdone + Kp;
             for (;;) {
                 // (an atomic read: coherent with the tiles' atomic increments on every XCD)
                 const unsigned seen = __hip_atomic_fetch_add(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -284,12 +290,29 @@ static __device__ void line_tail_wg(const LineTail &T, const double *x, int *err
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
+            kp_done = Kp;
         }
     };
     St A, Bs;
-    if (tid == 0) claim();
+    // pairs are claimed two rounds ahead (a returning atomic costs ~1 us under
+    // load); every workgroup ends on exactly one failed claim
+    if (tid == 0) {
+        claim();
+        if (read_claim() < (unsigned long long)T.nblk) {
+            const unsigned long long c0 = read_claim();
+            claim();
+            sync[2] = sync[0];
+            sync[3] = sync[1];
+            sync[0] = (unsigned)c0;
+            sync[1] = (unsigned)(c0 >> 32);
+        } else {
+            sync[2] = sync[0];
+            sync[3] = sync[1];
+        }
+    }
     __syncthreads();
     unsigned long long cur = read_claim();
+    unsigned long long nxt = ((unsigned long long)sync[3] << 32) | sync[2];
     __syncthreads();  // (sync is rewritten below)
     if (cur >= (unsigned long long)T.nblk) return;  // uniform
     stage(cur, A);
@@ -298,10 +321,10 @@ static __device__ void line_tail_wg(const LineTail &T, const double *x, int *err
         land(A, b);
         if (tid == 0) {
             wait_planes(cur);
-            claim();
+            if (nxt < (unsigned long long)T.nblk) claim();  // the pair after next
         }
-        __syncthreads();  // the pair's data in LDS, its planes final, the next pair claimed
-        const unsigned long long nxt = read_claim();
+        __syncthreads();  // the pair's data in LDS, its planes final, the pair after next claimed
+        const unsigned long long nxt2 = nxt < (unsigned long long)T.nblk ? read_claim() : ~0ull;
         stage(nxt, Bs);  // in flight while this pair's gathers run
         double zv = 0.0, v0 = 0.0, v1 = 0.0;
         if (act && A.blk >= 0) {
@@ -357,6 +380,7 @@ static __device__ void line_tail_wg(const LineTail &T, const double *x, int *err
         if (nxt >= (unsigned long long)T.nblk) break;  // uniform
         A = Bs;
         cur = nxt;
+        nxt = nxt2;
         b ^= 1;
     }
 }
