@@ -410,7 +410,7 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             atomicAdd(a.claim, (unsigned long long)a.ntiles + gridDim.x);
             if (OUT == 1 && a.tail) {  // ... and the tail's chunk claims and tile counts
-                atomicAdd(a.tl.claim, 2ull * ((a.tl.nblk + 1) / 2) + 2ull * gridDim.x);
+                atomicAdd(a.tl.claim, tail_claims(a.tl.nblk, gridDim.x));
                 for (int K = 0; K < a.tl.S; K++) atomicAdd(a.tl.kdone + K, (unsigned)a.tl.W);
             }
         }
@@ -770,7 +770,7 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
     }
     if constexpr (OUT == 1) {
         if (a.tail) {  // no tile left for this workgroup: its waves run the tail product
-            int *soff = reinterpret_cast<int *>(smem);  // (the ring's LDS is free now: TAIL_LDS_BYTES fit in it)
+            int *soff = reinterpret_cast<int *>(smem);  // (the ring's LDS is free now; linef_launch_t reserves TAIL_LDS_BYTES)
             __syncthreads();
             if (threadIdx.x < a.tl.ndiag) soff[threadIdx.x] = a.tl.off[threadIdx.x];
             __syncthreads();
@@ -840,9 +840,11 @@ int linef_gather(lssp_amd_ctx *c, const LineSweep &ls, int mirror, const double 
 template <int NA, int OUT>
 int linef_launch_t(lssp_amd_ctx *c, const LineSweep &ls, const FillArgs &a)
 {
-    constexpr int lds = lf::lds_bytes<NA, OUT, LINEF_D>();
+    // (the sweeps with natural-order output reserve what the tail product needs)
+    constexpr int lds0 = lf::lds_bytes<NA, OUT, LINEF_D>();
+    constexpr int lds = OUT == 1 && lds0 < TAIL_LDS_BYTES(0) ? TAIL_LDS_BYTES(0) : lds0;
     static_assert(lds <= 160 * 1024, "LDS");
-    static_assert(OUT != 1 || lds >= TAIL_LDS_BYTES(lf::waves(LF_NL, LF_SW)), "the tail product's LDS");
+    static_assert(OUT != 1 || lf::waves(LF_NL, LF_SW) >= TAIL_WAVES, "the tail product's roles");
     auto kern = k_linef<NA, OUT, LF_NL, LINEF_D, LINEF_DH, LF_SW>;
     static bool attr = false;
     if (!attr) {

@@ -1106,7 +1106,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             atomicAdd(a.claim, (unsigned long long)a.ntiles + gridDim.x);
             if (OUT == 1 && a.tail) {  // ... and the tail's chunk claims and tile counts
-                atomicAdd(a.tl.claim, 2ull * ((a.tl.nblk + 1) / 2) + 2ull * gridDim.x);
+                atomicAdd(a.tl.claim, tail_claims(a.tl.nblk, gridDim.x));
                 for (int K = 0; K < a.tl.S; K++) atomicAdd(a.tl.kdone + K, (unsigned)a.tl.W);
             }
         }
@@ -1114,6 +1114,8 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
     }
 
     int done_tile = -1;  // the tile this workgroup finished last (its completion is counted at the next claim)
+    if (OUT == 1 && a.tail && a.tl.dbg && threadIdx.x == 0)  // diagnostics: the workgroup's start
+        a.tl.dbg[6144 + blockIdx.x] = (unsigned)__builtin_amdgcn_s_memrealtime();
     for (;;) {
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -1488,7 +1490,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
     }
     if constexpr (OUT == 1) {
         if (a.tail) {  // no tile left for this workgroup: its waves run the tail product
-            int *soff = reinterpret_cast<int *>(smem);  // (the ring's LDS is free now: TAIL_LDS_BYTES fit in it)
+            int *soff = reinterpret_cast<int *>(smem);  // (the ring's LDS is free now; launch_line2_t reserves TAIL_LDS_BYTES)
             __syncthreads();  // (the loop's last barrier already passed; the ring is free)
             if (threadIdx.x < a.tl.ndiag) soff[threadIdx.x] = a.tl.off[threadIdx.x];
             __syncthreads();
@@ -1692,9 +1694,11 @@ static int launch_line2_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &
 template <int P, int LV, int NA, int OUT>
 static int launch_line2_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a)
 {
-    constexpr int lds = l2::lds_bytes<NA, OUT, line2_d<LV>(), P, LV>();
+    // (the sweeps with natural-order output reserve what the tail product needs)
+    constexpr int lds0 = l2::lds_bytes<NA, OUT, line2_d<LV>(), P, LV>();
+    constexpr int lds = OUT == 1 && lds0 < TAIL_LDS_BYTES(0) ? TAIL_LDS_BYTES(0) : lds0;
     static_assert(lds <= 160 * 1024, "LDS");
-    static_assert(OUT != 1 || lds >= TAIL_LDS_BYTES(l2::waves(P, LINE2_NL, LINE2_SW)), "the tail product's LDS");
+    static_assert(OUT != 1 || l2::waves(P, LINE2_NL, LINE2_SW) >= TAIL_WAVES, "the tail product's roles");
     // diagnostics only: LSSP_AMD_LINE_TRACE=path[:tile] appends one JSON line per sweep
     static const char *trp = getenv("LSSP_AMD_LINE_TRACE");
     if (!trp) return launch_line2_k<P, LV, NA, OUT, false>(c, ls, a, lds);
@@ -1902,7 +1906,7 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
     }
     // chunks are claimed in pairs and every workgroup of the grid ends on one
     // failed pair claim; every U tile counted once
-    li.tbase += 2ull * (unsigned long long)((nblk + 1) / 2) + 2ull * (unsigned long long)tail_waves;
+    li.tbase += tail_claims(nblk, tail_waves);
     li.kepoch++;
     return LSSP_AMD_OK;
 }

@@ -185,97 +185,128 @@ __device__ __forceinline__ void st_sc1d(double *p, double v)
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The tail product, workgroup-wide: every round the workgroup claims a PAIR of
-// 256-row chunks (threads 0..255 and 256..511 each run one as k_spmv3 runs a
-// block; the other waves only take part in the barriers).  The next pair's
-// staging loads (row bounds, the chunk's value and id ranges as 16-byte
-// vectors, the fused dots' operands -- none of them written by the sweep) are
-// in flight while the current pair's x gathers run, so a round costs about one
-// memory round trip; only the x gathers wait for the planes to be final.  LDS:
-// the offset table (1 KB), two sync words, then two buffers x two chunks of
-// TAIL_CH bytes.  (A first version with one 64-row group per wave and three
-// dependent round trips per group moved ~80 rows/us per CU and made the
-// product slower than k_spmv3: profiles/r05/r05c_tail_ab.txt.)
-constexpr int TAIL_CAP = 2048;                                   // staged entries per chunk (k_spmv3's SPMV_CAP)
-constexpr int TAIL_SX = 8 * (TAIL_CAP + 2);                      // values
-constexpr int TAIL_SD = 4 * (TAIL_CAP / 4 + 8);                  // diagonal ids
-constexpr int TAIL_CH = (TAIL_SX + TAIL_SD + 8 * 4 * 4 + 15) / 16 * 16;
-constexpr int TAIL_LDS_BYTES(int) { return 1024 + 64 + 4 * TAIL_CH; }
+// The tail product, workgroup-wide, in rounds of a GROUP of TAIL_CPR 256-row
+// chunks with split roles: threads 0..511 compute (two rows each, of chunks
+// c and c + 2 of the group), loader wave 0 claims groups and polls the tile
+// counts, loader waves 1 and 2 load.  Each role waits only for its own memory
+// operations (vmcnt is per wave): in round i the compute waves gather x for
+// group i from the LDS-staged values and ids, while the loaders LDS-DMA group
+// i+1's value and id ranges (from its row pointers, loaded a round earlier),
+// load group i+2's row pointers, make sure group i+1's planes are final and
+// claim group i+3 -- one memory round trip per round, ~3 us under the sweep's
+// load, so a round moves 1024 rows.  LDS (~150 KB; the sweep kernels reserve
+// it): the offset table, claims, 3 slots of row pointers, 2 buffers of the
+// group's values + ids, the reduction words.  (Earlier versions -- one 64-row
+// group per wave with three dependent round trips; staging loads in the
+// compute waves' own in-order queue; 512-row rounds -- moved 80 / 150 / 170
+// rows/us per CU and made the product slower than k_spmv3:
+// profiles/r05/r05c_tail_ab.txt.)
+constexpr int TAIL_CPR = 4;                     // chunks per round
+constexpr int TAIL_NXP = 15;                    // 1 KB value pieces per chunk
+constexpr int TAIL_NDP = 2;                     // 1 KB id pieces per chunk
+constexpr int TAIL_CAP = TAIL_NXP * 128 - 1;    // entries per chunk staged (7-pt: <= 1792)
+constexpr int TAIL_CHB = (TAIL_NXP + TAIL_NDP) * 1024;
+constexpr int TAIL_APC = 260;                   // row pointers per chunk (257 used)
+constexpr int TAIL_OFF_SYNC = 1024, TAIL_OFF_AP = 1088;
+constexpr int TAIL_OFF_BUF = TAIL_OFF_AP + 3 * TAIL_CPR * TAIL_APC * 4;
+constexpr int TAIL_OFF_RED = TAIL_OFF_BUF + 2 * TAIL_CPR * TAIL_CHB;
+constexpr int TAIL_WAVES = 11;  // the sweeps' workgroups: 8 compute + 3 loader waves
+constexpr int TAIL_LDS_BYTES(int) { return TAIL_OFF_RED + 2 * TAIL_CPR * 8 * 8; }
+static_assert(TAIL_LDS_BYTES(0) <= 160 * 1024, "the tail product's LDS");
+// claims one launch's tails consume: the groups, then one failed claim per workgroup
+__host__ __device__ inline unsigned long long tail_claims(long nblk, long grid)
+{
+    return (unsigned long long)TAIL_CPR * (unsigned long long)((nblk + TAIL_CPR - 1) / TAIL_CPR + grid);
+}
 static __device__ void line_tail_wg(const LineTail &T, const double *x, int *err, char *smem)
 {
-    typedef double d2_t __attribute__((ext_vector_type(2)));
-    typedef int i4_t __attribute__((ext_vector_type(4)));
-    constexpr int NX2 = (TAIL_CAP / 2 + 1 + 255) / 256;  // 16-byte value loads per thread
-    const int tid = threadIdx.x, c = tid >> 8, t = tid & 255;
-    const bool act = tid < 512;
+    constexpr int CPR = TAIL_CPR, AP_N = CPR * 257;
+    const int tid = threadIdx.x;
+    const bool comp = tid < 512;
+    const int c = (tid >> 8) & 1, t = tid & 255;  // compute: chunks c, c + 2 of the group; row in the chunk
+    const int lt = tid - 512;                     // loader thread 0..191 (waves past 11 idle)
+    const bool ldr = !comp && lt < 192;
+    const int lw = __builtin_amdgcn_readfirstlane(lt >> 6), lane = tid & 63;
     const int *soff = reinterpret_cast<const int *>(smem);
-    unsigned *sync = reinterpret_cast<unsigned *>(smem + 1024);
-    auto buf = [&](int b) { return smem + 1088 + (2 * b + c) * TAIL_CH; };
+    unsigned *sync = reinterpret_cast<unsigned *>(smem + TAIL_OFF_SYNC);
+    int *aps = reinterpret_cast<int *>(smem + TAIL_OFF_AP);          // [3][CPR][TAIL_APC]
+    double *reds = reinterpret_cast<double *>(smem + TAIL_OFF_RED);  // [2][CPR][8]
+    const unsigned lds0 = (unsigned)(uintptr_t)smem;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    // the staged state of one chunk (registers)
-    struct St {
-        long blk;
-        int r, rr, rb, re, base, cnt;
-        long xb, jb;
-        d2_t vx[NX2];
-        i4_t vj;
-        double w0p, w1p;
+    const unsigned long long NB = (unsigned long long)T.nblk;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(x), 0,
+                                                                        (int)min((long)T.nrows * 8, 0x7fffffffL), 0x00020000);
+    // x (the sweep's output): plain loads, cached in this XCD's L2.  Safe because
+    // every line of x a group touches is final before its first load: the group
+    // waits for the planes of its rows less the widest offset less 15 rows (a
+    // 128-byte line's other rows), x is not read by anything else in the kernel,
+    // and its writers' stores are write-through and drained before their tile is
+    // counted.
+    auto ldx = [&](int col) {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, col * 8, 0, 0));
     };
-    auto claim = [&]() {  // thread 0: the next pair's first chunk index (relative to base)
-        const unsigned long long cl = atomicAdd(T.claim, 2ull) - T.base;
-        sync[0] = (unsigned)cl;
-        sync[1] = (unsigned)(cl >> 32);
+    auto ldv = [&](const double *p, int i) { return p == x ? ldx(i) : p[i]; };
+    auto blk_of = [&](unsigned long long g, int k) {  // chunk k of a group, -1 past the end
+        return g + k < NB ? T.cend - 1 - (long)(g + k) : -1L;
     };
-    auto read_claim = [&]() { return ((unsigned long long)sync[1] << 32) | sync[0]; };
-    auto stage = [&](unsigned long long cl, St &S) {  // loads only; nothing here waits for the sweep
-        S.blk = cl + c < (unsigned long long)T.nblk ? T.cend - 1 - (long)(cl + c) : -1;
-        if (!act || S.blk < 0) return;
-        const int r0 = (int)(S.blk * 256);
-        S.r = r0 + t;
-        const int rend = min(r0 + 256, T.nrows);
-        S.base = T.Ap[r0];
-        S.cnt = T.Ap[rend] - S.base;
-        S.rr = min(S.r, T.nrows - 1);
-        S.rb = T.Ap[S.rr];
-        S.re = T.Ap[S.rr + 1];
-        S.w0p = S.w1p = 0.0;
-        if (T.nred > 0 && T.w0 != T.z) S.w0p = ld_sc1d(T.w0 + S.rr);
-        if (T.nred > 1 && T.w1 && T.w1 != T.z) S.w1p = ld_sc1d(T.w1 + S.rr);
-        if (S.cnt <= TAIL_CAP) {
-            S.xb = S.base & ~1L;
-            S.jb = S.base & ~15L;
-            const long last = S.cnt > 0 ? (long)S.base + S.cnt - 1 : (long)S.base;
-            const long xmax = min(last >> 1, (T.nnz_pad >> 1) - 1);
-            const long jmax = min(last >> 4, ((T.nnz_pad - 4 + 32) >> 4) - 1);
-            const d2_t *X2 = reinterpret_cast<const d2_t *>(T.Ax);
-            const i4_t *J4 = reinterpret_cast<const i4_t *>(T.Ad);
+    auto claim = [&]() { return atomicAdd(T.claim, (unsigned long long)CPR) - T.base; };
+    // loader waves 1, 2: a group's row pointers into slot q (257 per chunk)
+    auto load_ap = [&](unsigned long long g, int q) {
+        constexpr int U = (AP_N + 127) / 128;
+        int v[U], dst[U];
 #pragma unroll
-            for (int u = 0; u < NX2; u++) S.vx[u] = __builtin_nontemporal_load(X2 + min((S.xb >> 1) + t + 256 * u, xmax));
-            S.vj = __builtin_nontemporal_load(J4 + min((S.jb >> 4) + t, jmax));
+        for (int u = 0; u < U; u++) {
+            const int i = lt - 64 + 128 * u, k = i / 257, j = i % 257;
+            dst[u] = -1;
+            v[u] = 0;
+            const long blk = i < AP_N ? blk_of(g, k) : -1L;
+            if (blk >= 0) {
+                const long r = min(blk * 256 + j, (long)T.nrows);
+                v[u] = T.Ap[r];
+                dst[u] = (q * CPR + k) * TAIL_APC + j;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (dst[u] >= 0) aps[dst[u]] = v[u];
+    };
+    // loader waves 1, 2: LDS-DMA of a group's value and id ranges (from slot q) into buffer bb
+    auto load_vals = [&](unsigned long long g, int q, int bb) {
+#pragma unroll
+        for (int k = 0; k < CPR; k++) {
+            const long blk = blk_of(g, k);
+            if (blk < 0) continue;
+            const int *ap = aps + (q * CPR + k) * TAIL_APC;
+            const int rows = min(256, T.nrows - (int)(blk * 256));
+            const int base = ap[0], cnt = ap[rows] - base;
+            if (cnt > TAIL_CAP) continue;  // the compute reads this chunk from HBM
+            const long xb = base & ~1L, jb = base & ~15L;
+            const int npx = (int)((((long)base + cnt - xb) * 8 + 1023) / 1024);
+            const int npd = (int)(((long)base + cnt - jb + 1023) / 1024);
+            const unsigned bl = lds0 + TAIL_OFF_BUF + (bb * CPR + k) * TAIL_CHB;
+            const long xlast = (T.nnz_pad >> 1) - 1, dlast = ((T.nnz_pad - 4 + 32) >> 4) - 1;
+            for (int p = lw - 1; p < npx + npd; p += 2) {
+                if (p < npx) {
+                    const long v = min((xb >> 1) + p * 64 + lane, xlast);
+                    dma16(reinterpret_cast<const char *>(T.Ax) + v * 16, __builtin_amdgcn_readfirstlane(bl + p * 1024));
+                } else {
+                    const int pd = p - npx;
+                    const long v = min((jb >> 4) + pd * 64 + lane, dlast);
+                    dma16(reinterpret_cast<const char *>(T.Ad) + v * 16,
+                          __builtin_amdgcn_readfirstlane(bl + TAIL_NXP * 1024 + pd * 1024));
+                }
+            }
         }
     };
-    auto land = [&](const St &S, int b) {  // the staged vectors into this chunk's LDS buffer
-        if (!act || S.blk < 0 || S.cnt > TAIL_CAP) return;
-        char *B = buf(b);
-        const long last = S.cnt > 0 ? (long)S.base + S.cnt - 1 : (long)S.base;
-        const int xn = (int)(min(last >> 1, (T.nnz_pad >> 1) - 1) - (S.xb >> 1)) + 1;
-        const int jn = (int)(min(last >> 4, ((T.nnz_pad - 4 + 32) >> 4) - 1) - (S.jb >> 4)) + 1;
-#pragma unroll
-        for (int u = 0; u < NX2; u++)
-            if (t + 256 * u < xn) reinterpret_cast<d2_t *>(B)[t + 256 * u] = S.vx[u];
-        if (t < jn) reinterpret_cast<i4_t *>(B + TAIL_SX)[t] = S.vj;
-    };
-    // thread 0: the pair's rows read final planes only.  U tile rows Kp = S-1-K
-    // complete (nearly) in increasing Kp, and the pairs come from the top down,
-    // so thread 0 keeps the prefix of rows it has seen complete (kp_done) and
-    // asks the counters only about rows past it
+    // loader thread 0: the group's rows read final planes only.  U tile rows Kp =
+    // S-1-K complete (nearly) in increasing Kp, the groups come from the top down:
+    // the prefix of rows seen complete (kp_done) is not asked about again
     int kp_done = -1;
-    auto wait_planes = [&](unsigned long long cl) {
-        if (cl >= (unsigned long long)T.nblk) return;
-        const long hi = T.cend - 1 - (long)cl;                                   // upper chunk
-        const long lo = T.cend - 1 - (long)min(cl + 1, (unsigned long long)T.nblk - 1);
-        const int r0 = (int)(lo * 256), r1 = min((int)(hi * 256) + 256, T.nrows);
-        const int ka = max(r0 / (int)T.pl - 1, 0), kb = min((r1 - 1) / (int)T.pl + 1, T.nz - 1);
+    auto wait_planes = [&](unsigned long long g) {
+        if (g >= NB) return;
+        const long lo = T.cend - 1 - (long)min(g + CPR - 1, NB - 1);
+        const int r0 = (int)(lo * 256);
+        const int ka = max(max(r0 - 15, 0) / (int)T.pl - 1, 0);  // (lines of x: 16 rows)
         const int kpb = T.S - 1 - T.kof[ka];  // the highest U tile row needed
         for (int Kp = kp_done + 1; Kp <= kpb; Kp++) {
             unsigned *cnt = T.kdone + Kp;
@@ -293,95 +324,175 @@ static __device__ void line_tail_wg(const LineTail &T, const double *x, int *err
             kp_done = Kp;
         }
     };
-    St A, Bs;
-    // pairs are claimed two rounds ahead (a returning atomic costs ~1 us under
-    // load); every workgroup ends on exactly one failed claim
-    if (tid == 0) {
-        claim();
-        if (read_claim() < (unsigned long long)T.nblk) {
-            const unsigned long long c0 = read_claim();
-            claim();
-            sync[2] = sync[0];
-            sync[3] = sync[1];
-            sync[0] = (unsigned)c0;
-            sync[1] = (unsigned)(c0 >> 32);
-        } else {
-            sync[2] = sync[0];
-            sync[3] = sync[1];
+    // LSSP_AMD_TAIL_DIAG: per workgroup {target, entry, first group ready, exit, groups, plane-wait ticks}
+    unsigned *dw = T.dbg && tid == 512 ? T.dbg + 4096 + 8 * blockIdx.x : nullptr;
+    unsigned long long wticks = 0;
+    int ngroups = 0;
+    if (dw) {
+        dw[0] = T.ktarget;
+        dw[1] = (unsigned)t0;
+    }
+    // ---- prologue: claims of groups 0..2 (each only while the previous is valid),
+    // row pointers of groups 0 and 1, values of group 0, its planes
+    if (tid == 512) {
+        unsigned long long q[3] = {~0ull, ~0ull, ~0ull};
+        q[0] = claim();
+        if (q[0] < NB) q[1] = claim();
+        if (q[1] < NB) q[2] = claim();
+        for (int k = 0; k < 3; k++) {
+            sync[2 * k] = (unsigned)q[k];
+            sync[2 * k + 1] = (unsigned)(q[k] >> 32);
         }
     }
     __syncthreads();
-    unsigned long long cur = read_claim();
-    unsigned long long nxt = ((unsigned long long)sync[3] << 32) | sync[2];
-    __syncthreads();  // (sync is rewritten below)
-    if (cur >= (unsigned long long)T.nblk) return;  // uniform
-    stage(cur, A);
-    int b = 0;
+    auto rd = [&](int k) { return ((unsigned long long)sync[2 * k + 1] << 32) | sync[2 * k]; };
+    unsigned long long g0 = rd(0), g1 = rd(1), g2 = rd(2);
+    if (g0 >= NB) {  // uniform
+        if (dw) dw[3] = (unsigned)__builtin_amdgcn_s_memrealtime();
+        return;
+    }
+    if (ldr && lw > 0) {
+        load_ap(g0, 0);
+        load_ap(g1, 1);
+    }
+    __syncthreads();
+    if (ldr) {
+        if (lw > 0) load_vals(g0, 0, 0);
+        else if (lt == 0) wait_planes(g0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (dw) dw[2] = (unsigned)__builtin_amdgcn_s_memrealtime();
+    int b = 0, q = 0;  // buffer and row-pointer slot of the current group
     for (;;) {
-        land(A, b);
-        if (tid == 0) {
-            wait_planes(cur);
-            if (nxt < (unsigned long long)T.nblk) claim();  // the pair after next
-        }
-        __syncthreads();  // the pair's data in LDS, its planes final, the pair after next claimed
-        const unsigned long long nxt2 = nxt < (unsigned long long)T.nblk ? read_claim() : ~0ull;
-        stage(nxt, Bs);  // in flight while this pair's gathers run
-        double zv = 0.0, v0 = 0.0, v1 = 0.0;
-        if (act && A.blk >= 0) {
-            const char *B = buf(b);
-            const double *sx = reinterpret_cast<const double *>(B);
-            const unsigned char *sd = reinterpret_cast<const unsigned char *>(B + TAIL_SX);
-            double sum = 0.0;
-            if (A.r < T.nrows) {
-                if (A.cnt <= TAIL_CAP) {
-                    const int ox = (int)(A.base - A.xb) - A.base, oj = (int)(A.base - A.jb) - A.base;
-                    const int len = A.re - A.rb;
-                    if (len > 0 && len <= 8) {
-                        double pr[8];
+        // g0: this round's group (buffer b, slot q); g1: next (slot q+1); g2: after next
+        if (comp) {
+            // both rows' loads first (gathers of x, the dot operands), then the sums
+            double pr[2][8], w0p[2], w1p[2];
+            int len[2], row[2];
+            bool big[2];
 #pragma unroll
-                        for (int u = 0; u < 8; u++) {
-                            const int k = min(A.rb + u, A.re - 1);
-                            pr[u] = ld_sc1d(x + A.r + soff[sd[k + oj]]) * sx[k + ox];
-                        }
+            for (int h = 0; h < 2; h++) {
+                const int k = c + 2 * h;
+                const long blk = blk_of(g0, k);
+                row[h] = -1;
+                len[h] = 0;
+                big[h] = false;
+                w0p[h] = w1p[h] = 0.0;
+                if (blk < 0) continue;
+                const int *ap = aps + (q * CPR + k) * TAIL_APC;
+                const int r0 = (int)(blk * 256), rows = min(256, T.nrows - r0);
+                if (t >= rows) continue;
+                const int r = r0 + t;
+                const int base = ap[0], cnt = ap[rows] - base;
+                const int rb = ap[t], re = ap[t + 1];
+                row[h] = r;
+                len[h] = re - rb;
+                big[h] = cnt > TAIL_CAP || len[h] > 8;
+                if (T.nred > 0 && T.w0 != T.z) w0p[h] = ldv(T.w0, r);
+                if (T.nred > 1 && T.w1 && T.w1 != T.z) w1p[h] = ldv(T.w1, r);
+                if (big[h] || len[h] <= 0) continue;
+                const char *B = smem + TAIL_OFF_BUF + (b * CPR + k) * TAIL_CHB;
+                const double *sx = reinterpret_cast<const double *>(B);
+                const unsigned char *sd = reinterpret_cast<const unsigned char *>(B + TAIL_NXP * 1024);
+                const int ox = -(base & ~1), oj = -(base & ~15);
 #pragma unroll
-                        for (int u = 0; u < 8; u++)
-                            if (u < len) sum += pr[u];
-                    } else {
-                        for (int k = A.rb; k < A.re; k++) sum += ld_sc1d(x + A.r + soff[sd[k + oj]]) * sx[k + ox];
-                    }
-                } else {
-                    for (int k = A.rb; k < A.re; k++) sum += ld_sc1d(x + T.Aj[k]) * T.Ax[k];
+                for (int u = 0; u < 8; u++) {
+                    const int kk = min(rb + u, re - 1);
+                    pr[h][u] = ldx(r + soff[sd[kk + oj]]) * sx[kk + ox];
                 }
+            }
+            double v0[2] = {0.0, 0.0}, v1[2] = {0.0, 0.0};
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int r = row[h];
+                if (r < 0) continue;
+                double sum = 0.0;
+                if (!big[h]) {
+#pragma unroll
+                    for (int u = 0; u < 8; u++)
+                        if (u < len[h]) sum += pr[h][u];
+                } else {
+                    const int k = c + 2 * h;
+                    const int *ap = aps + (q * CPR + k) * TAIL_APC;
+                    const int rb = ap[t], re = ap[t + 1];
+                    const int rows = min(256, T.nrows - (r - t)), base = ap[0], cnt = ap[rows] - base;
+                    if (cnt <= TAIL_CAP) {
+                        const char *B = smem + TAIL_OFF_BUF + (b * CPR + k) * TAIL_CHB;
+                        const double *sx = reinterpret_cast<const double *>(B);
+                        const unsigned char *sd = reinterpret_cast<const unsigned char *>(B + TAIL_NXP * 1024);
+                        const int ox = -(base & ~1), oj = -(base & ~15);
+                        for (int kk = rb; kk < re; kk++) sum += ldx(r + soff[sd[kk + oj]]) * sx[kk + ox];
+                    } else {
+                        for (int kk = rb; kk < re; kk++) sum += ldx(T.Aj[kk]) * T.Ax[kk];
+                    }
+                }
+                double zv;
                 if (T.epi == EPI_MXY) zv = sum;
                 else if (T.epi == EPI_AMXY) zv = sum * T.alpha;
-                else if (T.epi == EPI_AXPBY) zv = ld_sc1d(T.y + A.r) * T.beta + T.alpha * sum;
+                else if (T.epi == EPI_AXPBY) zv = ldv(T.y, r) * T.beta + T.alpha * sum;
                 else zv = T.alpha * sum;
-                T.z[A.r] = zv;
-                if (T.nred > 0) v0 = zv * (T.w0 == T.z ? zv : A.w0p);
-                if (T.nred > 1) v1 = zv * (T.w1 && T.w1 != T.z ? A.w1p : zv);
+                T.z[r] = zv;
+                if (T.nred > 0) v0[h] = zv * (T.w0 == T.z ? zv : w0p[h]);
+                if (T.nred > 1) v1[h] = zv * (T.w1 && T.w1 != T.z ? w1p[h] : zv);
+            }
+            // chunk_reduce's order: each chunk's four wave halving trees, (w0 + w1) + (w2 + w3)
+            if (T.nred > 0) {
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const double s0 = wave_sum_d(v0[h]);
+                    const double s1 = T.nred > 1 ? wave_sum_d(v1[h]) : 0.0;
+                    if (lane == 0) {
+                        double *red = reds + (b * CPR + c + 2 * h) * 8;
+                        red[(tid >> 6) & 3] = s0;
+                        red[4 + ((tid >> 6) & 3)] = s1;
+                    }
+                }
+            }
+        } else if (ldr) {
+            // loaders: group g1's values (its row pointers are in slot q+1), group g2's
+            // row pointers (waves 1, 2); g1's planes and the claim of the group after
+            // g2 (wave 0) -- every wave waits for its own round trips only
+            const int q1 = q == 2 ? 0 : q + 1, q2 = q1 == 2 ? 0 : q1 + 1;
+            if (lw > 0) {
+                if (g1 < NB) load_vals(g1, q1, b ^ 1);
+                if (g2 < NB) load_ap(g2, q2);
+            } else if (lt == 0) {
+                const unsigned long long g3 = g2 < NB ? claim() : ~0ull;
+                const uint64_t tw = dw ? __builtin_amdgcn_s_memrealtime() : 0;
+                wait_planes(g1);
+                if (dw) wticks += __builtin_amdgcn_s_memrealtime() - tw;
+                sync[6] = (unsigned)g3;
+                sync[7] = (unsigned)(g3 >> 32);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();  // group g0 computed; g1 staged and its planes final; g2's pointers in; g3 claimed
+        if (T.nred > 0 && comp && t == 0) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const long blk = blk_of(g0, c + 2 * h);
+                const double *red = reds + (b * CPR + c + 2 * h) * 8;
+                if (blk >= 0) {
+                    T.part[blk] = (red[0] + red[1]) + (red[2] + red[3]);
+                    if (T.nred > 1) T.part[T.pcap + blk] = (red[4] + red[5]) + (red[6] + red[7]);
+                }
             }
         }
-        // chunk_reduce's order: the chunk's four wave halving trees, (w0 + w1) + (w2 + w3)
-        double *red = reinterpret_cast<double *>(buf(b) + TAIL_SX + TAIL_SD);  // [slot][wave]
-        const int wq = (tid >> 6) & 3;
-        if (T.nred > 0) {
-            const double s0 = wave_sum_d(v0);
-            const double s1 = T.nred > 1 ? wave_sum_d(v1) : 0.0;
-            if (act && (tid & 63) == 0) {
-                red[wq] = s0;
-                red[4 + wq] = s1;
-            }
-        }
-        __syncthreads();  // the pair's LDS is read (it is rewritten two rounds later) and reduced
-        if (T.nred > 0 && act && t == 0 && A.blk >= 0) {
-            T.part[A.blk] = (red[0] + red[1]) + (red[2] + red[3]);
-            if (T.nred > 1) T.part[T.pcap + A.blk] = (red[4] + red[5]) + (red[6] + red[7]);
-        }
-        if (nxt >= (unsigned long long)T.nblk) break;  // uniform
-        A = Bs;
-        cur = nxt;
-        nxt = nxt2;
+        const unsigned long long g3 = g2 < NB ? rd(3) : ~0ull;
+        ngroups++;
+        if (g1 >= NB) break;  // uniform
+        __syncthreads();  // (sync word 3 is rewritten next round)
+        g0 = g1;
+        g1 = g2;
+        g2 = g3;
         b ^= 1;
+        q = q == 2 ? 0 : q + 1;
+    }
+    if (dw) {
+        dw[3] = (unsigned)__builtin_amdgcn_s_memrealtime();
+        dw[4] = ngroups;
+        dw[5] = (unsigned)wticks;
     }
 }
 
