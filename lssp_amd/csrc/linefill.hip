@@ -840,15 +840,16 @@ int linef_gather(lssp_amd_ctx *c, const LineSweep &ls, int mirror, const double 
 template <int NA, int OUT>
 int linef_launch_t(lssp_amd_ctx *c, const LineSweep &ls, const FillArgs &a)
 {
-    // (the sweeps with natural-order output reserve what the tail product needs)
+    // (a sweep with natural-order output and the tail product reserves what the product needs)
     constexpr int lds0 = lf::lds_bytes<NA, OUT, LINEF_D>();
-    constexpr int lds = OUT == 1 && lds0 < TAIL_LDS_BYTES(0) ? TAIL_LDS_BYTES(0) : lds0;
-    static_assert(lds <= 160 * 1024, "LDS");
+    constexpr int ldst = OUT == 1 && lds0 < TAIL_LDS_BYTES(0) ? TAIL_LDS_BYTES(0) : lds0;
+    static_assert(ldst <= 160 * 1024, "LDS");
+    const int lds = a.tail ? ldst : lds0;
     static_assert(OUT != 1 || lf::waves(LF_NL, LF_SW) >= TAIL_WAVES, "the tail product's roles");
     auto kern = k_linef<NA, OUT, LF_NL, LINEF_D, LINEF_DH, LF_SW>;
     static bool attr = false;
     if (!attr) {
-        LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, ldst));
         attr = true;
     }
     const int grid = std::min(ls.ntiles, c->num_cus);

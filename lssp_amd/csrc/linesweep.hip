@@ -1694,10 +1694,11 @@ static int launch_line2_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &
 template <int P, int LV, int NA, int OUT>
 static int launch_line2_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a)
 {
-    // (the sweeps with natural-order output reserve what the tail product needs)
+    // (a sweep with natural-order output and the tail product reserves what the product needs)
     constexpr int lds0 = l2::lds_bytes<NA, OUT, line2_d<LV>(), P, LV>();
-    constexpr int lds = OUT == 1 && lds0 < TAIL_LDS_BYTES(0) ? TAIL_LDS_BYTES(0) : lds0;
-    static_assert(lds <= 160 * 1024, "LDS");
+    constexpr int ldst = OUT == 1 && lds0 < TAIL_LDS_BYTES(0) ? TAIL_LDS_BYTES(0) : lds0;
+    static_assert(ldst <= 160 * 1024, "LDS");
+    const int lds = a.tail ? ldst : lds0;
     static_assert(OUT != 1 || l2::waves(P, LINE2_NL, LINE2_SW) >= TAIL_WAVES, "the tail product's roles");
     // diagnostics only: LSSP_AMD_LINE_TRACE=path[:tile] appends one JSON line per sweep
     static const char *trp = getenv("LSSP_AMD_LINE_TRACE");
