@@ -181,7 +181,7 @@ constexpr int PK3_CAP = 4096;    // v6: packets per block (descriptors staged in
 // groups of 256 / P lines, each lane holds 2 planes, 2 compute waves.  Squarer
 // tiles = fewer tile-to-tile hand-offs on a sweep's critical path (216^3: 56
 // hops with 64 x 4 tiles, 26 with 16 x 16).
-enum { LT_KIN = 1, LT_JIN = 2, LT_KOUT = 4, LT_JOUT = 8 };
+enum { LT_KIN = 1, LT_JIN = 2, LT_KOUT = 4, LT_JOUT = 8, LT_SKIP = 16 };  // LT_SKIP: k_linef tile wholly off the grid
 struct LineGeom {
     int nx = 0, ny = 0, nz = 0;
     std::vector<char> kin;  // plane k has its (k-1) neighbour

@@ -315,6 +315,34 @@ int build_linefill(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std
             u.tk = Kp > 0 ? (Kp - 1) * W + Jp : -1;
             u.tj = Jp > 0 ? Kp * W + Jp - 1 : -1;
         }
+    // Tiles wholly off the grid -- every line j = j' - k of every plane outside
+    // [0, ny), and so is line -1 (the j-input a tile forwards to its k-successor
+    // through hk[Q][0]) -- hold only +0.0 rows: they are marked LT_SKIP (a
+    // workgroup that claims one counts it done at once) and their consumers
+    // read +0.0 inputs, as on the grid's edges.  In a cube about 40 % of the
+    // S x W skewed tiles (j' = j + k spans ny + nz - 1 columns, a plane's lines
+    // only ny of them).
+    auto skip_off_grid = [&](std::vector<LineTile> &tv) {
+        for (LineTile &t : tv) {
+            const int lo = t.j0 - 1 - (t.k0 + t.np - 1), hi = t.j0 + t.nj - 1 - t.k0;
+            if (hi < 0 || lo > g.ny - 1) t.flags |= LT_SKIP;
+        }
+        for (LineTile &t : tv) {
+            if (t.tk >= 0 && (tv[t.tk].flags & LT_SKIP)) {
+                t.flags &= ~LT_KIN;
+                t.tk = -1;
+            }
+            if (t.tj >= 0 && (tv[t.tj].flags & LT_SKIP)) {
+                t.flags &= ~LT_JIN;
+                t.tj = -1;
+            }
+        }
+    };
+    static const bool keep_all = getenv("LSSP_AMD_LINEF_ALLTILES") != nullptr;  // A/B and tests only
+    if (!keep_all) {
+        skip_off_grid(Lt);
+        skip_off_grid(Ut);
+    }
     const long pl = (long)g.nx * g.ny;
     const int NAL = g.unitL ? 6 : 7;
     FillCoef cl, cu;
@@ -431,6 +459,7 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
         if (t >= a.ntiles) break;
         done_tile = t;
         const LineTile d = a.tiles[t];
+        if (d.flags & LT_SKIP) continue;  // wholly off the grid (build_linefill)
         const int T = d.T, TS = T / LV, nj = d.nj, np = d.np;
         const long SB = (long)P * nj;  // rows per level block
         const bool kin = d.flags & LT_KIN, jin = d.flags & LT_JIN, kout = d.flags & LT_KOUT,
