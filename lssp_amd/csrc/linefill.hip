@@ -327,7 +327,16 @@ int build_linefill(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std
             const int lo = t.j0 - 1 - (t.k0 + t.np - 1), hi = t.j0 + t.nj - 1 - t.k0;
             if (hi < 0 || lo > g.ny - 1) t.flags |= LT_SKIP;
         }
+        // (a producer of a skipped tile does not publish: the L and U sweeps share
+        // the hand-off buffers, and an output no consumer re-arms would reach the
+        // other sweep's tile of the same index as a stale value)
         for (LineTile &t : tv) {
+            if (!(t.flags & LT_SKIP)) continue;
+            if (t.tk >= 0) tv[t.tk].flags &= ~LT_KOUT;
+            if (t.tj >= 0) tv[t.tj].flags &= ~LT_JOUT;
+        }
+        for (LineTile &t : tv) {
+            if (t.flags & LT_SKIP) continue;
             if (t.tk >= 0 && (tv[t.tk].flags & LT_SKIP)) {
                 t.flags &= ~LT_KIN;
                 t.tk = -1;
