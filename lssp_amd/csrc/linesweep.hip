@@ -1834,7 +1834,8 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
     const long nall = num_chunks(n);
     const long cb = dist ? A->ich0 : 0, ce = dist ? A->ich1 : nall;
     if (!on || li.kind > 1 || li.LV < 2 || li.ntiles == 0 || !A || (long)A->nrows != n || ce <= cb ||
-        (c->nranks > 1) != dist || A->ndiag == 0 || A->max_off_int > pl || nred < 0 || nred > 2 || x == z || !A->Ad)
+        (c->nranks > 1) != dist || A->ndiag == 0 || A->max_off_int > pl || nred < 0 || nred > 2 || x == z || !A->Ad ||
+        n >= (1L << 28))  // (x is read through a buffer resource: byte offsets below 2^31)
         return on == 2 ? LSSP_AMD_EINVAL : LSSP_AMD_EUNSUPPORTED;
     const int S = li.S, W = li.W, nz = li.g.nz;
     if (!li.d_kdone) {

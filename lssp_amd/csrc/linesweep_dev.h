@@ -243,7 +243,7 @@ static __device__ void line_tail_wg(const LineTail &T, const double *x, int *err
     // and its writers' stores are write-through and drained before their tile is
     // counted.
     auto ldx = [&](int col) {
-        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, col * 8, 0, 0));
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, (int)((unsigned)col * 8u), 0, 0));
     };
     auto ldv = [&](const double *p, int i) { return p == x ? ldx(i) : p[i]; };
     auto blk_of = [&](unsigned long long g, int k) {  // chunk k of a group, -1 past the end
@@ -364,34 +364,37 @@ static __device__ void line_tail_wg(const LineTail &T, const double *x, int *err
     __syncthreads();
     if (dw) dw[2] = (unsigned)__builtin_amdgcn_s_memrealtime();
     int b = 0, q = 0;  // buffer and row-pointer slot of the current group
+    // diagnostics: busy time per round of compute wave 0 and loader wave 1 (to their barrier)
+    unsigned *dwr = T.dbg && (tid == 0 || tid == 576) ? T.dbg + 4096 + 8 * blockIdx.x + (tid == 0 ? 6 : 7) : nullptr;
+    unsigned long long rticks = 0;
     for (;;) {
         // g0: this round's group (buffer b, slot q); g1: next (slot q+1); g2: after next
+        const uint64_t tr = dwr ? __builtin_amdgcn_s_memrealtime() : 0;
         if (comp) {
-            // both rows' loads first (gathers of x, the dot operands), then the sums
-            double pr[2][8], w0p[2], w1p[2];
+            // both rows' loads first (gathers of x, the dot operands), then the sums:
+            // no branch between the two rows' loads and the products, so every
+            // load of the round is in flight before the first wait (a row that
+            // is not computed here loads x out of the buffer's range: +0.0)
+            double xv[2][8], av[2][8], w0p[2], w1p[2];
             int len[2], row[2];
             bool big[2];
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int k = c + 2 * h;
                 const long blk = blk_of(g0, k);
-                row[h] = -1;
-                len[h] = 0;
-                big[h] = false;
-                w0p[h] = w1p[h] = 0.0;
-                if (blk < 0) continue;
+                const int r0 = blk >= 0 ? (int)(blk * 256) : 0;
+                const int rows = blk >= 0 ? min(256, T.nrows - r0) : 0;
+                const bool ok = blk >= 0 && t < rows;
                 const int *ap = aps + (q * CPR + k) * TAIL_APC;
-                const int r0 = (int)(blk * 256), rows = min(256, T.nrows - r0);
-                if (t >= rows) continue;
-                const int r = r0 + t;
                 const int base = ap[0], cnt = ap[rows] - base;
                 const int rb = ap[t], re = ap[t + 1];
-                row[h] = r;
-                len[h] = re - rb;
-                big[h] = cnt > TAIL_CAP || len[h] > 8;
-                if (T.nred > 0 && T.w0 != T.z) w0p[h] = ldv(T.w0, r);
-                if (T.nred > 1 && T.w1 && T.w1 != T.z) w1p[h] = ldv(T.w1, r);
-                if (big[h] || len[h] <= 0) continue;
+                const int r = ok ? r0 + t : 0;
+                row[h] = ok ? r : -1;
+                len[h] = ok ? re - rb : 0;
+                big[h] = ok && (cnt > TAIL_CAP || len[h] > 8);
+                const bool fast = ok && !big[h] && len[h] > 0;
+                w0p[h] = T.nred > 0 && T.w0 != T.z ? ldv(T.w0, r) : 0.0;
+                w1p[h] = T.nred > 1 && T.w1 && T.w1 != T.z ? ldv(T.w1, r) : 0.0;
                 const char *B = smem + TAIL_OFF_BUF + (b * CPR + k) * TAIL_CHB;
                 const double *sx = reinterpret_cast<const double *>(B);
                 const unsigned char *sd = reinterpret_cast<const unsigned char *>(B + TAIL_NXP * 1024);
@@ -399,9 +402,17 @@ static __device__ void line_tail_wg(const LineTail &T, const double *x, int *err
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
                     const int kk = min(rb + u, re - 1);
-                    pr[h][u] = ldx(r + soff[sd[kk + oj]]) * sx[kk + ox];
+                    const int ij = fast ? kk + oj : 0, ix = fast ? kk + ox : 0;
+                    const int col = fast ? r + soff[sd[ij]] : 0x1FFFFFFF;  // (past num_records: +0.0)
+                    xv[h][u] = ldx(col);
+                    av[h][u] = sx[ix];
                 }
             }
+            double pr[2][8];
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+                for (int u = 0; u < 8; u++) pr[h][u] = xv[h][u] * av[h][u];
             double v0[2] = {0.0, 0.0}, v1[2] = {0.0, 0.0};
 #pragma unroll
             for (int h = 0; h < 2; h++) {
@@ -467,6 +478,7 @@ static __device__ void line_tail_wg(const LineTail &T, const double *x, int *err
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        if (dwr) rticks += __builtin_amdgcn_s_memrealtime() - tr;
         __syncthreads();  // group g0 computed; g1 staged and its planes final; g2's pointers in; g3 claimed
         if (T.nred > 0 && comp && t == 0) {
 #pragma unroll
@@ -494,6 +506,7 @@ static __device__ void line_tail_wg(const LineTail &T, const double *x, int *err
         dw[4] = ngroups;
         dw[5] = (unsigned)wticks;
     }
+    if (dwr) *dwr = (unsigned)rticks;
 }
 
 }  // namespace lssp_amd

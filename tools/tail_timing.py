@@ -53,6 +53,8 @@ def main():
                           "ready_minus_enter_us_pct": q((ready - enter)[worked]),
                           "pairs_total": int(tl[:, 4].sum()), "pairs_pct": q(tl[worked, 4]),
                           "plane_wait_us_pct": q(tl[worked, 5] / 100.0),
+                          "compute_wave_us_per_round_pct": q(tl[worked, 6] / 100.0 / tl[worked, 4]),
+                          "loader_wave_us_per_round_pct": q(tl[worked, 7] / 100.0 / tl[worked, 4]),
                           "busy_us_per_pair_pct": q(((leave - ready)[worked] - tl[worked, 5] / 100.0) /
                                                     tl[worked, 4])}), flush=True)
     dev.close()
