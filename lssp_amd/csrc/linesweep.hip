@@ -1819,13 +1819,14 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
                            int epi, double alpha, double beta, const double *y, double *z, int nred,
                            const double *w0, const double *w1)
 {
-    // Off by default: measured SLOWER than the two steps (216^3 BiCGSTAB 443 vs
-    // 565 it/s, ILU(1) 282 vs 320; profiles/r05/r05c_tail_ab.txt): a sweep
-    // workgroup's 11 waves hold one 64-row group each, three dependent memory
-    // round trips per group, so the freed CUs move ~80 rows/us each against
-    // k_spmv3's 8 workgroups per CU, and only ~58 % of the product's CU time is
-    // free before the sweep ends.  LSSP_AMD_TAIL=1 selects it (A/B runs); =2:
-    // selected, and an ineligible call fails (EINVAL) instead of falling back (tests)
+    // Off by default: measured slower than the two steps (216^3 BiCGSTAB 531 vs
+    // 559 it/s, ILU(1) 328 vs 335; profiles/r05/r05c_tail_ab.txt): after the
+    // sweep the product moves ~0.75x k_spmv3's rows per us (one 1024-row round
+    // per CU in flight, ~6 us each), and during the sweep rows become ready one
+    // U tile row (all W tiles) at a time, so the freed workgroups cannot finish
+    // the product before the two-step path would.  LSSP_AMD_TAIL=1 selects it
+    // (A/B runs); =2: selected, and an ineligible call fails (EINVAL) instead of
+    // falling back (tests)
     const char *te = getenv("LSSP_AMD_TAIL");
     const int on = te ? atoi(te) : 0;
     const long pl = (long)li.g.nx * li.g.ny, n = pl * li.g.nz;
