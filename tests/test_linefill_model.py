@@ -41,7 +41,14 @@ def widths(m):
         return w
 
 
-def model_apply(nx, ny, nz, seed=1):
+def off_grid(j0, nj, k0, np_, ny):
+    """build_linefill's LT_SKIP rule: every line of every plane, and line -1
+    (forwarded to the k-successor), off the grid."""
+    lo, hi = j0 - 1 - (k0 + np_ - 1), j0 + nj - 1 - k0
+    return hi < 0 or lo > ny - 1
+
+
+def model_apply(nx, ny, nz, seed=1, skip=True):
     Ap, Aj, Ax = _box7(nx, ny, nz, seed)
     n = Ap.size - 1
     L, U = O.ilu(O.CSR(n, Ap, Aj, Ax), "iluk", level=1)
@@ -59,10 +66,15 @@ def model_apply(nx, ny, nz, seed=1):
     hk, hj = {}, {}
     out = np.full(n, np.nan)
     order = sorted([(K, J) for K in range(S) for J in range(W)], key=lambda t: (t[1] * 36 + t[0] * 13, t[0] * W + t[1]))
+    # skipped tiles do not run; their consumers read +0.0 inputs
+    skl = {(K, J) for K in range(S) for J in range(W)
+           if skip and off_grid(js[J], wd[J], K * P, min(P, nz - K * P), ny)}
     for K, J in order:
         j0, nj, k0, np_ = js[J], wd[J], K * P, min(P, nz - K * P)
+        if (K, J) in skl: continue
         T = nx + 2 * (nj - 1) + (np_ - 1) + sig(np_ - 1) + 1; T += T % 2
-        kin, jin, kout, jout = K > 0, J > 0, K < S - 1, J < W - 1
+        kin, jin = K > 0 and (K - 1, J) not in skl, J > 0 and (K, J - 1) not in skl
+        kout, jout = K < S - 1, J < W - 1
         def HK(Q, e):
             if not kin: return 0.0
             return hk[(K - 1, J, Q, e)]
@@ -141,12 +153,17 @@ def model_apply(nx, ny, nz, seed=1):
     # U tiles
     hk.clear(); hj.clear()
     outu = np.full(n, np.nan)
-    for Kp, Jp in order:
+    def u_geom(Kp, Jp):
         K, J = S - 1 - Kp, W - 1 - Jp
         nj, np_ = wd[J], min(P, nz - K * P)
-        j0 = m - js[J] - nj; k0 = nz - K * P - np_
+        return m - js[J] - nj, nj, nz - K * P - np_, np_
+    sku = {(Kp, Jp) for Kp in range(S) for Jp in range(W) if skip and off_grid(*u_geom(Kp, Jp), ny)}
+    for Kp, Jp in order:
+        j0, nj, k0, np_ = u_geom(Kp, Jp)
+        if (Kp, Jp) in sku: continue
         T = nx + 2 * (nj - 1) + (np_ - 1) + sig(np_ - 1) + 1; T += T % 2
-        kin, jin, kout, jout = Kp > 0, Jp > 0, Kp < S - 1, Jp < W - 1
+        kin, jin = Kp > 0 and (Kp - 1, Jp) not in sku, Jp > 0 and (Kp, Jp - 1) not in sku
+        kout, jout = Kp < S - 1, Jp < W - 1
         def HK(Q, e):
             if not kin: return 0.0
             return hk[(Kp - 1, Jp, Q, e)]
@@ -198,7 +215,20 @@ def model_apply(nx, ny, nz, seed=1):
     return ok_l, np.array_equal(outu, refu)
 
 
-@pytest.mark.parametrize("nx,ny,nz", [(9, 7, 13), (3, 3, 2), (6, 5, 1), (4, 9, 17)])
-def test_linefill_dataflow_model_bitwise_vs_oracle(nx, ny, nz):
-    ok_l, ok_u = model_apply(nx, ny, nz)
+@pytest.mark.parametrize("nx,ny,nz", [(9, 7, 13), (3, 3, 2), (6, 5, 1), (4, 9, 17), (4, 5, 33)])
+@pytest.mark.parametrize("skip", [True, False], ids=["skip-off-grid", "all-tiles"])
+def test_linefill_dataflow_model_bitwise_vs_oracle(nx, ny, nz, skip):
+    ok_l, ok_u = model_apply(nx, ny, nz, skip=skip)
     assert ok_l and ok_u
+
+
+def test_off_grid_rule_skips_tiles():
+    """The shapes above exercise the rule: (4, 9, 17) and (4, 5, 33) have
+    skipped tiles in both sweeps."""
+    for nx, ny, nz in ((4, 9, 17), (4, 5, 33)):
+        m = ny + nz - 1
+        wd = widths(m)
+        js = np.concatenate([[0], np.cumsum(wd)])
+        S = (nz + P - 1) // P
+        n_skip = sum(off_grid(js[J], wd[J], K * P, min(P, nz - K * P), ny) for K in range(S) for J in range(len(wd)))
+        assert n_skip > 0
