@@ -416,9 +416,13 @@ struct FillArgs {
     LineTail tl;
 };
 
-template <int NA, int OUT, int NL, int D, int DH, int SW>
+template <int NA, int OUT, int NL, int D, int DH, int SW, bool TL = false>
 __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
 {
+    // TL: the instantiation that can run the tail product (kept apart so the
+    // plain sweep does not carry the product's registers; k_line2 alike)
+    static_assert(!TL || OUT == 1, "the tail product follows the natural-order sweep");
+    const bool tail = TL && a.tail;
     using namespace lf;
     using SL = Slot<NA>;
     constexpr int LA = 2;  // the loaders complete step s+LA's slot during step s
@@ -446,7 +450,7 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
     if (a.guard && *a.guard != 0.0) {  // a batched iteration past the stop: consume the launch's tile claims
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             atomicAdd(a.claim, (unsigned long long)a.ntiles + gridDim.x);
-            if (OUT == 1 && a.tail) {  // ... and the tail's chunk claims and tile counts
+            if (OUT == 1 && tail) {  // ... and the tail's chunk claims and tile counts
                 atomicAdd(a.tl.claim, tail_claims(a.tl.nblk, gridDim.x));
                 for (int K = 0; K < a.tl.S; K++) atomicAdd(a.tl.kdone + K, (unsigned)a.tl.W);
             }
@@ -458,7 +462,7 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
     for (;;) {
         __syncthreads();
         if (threadIdx.x == 0) {
-            if (OUT == 1 && a.tail && done_tile >= 0)  // its storers' write-through stores drained before the barrier
+            if (OUT == 1 && tail && done_tile >= 0)  // its storers' write-through stores drained before the barrier
                 __hip_atomic_fetch_add(a.tl.kdone + done_tile / a.tl.W, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int c = (int)(atomicAdd(a.claim, 1ull) - a.base);
             *s_tile = c < a.ntiles ? a.order[c] : a.ntiles;
@@ -755,7 +759,7 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
                         const int j = d.j0 + l - d.k0 - p;
                         const double x = res[(q & (RSL - 1)) * ROWS + p * NJ + l];
                         if (p < np && l < nj && (unsigned)j < (unsigned)a.ny && (unsigned)i < (unsigned)nx) {
-                            if (a.tail) st_sc1d(a.out + nat(p, l, i), x);  // read by the tail product on other CUs
+                            if (tail) st_sc1d(a.out + nat(p, l, i), x);  // read by the tail product on other CUs
                             else a.out[nat(p, l, i)] = x;
                         }
                     }
@@ -768,7 +772,7 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
                 rearm(-1);  // step -1's entries (levels -2, -1)
                 // the last blocks' remaining quarters (every result is in LDS)
                 for (int s = TS + 1; s < 4 * ((T - 1) / 8) + 8; s++) slice(s);
-                if (a.tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // before the tile is counted
+                if (tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // before the tile is counted
             } else {
                 // step s-1's two levels: value k = 64 (w + SW u) + lane is level
                 // 2(s-1) + (k >> 7), plane (k >> 4) & 7, line k & 15; its place in the
@@ -806,7 +810,7 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
             }
         }
     }
-    if constexpr (OUT == 1) {
+    if constexpr (TL) {
         if (a.tail) {  // no tile left for this workgroup: its waves run the tail product
             int *soff = reinterpret_cast<int *>(smem);  // (the ring's LDS is free now; linef_launch_t reserves TAIL_LDS_BYTES)
             __syncthreads();
@@ -885,13 +889,15 @@ int linef_launch_t(lssp_amd_ctx *c, const LineSweep &ls, const FillArgs &a)
     const int lds = a.tail ? ldst : lds0;
     static_assert(OUT != 1 || lf::waves(LF_NL, LF_SW) >= TAIL_WAVES, "the tail product's roles");
     auto kern = k_linef<NA, OUT, LF_NL, LINEF_D, LINEF_DH, LF_SW>;
+    auto kernt = k_linef<NA, OUT, LF_NL, LINEF_D, LINEF_DH, LF_SW, OUT == 1>;
     static bool attr = false;
     if (!attr) {
-        LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, ldst));
+        LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds0));
+        LSSP_HIP(hipFuncSetAttribute((const void *)kernt, hipFuncAttributeMaxDynamicSharedMemorySize, ldst));
         attr = true;
     }
     const int grid = std::min(ls.ntiles, c->num_cus);
-    kern<<<grid, 64 * lf::waves(LF_NL, LF_SW), lds, c->stream>>>(a);
+    (a.tail ? kernt : kern)<<<grid, 64 * lf::waves(LF_NL, LF_SW), lds, c->stream>>>(a);
     ls.base += (unsigned long long)ls.ntiles + grid;
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;

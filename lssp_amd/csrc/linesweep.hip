@@ -1079,10 +1079,15 @@ constexpr int lds_bytes() { return (D + 1) * Slot<NA, P, LV>::BYTES + rsl<OUT, L
 constexpr int waves(int P, int NL, int SW) { return P / 4 + NL + 1 + SW; }
 }  // namespace l2
 
-template <int P, int LV, int NA, int OUT, int NL, int D, int DH, int SW, bool TRACE>
+template <int P, int LV, int NA, int OUT, int NL, int D, int DH, int SW, bool TRACE, bool TL = false>
 __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
 {
     using namespace l2;
+    // TL: the instantiation that can run the tail product (a separate kernel: the
+    // product's registers would otherwise raise the plain sweep's VGPRs 113 -> 162
+    // and its SGPR spills 63 -> 182, which cost the U sweep ~40 us at 216^3)
+    static_assert(!TL || OUT == 1, "the tail product follows the natural-order sweep");
+    const bool tail = TL && a.tail;
     using SL = Slot<NA, P, LV>;
     static_assert(LV == 2 || LV == 4, "levels per step");
     constexpr int CW = P / 4, ROWS = P * NJ;
@@ -1105,7 +1110,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
     if (a.guard && *a.guard != 0.0) {  // a batched iteration past the stop: consume the launch's tile claims
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             atomicAdd(a.claim, (unsigned long long)a.ntiles + gridDim.x);
-            if (OUT == 1 && a.tail) {  // ... and the tail's chunk claims and tile counts
+            if (OUT == 1 && tail) {  // ... and the tail's chunk claims and tile counts
                 atomicAdd(a.tl.claim, tail_claims(a.tl.nblk, gridDim.x));
                 for (int K = 0; K < a.tl.S; K++) atomicAdd(a.tl.kdone + K, (unsigned)a.tl.W);
             }
@@ -1114,12 +1119,12 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
     }
 
     int done_tile = -1;  // the tile this workgroup finished last (its completion is counted at the next claim)
-    if (OUT == 1 && a.tail && a.tl.dbg && threadIdx.x == 0)  // diagnostics: the workgroup's start
+    if (OUT == 1 && tail && a.tl.dbg && threadIdx.x == 0)  // diagnostics: the workgroup's start
         a.tl.dbg[6144 + blockIdx.x] = (unsigned)__builtin_amdgcn_s_memrealtime();
     for (;;) {
         __syncthreads();
         if (threadIdx.x == 0) {
-            if (OUT == 1 && a.tail && done_tile >= 0) {  // its storers' write-through stores drained before the barrier
+            if (OUT == 1 && tail && done_tile >= 0) {  // its storers' write-through stores drained before the barrier
                 __hip_atomic_fetch_add(a.tl.kdone + done_tile / a.tl.W, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (a.tl.dbg) a.tl.dbg[blockIdx.x] += 1;
             }
@@ -1435,7 +1440,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                         const double x = res[(q & (RSL - 1)) * ROWS + p * NJ + l];
                         if (!(a.diag & 1) && p < np && l < nj && (unsigned)i < (unsigned)nx) {
                             double *o = a.out + (a.mirror ? nb(p, l) - i : nb(p, l) + i);
-                            if (a.tail) st_sc1d(o, x);  // read by the tail product on other CUs
+                            if (tail) st_sc1d(o, x);  // read by the tail product on other CUs
                             else *o = x;
                         }
                     }
@@ -1449,7 +1454,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                 }
                 // the last blocks' remaining quarters (every result is in LDS)
                 for (int s = TS + 1; s < SPB * ((T - 1) / 8 + 2); s++) slice(s);
-                if (a.tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // before the tile is counted
+                if (tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // before the tile is counted
             } else {
                 // step s-1's LV levels: value k = 64 (w + SW it) + lane is level
                 // LV(s-1) + k / ROWS, plane (k >> 4) & (P-1), line k & 15; its place in the
@@ -1488,7 +1493,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
             }
         }
     }
-    if constexpr (OUT == 1) {
+    if constexpr (TL) {
         if (a.tail) {  // no tile left for this workgroup: its waves run the tail product
             int *soff = reinterpret_cast<int *>(smem);  // (the ring's LDS is free now; launch_line2_t reserves TAIL_LDS_BYTES)
             __syncthreads();  // (the loop's last barrier already passed; the ring is free)
@@ -1675,10 +1680,10 @@ constexpr int line2_d() { return LV == 4 ? 4 : LINE2_D; }
 #endif
 template <int LV, int OUT>
 constexpr int line2_dh() { return LV == 4 ? 2 : OUT == 1 ? LINE2_DH_U : LINE2_DH; }
-template <int P, int LV, int NA, int OUT, bool TRACE>
+template <int P, int LV, int NA, int OUT, bool TRACE, bool TL = false>
 static int launch_line2_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)
 {
-    auto kern = k_line2<P, LV, NA, OUT, LINE2_NL, line2_d<LV>(), line2_dh<LV, OUT>(), LINE2_SW, TRACE>;
+    auto kern = k_line2<P, LV, NA, OUT, LINE2_NL, line2_d<LV>(), line2_dh<LV, OUT>(), LINE2_SW, TRACE, TL>;
     static int attr = 0;
     if (lds > attr) {
         LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -1702,6 +1707,8 @@ static int launch_line2_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &
     static_assert(OUT != 1 || l2::waves(P, LINE2_NL, LINE2_SW) >= TAIL_WAVES, "the tail product's roles");
     // diagnostics only: LSSP_AMD_LINE_TRACE=path[:tile] appends one JSON line per sweep
     static const char *trp = getenv("LSSP_AMD_LINE_TRACE");
+    if constexpr (OUT == 1)
+        if (a.tail) return launch_line2_k<P, LV, NA, OUT, false, true>(c, ls, a, lds);  // (no trace variant)
     if (!trp) return launch_line2_k<P, LV, NA, OUT, false>(c, ls, a, lds);
     LineArgs g = a;
     const size_t tn = 8 * (size_t)ls.ntiles + 8 * (size_t)ls.tmax + 64;
