@@ -159,8 +159,7 @@ struct CoefSrc {
         for (long r = r0; r < r1; r++) {
             double *row = c.data() + (size_t)(upper ? n - 1 - r : r) * NA;
             const int b = Tp[r], e = Tp[r + 1];
-            if (NA >= 4) row[3] = upper ? Tx[b] : Tx[e - 1];
-            if (NA == 5) row[4] = 1.0 / row[3];  // RN(1/diag): k_line2's div_rcp
+            if (NA == 4) row[3] = upper ? Tx[b] : Tx[e - 1];
             for (int q = upper ? b + 1 : b; q < (upper ? e : e - 1); q++) {
                 const long off = upper ? Tj[q] - r : r - Tj[q];
                 const int a = off == plane ? 0 : off == nx ? 1 : 2;  // detect_grid: off is one of 1, nx, plane
@@ -360,9 +359,8 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
             u.tj = Jp > 0 ? Kp * W + Jp - 1 : -1;
         }
     const long plane = (long)g.nx * g.ny;
-    // coefficients per row: c_k, c_j, c_i (unit L), + diag (+ its reciprocal
-    // for k_line2, whose division is div_rcp: linesweep_dev.h)
-    const int NAD = LV == 2 ? 5 : 4;
+    // coefficients per row: c_k, c_j, c_i (unit L), + diag
+    const int NAD = 4;
     const int NAL = g.unitL ? 3 : NAD;
     CoefSrc cl, cu;
     cl.build(Lp, Lj, Lx, false, n, g.nx, plane, NAL);
@@ -1160,7 +1158,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
             const int pw = wave * 4 + gl;
             const int sg = (LV - 1) * wave;  // sigma of the wave's planes
             struct In {
-                double ck[LV], cj[LV], ci[LV], dg[LV], rc[LV], rh[LV], jv[LV];
+                double ck[LV], cj[LV], ci[LV], dg[LV], rh[LV], jv[LV];
             };
             // the step's inputs, read from LDS one step ahead (their slot was
             // completed before the barrier that ended the previous step)
@@ -1173,8 +1171,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     in.ck[v] = b[0];
                     in.cj[v] = b[1];
                     in.ci[v] = b[2];
-                    if constexpr (NA >= 4) in.dg[v] = b[3];
-                    if constexpr (NA == 5) in.rc[v] = b[4];
+                    if constexpr (NA == 4) in.dg[v] = b[3];
                     in.rh[v] = reinterpret_cast<const double *>(slot + SL::RHS)[r];
                     in.jv[v] = reinterpret_cast<const double *>(slot + SL::JFIN)[v * P + pw];
                 }
@@ -1237,12 +1234,9 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                 // (a SALU chain of shifts and per-group start tests measured 3 %
                 // slower per apply, profiles/r04/r04n_line2_compute_variants.txt)
                 uint64_t h[LV];
-                bool hv[LV];
 #pragma unroll
-                for (int lv = 0; lv < LV; lv++) {
-                    hv[lv] = lane_in && (unsigned)(LV * s + lv - loff) < (unsigned)nx;
-                    h[lv] = __builtin_amdgcn_ballot_w64(hv[lv]);
-                }
+                for (int lv = 0; lv < LV; lv++)
+                    h[lv] = __builtin_amdgcn_ballot_w64(lane_in && (unsigned)(LV * s + lv - loff) < (unsigned)nx);
                 if (s >= 0 && s < TS) {
                     double xq = xp;  // the previous level's value
                     double xu = xs;  // lane - 16's value of the previous level
@@ -1255,7 +1249,6 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                         v = v - cur.cj[lv] * xj;
                         v = v - cur.ci[lv] * xq;
                         if constexpr (NA == 4) v = v / cur.dg[lv];
-                        if constexpr (NA == 5) v = div_rcp(v, cur.dg[lv], cur.rc[lv], hv[lv]);
                         const double x = sel_lanes(h[lv], v, xq);
                         if (trs && wave == 0 && lv == LV - 1) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
 #if LINE2_EARLY_SHFL
@@ -1774,8 +1767,8 @@ static int launch_line2(lssp_amd_ctx *c, const LineILU &li, int which, const dou
     a.tail = tail != nullptr && outk == 1;
     if (a.tail) a.tl = *tail;
     // (the kernel is generic in LV; four levels per step measured slower)
-    if (outk == 2) return ls.NA == 3 ? launch_line2_t<8, 2, 3, 2>(c, ls, a) : launch_line2_t<8, 2, 5, 2>(c, ls, a);
-    return ls.NA == 3 ? launch_line2_t<8, 2, 3, 1>(c, ls, a) : launch_line2_t<8, 2, 5, 1>(c, ls, a);
+    if (outk == 2) return ls.NA == 3 ? launch_line2_t<8, 2, 3, 2>(c, ls, a) : launch_line2_t<8, 2, 4, 2>(c, ls, a);
+    return ls.NA == 3 ? launch_line2_t<8, 2, 3, 1>(c, ls, a) : launch_line2_t<8, 2, 4, 1>(c, ls, a);
 }
 
 static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const double *rhs, bool u_in, double *out,

@@ -37,34 +37,6 @@ __device__ __forceinline__ void line_barrier()
     asm volatile("" ::: "memory");
 }
 
-// a / b, bit for bit, from y = RN(1/b) computed by the host's IEEE division:
-// q0 = RN(a y), then two of Markstein's corrections q' = RN(q + RN-exact(a - b q) y).
-// The first brings q within one ulp of a/b, and with y correctly rounded the
-// second returns RN(a/b) (Markstein's theorem; the residual a - b q is exact
-// in the FMA when nothing underflows).  Five dependent FMA-pipe operations in
-// place of the division's ~11 (v_div_scale, v_rcp and its Newton steps, all
-// behind the numerator).  Outside |a|, |y| in [2^-500, 2^500] -- zeros (the
-// sign of a zero quotient), subnormals, inf, NaN -- a lane that needs its value
-// (need) runs the division itself; the branch is skipped when no lane does.
-// Checked against the division on 6.3e8 random and adversarial operand pairs
-// (significands of all ones, quotients near integers; 0 mismatches, and 0 for
-// the one-correction form too) -- tests/test_recip_div.py restates it on CPU.
-__device__ __forceinline__ double div_rcp(double a, double b, double y, bool need)
-{
-    const double q0 = a * y;
-    const double e0 = __builtin_fma(-b, q0, a);
-    const double q1 = __builtin_fma(e0, y, q0);
-    const double e1 = __builtin_fma(-b, q1, a);
-    double q = __builtin_fma(e1, y, q1);
-    const double aa = __builtin_fabs(a), ay = __builtin_fabs(y);
-    const bool fast = aa >= 0x1p-500 && aa <= 0x1p500 && ay >= 0x1p-500 && ay <= 0x1p500;
-    if (need && !fast) {
-        asm volatile(";; div_rcp: the division itself");  // (keeps the rare path a branch, not a select)
-        q = a / b;
-    }
-    return q;
-}
-
 __device__ __forceinline__ uint64_t line_ld_agent(const double *p)
 {
     return __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
