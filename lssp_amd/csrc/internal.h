@@ -226,6 +226,10 @@ struct LineILU {
     unsigned long long *d_tclaim = nullptr;
     mutable unsigned long long tbase = 0;
     mutable unsigned kepoch = 0;
+    // kind 1 on a small 2-D grid (linefill.hip k_lineg): ONE workgroup, lines on
+    // lanes; level-major streams [level][S, SE, W(, diag), rhs][lane] per sweep
+    int g2 = 0, g2V = 0, g2NYP = 0, g2NCL = 0, g2NCU = 0;
+    double *d_g2L = nullptr, *d_g2U = nullptr;
 };
 
 }  // namespace lssp_amd

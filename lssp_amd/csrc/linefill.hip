@@ -90,6 +90,8 @@ template <int NA, int OUT, int D>
 constexpr int lds_bytes() { return (D + 1) * Slot<NA>::BYTES + rsl<OUT>() * ROWS * 8 + 16 + 512; }
 constexpr int waves(int NL, int SW) { return 2 + NL + 1 + SW; }
 }  // namespace lf
+constexpr int G2_MAXNY = 256;  // k_lineg: lines (lanes) of one workgroup
+constexpr int G2_D = 6;        // k_lineg: levels of DMA lead (ring of G2_D + 1 slots)
 
 // ---------------------------------------------------------------------------
 // host: detection, tiles, streams
@@ -277,6 +279,57 @@ int fill_upload(lssp_amd_ctx *c, const LineGeom &g, const std::vector<LineTile> 
 
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// 2-D grids (the 5-point ILU(1) pattern, nz = 1; exam.cxx's 100 x 100) with at
+// most G2_MAXNY lines: ONE workgroup sweeps the whole grid, lane j = line j, one
+// level v = i + 2 j per step (row i = v - 2 j).  Per level the operands are the
+// lane's own x(v-1) (W), lane j-1's x(v-1) (SE: DPP wave_shr:1, or the previous
+// wave's lane 63 through LDS) and lane j-1's x(v-2) (S: the lane's SE of the
+// previous level), so a level is one shift, three multiply-subtracts (+ U's
+// division) and, with more than one wave, one LDS word and one barrier -- no
+// hand-offs between CUs.  The skewed tiles put one plane per tile on 16 of 128
+// lanes and chain W tiles through cross-CU hand-offs for the same levels.
+// Streams, level-major: [v][S, SE, W (, diag), rhs][lane] (rows off the grid
+// +0.0), the coefficients at build, the rhs per apply (k_lineg_rhs gathers the
+// first sweep's; the L sweep writes the U sweep's); each wave LDS-DMAs its
+// pieces G2_D levels ahead into a ring.
+// ---------------------------------------------------------------------------
+static int build_lineg(lssp_amd_ctx *c, const LineGeom &g, const FillCoef &cl, const FillCoef &cu, LineILU &li)
+{
+    const int nx = g.nx, ny = g.ny, NYP = (ny + 63) / 64 * 64, V = nx + 2 * (ny - 1);
+    const int NCL = cl.NA == 7 ? 4 : 3, NCU = 4;
+    auto make = [&](const FillCoef &src, int NC) {
+        std::vector<double> st((size_t)V * (NC + 1) * NYP + 128, 0.0);  // (+1 KB: whole DMA pieces)
+        for (int v = 0; v < V; v++)
+            for (int j = 0; j < ny; j++) {
+                const int i = v - 2 * j;
+                if (i < 0 || i >= nx) continue;
+                const double *cr = src.c.data() + ((size_t)j * nx + i) * src.NA;  // (sweep order: U mirrored)
+                for (int k = 0; k < 3; k++) st[((size_t)v * (NC + 1) + k) * NYP + j] = cr[3 + k];  // S, SE, W
+                if (NC == 4) st[((size_t)v * (NC + 1) + 3) * NYP + j] = cr[6];
+            }
+        return st;
+    };
+    const std::vector<double> sl = make(cl, NCL), su = make(cu, NCU);
+    LSSP_HIP(hipMalloc(&li.d_g2L, sizeof(double) * sl.size()));
+    LSSP_HIP(hipMemcpy(li.d_g2L, sl.data(), sizeof(double) * sl.size(), hipMemcpyHostToDevice));
+    LSSP_HIP(hipMalloc(&li.d_g2U, sizeof(double) * su.size()));
+    LSSP_HIP(hipMemcpy(li.d_g2U, su.data(), sizeof(double) * su.size(), hipMemcpyHostToDevice));
+    li.g = g;
+    li.kind = 1;
+    li.g2 = 1;
+    li.g2V = V;
+    li.g2NYP = NYP;
+    li.g2NCL = NCL;
+    li.g2NCU = NCU;
+    li.P = 1;
+    li.NJ = ny;
+    li.LV = 1;
+    li.W = li.S = 1;
+    li.ntiles = 1;  // (line sweeps active; no tiles, claims or hand-off buffers)
+    return LSSP_AMD_OK;
+}
+
 int build_linefill(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std::vector<int> &Lj,
                    const std::vector<double> &Lx, const std::vector<int> &Up, const std::vector<int> &Uj,
                    const std::vector<double> &Ux, LineILU &li)
@@ -284,6 +337,16 @@ int build_linefill(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std
     using namespace lf;
     LineGeom g;
     if (!detect_fill1(n, Lp, Lj, Lx, Up, Uj, g)) return LSSP_AMD_EUNSUPPORTED;
+    {
+        const char *e = getenv("LSSP_AMD_LINEG");  // (read per build: tests select either path)
+        if (g.nz == 1 && g.ny <= G2_MAXNY && !(e && !atoi(e))) {
+            const long pl = (long)g.nx * g.ny;
+            FillCoef cl, cu;
+            cl.build(Lp, Lj, Lx, false, n, g.nx, pl, g.unitL ? 6 : 7);
+            cu.build(Up, Uj, Ux, true, n, g.nx, pl, 7);
+            return build_lineg(c, g, cl, cu, li);
+        }
+    }
     const int m = g.ny + g.nz - 1;
     const std::vector<int> wd = fill_widths(m);
     const int W = (int)wd.size(), S = (g.nz + P - 1) / P;
@@ -856,6 +919,145 @@ __global__ __launch_bounds__(256) void k_linef_rhs(const LineTile *__restrict__ 
         if (o[it] >= 0) out[o[it]] = v[it];
 }
 
+// ---- k_lineg: the one-workgroup 2-D sweeps (build_lineg) ----
+struct G2Args {
+    int nx, ny, NYP, V;
+    long n;
+    double *sL, *sU;  // level-major streams (their rhs slots are written per apply)
+    int ncl, ncu;
+    int mode;         // 0: apply (L -> the U stream's rhs, U -> out); 1: L only; 2: U only (-> out)
+    double *out;      // natural order
+    const double *guard;
+};
+constexpr int G2_KP = 3;  // DMA pieces per wave per level (dummies fill up): 4 waves x 3 >= 10 pieces
+__host__ __device__ constexpr int g2_slot_bytes(int NC, int NYP) { return ((NC + 1) * NYP * 8 + 1023) / 1024 * 1024; }
+
+template <int NC>
+__device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, double *ustream, double *out, char *smem)
+{
+    constexpr int R = G2_D + 1;
+    const int j = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(j >> 6), lane = j & 63;
+    const int NW = blockDim.x >> 6, nx = a.nx, ny = a.ny, NYP = a.NYP, V = a.V;
+    const int SB = g2_slot_bytes(NC, NYP), NP = ((NC + 1) * NYP * 8 + 1023) / 1024;
+    double *bnd = reinterpret_cast<double *>(smem);  // [2][16]: each wave's lane 63 of the previous level
+    char *ring = smem + 256;
+    const unsigned lds0 = (unsigned)(uintptr_t)ring;
+    const long lvl = (long)(NC + 1) * NYP * 8;  // stream bytes per level
+    auto issue = [&](int v) {  // level v's pieces into slot v mod R; past V - 1: dummies (fixed counts)
+        const char *src = reinterpret_cast<const char *>(st) + (long)min(v, V - 1) * lvl;
+        const unsigned dst = lds0 + (unsigned)((v % R) * SB);
+#pragma unroll
+        for (int k = 0; k < G2_KP; k++) {
+            const int p = wave + k * NW, pp = p < NP ? p : 0;
+            dma16(src + pp * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(dst + pp * 1024));
+        }
+    };
+    // every level: 3 DMAs then 1 store per wave, so before level v's compute its
+    // pieces have 3 (G2_D - 1) + v (v < G2_D) or 4 (G2_D - 1) + 1 younger operations
+    static_assert(G2_D == 6, "the wait counts below");
+    auto wait_level = [&](int v) {
+        switch (v) {
+        case 0: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
+        }
+    };
+    constexpr int OOB = 0x40000000;
+    const __amdgpu_buffer_rsrc_t ro = ustream
+        ? __builtin_amdgcn_make_buffer_rsrc(ustream, 0, 0x7fffffff, 0x00020000)
+        : __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)min(a.n * 8, 0x7fffffffL), 0x00020000);
+    if (j < 32) bnd[j] = 0.0;  // (ordered before their first reader by level 0's barrier)
+    for (int v = 0; v < G2_D; v++) issue(v);
+    double xp = 0.0, sp = 0.0;  // the lane's x(v-1); lane j-1's x(v-2) (S)
+    for (int v = 0; v < V; v++) {
+        wait_level(v);
+        line_barrier();  // level v's pieces of every wave landed; level v-1's boundary words written; slot v-1 free
+        issue(v + G2_D);
+        const double *sl = reinterpret_cast<const double *>(ring + (v % R) * SB);
+        const double cS = sl[j], cSE = sl[NYP + j], cW = sl[2 * NYP + j], rh = sl[NC * NYP + j];
+        const double bprev = wave > 0 ? bnd[((v - 1) & 1) * 16 + wave - 1] : 0.0;
+        const double se = dpp_shr1(xp, bprev);  // lane j-1's x(v-1) (lane 0: the previous wave's lane 63)
+        // the reference's order: S (r - nx), SE (r - nx + 1), W (r - 1)
+        double x = rh - cS * sp;
+        x = x - cSE * se;
+        x = x - cW * xp;
+        if constexpr (NC == 4) x = x / sl[3 * NYP + j];
+        const int i = v - 2 * j;
+        const bool ok = j < ny && (unsigned)i < (unsigned)nx;
+        x = ok ? x : 0.0;  // rows off the grid hold +0.0
+        sp = se;
+        xp = x;
+        if (lane == 63) bnd[(v & 1) * 16 + wave] = x;
+        // one store per wave and level (off-grid lanes dropped): the U stream's rhs
+        // slot of its level V-1-v, lane ny-1-j (the mirror row), or the output
+        int vo;
+        if (ustream) vo = ok ? (int)((((long)(V - 1 - v) * (a.ncu + 1) + a.ncu) * NYP + (ny - 1 - j)) * 8) : OOB;
+        else {
+            const long r = (long)j * nx + i;
+            vo = ok ? (int)((mirror ? a.n - 1 - r : r) * 8) : OOB;
+        }
+        __builtin_amdgcn_raw_buffer_store_b64(split64((uint64_t)__double_as_longlong(x)), ro, vo, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int NCL>
+__global__ __launch_bounds__(G2_MAXNY) void k_lineg(G2Args a)
+{
+    if (a.guard && *a.guard != 0.0) return;  // a batched iteration past the stop (lssp_amd_ctx::guard)
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if (a.mode != 2) lineg_sweep<NCL>(a, a.sL, false, a.mode == 0 ? a.sU : nullptr, a.out, smem);
+    if (a.mode == 0) {
+        // the U stream's rhs slots were written by this workgroup: drained above
+        // (vmcnt 0); the workgroup fence and barrier order them before its DMAs
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __syncthreads();
+    }
+    if (a.mode != 1) lineg_sweep<4>(a, a.sU, true, nullptr, a.out, smem);
+}
+
+// the first sweep's rhs into its stream's rhs slots (level-major, lane = line)
+__global__ __launch_bounds__(256) void k_lineg_rhs(double *st, int NC, int V, int NYP, int nx, int ny, long n, int mirror,
+                                                   const double *__restrict__ rhs, const double *guard)
+{
+    if (guard && *guard != 0.0) return;
+    const long t = (long)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (long)V * NYP) return;
+    const int v = (int)(t / NYP), j = (int)(t % NYP), i = v - 2 * j;
+    if (j >= ny || i < 0 || i >= nx) return;
+    const long r = (long)j * nx + i;
+    st[((long)v * (NC + 1) + NC) * NYP + j] = rhs[mirror ? n - 1 - r : r];
+}
+
+static int launch_lineg(lssp_amd_ctx *c, const LineILU &li, int mode, double *x, const double *rhs)
+{
+    const LineGeom &g = li.g;
+    const long n = (long)g.nx * g.ny;
+    const int NYP = li.g2NYP, V = li.g2V;
+    // the first sweep's rhs
+    double *st0 = mode == 2 ? li.d_g2U : li.d_g2L;
+    const int nc0 = mode == 2 ? li.g2NCU : li.g2NCL;
+    const long nt = (long)V * NYP;
+    k_lineg_rhs<<<(nt + 255) / 256, 256, 0, c->stream>>>(st0, nc0, V, NYP, g.nx, g.ny, n, mode == 2, rhs, c->guard);
+    LSSP_HIP(hipGetLastError());
+    G2Args a{g.nx, g.ny, NYP, V, n, li.d_g2L, li.d_g2U, li.g2NCL, li.g2NCU, mode, x, c->guard};
+    const int lds = 256 + (G2_D + 1) * g2_slot_bytes(4, NYP);
+    auto kern = li.g2NCL == 4 ? k_lineg<4> : k_lineg<3>;
+    static bool attr[2] = {false, false};
+    if (!attr[li.g2NCL == 4]) {
+        LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     256 + (G2_D + 1) * g2_slot_bytes(4, G2_MAXNY)));
+        attr[li.g2NCL == 4] = true;
+    }
+    kern<<<1, NYP, lds, c->stream>>>(a);
+    LSSP_HIP(hipGetLastError());
+    return LSSP_AMD_OK;
+}
+
 namespace {
 #ifndef LINEF_D
 #define LINEF_D 6  // loader lead (steps of two levels)
@@ -937,6 +1139,7 @@ int linef_sweep(lssp_amd_ctx *c, const LineILU &li, int which, const double *str
 
 int launch_linefill_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs)
 {
+    if (li.g2) return launch_lineg(c, li, 0, x, rhs);
     LSSP_TRY(linef_gather(c, li.L, 0, rhs, li.d_lstream));
     LSSP_TRY(linef_sweep(c, li, 0, li.d_lstream, li.d_ustream, 2));
     return linef_sweep(c, li, 1, li.d_ustream, x, 1);
@@ -956,6 +1159,7 @@ int launch_linefill_apply_tail(lssp_amd_ctx *c, const LineILU &li, double *x, co
 
 int launch_linefill_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs)
 {
+    if (li.g2) return launch_lineg(c, li, which ? 2 : 1, x, rhs);
     double *st = which ? li.d_ustream : li.d_lstream;
     LSSP_TRY(linef_gather(c, which ? li.U : li.L, which, rhs, st));
     return linef_sweep(c, li, which, st, x, 1);

@@ -424,6 +424,10 @@ void free_line_sweep(LineILU &li)
     if (li.d_lstream) (void)hipFree(li.d_lstream);
     if (li.d_hk) (void)hipFree(li.d_hk);
     if (li.d_hj) (void)hipFree(li.d_hj);
+    if (li.d_g2L) (void)hipFree(li.d_g2L);
+    if (li.d_g2U) (void)hipFree(li.d_g2U);
+    li.d_g2L = li.d_g2U = nullptr;
+    li.g2 = 0;
     if (li.d_kdone) (void)hipFree(li.d_kdone);
     if (li.d_kof) (void)hipFree(li.d_kof);
     if (li.d_tclaim) (void)hipFree(li.d_tclaim);

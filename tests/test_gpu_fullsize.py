@@ -144,7 +144,7 @@ def test_ilu1_line_sweeps_128_and_exam_matrix_bitwise():
             Ap, Aj, Ax = lssp_amd.poisson(dim, N)
             n = Ap.size - 1
             M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=1)
-            assert M.sweep_layout() == (2, 16, 8)
+            assert M.sweep_layout() == ((2, 16, 8) if dim == 3 else (2, N, 1))  # 2-D: one workgroup (k_lineg)
             if dim == 3:
                 assert M.levelsL == 6 * N - 5
             L, U = O.ilu(O.CSR(n, Ap, Aj, Ax), "iluk", level=1)

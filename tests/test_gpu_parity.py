@@ -262,7 +262,8 @@ def test_line_sweep_ilu1_bitwise_vs_oracle(dev, nx, ny, nz):
     Ap, Aj, Ax = _box7(nx, ny, nz, 7 * nx + ny + nz)
     n = Ap.size - 1
     M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=1, level=1)
-    assert M.sweep_layout() == (2, 16, 8)
+    # 2-D grids of <= 256 lines: one workgroup, lines on lanes (k_lineg); else skewed tiles
+    assert M.sweep_layout() == ((2, ny, 1) if nz == 1 else (2, 16, 8))
     L, U = O.ilu(O.CSR(n, Ap, Aj, Ax), "iluk", level=1)
     (Lp, Lj, Lx), (Up, Uj, Ux) = M.factors()
     assert np.array_equal(Lj, L.Aj) and np.array_equal(Lx, L.Ax) and np.array_equal(Ux, U.Ax)
@@ -282,6 +283,45 @@ def test_line_sweep_ilu1_bitwise_vs_oracle(dev, nx, ny, nz):
     y = dev.vec(n, rhs)
     M.apply(y, y)
     assert np.array_equal(y.download(), O.ilu_apply(L, U, rhs))
+
+
+# The one-workgroup 2-D ILU(1) sweeps (linefill.hip k_lineg) and the skewed
+# tiles on the same 2-D grids (LSSP_AMD_LINEG=0): 1 to 4 waves of lines (a wave
+# with one line, the 256-line maximum), nx = 3, repeated applies, both single
+# sweeps, in-place; both equal to the oracle bit for bit.
+@pytest.mark.parametrize("nx,ny", [(3, 3), (30, 27), (100, 100), (9, 65), (5, 200), (7, 256), (64, 1 + 64 * 3)])
+@pytest.mark.parametrize("lineg", ["1", "0"], ids=["one-workgroup", "skewed-tiles"])
+def test_line_sweep_ilu1_2d_both_paths_bitwise_vs_oracle(dev, nx, ny, lineg):
+    import lssp_amd
+    Ap, Aj, Ax = _box7(nx, ny, 1, 5 * nx + ny)
+    n = Ap.size - 1
+    old = os.environ.get("LSSP_AMD_LINEG")
+    os.environ["LSSP_AMD_LINEG"] = lineg
+    try:
+        M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=1, level=1)
+    finally:
+        if old is None:
+            os.environ.pop("LSSP_AMD_LINEG", None)
+        else:
+            os.environ["LSSP_AMD_LINEG"] = old
+    assert M.sweep_layout() == ((2, ny, 1) if lineg == "1" else (2, 16, 8))
+    L, U = O.ilu(O.CSR(n, Ap, Aj, Ax), "iluk", level=1)
+    x = dev.vec(n)
+    for rep in range(3):
+        rhs = uniform(600 + rep, n)
+        M.apply(x, dev.vec(n, rhs))
+        assert np.array_equal(x.download(), O.ilu_apply(L, U, rhs)), rep
+    one = O.CSR(n, np.arange(n + 1, dtype=np.int32), np.arange(n, dtype=np.int32), np.ones(n))
+    rhs = uniform(700, n)
+    z = dev.vec(n)
+    M.trisolve(0, z, dev.vec(n, rhs))
+    assert np.array_equal(z.download(), O.ilu_apply(L, one, rhs))
+    M.trisolve(1, z, dev.vec(n, rhs))
+    assert np.array_equal(z.download(), O.ilu_apply(one, U, rhs))
+    y = dev.vec(n, rhs)
+    M.apply(y, y)
+    assert np.array_equal(y.download(), O.ilu_apply(L, U, rhs))
+    M.close()
 
 
 @pytest.mark.parametrize("seed,n,per_row,missing,blk", [(11, 3000, 6, 0, 0), (12, 2500, 9, 7, 0),

@@ -216,19 +216,22 @@ def general_ilu(args):
     dev = lssp_amd.Device(0)
     cases = []
 
-    def case(name, Ap, Aj, Ax, level, line, ref_iters=0):
+    def case(name, Ap, Aj, Ax, level, line, ref_iters=0, env=None):
         n, nnz = Ap.size - 1, int(Ap[-1])
         log(f"{name}: setup")
-        old = os.environ.get("LSSP_AMD_LINE")
+        env = dict(env or {})
         if not line:
-            os.environ["LSSP_AMD_LINE"] = "0"
+            env["LSSP_AMD_LINE"] = "0"
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
         t0 = time.perf_counter()
         M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=level)
         t_pc = time.perf_counter() - t0
-        if old is None:
-            os.environ.pop("LSSP_AMD_LINE", None)
-        else:
-            os.environ["LSSP_AMD_LINE"] = old
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         A = lssp_amd.DMat(dev, Ap, Aj, Ax)
         out = {"case": name, "rows": n, "nnz": nnz, "ilu": {"level": level, "nnzL": M.nnzL, "nnzU": M.nnzU,
                                                             "setup_s": round(t_pc, 2),
@@ -253,7 +256,9 @@ def general_ilu(args):
     case("7-pt 128^3 ILU(1), line sweeps", Ap, Aj, Ax, 1, True)
     case("7-pt 128^3 ILU(1), packet sweeps", Ap, Aj, Ax, 1, False)
     Ap, Aj, Ax = lssp_amd.poisson(2, 100)
-    case("5-pt 100^2 ILU(1) (exam.cxx's matrix), line sweeps", Ap, Aj, Ax, 1, True)
+    case("5-pt 100^2 ILU(1) (exam.cxx's matrix), one-workgroup line sweeps", Ap, Aj, Ax, 1, True)
+    case("5-pt 100^2 ILU(1) (exam.cxx's matrix), skewed-tile line sweeps", Ap, Aj, Ax, 1, True,
+         env={"LSSP_AMD_LINEG": "0"})
     case("5-pt 100^2 ILU(1) (exam.cxx's matrix), packet sweeps", Ap, Aj, Ax, 1, False)
     Ap, Aj, Ax = lssp_amd.poisson(3, args.grid)
     case(f"7-pt {args.grid}^3 ILU(0), packet sweeps", Ap, Aj, Ax, 0, False)
