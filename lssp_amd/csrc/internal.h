@@ -228,7 +228,7 @@ struct LineILU {
     mutable unsigned kepoch = 0;
     // kind 1 on a small 2-D grid (linefill.hip k_lineg): ONE workgroup, lines on
     // lanes; level-major streams [level][S, SE, W(, diag), rhs][lane] per sweep
-    int g2 = 0, g2V = 0, g2NYP = 0, g2NCL = 0, g2NCU = 0;
+    int g2 = 0, g2fill = 0, g2V = 0, g2NYP = 0, g2NCL = 0, g2NCU = 0;
     double *d_g2L = nullptr, *d_g2U = nullptr;
 };
 
@@ -388,7 +388,13 @@ int build_linefill(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std
                    const std::vector<double> &Lx, const std::vector<int> &Up, const std::vector<int> &Uj,
                    const std::vector<double> &Ux, LineILU &li);
 int launch_linefill_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs);
-struct LineTail;  // linesweep_dev.h
+struct LineTail;
+// small 2-D grids on one workgroup (linefill.hip): cl / cu hold the L / U rows in
+// sweep order, components S, (SE,) W (, diag); mode 0 apply, 1 L, 2 U
+int build_lineg(lssp_amd_ctx *c, const LineGeom &g, int fill, int ncl, const std::vector<double> &cl,
+                const std::vector<double> &cu, LineILU &li);
+int launch_lineg(lssp_amd_ctx *c, const LineILU &li, int mode, double *x, const double *rhs);
+constexpr int G2_MAXNY = 256;  // k_lineg: lines (lanes) of one workgroup  // linesweep_dev.h
 int launch_linefill_apply_tail(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs, const LineTail &T,
                                long *tail_waves);
 int launch_linefill_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs);

@@ -90,7 +90,6 @@ template <int NA, int OUT, int D>
 constexpr int lds_bytes() { return (D + 1) * Slot<NA>::BYTES + rsl<OUT>() * ROWS * 8 + 16 + 512; }
 constexpr int waves(int NL, int SW) { return 2 + NL + 1 + SW; }
 }  // namespace lf
-constexpr int G2_MAXNY = 256;  // k_lineg: lines (lanes) of one workgroup
 constexpr int G2_D = 6;        // k_lineg: levels of DMA lead (ring of G2_D + 1 slots)
 
 // ---------------------------------------------------------------------------
@@ -280,48 +279,50 @@ int fill_upload(lssp_amd_ctx *c, const LineGeom &g, const std::vector<LineTile> 
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// 2-D grids (the 5-point ILU(1) pattern, nz = 1; exam.cxx's 100 x 100) with at
-// most G2_MAXNY lines: ONE workgroup sweeps the whole grid, lane j = line j, one
-// level v = i + 2 j per step (row i = v - 2 j).  Per level the operands are the
-// lane's own x(v-1) (W), lane j-1's x(v-1) (SE: DPP wave_shr:1, or the previous
-// wave's lane 63 through LDS) and lane j-1's x(v-2) (S: the lane's SE of the
-// previous level), so a level is one shift, three multiply-subtracts (+ U's
-// division) and, with more than one wave, one LDS word and one barrier -- no
-// hand-offs between CUs.  The skewed tiles put one plane per tile on 16 of 128
-// lanes and chain W tiles through cross-CU hand-offs for the same levels.
-// Streams, level-major: [v][S, SE, W (, diag), rhs][lane] (rows off the grid
-// +0.0), the coefficients at build, the rhs per apply (k_lineg_rhs gathers the
-// first sweep's; the L sweep writes the U sweep's); each wave LDS-DMAs its
-// pieces G2_D levels ahead into a ring.
+// 2-D grids (5-point ILU(0), and the 5-point ILU(1) pattern, nz = 1; exam.cxx's
+// matrices) with at most G2_MAXNY lines: ONE workgroup sweeps the whole grid,
+// lane j = line j, one level per step -- v = i + j (ILU(0)) or i + 2 j (ILU(1)),
+// row i = v - j or v - 2 j.  Per level the operands are the lane's own x(v-1)
+// (W), lane j-1's x(v-1) (ILU(0): S; ILU(1): SE -- DPP wave_shr:1, or the
+// previous wave's lane 63 through LDS) and, for ILU(1), lane j-1's x(v-2) (S:
+// the lane's SE of the previous level), so a level is one shift, two or three
+// multiply-subtracts (+ U's division) and, with more than one wave, one LDS
+// word and one barrier -- no hand-offs between CUs.  The tiled sweeps put one
+// plane per tile on 16 of 128 lanes and chain the tiles of a 2-D grid through
+// cross-CU hand-offs for the same levels.  Streams, level-major: [v][S, (SE,)
+// W, (diag,) rhs][lane] (rows off the grid +0.0), the coefficients at build,
+// the rhs per apply (k_lineg_rhs gathers the first sweep's; the L sweep writes
+// the U sweep's); each wave LDS-DMAs its pieces G2_D levels ahead into a ring.
 // ---------------------------------------------------------------------------
-static int build_lineg(lssp_amd_ctx *c, const LineGeom &g, const FillCoef &cl, const FillCoef &cu, LineILU &li)
+int build_lineg(lssp_amd_ctx *c, const LineGeom &g, int fill, int ncl, const std::vector<double> &cl,
+                const std::vector<double> &cu, LineILU &li)
 {
-    const int nx = g.nx, ny = g.ny, NYP = (ny + 63) / 64 * 64, V = nx + 2 * (ny - 1);
-    const int NCL = cl.NA == 7 ? 4 : 3, NCU = 4;
-    auto make = [&](const FillCoef &src, int NC) {
+    const int nx = g.nx, ny = g.ny, NYP = (ny + 63) / 64 * 64, sk = fill ? 2 : 1, V = nx + sk * (ny - 1);
+    const int ncu = fill ? 4 : 3;
+    auto make = [&](const std::vector<double> &src, int NC) {
         std::vector<double> st((size_t)V * (NC + 1) * NYP + 128, 0.0);  // (+1 KB: whole DMA pieces)
         for (int v = 0; v < V; v++)
             for (int j = 0; j < ny; j++) {
-                const int i = v - 2 * j;
+                const int i = v - sk * j;
                 if (i < 0 || i >= nx) continue;
-                const double *cr = src.c.data() + ((size_t)j * nx + i) * src.NA;  // (sweep order: U mirrored)
-                for (int k = 0; k < 3; k++) st[((size_t)v * (NC + 1) + k) * NYP + j] = cr[3 + k];  // S, SE, W
-                if (NC == 4) st[((size_t)v * (NC + 1) + 3) * NYP + j] = cr[6];
+                const double *cr = src.data() + ((size_t)j * nx + i) * NC;  // (sweep order: U mirrored)
+                for (int k = 0; k < NC; k++) st[((size_t)v * (NC + 1) + k) * NYP + j] = cr[k];
             }
         return st;
     };
-    const std::vector<double> sl = make(cl, NCL), su = make(cu, NCU);
+    const std::vector<double> sl = make(cl, ncl), su = make(cu, ncu);
     LSSP_HIP(hipMalloc(&li.d_g2L, sizeof(double) * sl.size()));
     LSSP_HIP(hipMemcpy(li.d_g2L, sl.data(), sizeof(double) * sl.size(), hipMemcpyHostToDevice));
     LSSP_HIP(hipMalloc(&li.d_g2U, sizeof(double) * su.size()));
     LSSP_HIP(hipMemcpy(li.d_g2U, su.data(), sizeof(double) * su.size(), hipMemcpyHostToDevice));
     li.g = g;
-    li.kind = 1;
+    li.kind = fill;
     li.g2 = 1;
+    li.g2fill = fill;
     li.g2V = V;
     li.g2NYP = NYP;
-    li.g2NCL = NCL;
-    li.g2NCU = NCU;
+    li.g2NCL = ncl;
+    li.g2NCU = ncu;
     li.P = 1;
     li.NJ = ny;
     li.LV = 1;
@@ -341,10 +342,17 @@ int build_linefill(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std
         const char *e = getenv("LSSP_AMD_LINEG");  // (read per build: tests select either path)
         if (g.nz == 1 && g.ny <= G2_MAXNY && !(e && !atoi(e))) {
             const long pl = (long)g.nx * g.ny;
-            FillCoef cl, cu;
-            cl.build(Lp, Lj, Lx, false, n, g.nx, pl, g.unitL ? 6 : 7);
-            cu.build(Up, Uj, Ux, true, n, g.nx, pl, 7);
-            return build_lineg(c, g, cl, cu, li);
+            FillCoef fl, fu;
+            fl.build(Lp, Lj, Lx, false, n, g.nx, pl, g.unitL ? 6 : 7);
+            fu.build(Up, Uj, Ux, true, n, g.nx, pl, 7);
+            // k_lineg's components: S, SE, W (, diag) = FillCoef's 3, 4, 5 (, 6)
+            const int ncl = g.unitL ? 3 : 4;
+            std::vector<double> cl((size_t)n * ncl), cu((size_t)n * 4);
+            for (long r = 0; r < n; r++) {
+                for (int k = 0; k < ncl; k++) cl[r * ncl + k] = fl.c[r * fl.NA + 3 + k];
+                for (int k = 0; k < 4; k++) cu[r * 4 + k] = fu.c[r * fu.NA + 3 + k];
+            }
+            return build_lineg(c, g, 1, ncl, cl, cu, li);
         }
     }
     const int m = g.ny + g.nz - 1;
@@ -932,9 +940,10 @@ struct G2Args {
 constexpr int G2_KP = 3;  // DMA pieces per wave per level (dummies fill up): 4 waves x 3 >= 10 pieces
 __host__ __device__ constexpr int g2_slot_bytes(int NC, int NYP) { return ((NC + 1) * NYP * 8 + 1023) / 1024 * 1024; }
 
-template <int NC>
+template <int FILL, int NC>
 __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, double *ustream, double *out, char *smem)
 {
+    constexpr int SK = FILL ? 2 : 1;  // row i = v - SK j
     constexpr int R = G2_D + 1;
     const int j = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(j >> 6), lane = j & 63;
     const int NW = blockDim.x >> 6, nx = a.nx, ny = a.ny, NYP = a.NYP, V = a.V;
@@ -978,15 +987,23 @@ __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, doub
         line_barrier();  // level v's pieces of every wave landed; level v-1's boundary words written; slot v-1 free
         issue(v + G2_D);
         const double *sl = reinterpret_cast<const double *>(ring + (v % R) * SB);
-        const double cS = sl[j], cSE = sl[NYP + j], cW = sl[2 * NYP + j], rh = sl[NC * NYP + j];
+        const double rh = sl[NC * NYP + j];
         const double bprev = wave > 0 ? bnd[((v - 1) & 1) * 16 + wave - 1] : 0.0;
         const double se = dpp_shr1(xp, bprev);  // lane j-1's x(v-1) (lane 0: the previous wave's lane 63)
-        // the reference's order: S (r - nx), SE (r - nx + 1), W (r - 1)
-        double x = rh - cS * sp;
-        x = x - cSE * se;
-        x = x - cW * xp;
-        if constexpr (NC == 4) x = x / sl[3 * NYP + j];
-        const int i = v - 2 * j;
+        double x;
+        if constexpr (FILL) {
+            // the reference's order: S (r - nx), SE (r - nx + 1), W (r - 1)
+            x = rh - sl[j] * sp;
+            x = x - sl[NYP + j] * se;
+            x = x - sl[2 * NYP + j] * xp;
+            if constexpr (NC == 4) x = x / sl[3 * NYP + j];
+        } else {
+            // S (r - nx) = lane j-1's x(v-1), W (r - 1)
+            x = rh - sl[j] * se;
+            x = x - sl[NYP + j] * xp;
+            if constexpr (NC == 3) x = x / sl[2 * NYP + j];
+        }
+        const int i = v - SK * j;
         const bool ok = j < ny && (unsigned)i < (unsigned)nx;
         x = ok ? x : 0.0;  // rows off the grid hold +0.0
         sp = se;
@@ -1005,35 +1022,35 @@ __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, doub
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int NCL>
+template <int FILL, int NCL>
 __global__ __launch_bounds__(G2_MAXNY) void k_lineg(G2Args a)
 {
     if (a.guard && *a.guard != 0.0) return;  // a batched iteration past the stop (lssp_amd_ctx::guard)
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    if (a.mode != 2) lineg_sweep<NCL>(a, a.sL, false, a.mode == 0 ? a.sU : nullptr, a.out, smem);
+    if (a.mode != 2) lineg_sweep<FILL, NCL>(a, a.sL, false, a.mode == 0 ? a.sU : nullptr, a.out, smem);
     if (a.mode == 0) {
         // the U stream's rhs slots were written by this workgroup: drained above
         // (vmcnt 0); the workgroup fence and barrier order them before its DMAs
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         __syncthreads();
     }
-    if (a.mode != 1) lineg_sweep<4>(a, a.sU, true, nullptr, a.out, smem);
+    if (a.mode != 1) lineg_sweep<FILL, FILL ? 4 : 3>(a, a.sU, true, nullptr, a.out, smem);
 }
 
 // the first sweep's rhs into its stream's rhs slots (level-major, lane = line)
-__global__ __launch_bounds__(256) void k_lineg_rhs(double *st, int NC, int V, int NYP, int nx, int ny, long n, int mirror,
-                                                   const double *__restrict__ rhs, const double *guard)
+__global__ __launch_bounds__(256) void k_lineg_rhs(double *st, int NC, int sk, int V, int NYP, int nx, int ny, long n,
+                                                   int mirror, const double *__restrict__ rhs, const double *guard)
 {
     if (guard && *guard != 0.0) return;
     const long t = (long)blockIdx.x * 256 + threadIdx.x;
     if (t >= (long)V * NYP) return;
-    const int v = (int)(t / NYP), j = (int)(t % NYP), i = v - 2 * j;
+    const int v = (int)(t / NYP), j = (int)(t % NYP), i = v - sk * j;
     if (j >= ny || i < 0 || i >= nx) return;
     const long r = (long)j * nx + i;
     st[((long)v * (NC + 1) + NC) * NYP + j] = rhs[mirror ? n - 1 - r : r];
 }
 
-static int launch_lineg(lssp_amd_ctx *c, const LineILU &li, int mode, double *x, const double *rhs)
+int launch_lineg(lssp_amd_ctx *c, const LineILU &li, int mode, double *x, const double *rhs)
 {
     const LineGeom &g = li.g;
     const long n = (long)g.nx * g.ny;
@@ -1042,16 +1059,19 @@ static int launch_lineg(lssp_amd_ctx *c, const LineILU &li, int mode, double *x,
     double *st0 = mode == 2 ? li.d_g2U : li.d_g2L;
     const int nc0 = mode == 2 ? li.g2NCU : li.g2NCL;
     const long nt = (long)V * NYP;
-    k_lineg_rhs<<<(nt + 255) / 256, 256, 0, c->stream>>>(st0, nc0, V, NYP, g.nx, g.ny, n, mode == 2, rhs, c->guard);
+    k_lineg_rhs<<<(nt + 255) / 256, 256, 0, c->stream>>>(st0, nc0, li.g2fill ? 2 : 1, V, NYP, g.nx, g.ny, n, mode == 2,
+                                                         rhs, c->guard);
     LSSP_HIP(hipGetLastError());
     G2Args a{g.nx, g.ny, NYP, V, n, li.d_g2L, li.d_g2U, li.g2NCL, li.g2NCU, mode, x, c->guard};
     const int lds = 256 + (G2_D + 1) * g2_slot_bytes(4, NYP);
-    auto kern = li.g2NCL == 4 ? k_lineg<4> : k_lineg<3>;
-    static bool attr[2] = {false, false};
-    if (!attr[li.g2NCL == 4]) {
+    // (ILU(1): L 3 or 4 components, U 4; ILU(0): L 2 or 3, U 3)
+    const int kv = li.g2fill * 2 + (li.g2NCL == (li.g2fill ? 4 : 3));
+    auto kern = kv == 3 ? k_lineg<1, 4> : kv == 2 ? k_lineg<1, 3> : kv == 1 ? k_lineg<0, 3> : k_lineg<0, 2>;
+    static bool attr[4] = {false, false, false, false};
+    if (!attr[kv]) {
         LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      256 + (G2_D + 1) * g2_slot_bytes(4, G2_MAXNY)));
-        attr[li.g2NCL == 4] = true;
+        attr[kv] = true;
     }
     kern<<<1, NYP, lds, c->stream>>>(a);
     LSSP_HIP(hipGetLastError());

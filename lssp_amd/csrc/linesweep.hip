@@ -335,6 +335,25 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
     if (env && !atoi(env)) return LSSP_AMD_EUNSUPPORTED;
     LineGeom g;
     if (!detect_grid(n, Lp, Lj, Lx, Up, Uj, g)) return build_linefill(c, n, Lp, Lj, Lx, Up, Uj, Ux, li);
+    {
+        // a small 2-D grid (exam.cxx's 5-point Poisson): one workgroup, lines on
+        // lanes (linefill.hip k_lineg); LSSP_AMD_LINEG=0 keeps the tiles
+        const char *e = getenv("LSSP_AMD_LINEG");
+        if (g.nz == 1 && g.ny <= G2_MAXNY && !(e && !atoi(e))) {
+            const long plane = (long)g.nx * g.ny;
+            const int ncl = g.unitL ? 2 : 3;
+            CoefSrc sl, su;
+            sl.build(Lp, Lj, Lx, false, n, g.nx, plane, g.unitL ? 3 : 4);
+            su.build(Up, Uj, Ux, true, n, g.nx, plane, 4);
+            // k_lineg's components: S, W (, diag) = CoefSrc's 1, 2 (, 3)
+            std::vector<double> cl((size_t)n * ncl), cu((size_t)n * 3);
+            for (long r = 0; r < n; r++) {
+                for (int k = 0; k < ncl; k++) cl[r * ncl + k] = sl.get(r, 1 + k);
+                for (int k = 0; k < 3; k++) cu[r * 3 + k] = su.get(r, 1 + k);
+            }
+            return build_lineg(c, g, 0, ncl, cl, cu, li);
+        }
+    }
     int P, NJ, LV;
     line_plan(g, P, NJ, LV);
     const int W = (g.ny + NJ - 1) / NJ;
@@ -1809,6 +1828,7 @@ static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const doub
 
 int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs)
 {
+    if (li.g2) return launch_lineg(c, li, 0, x, rhs);
     if (li.kind == 1) return launch_linefill_apply(c, li, x, rhs);
     if (li.LV >= 2) {  // k_line2: gather, L sweep -> the U rhs stream, U sweep -> x
         LSSP_TRY(launch_line_gather(c, li.L, 0, rhs, li.d_lstream));

@@ -285,27 +285,31 @@ def test_line_sweep_ilu1_bitwise_vs_oracle(dev, nx, ny, nz):
     assert np.array_equal(y.download(), O.ilu_apply(L, U, rhs))
 
 
-# The one-workgroup 2-D ILU(1) sweeps (linefill.hip k_lineg) and the skewed
-# tiles on the same 2-D grids (LSSP_AMD_LINEG=0): 1 to 4 waves of lines (a wave
-# with one line, the 256-line maximum), nx = 3, repeated applies, both single
-# sweeps, in-place; both equal to the oracle bit for bit.
+# The one-workgroup 2-D sweeps (linefill.hip k_lineg: ILU(0) of a 5-point grid,
+# exam.cxx's configuration, and its ILU(1) pattern) and the tiled sweeps on the
+# same 2-D grids (LSSP_AMD_LINEG=0): 1 to 4 waves of lines (a wave with one line,
+# the 256-line maximum), nx = 3, repeated applies, both single sweeps, in-place;
+# both equal to the oracle bit for bit.
 @pytest.mark.parametrize("nx,ny", [(3, 3), (30, 27), (100, 100), (9, 65), (5, 200), (7, 256), (64, 1 + 64 * 3)])
-@pytest.mark.parametrize("lineg", ["1", "0"], ids=["one-workgroup", "skewed-tiles"])
-def test_line_sweep_ilu1_2d_both_paths_bitwise_vs_oracle(dev, nx, ny, lineg):
+@pytest.mark.parametrize("lineg", ["1", "0"], ids=["one-workgroup", "tiles"])
+@pytest.mark.parametrize("level", [0, 1], ids=["ilu0", "ilu1"])
+def test_line_sweep_2d_both_paths_bitwise_vs_oracle(dev, nx, ny, lineg, level):
     import lssp_amd
+    if level == 0 and ny < 8:
+        pytest.skip("not a line-sweep grid for ILU(0) (detect_grid: ny >= 8)")
     Ap, Aj, Ax = _box7(nx, ny, 1, 5 * nx + ny)
     n = Ap.size - 1
     old = os.environ.get("LSSP_AMD_LINEG")
     os.environ["LSSP_AMD_LINEG"] = lineg
     try:
-        M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=1, level=1)
+        M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=1, level=level)
     finally:
         if old is None:
             os.environ.pop("LSSP_AMD_LINEG", None)
         else:
             os.environ["LSSP_AMD_LINEG"] = old
-    assert M.sweep_layout() == ((2, ny, 1) if lineg == "1" else (2, 16, 8))
-    L, U = O.ilu(O.CSR(n, Ap, Aj, Ax), "iluk", level=1)
+    assert M.sweep_layout() == ((1 + level, ny, 1) if lineg == "1" else (1 + level, 16, 8))
+    L, U = O.ilu(O.CSR(n, Ap, Aj, Ax), "iluk", level=level)
     x = dev.vec(n)
     for rep in range(3):
         rhs = uniform(600 + rep, n)
