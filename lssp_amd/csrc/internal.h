@@ -394,7 +394,14 @@ struct LineTail;
 int build_lineg(lssp_amd_ctx *c, const LineGeom &g, int fill, int ncl, const std::vector<double> &cl,
                 const std::vector<double> &cu, LineILU &li);
 int launch_lineg(lssp_amd_ctx *c, const LineILU &li, int mode, double *x, const double *rhs);
-constexpr int G2_MAXNY = 256;  // k_lineg: lines (lanes) of one workgroup  // linesweep_dev.h
+constexpr int G2_MAXNY = 256;  // k_lineg: lines (lanes) of one workgroup
+// k_lineg addresses its streams and output through buffer resources: every
+// byte offset (and the dropped-store offset 2^30) within 32 bits
+inline bool lineg_fits(const LineGeom &g, int fill)
+{
+    const long nyp = (g.ny + 63) / 64 * 64, V = g.nx + (fill ? 2L : 1L) * (g.ny - 1);
+    return (long)g.nx * g.ny * 8 < (1L << 30) && V * 5 * nyp * 8 + 1024 < (1L << 30);
+}  // linesweep_dev.h
 int launch_linefill_apply_tail(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs, const LineTail &T,
                                long *tail_waves);
 int launch_linefill_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs);

@@ -340,7 +340,7 @@ int build_linefill(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std
     if (!detect_fill1(n, Lp, Lj, Lx, Up, Uj, g)) return LSSP_AMD_EUNSUPPORTED;
     {
         const char *e = getenv("LSSP_AMD_LINEG");  // (read per build: tests select either path)
-        if (g.nz == 1 && g.ny <= G2_MAXNY && !(e && !atoi(e))) {
+        if (g.nz == 1 && g.ny <= G2_MAXNY && lineg_fits(g, 1) && !(e && !atoi(e))) {
             const long pl = (long)g.nx * g.ny;
             FillCoef fl, fu;
             fl.build(Lp, Lj, Lx, false, n, g.nx, pl, g.unitL ? 6 : 7);
@@ -976,9 +976,10 @@ __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, doub
         }
     };
     constexpr int OOB = 0x40000000;
+    // (num_records bound every store: the off-grid lanes' offset OOB lies past them)
     const __amdgpu_buffer_rsrc_t ro = ustream
-        ? __builtin_amdgcn_make_buffer_rsrc(ustream, 0, 0x7fffffff, 0x00020000)
-        : __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)min(a.n * 8, 0x7fffffffL), 0x00020000);
+        ? __builtin_amdgcn_make_buffer_rsrc(ustream, 0, (int)((long)a.V * (a.ncu + 1) * NYP * 8), 0x00020000)
+        : __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(a.n * 8), 0x00020000);
     if (j < 32) bnd[j] = 0.0;  // (ordered before their first reader by level 0's barrier)
     for (int v = 0; v < G2_D; v++) issue(v);
     double xp = 0.0, sp = 0.0;  // the lane's x(v-1); lane j-1's x(v-2) (S)

@@ -339,7 +339,7 @@ int build_line_sweep(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const s
         // a small 2-D grid (exam.cxx's 5-point Poisson): one workgroup, lines on
         // lanes (linefill.hip k_lineg); LSSP_AMD_LINEG=0 keeps the tiles
         const char *e = getenv("LSSP_AMD_LINEG");
-        if (g.nz == 1 && g.ny <= G2_MAXNY && !(e && !atoi(e))) {
+        if (g.nz == 1 && g.ny <= G2_MAXNY && lineg_fits(g, 0) && !(e && !atoi(e))) {
             const long plane = (long)g.nx * g.ny;
             const int ncl = g.unitL ? 2 : 3;
             CoefSrc sl, su;
