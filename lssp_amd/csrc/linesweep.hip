@@ -1947,6 +1947,7 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
 
 int launch_line_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs)
 {
+    if (li.g2) return launch_lineg(c, li, which ? 2 : 1, x, rhs);
     if (li.kind == 1) return launch_linefill_sweep(c, li, which, x, rhs);
     if (li.LV >= 2) {  // one sweep: its rhs gathered into its own stream, natural-order output
         double *st = which ? li.d_ustream : li.d_lstream;
