@@ -90,7 +90,8 @@ template <int NA, int OUT, int D>
 constexpr int lds_bytes() { return (D + 1) * Slot<NA>::BYTES + rsl<OUT>() * ROWS * 8 + 16 + 512; }
 constexpr int waves(int NL, int SW) { return 2 + NL + 1 + SW; }
 }  // namespace lf
-constexpr int G2_D = 6;        // k_lineg: levels of DMA lead (ring of G2_D + 1 slots)
+constexpr int G2_D = 16;       // k_lineg: levels of DMA lead (ring of D + 1 slots), up to 192 lines
+constexpr int G2_DW = 14;      // ... for 193 - 256 lines (15 slots of 10 KB)
 
 // ---------------------------------------------------------------------------
 // host: detection, tiles, streams
@@ -940,11 +941,11 @@ struct G2Args {
 constexpr int G2_KP = 3;  // DMA pieces per wave per level (dummies fill up): 4 waves x 3 >= 10 pieces
 __host__ __device__ constexpr int g2_slot_bytes(int NC, int NYP) { return ((NC + 1) * NYP * 8 + 1023) / 1024 * 1024; }
 
-template <int FILL, int NC>
+template <int FILL, int NC, int D>
 __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, double *ustream, double *out, char *smem)
 {
     constexpr int SK = FILL ? 2 : 1;  // row i = v - SK j
-    constexpr int R = G2_D + 1;
+    constexpr int R = D + 1;
     const int j = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(j >> 6), lane = j & 63;
     const int NW = blockDim.x >> 6, nx = a.nx, ny = a.ny, NYP = a.NYP, V = a.V;
     const int SB = g2_slot_bytes(NC, NYP), NP = ((NC + 1) * NYP * 8 + 1023) / 1024;
@@ -961,32 +962,27 @@ __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, doub
             dma16(src + pp * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(dst + pp * 1024));
         }
     };
-    // every level: 3 DMAs then 1 store per wave, so before level v's compute its
-    // pieces have 3 (G2_D - 1) + v (v < G2_D) or 4 (G2_D - 1) + 1 younger operations
-    static_assert(G2_D == 6, "the wait counts below");
-    auto wait_level = [&](int v) {
-        switch (v) {
-        case 0: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
-        case 5: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
-        }
-    };
+    // the wave's vector-memory queue holds, per level, its G2_KP DMAs of level
+    // v + D and then one store of level v (the prologue's levels a dropped
+    // store each), so at level v's wait its pieces have exactly
+    // 1 + (G2_KP + 1)(D - 1) younger operations: one wait count for every level
+    constexpr int WAITN = 1 + (G2_KP + 1) * (D - 1);
+    static_assert(WAITN <= 63, "gfx9 vmcnt");
     constexpr int OOB = 0x40000000;
     // (num_records bound every store: the off-grid lanes' offset OOB lies past them)
     const __amdgpu_buffer_rsrc_t ro = ustream
         ? __builtin_amdgcn_make_buffer_rsrc(ustream, 0, (int)((long)a.V * (a.ncu + 1) * NYP * 8), 0x00020000)
         : __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(a.n * 8), 0x00020000);
     if (j < 32) bnd[j] = 0.0;  // (ordered before their first reader by level 0's barrier)
-    for (int v = 0; v < G2_D; v++) issue(v);
+    for (int v = 0; v < D; v++) {
+        issue(v);
+        __builtin_amdgcn_raw_buffer_store_b64(split64(0), ro, OOB, 0, 0);  // (dropped: keeps the counts)
+    }
     double xp = 0.0, sp = 0.0;  // the lane's x(v-1); lane j-1's x(v-2) (S)
     for (int v = 0; v < V; v++) {
-        wait_level(v);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAITN) : "memory");
         line_barrier();  // level v's pieces of every wave landed; level v-1's boundary words written; slot v-1 free
-        issue(v + G2_D);
+        issue(v + D);
         const double *sl = reinterpret_cast<const double *>(ring + (v % R) * SB);
         const double rh = sl[NC * NYP + j];
         const double bprev = wave > 0 ? bnd[((v - 1) & 1) * 16 + wave - 1] : 0.0;
@@ -1023,19 +1019,19 @@ __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, doub
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int FILL, int NCL>
+template <int FILL, int NCL, int D>
 __global__ __launch_bounds__(G2_MAXNY) void k_lineg(G2Args a)
 {
     if (a.guard && *a.guard != 0.0) return;  // a batched iteration past the stop (lssp_amd_ctx::guard)
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    if (a.mode != 2) lineg_sweep<FILL, NCL>(a, a.sL, false, a.mode == 0 ? a.sU : nullptr, a.out, smem);
+    if (a.mode != 2) lineg_sweep<FILL, NCL, D>(a, a.sL, false, a.mode == 0 ? a.sU : nullptr, a.out, smem);
     if (a.mode == 0) {
         // the U stream's rhs slots were written by this workgroup: drained above
         // (vmcnt 0); the workgroup fence and barrier order them before its DMAs
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         __syncthreads();
     }
-    if (a.mode != 1) lineg_sweep<FILL, FILL ? 4 : 3>(a, a.sU, true, nullptr, a.out, smem);
+    if (a.mode != 1) lineg_sweep<FILL, FILL ? 4 : 3, D>(a, a.sU, true, nullptr, a.out, smem);
 }
 
 // the first sweep's rhs into its stream's rhs slots (level-major, lane = line)
@@ -1064,15 +1060,22 @@ int launch_lineg(lssp_amd_ctx *c, const LineILU &li, int mode, double *x, const 
                                                          rhs, c->guard);
     LSSP_HIP(hipGetLastError());
     G2Args a{g.nx, g.ny, NYP, V, n, li.d_g2L, li.d_g2U, li.g2NCL, li.g2NCU, mode, x, c->guard};
-    const int lds = 256 + (G2_D + 1) * g2_slot_bytes(4, NYP);
-    // (ILU(1): L 3 or 4 components, U 4; ILU(0): L 2 or 3, U 3)
+    // (ILU(1): L 3 or 4 components, U 4; ILU(0): L 2 or 3, U 3).  The DMA lead D
+    // covers the memory latency at ~0.1 us per level: 16 levels where 17 slots
+    // of up to 192 lines fit the LDS, 14 for 256 lines
     const int kv = li.g2fill * 2 + (li.g2NCL == (li.g2fill ? 4 : 3));
-    auto kern = kv == 3 ? k_lineg<1, 4> : kv == 2 ? k_lineg<1, 3> : kv == 1 ? k_lineg<0, 3> : k_lineg<0, 2>;
-    static bool attr[4] = {false, false, false, false};
-    if (!attr[kv]) {
-        LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     256 + (G2_D + 1) * g2_slot_bytes(4, G2_MAXNY)));
-        attr[kv] = true;
+    const bool wide = NYP > 192;
+    const int D = wide ? G2_DW : G2_D;
+    const int lds = 256 + (D + 1) * g2_slot_bytes(4, NYP);
+    static_assert(256 + (G2_D + 1) * g2_slot_bytes(4, 192) <= 160 * 1024 &&
+                  256 + (G2_DW + 1) * g2_slot_bytes(4, G2_MAXNY) <= 160 * 1024, "k_lineg LDS");
+    void (*kern)(G2Args);
+    if (wide) kern = kv == 3 ? k_lineg<1, 4, G2_DW> : kv == 2 ? k_lineg<1, 3, G2_DW> : kv == 1 ? k_lineg<0, 3, G2_DW> : k_lineg<0, 2, G2_DW>;
+    else kern = kv == 3 ? k_lineg<1, 4, G2_D> : kv == 2 ? k_lineg<1, 3, G2_D> : kv == 1 ? k_lineg<0, 3, G2_D> : k_lineg<0, 2, G2_D>;
+    static bool attr[8] = {};
+    if (!attr[kv + 4 * wide]) {
+        LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr[kv + 4 * wide] = true;
     }
     kern<<<1, NYP, lds, c->stream>>>(a);
     LSSP_HIP(hipGetLastError());
