@@ -57,6 +57,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <cstdio>
 #include <vector>
 
 #include "internal.h"
@@ -91,7 +92,15 @@ constexpr int lds_bytes() { return (D + 1) * Slot<NA>::BYTES + rsl<OUT>() * ROWS
 constexpr int waves(int NL, int SW) { return 2 + NL + 1 + SW; }
 }  // namespace lf
 constexpr int G2_D = 16;       // k_lineg: levels of DMA lead (ring of D + 1 slots), up to 192 lines
-constexpr int G2_DW = 14;      // ... for 193 - 256 lines (15 slots of 10 KB)
+constexpr int G2_DW = 12;      // ... for 193 - 256 lines (4 waves' rings of 13 slots of 3 KB)
+// Streams are [level][wave][S, (SE,) W, (diag,) rhs][64 lanes]: each wave DMAs
+// only its own lanes' block, so a level's data needs no barrier, only the
+// boundary word of the previous wave does.
+__host__ __device__ constexpr int g2_pw(int NC) { return (NC + 2) / 2; }  // 1 KB DMA pieces per wave and level
+__host__ __device__ inline long g2_at(long v, int NW, int NC, int k, int j)  // stream index of (level, line, component)
+{
+    return ((v * NW + (j >> 6)) * (NC + 1) + k) * 64 + (j & 63);
+}
 
 // ---------------------------------------------------------------------------
 // host: detection, tiles, streams
@@ -300,6 +309,7 @@ int build_lineg(lssp_amd_ctx *c, const LineGeom &g, int fill, int ncl, const std
 {
     const int nx = g.nx, ny = g.ny, NYP = (ny + 63) / 64 * 64, sk = fill ? 2 : 1, V = nx + sk * (ny - 1);
     const int ncu = fill ? 4 : 3;
+    const int NW = NYP / 64;
     auto make = [&](const std::vector<double> &src, int NC) {
         std::vector<double> st((size_t)V * (NC + 1) * NYP + 128, 0.0);  // (+1 KB: whole DMA pieces)
         for (int v = 0; v < V; v++)
@@ -307,7 +317,7 @@ int build_lineg(lssp_amd_ctx *c, const LineGeom &g, int fill, int ncl, const std
                 const int i = v - sk * j;
                 if (i < 0 || i >= nx) continue;
                 const double *cr = src.data() + ((size_t)j * nx + i) * NC;  // (sweep order: U mirrored)
-                for (int k = 0; k < NC; k++) st[((size_t)v * (NC + 1) + k) * NYP + j] = cr[k];
+                for (int k = 0; k < NC; k++) st[g2_at(v, NW, NC, k, j)] = cr[k];
             }
         return st;
     };
@@ -937,68 +947,70 @@ struct G2Args {
     int mode;         // 0: apply (L -> the U stream's rhs, U -> out); 1: L only; 2: U only (-> out)
     double *out;      // natural order
     const double *guard;
+    unsigned long long *trace;  // diagnostics (LSSP_AMD_LINEG_TRACE): wave 0's clocks per level of the first sweep
 };
-constexpr int G2_KP = 3;  // DMA pieces per wave per level (dummies fill up): 4 waves x 3 >= 10 pieces
-__host__ __device__ constexpr int g2_slot_bytes(int NC, int NYP) { return ((NC + 1) * NYP * 8 + 1023) / 1024 * 1024; }
-
 template <int FILL, int NC, int D>
 __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, double *ustream, double *out, char *smem)
 {
     constexpr int SK = FILL ? 2 : 1;  // row i = v - SK j
-    constexpr int R = D + 1;
+    constexpr int R = D + 1, PW = g2_pw(NC), WSB = PW * 1024;
     const int j = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(j >> 6), lane = j & 63;
-    const int NW = blockDim.x >> 6, nx = a.nx, ny = a.ny, NYP = a.NYP, V = a.V;
-    const int SB = g2_slot_bytes(NC, NYP), NP = ((NC + 1) * NYP * 8 + 1023) / 1024;
-    double *bnd = reinterpret_cast<double *>(smem);  // [2][16]: each wave's lane 63 of the previous level
-    char *ring = smem + 256;
-    const unsigned lds0 = (unsigned)(uintptr_t)ring;
-    const long lvl = (long)(NC + 1) * NYP * 8;  // stream bytes per level
-    auto issue = [&](int v) {  // level v's pieces into slot v mod R; past V - 1: dummies (fixed counts)
-        const char *src = reinterpret_cast<const char *>(st) + (long)min(v, V - 1) * lvl;
-        const unsigned dst = lds0 + (unsigned)((v % R) * SB);
+    const int NW = blockDim.x >> 6, nx = a.nx, ny = a.ny, V = a.V;
+    double *bnd = reinterpret_cast<double *>(smem);  // [2][16]: each wave's lane 63 of a level
+    char *wring = smem + 256 + wave * R * WSB;       // this wave's ring (slots of its own blocks)
+    const unsigned wl0 = (unsigned)(uintptr_t)wring;
+    constexpr long BLK = (NC + 1) * 64 * 8;  // bytes of a wave's block per level
+    auto issue = [&](int v) {  // this wave's block of level v into slot v mod R; past V - 1: dummies
+        const char *src = reinterpret_cast<const char *>(st) + ((long)min(v, V - 1) * NW + wave) * BLK;
+        const unsigned dst = wl0 + (unsigned)((v % R) * WSB);
 #pragma unroll
-        for (int k = 0; k < G2_KP; k++) {
-            const int p = wave + k * NW, pp = p < NP ? p : 0;
-            dma16(src + pp * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(dst + pp * 1024));
-        }
+        for (int p = 0; p < PW; p++) dma16(src + p * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(dst + p * 1024));
     };
-    // the wave's vector-memory queue holds, per level, its G2_KP DMAs of level
-    // v + D and then one store of level v (the prologue's levels a dropped
-    // store each), so at level v's wait its pieces have exactly
-    // 1 + (G2_KP + 1)(D - 1) younger operations: one wait count for every level
-    constexpr int WAITN = 1 + (G2_KP + 1) * (D - 1);
+    // per level the wave's vector-memory queue gets one store (level v) and then
+    // its PW DMAs (level v + D) -- the prologue a dropped store before each
+    // level's DMAs -- so when level v + 1's pieces are waited for (at the end of
+    // level v) exactly (PW + 1)(D - 1) younger operations exist: one count
+    constexpr int WAITN = (PW + 1) * (D - 1);
     static_assert(WAITN <= 63, "gfx9 vmcnt");
     constexpr int OOB = 0x40000000;
     // (num_records bound every store: the off-grid lanes' offset OOB lies past them)
     const __amdgpu_buffer_rsrc_t ro = ustream
-        ? __builtin_amdgcn_make_buffer_rsrc(ustream, 0, (int)((long)a.V * (a.ncu + 1) * NYP * 8), 0x00020000)
+        ? __builtin_amdgcn_make_buffer_rsrc(ustream, 0, (int)((long)a.V * NW * (a.ncu + 1) * 512), 0x00020000)
         : __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(a.n * 8), 0x00020000);
     if (j < 32) bnd[j] = 0.0;  // (ordered before their first reader by level 0's barrier)
     for (int v = 0; v < D; v++) {
-        issue(v);
         __builtin_amdgcn_raw_buffer_store_b64(split64(0), ro, OOB, 0, 0);  // (dropped: keeps the counts)
+        issue(v);
     }
+    double cf[NC + 1];  // the next level's components, read from the ring one level ahead
+    auto prefetch = [&](int v) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAITN) : "memory");  // this wave's block of level v landed
+        const double *sl = reinterpret_cast<const double *>(wring + (v % R) * WSB);
+#pragma unroll
+        for (int k = 0; k <= NC; k++) cf[k] = sl[k * 64 + lane];
+    };
+    prefetch(0);
     double xp = 0.0, sp = 0.0;  // the lane's x(v-1); lane j-1's x(v-2) (S)
+    unsigned long long *tr = a.trace && !mirror && j == 0 ? a.trace : nullptr;
     for (int v = 0; v < V; v++) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAITN) : "memory");
-        line_barrier();  // level v's pieces of every wave landed; level v-1's boundary words written; slot v-1 free
-        issue(v + D);
-        const double *sl = reinterpret_cast<const double *>(ring + (v % R) * SB);
-        const double rh = sl[NC * NYP + j];
+        const unsigned long long c0 = tr ? __builtin_amdgcn_s_memtime() : 0;
+        if (NW > 1) line_barrier();  // level v-1's boundary words written
+        const unsigned long long c1 = tr ? __builtin_amdgcn_s_memtime() : 0;
         const double bprev = wave > 0 ? bnd[((v - 1) & 1) * 16 + wave - 1] : 0.0;
         const double se = dpp_shr1(xp, bprev);  // lane j-1's x(v-1) (lane 0: the previous wave's lane 63)
+        const double rh = cf[NC];
         double x;
         if constexpr (FILL) {
             // the reference's order: S (r - nx), SE (r - nx + 1), W (r - 1)
-            x = rh - sl[j] * sp;
-            x = x - sl[NYP + j] * se;
-            x = x - sl[2 * NYP + j] * xp;
-            if constexpr (NC == 4) x = x / sl[3 * NYP + j];
+            x = rh - cf[0] * sp;
+            x = x - cf[1] * se;
+            x = x - cf[2] * xp;
+            if constexpr (NC == 4) x = x / cf[3];
         } else {
             // S (r - nx) = lane j-1's x(v-1), W (r - 1)
-            x = rh - sl[j] * se;
-            x = x - sl[NYP + j] * xp;
-            if constexpr (NC == 3) x = x / sl[2 * NYP + j];
+            x = rh - cf[0] * se;
+            x = x - cf[1] * xp;
+            if constexpr (NC == 3) x = x / cf[2];
         }
         const int i = v - SK * j;
         const bool ok = j < ny && (unsigned)i < (unsigned)nx;
@@ -1007,14 +1019,24 @@ __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, doub
         xp = x;
         if (lane == 63) bnd[(v & 1) * 16 + wave] = x;
         // one store per wave and level (off-grid lanes dropped): the U stream's rhs
-        // slot of its level V-1-v, lane ny-1-j (the mirror row), or the output
+        // slot of its level V-1-v, line ny-1-j (the mirror row), or the output
         int vo;
-        if (ustream) vo = ok ? (int)((((long)(V - 1 - v) * (a.ncu + 1) + a.ncu) * NYP + (ny - 1 - j)) * 8) : OOB;
+        if (ustream) vo = ok ? (int)(g2_at(V - 1 - v, NW, a.ncu, a.ncu, ny - 1 - j) * 8) : OOB;
         else {
             const long r = (long)j * nx + i;
             vo = ok ? (int)((mirror ? a.n - 1 - r : r) * 8) : OOB;
         }
         __builtin_amdgcn_raw_buffer_store_b64(split64((uint64_t)__double_as_longlong(x)), ro, vo, 0, 0);
+        const unsigned long long c2 = tr ? __builtin_amdgcn_s_memtime() : 0;
+        issue(v + D);  // (slot (v - 1) mod R: read before level v-1)
+        prefetch(v + 1);
+        if (tr && v < 512) {  // (a vector store from lane 0, after the counted wait)
+            const unsigned long long c3 = __builtin_amdgcn_s_memtime();
+            tr[4 * v] = c0;
+            tr[4 * v + 1] = c1;
+            tr[4 * v + 2] = c2;
+            tr[4 * v + 3] = c3;
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -1034,7 +1056,7 @@ __global__ __launch_bounds__(G2_MAXNY) void k_lineg(G2Args a)
     if (a.mode != 1) lineg_sweep<FILL, FILL ? 4 : 3, D>(a, a.sU, true, nullptr, a.out, smem);
 }
 
-// the first sweep's rhs into its stream's rhs slots (level-major, lane = line)
+// the first sweep's rhs into its stream's rhs slots
 __global__ __launch_bounds__(256) void k_lineg_rhs(double *st, int NC, int sk, int V, int NYP, int nx, int ny, long n,
                                                    int mirror, const double *__restrict__ rhs, const double *guard)
 {
@@ -1044,7 +1066,7 @@ __global__ __launch_bounds__(256) void k_lineg_rhs(double *st, int NC, int sk, i
     const int v = (int)(t / NYP), j = (int)(t % NYP), i = v - sk * j;
     if (j >= ny || i < 0 || i >= nx) return;
     const long r = (long)j * nx + i;
-    st[((long)v * (NC + 1) + NC) * NYP + j] = rhs[mirror ? n - 1 - r : r];
+    st[g2_at(v, NYP >> 6, NC, NC, j)] = rhs[mirror ? n - 1 - r : r];
 }
 
 int launch_lineg(lssp_amd_ctx *c, const LineILU &li, int mode, double *x, const double *rhs)
@@ -1059,16 +1081,18 @@ int launch_lineg(lssp_amd_ctx *c, const LineILU &li, int mode, double *x, const 
     k_lineg_rhs<<<(nt + 255) / 256, 256, 0, c->stream>>>(st0, nc0, li.g2fill ? 2 : 1, V, NYP, g.nx, g.ny, n, mode == 2,
                                                          rhs, c->guard);
     LSSP_HIP(hipGetLastError());
-    G2Args a{g.nx, g.ny, NYP, V, n, li.d_g2L, li.d_g2U, li.g2NCL, li.g2NCU, mode, x, c->guard};
+    G2Args a{g.nx, g.ny, NYP, V, n, li.d_g2L, li.d_g2U, li.g2NCL, li.g2NCU, mode, x, c->guard, nullptr};
+    static const char *trp = getenv("LSSP_AMD_LINEG_TRACE");  // diagnostics: path of a JSON line per launch
+    if (trp) LSSP_HIP(hipMalloc(&a.trace, sizeof(unsigned long long) * 4 * 512));
     // (ILU(1): L 3 or 4 components, U 4; ILU(0): L 2 or 3, U 3).  The DMA lead D
-    // covers the memory latency at ~0.1 us per level: 16 levels where 17 slots
-    // of up to 192 lines fit the LDS, 14 for 256 lines
+    // covers the memory latency at ~0.1 us per level: 16 levels where the waves'
+    // rings of 17 slots fit the LDS (up to 3 waves), 12 for 4 waves
     const int kv = li.g2fill * 2 + (li.g2NCL == (li.g2fill ? 4 : 3));
     const bool wide = NYP > 192;
     const int D = wide ? G2_DW : G2_D;
-    const int lds = 256 + (D + 1) * g2_slot_bytes(4, NYP);
-    static_assert(256 + (G2_D + 1) * g2_slot_bytes(4, 192) <= 160 * 1024 &&
-                  256 + (G2_DW + 1) * g2_slot_bytes(4, G2_MAXNY) <= 160 * 1024, "k_lineg LDS");
+    const int lds = 256 + (NYP >> 6) * (D + 1) * g2_pw(4) * 1024;
+    static_assert(256 + 3 * (G2_D + 1) * g2_pw(4) * 1024 <= 160 * 1024 &&
+                  256 + 4 * (G2_DW + 1) * g2_pw(4) * 1024 <= 160 * 1024, "k_lineg LDS");
     void (*kern)(G2Args);
     if (wide) kern = kv == 3 ? k_lineg<1, 4, G2_DW> : kv == 2 ? k_lineg<1, 3, G2_DW> : kv == 1 ? k_lineg<0, 3, G2_DW> : k_lineg<0, 2, G2_DW>;
     else kern = kv == 3 ? k_lineg<1, 4, G2_D> : kv == 2 ? k_lineg<1, 3, G2_D> : kv == 1 ? k_lineg<0, 3, G2_D> : k_lineg<0, 2, G2_D>;
@@ -1079,6 +1103,19 @@ int launch_lineg(lssp_amd_ctx *c, const LineILU &li, int mode, double *x, const 
     }
     kern<<<1, NYP, lds, c->stream>>>(a);
     LSSP_HIP(hipGetLastError());
+    if (trp) {
+        std::vector<unsigned long long> h(4 * 512);
+        LSSP_HIP(hipMemcpyAsync(h.data(), a.trace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, c->stream));
+        LSSP_HIP(hipStreamSynchronize(c->stream));
+        (void)hipFree(a.trace);
+        FILE *f = fopen(trp, "a");
+        if (f) {
+            fprintf(f, "{\"mode\": %d, \"V\": %d, \"NYP\": %d, \"clk\": [", mode, V, NYP);
+            for (size_t q = 0; q < h.size(); q++) fprintf(f, "%s%llu", q ? ", " : "", h[q]);
+            fprintf(f, "]}\n");
+            fclose(f);
+        }
+    }
     return LSSP_AMD_OK;
 }
 
