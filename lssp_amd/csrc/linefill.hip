@@ -960,17 +960,23 @@ __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, doub
     char *wring = smem + 256 + wave * R * WSB;       // this wave's ring (slots of its own blocks)
     const unsigned wl0 = (unsigned)(uintptr_t)wring;
     constexpr long BLK = (NC + 1) * 64 * 8;  // bytes of a wave's block per level
-    auto issue = [&](int v) {  // this wave's block of level v into slot v mod R; past V - 1: dummies
-        const char *src = reinterpret_cast<const char *>(st) + ((long)min(v, V - 1) * NW + wave) * BLK;
-        const unsigned dst = wl0 + (unsigned)((v % R) * WSB);
+    // the DMA cursor: level vi's block (source advanced per level, clamped at
+    // V - 1: past it the loads are dummies that keep the counts), its ring slot
+    const char *src = reinterpret_cast<const char *>(st) + (long)wave * BLK + lane * 16;
+    const long step = (long)NW * BLK;
+    int vi = 0, si = 0;
+    auto issue = [&]() {
+        const unsigned dst = __builtin_amdgcn_readfirstlane(wl0 + (unsigned)(si * WSB));
 #pragma unroll
-        for (int p = 0; p < PW; p++) dma16(src + p * 1024 + lane * 16, __builtin_amdgcn_readfirstlane(dst + p * 1024));
+        for (int p = 0; p < PW; p++) dma16(src + p * 1024, dst + p * 1024);
+        if (++vi < V) src += step;
+        si = si == R - 1 ? 0 : si + 1;
     };
     // per level the wave's vector-memory queue gets one store (level v) and then
     // its PW DMAs (level v + D) -- the prologue a dropped store before each
-    // level's DMAs -- so when level v + 1's pieces are waited for (at the end of
-    // level v) exactly (PW + 1)(D - 1) younger operations exist: one count
-    constexpr int WAITN = (PW + 1) * (D - 1);
+    // level's DMAs -- so when level v + 2's pieces are waited for (at the end of
+    // level v) exactly (PW + 1)(D - 2) younger operations exist: one count
+    constexpr int WAITN = (PW + 1) * (D - 2);
     static_assert(WAITN <= 63, "gfx9 vmcnt");
     constexpr int OOB = 0x40000000;
     // (num_records bound every store: the off-grid lanes' offset OOB lies past them)
@@ -980,16 +986,24 @@ __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, doub
     if (j < 32) bnd[j] = 0.0;  // (ordered before their first reader by level 0's barrier)
     for (int v = 0; v < D; v++) {
         __builtin_amdgcn_raw_buffer_store_b64(split64(0), ro, OOB, 0, 0);  // (dropped: keeps the counts)
-        issue(v);
+        issue();
     }
-    double cf[NC + 1];  // the next level's components, read from the ring one level ahead
-    auto prefetch = [&](int v) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAITN) : "memory");  // this wave's block of level v landed
-        const double *sl = reinterpret_cast<const double *>(wring + (v % R) * WSB);
+    // components of levels v (cf) and v + 1 (cn) in registers: level v+2's are
+    // read from the ring at the end of level v, a level before their use
+    double cf[NC + 1], cn[NC + 1];
+    int sr = 0;  // the ring slot of the next level to read
+    auto fetch = [&](double (&c)[NC + 1]) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAITN) : "memory");  // this wave's block of that level landed
+        const double *sl = reinterpret_cast<const double *>(wring + sr * WSB);
 #pragma unroll
-        for (int k = 0; k <= NC; k++) cf[k] = sl[k * 64 + lane];
+        for (int k = 0; k <= NC; k++) c[k] = sl[k * 64 + lane];
+        sr = sr == R - 1 ? 0 : sr + 1;
     };
-    prefetch(0);
+    // (the first two levels' waits: level 0's and 1's blocks have fewer younger
+    // operations than the count, so wait for everything once)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    fetch(cf);
+    fetch(cn);
     double xp = 0.0, sp = 0.0;  // the lane's x(v-1); lane j-1's x(v-2) (S)
     unsigned long long *tr = a.trace && !mirror && j == 0 ? a.trace : nullptr;
     for (int v = 0; v < V; v++) {
@@ -1000,6 +1014,8 @@ __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, doub
         const double se = dpp_shr1(xp, bprev);  // lane j-1's x(v-1) (lane 0: the previous wave's lane 63)
         const double rh = cf[NC];
         double x;
+        // (the store and DMAs of this level, and level v+2's reads, are issued
+        // after the arithmetic; cf is replaced by cn at the end)
         if constexpr (FILL) {
             // the reference's order: S (r - nx), SE (r - nx + 1), W (r - 1)
             x = rh - cf[0] * sp;
@@ -1028,8 +1044,10 @@ __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, doub
         }
         __builtin_amdgcn_raw_buffer_store_b64(split64((uint64_t)__double_as_longlong(x)), ro, vo, 0, 0);
         const unsigned long long c2 = tr ? __builtin_amdgcn_s_memtime() : 0;
-        issue(v + D);  // (slot (v - 1) mod R: read before level v-1)
-        prefetch(v + 1);
+        issue();  // level v + D into the slot of level v - 1 (read at the end of level v - 3)
+#pragma unroll
+        for (int k = 0; k <= NC; k++) cf[k] = cn[k];
+        fetch(cn);  // level v + 2
         if (tr && v < 512) {  // (a vector store from lane 0, after the counted wait)
             const unsigned long long c3 = __builtin_amdgcn_s_memtime();
             tr[4 * v] = c0;
