@@ -92,7 +92,8 @@ constexpr int lds_bytes() { return (D + 1) * Slot<NA>::BYTES + rsl<OUT>() * ROWS
 constexpr int waves(int NL, int SW) { return 2 + NL + 1 + SW; }
 }  // namespace lf
 constexpr int G2_D = 16;       // k_lineg: levels of DMA lead (ring of D + 1 slots), up to 192 lines
-constexpr int G2_DW = 12;      // ... for 193 - 256 lines (4 waves' rings of 13 slots of 3 KB)
+constexpr int G2_DW = 11;      // ... for 193 - 256 lines (4 waves' rings of 12 slots of 3 KB)
+constexpr int G2_BND = 2 * 5 * 64 * 8;  // k_lineg's boundary words
 // Streams are [level][wave][S, (SE,) W, (diag,) rhs][64 lanes]: each wave DMAs
 // only its own lanes' block, so a level's data needs no barrier, only the
 // boundary word of the previous wave does.
@@ -947,17 +948,20 @@ struct G2Args {
     int mode;         // 0: apply (L -> the U stream's rhs, U -> out); 1: L only; 2: U only (-> out)
     double *out;      // natural order
     const double *guard;
-    unsigned long long *trace;  // diagnostics (LSSP_AMD_LINEG_TRACE): wave 0's clocks per level of the first sweep
 };
-template <int FILL, int NC, int D>
+// (a single wave issues every instruction of a level, so the level's cost is
+// its instruction count: no branches, no per-level address arithmetic)
+template <int FILL, int NC, int D, bool TOU>
 __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, double *ustream, double *out, char *smem)
 {
     constexpr int SK = FILL ? 2 : 1;  // row i = v - SK j
     constexpr int R = D + 1, PW = g2_pw(NC), WSB = PW * 1024;
     const int j = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(j >> 6), lane = j & 63;
     const int NW = blockDim.x >> 6, nx = a.nx, ny = a.ny, V = a.V;
-    double *bnd = reinterpret_cast<double *>(smem);  // [2][16]: each wave's lane 63 of a level
-    char *wring = smem + 256 + wave * R * WSB;       // this wave's ring (slots of its own blocks)
+    // boundary words [2][1 + waves][64]: wave w's lanes write row 1 + w, wave w
+    // reads lane 63 of row w (row 0 stays +0.0: wave 0's line -1)
+    double *bnd = reinterpret_cast<double *>(smem);
+    char *wring = smem + G2_BND + wave * R * WSB;  // this wave's ring (slots of its own blocks)
     const unsigned wl0 = (unsigned)(uintptr_t)wring;
     constexpr long BLK = (NC + 1) * 64 * 8;  // bytes of a wave's block per level
     // the DMA cursor: level vi's block (source advanced per level, clamped at
@@ -974,23 +978,23 @@ __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, doub
     };
     // per level the wave's vector-memory queue gets one store (level v) and then
     // its PW DMAs (level v + D) -- the prologue a dropped store before each
-    // level's DMAs -- so when level v + 2's pieces are waited for (at the end of
-    // level v) exactly (PW + 1)(D - 2) younger operations exist: one count
-    constexpr int WAITN = (PW + 1) * (D - 2);
+    // level's DMAs -- so when level v + 2's pieces are waited for (early in
+    // level v) exactly (PW + 1)(D - 3) younger operations exist: one count
+    constexpr int WAITN = (PW + 1) * (D - 3);
     static_assert(WAITN <= 63, "gfx9 vmcnt");
     constexpr int OOB = 0x40000000;
     // (num_records bound every store: the off-grid lanes' offset OOB lies past them)
-    const __amdgpu_buffer_rsrc_t ro = ustream
+    const __amdgpu_buffer_rsrc_t ro = TOU
         ? __builtin_amdgcn_make_buffer_rsrc(ustream, 0, (int)((long)a.V * NW * (a.ncu + 1) * 512), 0x00020000)
         : __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(a.n * 8), 0x00020000);
-    if (j < 32) bnd[j] = 0.0;  // (ordered before their first reader by level 0's barrier)
+    for (int q = j; q < 2 * 5 * 64; q += blockDim.x) bnd[q] = 0.0;  // (before level 0's barrier)
     for (int v = 0; v < D; v++) {
         __builtin_amdgcn_raw_buffer_store_b64(split64(0), ro, OOB, 0, 0);  // (dropped: keeps the counts)
         issue();
     }
-    // components of levels v (cf) and v + 1 (cn) in registers: level v+2's are
-    // read from the ring at the end of level v, a level before their use
-    double cf[NC + 1], cn[NC + 1];
+    // components of levels v (cf), v + 1 (cn) and v + 2 (cq) in registers: level
+    // v+2's LDS reads are issued early in level v, so no level waits for them
+    double cf[NC + 1], cn[NC + 1], cq[NC + 1];
     int sr = 0;  // the ring slot of the next level to read
     auto fetch = [&](double (&c)[NC + 1]) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAITN) : "memory");  // this wave's block of that level landed
@@ -999,23 +1003,22 @@ __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, doub
         for (int k = 0; k <= NC; k++) c[k] = sl[k * 64 + lane];
         sr = sr == R - 1 ? 0 : sr + 1;
     };
-    // (the first two levels' waits: level 0's and 1's blocks have fewer younger
-    // operations than the count, so wait for everything once)
+    // (the first two levels' waits: their blocks have fewer younger operations
+    // than the count, so wait for everything once)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     fetch(cf);
     fetch(cn);
     double xp = 0.0, sp = 0.0;  // the lane's x(v-1); lane j-1's x(v-2) (S)
-    unsigned long long *tr = a.trace && !mirror && j == 0 ? a.trace : nullptr;
+    // per-lane store offsets advance with the level: row i = v - SK j (natural
+    // r = j nx + i, mirrored n-1-r), or the U stream's slot of level V-1-v
+    const long r0 = (long)j * nx - (long)SK * j;  // r at level 0
     for (int v = 0; v < V; v++) {
-        const unsigned long long c0 = tr ? __builtin_amdgcn_s_memtime() : 0;
         if (NW > 1) line_barrier();  // level v-1's boundary words written
-        const unsigned long long c1 = tr ? __builtin_amdgcn_s_memtime() : 0;
-        const double bprev = wave > 0 ? bnd[((v - 1) & 1) * 16 + wave - 1] : 0.0;
+        const double bprev = bnd[((v - 1) & 1) * 320 + wave * 64 + 63];  // wave w-1's lane 63 (wave 0: +0.0)
+        fetch(cq);  // level v + 2 (behind the boundary read in the LDS queue)
         const double se = dpp_shr1(xp, bprev);  // lane j-1's x(v-1) (lane 0: the previous wave's lane 63)
         const double rh = cf[NC];
         double x;
-        // (the store and DMAs of this level, and level v+2's reads, are issued
-        // after the arithmetic; cf is replaced by cn at the end)
         if constexpr (FILL) {
             // the reference's order: S (r - nx), SE (r - nx + 1), W (r - 1)
             x = rh - cf[0] * sp;
@@ -1033,27 +1036,21 @@ __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, doub
         x = ok ? x : 0.0;  // rows off the grid hold +0.0
         sp = se;
         xp = x;
-        if (lane == 63) bnd[(v & 1) * 16 + wave] = x;
+        bnd[(v & 1) * 320 + (wave + 1) * 64 + lane] = x;
         // one store per wave and level (off-grid lanes dropped): the U stream's rhs
         // slot of its level V-1-v, line ny-1-j (the mirror row), or the output
         int vo;
-        if (ustream) vo = ok ? (int)(g2_at(V - 1 - v, NW, a.ncu, a.ncu, ny - 1 - j) * 8) : OOB;
+        if constexpr (TOU) vo = ok ? (int)(g2_at(V - 1 - v, NW, a.ncu, a.ncu, ny - 1 - j) * 8) : OOB;
         else {
-            const long r = (long)j * nx + i;
+            const long r = r0 + v;
             vo = ok ? (int)((mirror ? a.n - 1 - r : r) * 8) : OOB;
         }
         __builtin_amdgcn_raw_buffer_store_b64(split64((uint64_t)__double_as_longlong(x)), ro, vo, 0, 0);
-        const unsigned long long c2 = tr ? __builtin_amdgcn_s_memtime() : 0;
-        issue();  // level v + D into the slot of level v - 1 (read at the end of level v - 3)
+        issue();  // level v + D into the slot of level v - 1 (read early in level v - 3)
 #pragma unroll
-        for (int k = 0; k <= NC; k++) cf[k] = cn[k];
-        fetch(cn);  // level v + 2
-        if (tr && v < 512) {  // (a vector store from lane 0, after the counted wait)
-            const unsigned long long c3 = __builtin_amdgcn_s_memtime();
-            tr[4 * v] = c0;
-            tr[4 * v + 1] = c1;
-            tr[4 * v + 2] = c2;
-            tr[4 * v + 3] = c3;
+        for (int k = 0; k <= NC; k++) {
+            cf[k] = cn[k];
+            cn[k] = cq[k];
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1064,14 +1061,15 @@ __global__ __launch_bounds__(G2_MAXNY) void k_lineg(G2Args a)
 {
     if (a.guard && *a.guard != 0.0) return;  // a batched iteration past the stop (lssp_amd_ctx::guard)
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    if (a.mode != 2) lineg_sweep<FILL, NCL, D>(a, a.sL, false, a.mode == 0 ? a.sU : nullptr, a.out, smem);
+    if (a.mode == 0) lineg_sweep<FILL, NCL, D, true>(a, a.sL, false, a.sU, a.out, smem);
+    if (a.mode == 1) lineg_sweep<FILL, NCL, D, false>(a, a.sL, false, nullptr, a.out, smem);
     if (a.mode == 0) {
         // the U stream's rhs slots were written by this workgroup: drained above
         // (vmcnt 0); the workgroup fence and barrier order them before its DMAs
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         __syncthreads();
     }
-    if (a.mode != 1) lineg_sweep<FILL, FILL ? 4 : 3, D>(a, a.sU, true, nullptr, a.out, smem);
+    if (a.mode != 1) lineg_sweep<FILL, FILL ? 4 : 3, D, false>(a, a.sU, true, nullptr, a.out, smem);
 }
 
 // the first sweep's rhs into its stream's rhs slots
@@ -1099,18 +1097,16 @@ int launch_lineg(lssp_amd_ctx *c, const LineILU &li, int mode, double *x, const 
     k_lineg_rhs<<<(nt + 255) / 256, 256, 0, c->stream>>>(st0, nc0, li.g2fill ? 2 : 1, V, NYP, g.nx, g.ny, n, mode == 2,
                                                          rhs, c->guard);
     LSSP_HIP(hipGetLastError());
-    G2Args a{g.nx, g.ny, NYP, V, n, li.d_g2L, li.d_g2U, li.g2NCL, li.g2NCU, mode, x, c->guard, nullptr};
-    static const char *trp = getenv("LSSP_AMD_LINEG_TRACE");  // diagnostics: path of a JSON line per launch
-    if (trp) LSSP_HIP(hipMalloc(&a.trace, sizeof(unsigned long long) * 4 * 512));
+    G2Args a{g.nx, g.ny, NYP, V, n, li.d_g2L, li.d_g2U, li.g2NCL, li.g2NCU, mode, x, c->guard};
     // (ILU(1): L 3 or 4 components, U 4; ILU(0): L 2 or 3, U 3).  The DMA lead D
     // covers the memory latency at ~0.1 us per level: 16 levels where the waves'
     // rings of 17 slots fit the LDS (up to 3 waves), 12 for 4 waves
     const int kv = li.g2fill * 2 + (li.g2NCL == (li.g2fill ? 4 : 3));
     const bool wide = NYP > 192;
     const int D = wide ? G2_DW : G2_D;
-    const int lds = 256 + (NYP >> 6) * (D + 1) * g2_pw(4) * 1024;
-    static_assert(256 + 3 * (G2_D + 1) * g2_pw(4) * 1024 <= 160 * 1024 &&
-                  256 + 4 * (G2_DW + 1) * g2_pw(4) * 1024 <= 160 * 1024, "k_lineg LDS");
+    const int lds = G2_BND + (NYP >> 6) * (D + 1) * g2_pw(4) * 1024;
+    static_assert(G2_BND + 3 * (G2_D + 1) * g2_pw(4) * 1024 <= 160 * 1024 &&
+                  G2_BND + 4 * (G2_DW + 1) * g2_pw(4) * 1024 <= 160 * 1024, "k_lineg LDS");
     void (*kern)(G2Args);
     if (wide) kern = kv == 3 ? k_lineg<1, 4, G2_DW> : kv == 2 ? k_lineg<1, 3, G2_DW> : kv == 1 ? k_lineg<0, 3, G2_DW> : k_lineg<0, 2, G2_DW>;
     else kern = kv == 3 ? k_lineg<1, 4, G2_D> : kv == 2 ? k_lineg<1, 3, G2_D> : kv == 1 ? k_lineg<0, 3, G2_D> : k_lineg<0, 2, G2_D>;
@@ -1121,19 +1117,6 @@ int launch_lineg(lssp_amd_ctx *c, const LineILU &li, int mode, double *x, const 
     }
     kern<<<1, NYP, lds, c->stream>>>(a);
     LSSP_HIP(hipGetLastError());
-    if (trp) {
-        std::vector<unsigned long long> h(4 * 512);
-        LSSP_HIP(hipMemcpyAsync(h.data(), a.trace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost, c->stream));
-        LSSP_HIP(hipStreamSynchronize(c->stream));
-        (void)hipFree(a.trace);
-        FILE *f = fopen(trp, "a");
-        if (f) {
-            fprintf(f, "{\"mode\": %d, \"V\": %d, \"NYP\": %d, \"clk\": [", mode, V, NYP);
-            for (size_t q = 0; q < h.size(); q++) fprintf(f, "%s%llu", q ? ", " : "", h[q]);
-            fprintf(f, "]}\n");
-            fclose(f);
-        }
-    }
     return LSSP_AMD_OK;
 }
 
