@@ -1012,6 +1012,7 @@ __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, doub
     // per-lane store offsets advance with the level: row i = v - SK j (natural
     // r = j nx + i, mirrored n-1-r), or the U stream's slot of level V-1-v
     const long r0 = (long)j * nx - (long)SK * j;  // r at level 0
+#pragma unroll 2
     for (int v = 0; v < V; v++) {
         if (NW > 1) line_barrier();  // level v-1's boundary words written
         const double bprev = bnd[((v - 1) & 1) * 320 + wave * 64 + 63];  // wave w-1's lane 63 (wave 0: +0.0)
@@ -1040,11 +1041,13 @@ __device__ void lineg_sweep(const G2Args &a, const double *st, bool mirror, doub
         // one store per wave and level (off-grid lanes dropped): the U stream's rhs
         // slot of its level V-1-v, line ny-1-j (the mirror row), or the output
         int vo;
-        if constexpr (TOU) vo = ok ? (int)(g2_at(V - 1 - v, NW, a.ncu, a.ncu, ny - 1 - j) * 8) : OOB;
+        if constexpr (TOU) vo = (int)(g2_at(V - 1 - v, NW, a.ncu, a.ncu, ny - 1 - j) * 8);
         else {
             const long r = r0 + v;
-            vo = ok ? (int)((mirror ? a.n - 1 - r : r) * 8) : OOB;
+            vo = (int)((mirror ? a.n - 1 - r : r) * 8);
         }
+        const int msk = -(int)ok;
+        vo = (vo & msk) | (OOB & ~msk);  // (a select without a branch)
         __builtin_amdgcn_raw_buffer_store_b64(split64((uint64_t)__double_as_longlong(x)), ro, vo, 0, 0);
         issue();  // level v + D into the slot of level v - 1 (read early in level v - 3)
 #pragma unroll
