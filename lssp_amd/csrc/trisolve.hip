@@ -167,9 +167,6 @@ __device__ __forceinline__ int rec16(int n1)
     auto pad4 = [](int w) { return (w + 3) & ~3; };
     return (pad4((EP / 2) * n1) + 2 * EP * n1 + pad4(2 * n1) + pad4(n1)) / 4;
 }
-#ifndef PK6_SPLIT
-#define PK6_SPLIT 1  // LREC packets of <= 64 rows: products on four waves, the chain on one (A/B: 0)
-#endif
 constexpr int PK6_REC16 = 1024;  // LREC: record bytes per packet <= 16 KB (4 loads x 256 loader lanes)
 
 struct PkLd {
@@ -266,10 +263,6 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
     __shared__ double rbuf[2][NR];
     __shared__ int4 sdesc[PK3_CAP];
     __shared__ v4u recbuf[LREC ? 2 : 1][LREC ? PK6_REC16 : 1];
-    // LREC, packets of <= 64 rows: the products of entry chunks 1..3 (waves 1..3)
-    // for wave 0's subtraction chain, and their arrival count
-    __shared__ double sprod[LREC && PK6_SPLIT ? 3 * (EP / 4) * 64 : 1];
-    __shared__ unsigned s_pcnt;
     __shared__ int s_blk;
     const int tid = threadIdx.x;
     const int role = __builtin_amdgcn_readfirstlane(tid) / NR;  // 0 compute, 1 loader
@@ -290,7 +283,6 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
         const bool trs = TRACE && b == a.tblk && t == 0;
         const int bbase = b * a.B;  // first schedule position of the block
         for (int i = tid; i < np; i += blockDim.x) sdesc[i] = a.desc[q0 + i];
-        if (tid == 0) s_pcnt = 0;
         __syncthreads();
         // both roles run steps J0 .. J0+T-1 (T a multiple of Q); out-of-range
         // packets turn into loads from valid dummy addresses
@@ -311,62 +303,13 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
         if (LREC && role == 0) {
             // compute lanes, record from LDS (landed by the loaders one step ahead)
             int4 draw = dread(J0);
-            unsigned nsplit = 0;  // split steps of this block so far (s_pcnt counts 3 per step)
             for (int j = J0; j < J0 + T; j++) {
                 if (trs && j >= 0 && j < np) ts[4L * j] = __builtin_amdgcn_s_memtime();
                 if (TRACE && tid == 0 && j == 0) a.trace[8L * b + 1] = __builtin_amdgcn_s_memrealtime();
                 const int4 d = duni(draw, j);
                 draw = dread(j + 1);
                 const int nr = d.z & 0x3ff;
-                if (PK6_SPLIT && nr <= 64) {
-                    // A packet's rows on lanes of ALL four compute waves: wave c forms
-                    // the products of entries [c EC, c EC + EC) of every row (the
-                    // single-wave form issued all 24 operand reads and products of a
-                    // row from one wave: the step was bound by that wave's issue);
-                    // waves 1..3 pass theirs through LDS and wave 0 subtracts all
-                    // EP in the reference's order (each product rounded as before:
-                    // the same values, bitwise)
-                    constexpr int EC = EP / 4;
-                    const int wv = t >> 6, ln = t & 63;
-                    typedef double v2d __attribute__((ext_vector_type(2)));
-                    const unsigned *w = reinterpret_cast<const unsigned *>(recbuf[j & 1]);
-                    const int wc = ((EP / 2) * nr + 3) & ~3;
-                    const v2d *V = reinterpret_cast<const v2d *>(w + wc);
-                    const char *xsb = reinterpret_cast<const char *>(xs);
-                    const int lr = min(ln, max(nr - 1, 0));  // (lanes past the packet read row 0's entries)
-                    double pr[EC];
-#pragma unroll
-                    for (int k = 0; k < EC; k++) {
-                        const int e = wv * EC + k;
-                        const unsigned ww = w[(EP / 2) * lr + e / 2];
-                        const unsigned o = (e & 1) ? (ww >> 16) : (ww & 0xffffu);
-                        const v2d v = V[(e / 2) * nr + lr];
-                        pr[k] = ((e & 1) ? v.y : v.x) * *reinterpret_cast<const double *>(xsb + o);
-                    }
-                    if (wv > 0) {
-#pragma unroll
-                        for (int k = 0; k < EC; k++) sprod[((wv - 1) * EC + k) * 64 + ln] = pr[k];
-                        __builtin_amdgcn_s_waitcnt(0xc07f);  // (lgkmcnt 0: the products are in LDS)
-                        if (ln == 0) __hip_atomic_fetch_add(&s_pcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    } else {
-                        double acc = rbuf[j & 1][lr];
-#pragma unroll
-                        for (int k = 0; k < EC; k++) acc = acc - pr[k];
-                        const unsigned want = 3u * (nsplit + 1);
-                        while (__hip_atomic_load(&s_pcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
-                        }
-#pragma unroll
-                        for (int k = 0; k < 3 * EC; k++) acc = acc - sprod[k * 64 + ln];
-                        if (ln < nr) {
-                            const double dg = reinterpret_cast<const double *>(V + (EP / 2) * nr)[ln];
-                            const double xi = a.unit ? acc : acc / dg;
-                            const int pos = d.w + ln;
-                            ring[(pos - bbase) & (BP_RING - 1)] = xi;
-                            st_agent(a.sh + pos, xi);
-                        }
-                    }
-                    nsplit++;
-                } else if (t < nr) {
+                if (t < nr) {
                     const unsigned *w = reinterpret_cast<const unsigned *>(recbuf[j & 1]);
                     const int wc = ((EP / 2) * nr + 3) & ~3;
                     typedef double v2d __attribute__((ext_vector_type(2)));
