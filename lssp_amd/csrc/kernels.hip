@@ -241,7 +241,10 @@ struct SerialArgs {
 // previous rank's running sum, itself such a sum) is never -0.0, and s + 0.0
 // == s for every other s, so the padding never changes a bit.
 constexpr int SER_C = 2048;  // elements per LDS chunk
-constexpr int SER_B = 16;    // elements per register batch of the chain
+#ifndef SER_BATCH
+#define SER_BATCH 16
+#endif
+constexpr int SER_B = SER_BATCH;  // elements per register batch of the chain
 static_assert(SER_C % SER_B == 0, "whole batches per chunk");
 // carry (multi-rank): the running sums of the ranks before this one, so the
 // chain continues theirs and the P ranks add in global index order.
