@@ -364,6 +364,8 @@ struct SpmvArgs {
     const double *guard;  // lssp_amd_ctx::guard
     long blk0;            // first chunk of this launch (spmv_halo splits a product)
     int streams;          // concurrent block streams (a multiple of 8, spmv_streams)
+    int pbpp, pz, pw;     // column-group block order (spmv_group_env): blocks per plane, planes, group width; 0: natural
+    int ntv;              // w0 / w1 / z as non-temporal accesses
 };
 
 // The 256-row blocks are dealt so that each of the 8 XCDs owns one contiguous
@@ -388,8 +390,12 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
     __shared__ double lds[MAX_SLOTS][4];
     if (a.guard && *a.guard != 0.0) return;
     const long per = gridDim.x / a.streams;
-    const long lb = (blockIdx.x % a.streams) * per + blockIdx.x / a.streams;
+    long lb = (blockIdx.x % a.streams) * per + blockIdx.x / a.streams;
     if (lb >= nblk) return;
+    if (a.pbpp > 0 && lb < (long)a.pbpp * a.pz) {
+        const long gs = (long)a.pw * a.pz, g = lb / gs, rem = lb - g * gs;
+        lb = (rem / a.pw) * a.pbpp + g * a.pw + rem % a.pw;
+    }
     const long blk = a.blk0 + lb;
     const int r0 = (int)(blk * 256);
     const int tid = threadIdx.x;
@@ -404,8 +410,13 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
     // then they are read as the value just stored, zv, below)
     double w0p = 0.0, w1p = 0.0;
     if (NRED > 0) {
-        if (a.w0 != a.z) w0p = a.w0[rr];
-        if (NRED > 1 && a.w1 && a.w1 != a.z) w1p = a.w1[rr];
+        if (a.ntv) {
+            if (a.w0 != a.z) w0p = __builtin_nontemporal_load(a.w0 + rr);
+            if (NRED > 1 && a.w1 && a.w1 != a.z) w1p = __builtin_nontemporal_load(a.w1 + rr);
+        } else {
+            if (a.w0 != a.z) w0p = a.w0[rr];
+            if (NRED > 1 && a.w1 && a.w1 != a.z) w1p = a.w1[rr];
+        }
     }
     double sum = 0;
     if (cnt <= SPMV_CAP) {
@@ -466,7 +477,8 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
         else if (EPI == EPI_AMXY) zv = sum * a.alpha;
         else if (EPI == EPI_AXPBY) zv = a.y[r] * a.beta + a.alpha * sum;
         else zv = a.alpha * sum;
-        a.z[r] = zv;
+        if (a.ntv) __builtin_nontemporal_store(zv, a.z + r);
+        else a.z[r] = zv;
     }
     if (NRED > 0) {
         double v[NRED > 0 ? NRED : 1];
@@ -625,6 +637,42 @@ static void spmv_sell_dispatch(const SpmvArgs &a, const lssp_amd_mat *A, int nre
 // K = 8 measured fastest: 143.7 us at 216^3 against 148-159 us for K = 16 ..
 // 256 (profiles/r04/r04c_stream_order.txt; the x re-use out of L2 is worth
 // more).  LSSP_AMD_SPMV_STREAMS overrides it (A/B runs).
+// Column-group block order (stencil matrices whose widest offset, the plane,
+// is a whole number of 256-row blocks): the plane's blocks are cut into
+// groups of W consecutive blocks, and position t of the traversal takes, group
+// by group, block jb of the group in every plane in turn (t -> group, plane,
+// block).  With the natural order a block's +-plane gathers are re-read one
+// plane of rows later, after ~16 MB of the matrix streamed through the XCD's
+// 4 MB L2, so x is fetched ~3 times when the plane is large (512^2 z-slab:
+// 1538 MB against 1248 algorithmic, rocprofv3 FETCH_SIZE); in a group its
+// neighbours in the traversal are the next plane's blocks, and x is fetched
+// ~1.1 times (W = 128: 1277 MB).  The time gained is smaller than the bytes
+// (the re-reads mostly hit the MALL): 512^3 y = A x 2.32 -> 2.17 ms, the
+// 8-rank slab's BiCGSTAB iteration -1.6 %, 512^2 x 64 alone unchanged
+// (profiles/r05/r05l_spmv_group_order.txt).  Automatic for planes of >= 512
+// blocks (128 Ki rows; smaller planes keep x in L2 anyway) with W = 128;
+// LSSP_AMD_SPMV_ORDER=W forces a width (0: natural order; tests, A/B runs).
+static int spmv_group_env()
+{
+    static const int k = [] {
+        const char *e = getenv("LSSP_AMD_SPMV_ORDER");
+        return e ? std::max(0, atoi(e)) : -1;
+    }();
+    return k;
+}
+
+// w0 / w1 loads and the z store as non-temporal accesses (no other block
+// re-reads them): the 8-rank slab's iteration -0.3 .. -0.6 %.
+// LSSP_AMD_SPMV_NTV=0 turns them off (A/B runs).
+static int spmv_ntv()
+{
+    static const int k = [] {
+        const char *e = getenv("LSSP_AMD_SPMV_NTV");
+        return e ? atoi(e) : 1;
+    }();
+    return k;
+}
+
 static int spmv_streams()
 {
     static const int k = [] {
@@ -663,7 +711,18 @@ int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, c
     const long nb = ce - cb;
     if (nb == 0) return LSSP_AMD_OK;
     SpmvArgs a{A->nrows, A->Ap, A->Aj, A->Ax, x, y, z, alpha, beta, w0, w1, c->d_part, c->part_cap,
-               A->Ad, A->d_off, A->ndiag, c->guard, cb, spmv_streams()};
+               A->Ad, A->d_off, A->ndiag, c->guard, cb, spmv_streams(), 0, 0, 0, spmv_ntv()};
+    const long plane = A->max_off_int;
+    if (A->ndiag > 0 && plane >= 256 * 8 && plane % 256 == 0) {
+        const long bpp = plane / 256;
+        const int env = spmv_group_env();
+        const int pw = env >= 0 ? env : (bpp >= 512 && bpp % 128 == 0 ? 128 : 0);
+        if (pw > 0 && bpp % pw == 0 && nb / bpp >= 2) {
+            a.pbpp = (int)bpp;
+            a.pz = (int)(nb / bpp);
+            a.pw = pw;
+        }
+    }
     if (A->d_win && nb == nall) {
         switch (epi) {
         case EPI_MXY: spmv_sell_dispatch<EPI_MXY>(a, A, nred, c->stream); break;

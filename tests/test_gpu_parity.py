@@ -518,3 +518,52 @@ def test_sliced_copy_footprint_and_cap_fallback(dev, monkeypatch):
     assert np.array_equal(z.download(), ref)
     M.mv_mxy(x, z)
     assert np.array_equal(z.download(), ref)
+
+
+def test_spmv_group_order_bitwise_vs_oracle():
+    """The product's column-group block order (kernels.hip, spmv_group_env:
+    automatic only for planes of >= 512 blocks, forced here through
+    LSSP_AMD_SPMV_ORDER on a 64^3 grid, plane = 16 blocks) and its
+    non-temporal vector operands (LSSP_AMD_SPMV_NTV) change which workgroup
+    takes which 256-row block, never a sum: every product, fused dot and
+    solver trace is bitwise the oracle's, for the full cube and for a slab
+    with a ragged last plane (blocks past the last whole plane keep the
+    natural order)."""
+    import subprocess
+    import sys
+    code = r'''
+import sys, numpy as np
+sys.path.insert(0, "ROOT"); sys.path.insert(0, "ROOT/tests")
+import lssp_amd, oracle as O
+from inputs import uniform
+from bench import local_block
+dev = lssp_amd.Device(0, reduction=lssp_amd.TREE)
+N = 64
+for nl in (N ** 3, N * N * 37 + 100):
+    Ap, Aj, Ax = local_block(*lssp_amd.poisson(3, N, 0, nl), 0, nl)
+    A = O.CSR(nl, Ap, Aj, Ax)
+    D = lssp_amd.DMat(dev, Ap, Aj, Ax)
+    xh, yh = uniform(11, nl), uniform(12, nl)
+    x, y, z = dev.vec(nl, xh), dev.vec(nl, yh), dev.vec(nl)
+    D.mv_mxy(x, z)
+    assert np.array_equal(z.download().view(np.int64), O.spmv(0, A, xh).view(np.int64))
+    D.mv_amxpbyz(0.75, x, -1.25, y, z)
+    assert np.array_equal(z.download().view(np.int64), O.spmv(3, A, xh, 0.75, -1.25, yh).view(np.int64))
+    L, U = O.ilu(A, "iluk", level=0)
+    M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=lssp_amd.ILUK, level=0)
+    for solver, pc in ((lssp_amd.BICGSTAB, True), (lssp_amd.CG, False)):
+        xs, b = dev.vec(nl, np.zeros(nl)), dev.vec(nl, np.ones(nl))
+        r = lssp_amd.solve(dev, D, M if pc else None, xs, b, solver=solver, tol_rel=0.0, tol_abs=0.0, tol_rb=0.0,
+                           maxit=12, trace_cap=200)
+        o = O.solve(solver, A, np.ones(nl), L=L if pc else None, U=U if pc else None, rtol=0.0, atol=0.0,
+                    rbtol=0.0, maxit=12, mode=O.TREE, trace_cap=200)
+        assert r.nits == o.nits == 12 and np.array_equal(r.trace, o.trace)
+        assert np.array_equal(xs.download().view(np.int64), o.x.view(np.int64))
+    M.close(); D.close()
+print("ok")
+'''.replace("ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    for env in ({"LSSP_AMD_SPMV_ORDER": "2"}, {"LSSP_AMD_SPMV_ORDER": "4", "LSSP_AMD_SPMV_NTV": "0"},
+                {"LSSP_AMD_SPMV_ORDER": "0", "LSSP_AMD_SPMV_NTV": "1"}):
+        res = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,
+                             timeout=170)
+        assert res.returncode == 0 and "ok" in res.stdout, (env, res.stdout[-2000:], res.stderr[-2000:])

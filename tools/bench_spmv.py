@@ -14,6 +14,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--grid", type=int, default=216)
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--nz", type=int, default=0, help="a z-slab of NZ planes of the grid (block-Jacobi block)")
     ap.add_argument("--thermal", action="store_true", help="config 5's thermal2-like matrix instead")
     ap.add_argument("--window", type=int, default=4096, help="thermal: numbering shuffle window (1: none)")
     args = ap.parse_args()
@@ -22,6 +23,10 @@ def main():
     if args.thermal:
         from lssp_amd.synthetic import thermal_like
         Ap, Aj, Ax = thermal_like(window=args.window)
+    elif args.nz:
+        from bench import local_block
+        nl = args.grid * args.grid * args.nz
+        Ap, Aj, Ax = local_block(*lssp_amd.poisson(3, args.grid, 0, nl), 0, nl)
     else:
         Ap, Aj, Ax = lssp_amd.poisson(3, args.grid)
     n = Ap.size - 1
@@ -43,7 +48,8 @@ def main():
     e1.synchronize()
     ms = e0.elapsed_time(e1) / args.reps
     b = 12 * int(Ap[-1]) + 20 * n + 4
-    print(json.dumps({"matrix": f"thermal window {args.window}" if args.thermal else f"poisson {args.grid}^3",
+    print(json.dumps({"matrix": f"thermal window {args.window}" if args.thermal else
+                      f"poisson {args.grid}^2 x {args.nz}" if args.nz else f"poisson {args.grid}^3",
                       "rows": n, "ndiag": A.ndiag, "ms": round(ms, 5),
                       "GBps": round(b / ms / 1e6, 1), "sum": float(y.download().sum())}))
 
