@@ -217,6 +217,10 @@ struct LineILU {
     LineSweep L, U;
     double *d_ustream = nullptr;  // the U sweep's rhs, written by the L sweep
     double *d_lstream = nullptr;  // the L sweep's rhs in its stream layout (k_line_rhs)
+    // the natural-order vector d_lstream already holds (written with it by a
+    // solver pass, launch_line_gather_ew): the next apply of exactly that rhs
+    // skips its gather; every apply / sweep clears it
+    mutable const double *lstream_of = nullptr;
     double *d_hk = nullptr, *d_hj = nullptr;  // hand-off buffers (armed with TRI_SENTINEL)
     long hk_stride = 0, hj_stride = 0, hk_n = 0, hj_n = 0;
     // the U sweep's tail product (launch_line_apply_spmv): U tiles finished per
@@ -419,6 +423,16 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
 int spmv_boundary(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, double *x, double beta,
                   const double *y, double *z, int nred, const double *w0, const double *w1);
 int launch_line_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs);
+// A BiCGSTAB vector pass fused with the next apply's rhs gather: out (natural
+// order, n rows) = op(x, y, out) and the same values into the L sweep's
+// stream, which the next launch_line_apply of rhs == out then reads as is.
+// op: GEW_BICG_P out = x + beta*(out - omega*y), GEW_BICG_S out = x - alpha*y
+// (scalars from scal; k_ew's EW_BICG_P / EW_BICG_S arithmetic).  Eligible
+// (line_gather_ew_ok) for the k_line2 sweeps of an n-row grid factor.
+enum { GEW_BICG_P = 1, GEW_BICG_S = 2 };
+bool line_gather_ew_ok(const LineILU &li, long n);
+int launch_line_gather_ew(lssp_amd_ctx *c, const LineILU &li, int op, const double *x, const double *y, double *out,
+                          const double *scal);
 void free_trisched(TriSched &t);
 
 // reductions with the context's mode; result left in d_sums / scal per Fin

@@ -355,7 +355,7 @@ struct SpmvArgs {
     const double *Ax, *x, *y;
     double *z;
     double alpha, beta;
-    const double *w0, *w1;  // fused dot operands: red0 = z*w0, red1 = z*(w1 ? w1 : z)
+    const double *w0, *w1;  // fused dot operands: red0 = z*w0, red1 = z*(w1 ? w1 : z), red2 = w0*w0
     double *part;
     long pcap;
     const uint8_t *Ad;  // diagonal-id column coding (lssp_amd_mat::Ad), CMP kernels
@@ -485,6 +485,7 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
         if (r < a.nrows) {
             v[0] = zv * (a.w0 == a.z ? zv : w0p);
             if (NRED > 1) v[NRED > 1 ? 1 : 0] = zv * (a.w1 && a.w1 != a.z ? w1p : zv);
+            if (NRED > 2) v[NRED > 2 ? 2 : 0] = w0p * w0p;  // (launch_spmv: w0 != z)
         } else {
 #pragma unroll
             for (int q = 0; q < NRED; q++) v[q] = 0.0;
@@ -689,7 +690,8 @@ static void spmv_dispatch(const SpmvArgs &a, int nred, long nblocks, hipStream_t
     const long g = (nblocks + a.streams - 1) / a.streams * a.streams;  // a multiple of K: whole stream shares
     if (nred == 0) k_spmv3<EPI, 0, CMP><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
     else if (nred == 1) k_spmv3<EPI, 1, CMP><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
-    else k_spmv3<EPI, 2, CMP><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
+    else if (nred == 2 || EPI != EPI_AMX) k_spmv3<EPI, 2, CMP><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
+    else k_spmv3<EPI_AMX, 3, CMP><<<g, 256, 0, s>>>(a, nblocks, nnz_pad);
 }
 
 template <int EPI>
@@ -708,6 +710,8 @@ int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, c
     LSSP_TRY(ensure_part(c, nall));
     if (ce < 0) ce = nall;
     if (cb < 0 || cb > ce || ce > nall) return LSSP_AMD_EINVAL;
+    // three fused dots (BiCGSTAB's t = A sh with t.s, t.t, s.s): EPI_AMX on k_spmv3 only
+    if (nred == 3 && (epi != EPI_AMX || A->d_win || !w0 || w0 == z || w1)) return LSSP_AMD_EINVAL;
     const long nb = ce - cb;
     if (nb == 0) return LSSP_AMD_OK;
     SpmvArgs a{A->nrows, A->Ap, A->Aj, A->Ax, x, y, z, alpha, beta, w0, w1, c->d_part, c->part_cap,

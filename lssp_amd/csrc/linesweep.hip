@@ -1667,18 +1667,116 @@ __global__ __launch_bounds__(256) void k_line_rhs(const LineTile *__restrict__ t
     }
 }
 
+// k_line2's gather (P = 8 planes x NJ = 16 lines, level skew 1) through LDS:
+// a block moves RUN consecutive steps of one tile; it loads every line's RUN
+// consecutive entries (a RUN x 8-byte natural-order run per line), then
+// stores step by step, 128 consecutive stream entries (1 KB) per step.
+// OP as k_line_rhs's.
+#ifndef LRHS2_RUN
+#define LRHS2_RUN 32
+#endif
+template <int RUN, int OP>
+__global__ __launch_bounds__(256) void k_line_rhs2(const LineTile *__restrict__ tiles, int ntiles, int nq, int nx,
+                                                  int ny, const double *__restrict__ rhs, double *__restrict__ out,
+                                                  const double *guard, const double *__restrict__ y, double *nat,
+                                                  const double *scal)
+{
+    constexpr int P = 8, NJ = 16, NL = P * NJ, NV = RUN * NL / 256;
+    static_assert(NV >= 1 && RUN * NL % 256 == 0, "block");
+    __shared__ double tb[RUN][NL + 1];
+    if (guard && *guard != 0.0) return;
+    const long b = blockIdx.x, j = b >> 3;
+    const int t = (int)(b & 7) + 8 * (int)(j / nq), q0 = (int)(j % nq) * RUN;
+    if (t >= ntiles) return;
+    const LineTile d = tiles[t];
+    if (q0 >= d.T) return;
+    double c0 = 0.0, c1 = 0.0;
+    if (OP == GEW_BICG_P) c0 = scal[S_BETA], c1 = scal[S_OMEGA];
+    if (OP == GEW_BICG_S) c0 = scal[S_ALPHA];
+    double v[NV];
+#pragma unroll
+    for (int it = 0; it < NV; it++) {
+        const int k = it * 256 + threadIdx.x, m = k % RUN, ln = k / RUN, p = ln / NJ, l = ln % NJ;
+        const int i = q0 + m - l - p - p / 4;
+        const bool ok = q0 + m < d.T && p < d.np && l < d.nj && (unsigned)i < (unsigned)nx;
+        const long r = ((long)(d.k0 + p) * ny + (d.j0 + l)) * nx + i;
+        if (OP == 0) {
+            v[it] = ok ? rhs[r] : 0.0;
+        } else {
+            v[it] = 0.0;
+            if (ok) {
+                if (OP == GEW_BICG_P) v[it] = rhs[r] + c0 * (nat[r] - c1 * y[r]);
+                else v[it] = rhs[r] - c0 * y[r];
+                nat[r] = v[it];
+            }
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < NV; it++) {
+        const int k = it * 256 + threadIdx.x;
+        tb[k % RUN][k / RUN] = v[it];
+    }
+    __syncthreads();
+    const long SB = (long)P * d.nj;
+#pragma unroll
+    for (int it = 0; it < NV; it++) {
+        const int k = it * 256 + threadIdx.x, ln = k % NL, m = k / NL, p = ln / NJ, l = ln % NJ;
+        const int i = q0 + m - l - p - p / 4;
+        if (q0 + m < d.T && p < d.np && l < d.nj && (unsigned)i < (unsigned)nx)
+            out[d.cbase + (q0 + m) * SB + p * d.nj + l] = tb[m][ln];
+    }
+}
+
 // the natural-order rhs into a sweep's stream layout (stream: li.d_lstream for
 // the L sweep, li.d_ustream for the U sweep)
 static int launch_line_gather(lssp_amd_ctx *c, const LineSweep &ls, int mirror, const double *rhs, double *stream)
 {
+    if (ls.LV >= 2 && (ls.P != 8 || ls.NJ != 16)) return LSSP_AMD_EUNSUPPORTED;
+    if (ls.LV == 2 && !mirror) {
+        const int nq2 = (ls.tmax + LRHS2_RUN - 1) / LRHS2_RUN;
+        k_line_rhs2<LRHS2_RUN, 0><<<8L * ((ls.ntiles + 7) / 8) * nq2, 256, 0, c->stream>>>(
+            ls.d_tiles, ls.ntiles, nq2, ls.nx, ls.ny, rhs, stream, c->guard, nullptr, nullptr, nullptr);
+        LSSP_HIP(hipGetLastError());
+        return LSSP_AMD_OK;
+    }
     const int nq = (ls.tmax + LRHS_RUN - 1) / LRHS_RUN;
     const long grid = 8L * ((ls.ntiles + 7) / 8) * nq;
     auto kr = ls.LV == 4 ? k_line_rhs<8, 16, 3> : ls.LV == 2 ? k_line_rhs<8, 16, 1>
               : ls.P == 16 ? k_line_rhs<16, 16, 0> : ls.P == 8 ? k_line_rhs<8, 32, 0> : k_line_rhs<4, 64, 0>;
-    if (ls.LV >= 2 && (ls.P != 8 || ls.NJ != 16)) return LSSP_AMD_EUNSUPPORTED;
     const long n = (long)ls.nx * ls.ny * ls.nz;
     kr<<<grid, 256, 0, c->stream>>>(ls.d_tiles, ls.ntiles, nq, ls.nx, ls.ny, n, mirror, rhs, stream, c->guard);
     LSSP_HIP(hipGetLastError());
+    return LSSP_AMD_OK;
+}
+
+// Fusing BiCGSTAB's p / s passes with the gather saves the gather's read of
+// the vector just written and its launch: 216^3, 2 x 33.7 us of k_line_rhs per
+// iteration become two passes ~10 us longer than k_ew's (the values leave in
+// 64-byte runs of a line, the stream in 128-byte steps).  LSSP_AMD_GATHER_EW=0
+// keeps the separate passes (A/B runs).
+bool line_gather_ew_ok(const LineILU &li, long n)
+{
+    static const int on = [] {
+        const char *e = getenv("LSSP_AMD_GATHER_EW");
+        return e ? atoi(e) : 1;
+    }();
+    const char *te = getenv("LSSP_AMD_TAIL");  // the tail product gathers itself (and its EINVAL mode)
+    return on && !(te && atoi(te)) && li.ntiles > 0 && li.kind == 0 && !li.g2 && li.LV == 2 && li.L.P == 8 &&
+           li.L.NJ == 16 && li.d_lstream && (long)li.L.nx * li.L.ny * li.L.nz == n;
+}
+
+int launch_line_gather_ew(lssp_amd_ctx *c, const LineILU &li, int op, const double *x, const double *y, double *out,
+                          const double *scal)
+{
+    const LineSweep &ls = li.L;
+    if (!line_gather_ew_ok(li, (long)ls.nx * ls.ny * ls.nz) || (op != GEW_BICG_P && op != GEW_BICG_S))
+        return LSSP_AMD_EINVAL;
+    const int nq = (ls.tmax + LRHS2_RUN - 1) / LRHS2_RUN;
+    const long grid = 8L * ((ls.ntiles + 7) / 8) * nq;
+    auto kr = op == GEW_BICG_P ? k_line_rhs2<LRHS2_RUN, GEW_BICG_P> : k_line_rhs2<LRHS2_RUN, GEW_BICG_S>;
+    kr<<<grid, 256, 0, c->stream>>>(ls.d_tiles, ls.ntiles, nq, ls.nx, ls.ny, x, li.d_lstream, c->guard, y, out, scal);
+    LSSP_HIP(hipGetLastError());
+    li.lstream_of = out;
     return LSSP_AMD_OK;
 }
 
@@ -1828,10 +1926,12 @@ static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const doub
 
 int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs)
 {
+    const bool ready = rhs == li.lstream_of;  // the stream holds rhs already (launch_line_gather_ew)
+    li.lstream_of = nullptr;
     if (li.g2) return launch_lineg(c, li, 0, x, rhs);
     if (li.kind == 1) return launch_linefill_apply(c, li, x, rhs);
     if (li.LV >= 2) {  // k_line2: gather, L sweep -> the U rhs stream, U sweep -> x
-        LSSP_TRY(launch_line_gather(c, li.L, 0, rhs, li.d_lstream));
+        if (!ready) LSSP_TRY(launch_line_gather(c, li.L, 0, rhs, li.d_lstream));
         LSSP_TRY(launch_line2(c, li, 0, li.d_lstream, li.d_ustream, 2));
         return launch_line2(c, li, 1, li.d_ustream, x, 1);
     }
@@ -1931,10 +2031,12 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
         T.dbg = dbg_d;
     }
     long tail_waves = (long)std::min(li.U.ntiles, c->num_cus);  // (the tail's claimants: workgroups)
+    const bool ready = rhs == li.lstream_of;
+    li.lstream_of = nullptr;
     if (li.kind == 1) {  // the 7-/5-point ILU(1) line sweeps (linefill.hip)
         LSSP_TRY(launch_linefill_apply_tail(c, li, x, rhs, T, &tail_waves));
     } else {
-        LSSP_TRY(launch_line_gather(c, li.L, 0, rhs, li.d_lstream));
+        if (!ready) LSSP_TRY(launch_line_gather(c, li.L, 0, rhs, li.d_lstream));
         LSSP_TRY(launch_line2(c, li, 0, li.d_lstream, li.d_ustream, 2));
         LSSP_TRY(launch_line2(c, li, 1, li.d_ustream, x, 1, &T));
     }
@@ -1947,6 +2049,7 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
 
 int launch_line_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, const double *rhs)
 {
+    li.lstream_of = nullptr;
     if (li.g2) return launch_lineg(c, li, which ? 2 : 1, x, rhs);
     if (li.kind == 1) return launch_linefill_sweep(c, li, which, x, rhs);
     if (li.LV >= 2) {  // one sweep: its rhs gathered into its own stream, natural-order output

@@ -247,40 +247,51 @@ int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
     const bool merge_s = R.tree;
     // one iteration :94-141 queued on the stream; fin_res: the finalize of its
     // last reduction; *pos_s: the trace position before its ||s|| (:117)
+    // line-swept ILU(0): the p and s passes also write the next apply's rhs
+    // stream (launch_line_gather_ew), and in tree mode ||s||^2's partials come
+    // from the product t = A sh, which reads s anyway (its third fused dot)
+    const bool gew = R.M && !R.gpc && line_gather_ew_ok(R.M->line, R.n);
     auto enqueue = [&](int k, int fin_res, long *pos_s) -> int {
         Ew e;
         if (k == 0) {
             e.kind = K_COPY;  // :96
             e.x = r;
             e.out0 = p;
+            LSSP_TRY(R.ew(e));
+        } else if (gew) {
+            LSSP_TRY(launch_line_gather_ew(R.c, R.M->line, GEW_BICG_P, r, v, p, R.c->d_scal));  // :99-102
         } else {
             e.kind = K_BICG_P;  // :99-102
             e.x = r;
             e.y = v;
             e.out0 = p;
+            LSSP_TRY(R.ew(e));
         }
-        LSSP_TRY(R.ew(e));
         LSSP_TRY(R.pc_spmv(ph, p, EPI_AMX, 1, 0, p, v, 1, rh));  // :107-108, :110
         LSSP_TRY(R.fin1(rh, v, R.fin(FIN_BICG_ALPHA, 1, R.T())));  // :112
-        e = Ew();
-        e.kind = K_BICG_S;  // :113-115
-        e.x = r;
-        e.y = v;
-        e.out0 = s;
-        e.nred = 1;
-        e.r0a = s;
-        e.r0b = s;
-        // tree mode: ||s||^2's partials go to row 2 and ride with the omega
-        // round (t.s, t.t in rows 0, 1 from the product): one level 2 and, on P
-        // ranks, one all-gather fewer per iteration.  The break test (:117)
-        // only steers the x/r update, which follows the omega round anyway;
-        // the preconditioner apply and product on s run in either case.
-        if (merge_s) e.pslot = 2;
-        LSSP_TRY(R.ew(e));
+        if (gew) {
+            LSSP_TRY(launch_line_gather_ew(R.c, R.M->line, GEW_BICG_S, r, v, s, R.c->d_scal));  // :113-115
+        } else {
+            e = Ew();
+            e.kind = K_BICG_S;  // :113-115
+            e.x = r;
+            e.y = v;
+            e.out0 = s;
+            e.nred = 1;
+            e.r0a = s;
+            e.r0b = s;
+            // tree mode: ||s||^2's partials go to row 2 and ride with the omega
+            // round (t.s, t.t in rows 0, 1 from the product): one level 2 and, on P
+            // ranks, one all-gather fewer per iteration.  The break test (:117)
+            // only steers the x/r update, which follows the omega round anyway;
+            // the preconditioner apply and product on s run in either case.
+            if (merge_s) e.pslot = 2;
+            LSSP_TRY(R.ew(e));
+        }
         *pos_s = R.tl;
         const Fin fs = R.fin(FIN_BICG_S, 1, R.T());          // :117
         if (!merge_s) LSSP_TRY(R.fin1(s, s, fs));
-        LSSP_TRY(R.pc_spmv(sh, s, EPI_AMX, 1, 0, p, t, 2, s, nullptr));  // :130-131, :133
+        LSSP_TRY(R.pc_spmv(sh, s, EPI_AMX, 1, 0, p, t, gew && merge_s ? 3 : 2, s, nullptr));  // :130-131, :133
         {
             int t0 = R.T(), t1 = R.T();
             if (merge_s) {
