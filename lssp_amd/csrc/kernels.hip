@@ -490,7 +490,11 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
 #pragma unroll
             for (int q = 0; q < NRED; q++) v[q] = 0.0;
         }
+#ifdef SPMV_DIAG_NORED  // tuning builds: no chunk reduction (WRONG dots), the cost of chunk_reduce
+        if (v[0] == 12345.678) a.part[blk] = v[0];
+#else
         chunk_reduce<NRED>(v, a.part, a.pcap, blk, lds);
+#endif
     }
 }
 
@@ -844,9 +848,17 @@ __global__ __launch_bounds__(256) void k_ew(EwArgs g)
                 if (g.scal[S_BREAK] != 0.0) {
                     w0 = true, g.out0[i] = o0 = g.out0[i] + alpha * g.x[i];
                 } else {
+                    // every operand loaded before the first store (the compiler
+                    // may not move u, v above a store to out0 they might alias)
                     const double omega = g.scal[S_OMEGA];
+#ifdef EW_XR_LATE  // tuning builds: round 4's order (u, v loaded after the out0 store)
                     w0 = true, g.out0[i] = o0 = g.out0[i] + alpha * g.x[i] + omega * g.y[i];
                     w1 = true, g.out1[i] = o1 = g.u[i] - omega * g.v[i];
+#else
+                    const double xo = g.out0[i], xp = g.x[i], xs = g.y[i], su = g.u[i], tv = g.v[i];
+                    w0 = true, g.out0[i] = o0 = xo + alpha * xp + omega * xs;
+                    w1 = true, g.out1[i] = o1 = su - omega * tv;
+#endif
                 }
                 break;
             }
