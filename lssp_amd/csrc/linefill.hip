@@ -780,8 +780,9 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
                 const uint64_t jvb = vj ? (uint64_t)__double_as_longlong(*jslot) : 0;
                 const bool bk = vk && kvb == TRI_SENTINEL, bj = vj && jvb == TRI_SENTINEL;
                 if (__any(bk || bj)) {
-                    // resync: drain, wait for these values and for the furthest step
-                    // in flight, re-issue
+                    // resync: drain, wait for these values, re-issue the later polls
+                    // (k_line2's episode; -DLINEF_RESYNC_FAR: also wait for the
+                    // furthest step in flight)
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     auto spin = [&](const double *src) {
                         for (;;) {
@@ -796,8 +797,10 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
                     };
                     if (bk) *kslot = __longlong_as_double((long long)spin(kaddr(qk)));
                     if (bj) *jslot = __longlong_as_double((long long)spin(jaddr(qj)));
+#ifdef LINEF_RESYNC_FAR
                     if (kin && kval(s + DH) && 2 * (s + DH) + 2 <= kmax) (void)spin(kaddr(s + DH));
                     if (jin && jval(s + DH + 1) && 2 * (s + DH + 1) + 1 + HJ0 <= jmax) (void)spin(jaddr(s + DH + 1));
+#endif
                     for (int k = 2; k <= DH; k++) issue(s + k);  // the polls issued at steps s+k-DH
                 }
                 line_barrier();

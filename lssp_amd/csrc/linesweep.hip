@@ -1398,8 +1398,12 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                 const uint64_t jvb = vj ? (uint64_t)__double_as_longlong(*jslot) : 0;
                 const bool bk = vk && kvb == TRI_SENTINEL, bj = vj && jvb == TRI_SENTINEL;
                 if (__any(bk || bj)) {
-                    // resync episode (k_line's): drain, wait for these values and for
-                    // the furthest step in flight, re-issue
+                    // resync episode: drain, wait for these values, re-issue the polls
+                    // of the steps after them.  (k_line's episode also waits for the
+                    // furthest step in flight, so the re-issued polls cannot miss; that
+                    // holds the tile DH steps behind its producer after every episode:
+                    // 216^3 apply 528.5 -> 508.9 us without it, bitwise the same,
+                    // profiles/r05/r05p_resync_near.txt.  -DLINE2_RESYNC_FAR restores it)
                     polls++;
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     auto spin = [&](const double *src) {
@@ -1415,9 +1419,11 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     };
                     if (bk) *kslot = __longlong_as_double((long long)spin(hk + (long)lk * NJ + kl));
                     if (bj) *jslot = __longlong_as_double((long long)spin(hj + (long)lj * P + jp));
+#ifdef LINE2_RESYNC_FAR  // tuning builds: also wait for the furthest step in flight
                     const int fk = LV * (s + DH) + kv, fj = LV * (s + DH + 1) + jv;
                     if (kin && kval(fk)) (void)spin(hk + (long)fk * NJ + kl);
                     if (jin && jval(fj)) (void)spin(hj + (long)fj * P + jp);
+#endif
                     for (int k = 2; k <= DH; k++) issue(s + k);  // the polls issued at steps s+k-DH
                 }
                 if (trs && s >= 0 && s < TS) ts[8 * s + 2] = __builtin_amdgcn_s_memtime() - w0;
