@@ -1414,7 +1414,10 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                                 atomicOr(a.err, 8);
                                 return (uint64_t)0x7FF8000000000000ull;
                             }
-                            __builtin_amdgcn_s_sleep(1);
+#ifndef LINE2_SPIN_SLEEP
+#define LINE2_SPIN_SLEEP 0  // resync spin: back-to-back polls (r05q)
+#endif
+                            if (LINE2_SPIN_SLEEP) __builtin_amdgcn_s_sleep(LINE2_SPIN_SLEEP);
                         }
                     };
                     if (bk) *kslot = __longlong_as_double((long long)spin(hk + (long)lk * NJ + kl));
@@ -1788,7 +1791,7 @@ int launch_line_gather_ew(lssp_amd_ctx *c, const LineILU &li, int op, const doub
 
 // ---- k_line2 launches -------------------------------------------------------
 #ifndef LINE2_D
-#define LINE2_D 6  // loader lead (steps of two levels)
+#define LINE2_D 7  // loader lead (steps of two levels; 7 with the near resync: profiles/r05/r05q_line2_leads.txt)
 #endif
 #ifndef LINE2_DH
 #define LINE2_DH 3  // poller lead (steps)
