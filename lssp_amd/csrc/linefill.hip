@@ -792,7 +792,10 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
                                 atomicOr(a.err, 8);
                                 return (uint64_t)0x7FF8000000000000ull;
                             }
-                            __builtin_amdgcn_s_sleep(1);
+#ifndef LINEF_SPIN_SLEEP
+#define LINEF_SPIN_SLEEP 1
+#endif
+                            if (LINEF_SPIN_SLEEP) __builtin_amdgcn_s_sleep(LINEF_SPIN_SLEEP);
                         }
                     };
                     if (bk) *kslot = __longlong_as_double((long long)spin(kaddr(qk)));

@@ -1806,7 +1806,7 @@ int launch_line_gather_ew(lssp_amd_ctx *c, const LineILU &li, int op, const doub
 template <int LV>
 constexpr int line2_d() { return LV == 4 ? 4 : LINE2_D; }
 #ifndef LINE2_DH_U
-#define LINE2_DH_U LINE2_DH  // the poller lead of the sweeps with natural-order output (OUT 1)
+#define LINE2_DH_U 2  // the poller lead of the sweeps with natural-order output (OUT 1): 2 with the near resync (U 311 -> 296 us, profiles/r05/r05r_line2_dh.txt)
 #endif
 template <int LV, int OUT>
 constexpr int line2_dh() { return LV == 4 ? 2 : OUT == 1 ? LINE2_DH_U : LINE2_DH; }
