@@ -1381,7 +1381,10 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     if (!jin && lane < LV * P) reinterpret_cast<double *>(ring + q * SL::BYTES + SL::JFIN)[lane] = 0.0;
                 }
             }
-            __builtin_amdgcn_s_setprio(3);  // the polls enter the CU's memory queue ahead of the coefficient DMAs
+#ifndef LINE2_POLL_PRIO
+#define LINE2_POLL_PRIO 3
+#endif
+            __builtin_amdgcn_s_setprio(LINE2_POLL_PRIO);  // the polls enter the CU's memory queue ahead of the coefficient DMAs
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             unsigned polls = 0;
             for (int s = S0; s <= TS; s++) {
@@ -1803,8 +1806,11 @@ int launch_line_gather_ew(lssp_amd_ctx *c, const LineILU &li, int op, const doub
 #define LINE2_SW 4
 #endif
 // four levels per step (measured with leads 4 / 2 steps) are not instantiated
-template <int LV>
-constexpr int line2_d() { return LV == 4 ? 4 : LINE2_D; }
+#ifndef LINE2_D_U
+#define LINE2_D_U LINE2_D  // the loader lead of the natural-order-output sweeps (OUT 1)
+#endif
+template <int LV, int OUT = 2>
+constexpr int line2_d() { return LV == 4 ? 4 : OUT == 1 ? LINE2_D_U : LINE2_D; }
 #ifndef LINE2_DH_U
 #define LINE2_DH_U 2  // the poller lead of the sweeps with natural-order output (OUT 1): 2 with the near resync (U 311 -> 296 us, profiles/r05/r05r_line2_dh.txt)
 #endif
@@ -1813,7 +1819,7 @@ constexpr int line2_dh() { return LV == 4 ? 2 : OUT == 1 ? LINE2_DH_U : LINE2_DH
 template <int P, int LV, int NA, int OUT, bool TRACE, bool TL = false>
 static int launch_line2_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)
 {
-    auto kern = k_line2<P, LV, NA, OUT, LINE2_NL, line2_d<LV>(), line2_dh<LV, OUT>(), LINE2_SW, TRACE, TL>;
+    auto kern = k_line2<P, LV, NA, OUT, LINE2_NL, line2_d<LV, OUT>(), line2_dh<LV, OUT>(), LINE2_SW, TRACE, TL>;
     static int attr = 0;
     if (lds > attr) {
         LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -1830,7 +1836,7 @@ template <int P, int LV, int NA, int OUT>
 static int launch_line2_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a)
 {
     // (a sweep with natural-order output and the tail product reserves what the product needs)
-    constexpr int lds0 = l2::lds_bytes<NA, OUT, line2_d<LV>(), P, LV>();
+    constexpr int lds0 = l2::lds_bytes<NA, OUT, line2_d<LV, OUT>(), P, LV>();
     constexpr int ldst = OUT == 1 && lds0 < TAIL_LDS_BYTES(0) ? TAIL_LDS_BYTES(0) : lds0;
     static_assert(ldst <= 160 * 1024, "LDS");
     const int lds = a.tail ? ldst : lds0;
