@@ -152,7 +152,10 @@ __device__ __forceinline__ uint64_t poll_ready(const double *p, int *err)
             atomicOr(err, 4);
             return 0x7FF8000000000000ull;
         }
-        __builtin_amdgcn_s_sleep(1);
+#ifndef PK_SPIN_SLEEP
+#define PK_SPIN_SLEEP 1
+#endif
+        if (PK_SPIN_SLEEP) __builtin_amdgcn_s_sleep(PK_SPIN_SLEEP);
     }
 }
 
