@@ -1783,9 +1783,12 @@ int launch_line_gather_ew(lssp_amd_ctx *c, const LineILU &li, int op, const doub
     const LineSweep &ls = li.L;
     if (!line_gather_ew_ok(li, (long)ls.nx * ls.ny * ls.nz) || (op != GEW_BICG_P && op != GEW_BICG_S))
         return LSSP_AMD_EINVAL;
-    const int nq = (ls.tmax + LRHS2_RUN - 1) / LRHS2_RUN;
+#ifndef LRHS2_RUN_EW
+#define LRHS2_RUN_EW LRHS2_RUN
+#endif
+    const int nq = (ls.tmax + LRHS2_RUN_EW - 1) / LRHS2_RUN_EW;
     const long grid = 8L * ((ls.ntiles + 7) / 8) * nq;
-    auto kr = op == GEW_BICG_P ? k_line_rhs2<LRHS2_RUN, GEW_BICG_P> : k_line_rhs2<LRHS2_RUN, GEW_BICG_S>;
+    auto kr = op == GEW_BICG_P ? k_line_rhs2<LRHS2_RUN_EW, GEW_BICG_P> : k_line_rhs2<LRHS2_RUN_EW, GEW_BICG_S>;
     kr<<<grid, 256, 0, c->stream>>>(ls.d_tiles, ls.ntiles, nq, ls.nx, ls.ny, x, li.d_lstream, c->guard, y, out, scal);
     LSSP_HIP(hipGetLastError());
     li.lstream_of = out;
