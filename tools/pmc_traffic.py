@@ -14,6 +14,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 
@@ -34,7 +35,10 @@ def main(fetch_dir, write_dir, out):
     res = {}
     for k in find("k_spmv3<0, 0"):  # y = A x (any column coding)
         res["k_spmv3"] = int(2 * fe[k] + wr.get(k, 0))
-    line = find("k_line<") + find("k_line2<") + find("k_line_rhs")  # line sweeps: rhs gather + one L and one U launch
+    # line sweeps: the apply's plain rhs gather + one L and one U launch (not
+    # BiCGSTAB's p / s passes fused with the gather, k_line_rhs2<RUN, 1 | 2>)
+    gathers = [k for k in find("k_line_rhs") if "k_line_rhs<" in k or re.search(r"k_line_rhs2<\d+, 0>", k)]
+    line = find("k_line<") + find("k_line2<") + gathers
     if line:
         res["ilu_apply"] = int(sum(2 * fe[k] + wr.get(k, 0) for k in line))
     tri = find("k_tri_pk6")
