@@ -1968,22 +1968,26 @@ int launch_line_apply_spmv(lssp_amd_ctx *c, const LineILU &li, double *x, const 
                            int epi, double alpha, double beta, const double *y, double *z, int nred,
                            const double *w0, const double *w1)
 {
-    // Off by default: measured slower than the two steps (216^3 BiCGSTAB 531 vs
-    // 559 it/s, ILU(1) 328 vs 335; profiles/r05/r05c_tail_ab.txt): after the
+    // Off by default for ILU(0): measured slower than the two steps (216^3 BiCGSTAB 531 vs
+    // 559 it/s, ILU(1) 328 vs 335 at the time; profiles/r05/r05c_tail_ab.txt): after the
     // sweep the product moves ~0.75x k_spmv3's rows per us (one 1024-row round
     // per CU in flight, ~6 us each), and during the sweep rows become ready one
     // U tile row (all W tiles) at a time, so the freed workgroups cannot finish
     // the product before the two-step path would.  LSSP_AMD_TAIL=1 selects it
     // (A/B runs); =2: selected, and an ineligible call fails (EINVAL) instead of
     // falling back (tests)
+    // The ILU(1) sweeps (k_linef) run it by default: there it gains (216^3
+    // BiCGSTAB+ILU(1) 340.2 -> 352.4 it/s, bitwise; profiles/r05/r05v_tail_ilu1.txt);
+    // ILU(0) keeps the two steps, whose p / s passes carry the rhs gathers
+    // (628.9 against 559.7 it/s with the tail, same session).
     const char *te = getenv("LSSP_AMD_TAIL");
-    const int on = te ? atoi(te) : 0;
+    const int on = te ? atoi(te) : li.kind == 1 ? 1 : 0;
     const long pl = (long)li.g.nx * li.g.ny, n = pl * li.g.nz;
     // one rank: every chunk; P ranks: the halo-free chunks (the caller runs the rest)
     const bool dist = A && A->nhalo > 0;
     const long nall = num_chunks(n);
     const long cb = dist ? A->ich0 : 0, ce = dist ? A->ich1 : nall;
-    if (!on || li.kind > 1 || li.LV < 2 || li.ntiles == 0 || !A || (long)A->nrows != n || ce <= cb ||
+    if (!on || li.kind > 1 || li.g2 || li.LV < 2 || li.ntiles == 0 || !A || (long)A->nrows != n || ce <= cb ||
         (c->nranks > 1) != dist || A->ndiag == 0 || A->max_off_int > pl || nred < 0 || nred > 2 || x == z || !A->Ad ||
         n >= (1L << 28))  // (x is read through a buffer resource: byte offsets below 2^31)
         return on == 2 ? LSSP_AMD_EINVAL : LSSP_AMD_EUNSUPPORTED;
