@@ -1717,9 +1717,24 @@ __global__ __launch_bounds__(256) void k_line_rhs2(const LineTile *__restrict__ 
         } else {
             v[it] = 0.0;
             if (ok) {
+#if !defined(GEW_TEMPORAL_LOADS)
+                // non-temporal operand loads (r, p, v, read once here): 216^3
+                // 645.9 -> 658.4 it/s, profiles/r05/r05x_xr_nt_ab.txt; the
+                // natural-order output stays temporal (a non-temporal store
+                // measured no better).  -DGEW_TEMPORAL_LOADS: plain loads (A/B)
+                if (OP == GEW_BICG_P)
+                    v[it] = __builtin_nontemporal_load(rhs + r) +
+                            c0 * (__builtin_nontemporal_load(nat + r) - c1 * __builtin_nontemporal_load(y + r));
+                else v[it] = __builtin_nontemporal_load(rhs + r) - c0 * __builtin_nontemporal_load(y + r);
+#else
                 if (OP == GEW_BICG_P) v[it] = rhs[r] + c0 * (nat[r] - c1 * y[r]);
                 else v[it] = rhs[r] - c0 * y[r];
+#endif
+#if defined(GEW_NT_STORE)  // tuning builds: the natural-order output non-temporal too
+                __builtin_nontemporal_store(v[it], nat + r);
+#else
                 nat[r] = v[it];
+#endif
             }
         }
     }
