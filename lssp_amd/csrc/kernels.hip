@@ -871,7 +871,12 @@ __global__ __launch_bounds__(256) void k_ew(EwArgs g)
                                  tv = __builtin_nontemporal_load(g.v + i);
                     w0 = true, o0 = xo + alpha * xp + omega * xs;
                     __builtin_nontemporal_store(o0, g.out0 + i);
+#ifdef EW_XR_RNT  // tuning builds: r stored non-temporal too
+                    w1 = true, o1 = su - omega * tv;
+                    __builtin_nontemporal_store(o1, g.out1 + i);
+#else
                     w1 = true, g.out1[i] = o1 = su - omega * tv;
+#endif
 #else
                     const double xo = g.out0[i], xp = g.x[i], xs = g.y[i], su = g.u[i], tv = g.v[i];
                     w0 = true, g.out0[i] = o0 = xo + alpha * xp + omega * xs;

@@ -1476,7 +1476,11 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                         if (!(a.diag & 1) && p < np && l < nj && (unsigned)i < (unsigned)nx) {
                             double *o = a.out + (a.mirror ? nb(p, l) - i : nb(p, l) + i);
                             if (tail) st_sc1d(o, x);  // read by the tail product on other CUs
+#ifdef LINE2_OUT_NT  // tuning builds: the natural-order output as non-temporal stores
+                            else __builtin_nontemporal_store(x, o);
+#else
                             else *o = x;
+#endif
                         }
                     }
                 };
