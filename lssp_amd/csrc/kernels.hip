@@ -843,12 +843,26 @@ __global__ __launch_bounds__(256) void k_ew(EwArgs g)
             case EW_SCALE: w0 = true, g.out0[i] = o0 = g.out0[i] * g.a; break;
             case EW_DIVS: w0 = true, g.out0[i] = o0 = g.out0[i] / g.scal[g.sidx]; break;
             case EW_DOT: break;
+#ifdef EW_PS_NT  // tuning builds: the p / s passes' operands as non-temporal loads
+            case EW_BICG_P: {
+                const double beta = g.scal[S_BETA], omega = g.scal[S_OMEGA];
+                w0 = true, g.out0[i] = o0 = __builtin_nontemporal_load(g.x + i) +
+                                           beta * (__builtin_nontemporal_load(g.out0 + i) -
+                                                   omega * __builtin_nontemporal_load(g.y + i));
+                break;
+            }
+            case EW_BICG_S:
+                w0 = true, g.out0[i] = o0 = __builtin_nontemporal_load(g.x + i) -
+                                           g.scal[S_ALPHA] * __builtin_nontemporal_load(g.y + i);
+                break;
+#else
             case EW_BICG_P: {
                 const double beta = g.scal[S_BETA], omega = g.scal[S_OMEGA];
                 w0 = true, g.out0[i] = o0 = g.x[i] + beta * (g.out0[i] - omega * g.y[i]);
                 break;
             }
             case EW_BICG_S: w0 = true, g.out0[i] = o0 = g.x[i] - g.scal[S_ALPHA] * g.y[i]; break;
+#endif
             case EW_BICG_XR: {
                 const double alpha = g.scal[S_ALPHA];
                 if (g.scal[S_BREAK] != 0.0) {
