@@ -937,7 +937,11 @@ __global__ __launch_bounds__(256) void k_linef_rhs(const LineTile *__restrict__ 
         const int lv = q0 + m, i = lv - 2 * l - p - sig(p), j = d.j0 + l - d.k0 - p;
         const bool ok = lv < d.T && p < d.np && l < d.nj && (unsigned)j < (unsigned)ny && (unsigned)i < (unsigned)nx;
         const long r = ((long)(d.k0 + p) * ny + j) * nx + i;
+#ifdef LFRHS_NT  // tuning builds: the apply's rhs read non-temporal
+        v[it] = ok ? __builtin_nontemporal_load(rhs + (mirror ? n - 1 - r : r)) : 0.0;
+#else
         v[it] = ok ? rhs[mirror ? n - 1 - r : r] : 0.0;
+#endif
         o[it] = ok ? d.cbase + (long)lv * P * d.nj + p * d.nj + l : -1;
     }
 #pragma unroll

@@ -1717,7 +1717,11 @@ __global__ __launch_bounds__(256) void k_line_rhs2(const LineTile *__restrict__ 
         const bool ok = q0 + m < d.T && p < d.np && l < d.nj && (unsigned)i < (unsigned)nx;
         const long r = ((long)(d.k0 + p) * ny + (d.j0 + l)) * nx + i;
         if (OP == 0) {
+#ifdef LRHS2_NT  // tuning builds: the apply's rhs read non-temporal
+            v[it] = ok ? __builtin_nontemporal_load(rhs + r) : 0.0;
+#else
             v[it] = ok ? rhs[r] : 0.0;
+#endif
         } else {
             v[it] = 0.0;
             if (ok) {
