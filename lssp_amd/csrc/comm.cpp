@@ -229,10 +229,13 @@ int comm_destroy(lssp_amd_ctx *c)
 int comm_gather_int(lssp_amd_ctx *c, int v, std::vector<int> &all)
 {
     all.assign(c->nranks, INT_MIN);
-    if (c->nranks <= 1 || !c->d_igather) {
+    if (c->nranks <= 1) {
         all.assign(c->nranks, v);
         return LSSP_AMD_OK;
     }
+    // P ranks without the scratch: lssp_amd_comm_init failed part-way; no
+    // agreement can be reported that never happened
+    if (!c->d_igather) return LSSP_AMD_EHIP;
     (void)hipSetDevice(c->device);
     int *d = c->d_igather;  // [mine | all ranks]
     if (hipMemcpyAsync(d, &v, sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess) {

@@ -253,7 +253,7 @@ __global__ __launch_bounds__(1024) void k_dot_serial(SerialArgs g, long n, int n
                                                      const double *guard)
 {
     if (guard && *guard != 0.0) return;
-    __shared__ double buf[2][MAX_SLOTS][SER_C];
+    __shared__ __attribute__((aligned(16))) double buf[2][MAX_SLOTS][SER_C];  // read as double2
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const long nch = (n + SER_C - 1) / SER_C;
     const bool producer = (wave & 3) != 0;
@@ -714,8 +714,9 @@ int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, c
     LSSP_TRY(ensure_part(c, nall));
     if (ce < 0) ce = nall;
     if (cb < 0 || cb > ce || ce > nall) return LSSP_AMD_EINVAL;
-    // three fused dots (BiCGSTAB's t = A sh with t.s, t.t, s.s): EPI_AMX on k_spmv3 only
-    if (nred == 3 && (epi != EPI_AMX || A->d_win || !w0 || w0 == z || w1)) return LSSP_AMD_EINVAL;
+    // three fused dots (BiCGSTAB's t = A sh with t.s, t.t, s.s): EPI_AMX on k_spmv3
+    // only -- a windowed matrix keeps its CSR resident, so k_spmv3 serves it
+    if (nred == 3 && (epi != EPI_AMX || !w0 || w0 == z || w1)) return LSSP_AMD_EINVAL;
     const long nb = ce - cb;
     if (nb == 0) return LSSP_AMD_OK;
     SpmvArgs a{A->nrows, A->Ap, A->Aj, A->Ax, x, y, z, alpha, beta, w0, w1, c->d_part, c->part_cap,
@@ -731,7 +732,7 @@ int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, c
             a.pw = pw;
         }
     }
-    if (A->d_win && nb == nall) {
+    if (A->d_win && nb == nall && nred <= 2) {
         switch (epi) {
         case EPI_MXY: spmv_sell_dispatch<EPI_MXY>(a, A, nred, c->stream); break;
         case EPI_AMXY: spmv_sell_dispatch<EPI_AMXY>(a, A, nred, c->stream); break;

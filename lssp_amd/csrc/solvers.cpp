@@ -52,6 +52,9 @@ struct Run {
     ~Run()
     {
         (void)hipStreamSynchronize(c->stream);
+        // the gathered-stream cache lives only between a p / s pass and the
+        // apply right after it; an error exit between the two must not leave it
+        if (M) M->line.lstream_of = nullptr;
         for (double *p : bufs)
             for (auto &w : c->pool)
                 if (w.p == p) w.used = false;
@@ -2262,6 +2265,7 @@ extern "C" int lssp_amd_solve(lssp_amd_ctx *c, const lssp_amd_mat *A, const lssp
     R.c = c;
     R.A = A;
     R.M = M;
+    if (M) M->line.lstream_of = nullptr;
     R.gpc = gpc;
     R.n = A->nrows;
     R.nx = (long)A->nrows + A->nhalo;

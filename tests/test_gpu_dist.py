@@ -276,11 +276,17 @@ def test_multirank_on_one_gpu_equals_oracle_prank_mode(world, N, solver):
     assert np.array_equal(x, o.x)
 
 
+@pytest.mark.parametrize("tail", ["default", "2"], ids=["tail-default", "tail-forced"])
 @pytest.mark.parametrize("world,N", [(2, 16), (4, 16)])
-def test_multirank_ilu1_line_sweeps_equal_oracle_prank_mode(world, N):
+def test_multirank_ilu1_line_sweeps_equal_oracle_prank_mode(world, N, tail, monkeypatch):
     """block-Jacobi ILU(1) (the reference's default level) per rank: each whole-plane
     slab's factor runs on the skewed line sweeps; BiCGSTAB in tree order equals the
-    oracle's P-rank mode bit for bit"""
+    oracle's P-rank mode bit for bit.  LSSP_AMD_TAIL=2 (inherited by the spawned
+    ranks) makes an ineligible tail product fail instead of falling back, so the
+    forced case proves the distributed tail (halo-free chunks in the U sweep, then
+    spmv_boundary) ran."""
+    if tail != "default":
+        monkeypatch.setenv("LSSP_AMD_TAIL", tail)
     nits, res, trace, y, x = _run(world, N, "bicgstab", O.TREE, level=1)
     A = O.poisson(3, N)
     L, U = O.ilu(A, "iluk", level=1, blk=(A.n + world - 1) // world)

@@ -196,3 +196,49 @@ def test_bicgstab_breakdown_without_pc_bitwise_vs_oracle(dev, mode, n):
     assert _same([r.residual], [o.residual])
     assert _same(r.trace, o.trace)
     assert _same(x.download(), o.x)
+
+
+def _grid_plus_far_couplings(N=20, seed=5):
+    """The 7-pt N^3 grid with two weak couplings per row at offsets +-(N^2+1 ..
+    N^2+900): > 255 distinct offsets (no diagonal-id coding) while every 1024-row
+    block spans < 16 K columns, so the matrix is served windowed (k_spmv_sell)."""
+    import lssp_amd
+    Ap, Aj, Ax = lssp_amd.poisson(3, N)
+    n = Ap.size - 1
+    rng = np.random.default_rng(seed)
+    rows = []
+    for i in range(n):
+        cols = {int(Aj[k]): float(Ax[k]) for k in range(Ap[i], Ap[i + 1])}
+        for sgn in (-1, 1):
+            c = i + sgn * (N * N + 1 + int(rng.integers(0, 900)))
+            if 0 <= c < n and c not in cols:
+                cols[c] = -1e-3 * float(rng.random())
+        rows.append(sorted(cols.items()))
+    return (Ap, Aj, Ax), _csr_rows(rows, n)
+
+
+def test_windowed_matrix_with_grid_line_sweep_preconditioner(dev):
+    """BiCGSTAB in TREE mode with a windowed A and a grid ILU(0) M: the fused
+    p / s gather passes move ||s||^2 into t = A sh's third dot, which the
+    windowed product does not carry -- k_spmv3 serves that call (ADVICE r05:
+    this combination used to fail with EINVAL)."""
+    import lssp_amd
+    (gp, gj, gx), (Ap, Aj, Ax) = _grid_plus_far_couplings()
+    n = Ap.size - 1
+    A = lssp_amd.DMat(dev, Ap, Aj, Ax)
+    assert A.ndiag == 0 and A.windowed
+    M = lssp_amd.DILU.create(dev, gp, gj, gx, kind=lssp_amd.ILUK, level=0)
+    assert M.sweep_layout()[0] == 1  # the grid line sweeps
+    b = uniform(77, n)
+    x = dev.vec(n, np.zeros(n))
+    r = lssp_amd.solve(dev, A, M, x, dev.vec(n, b), solver=lssp_amd.BICGSTAB, tol_rel=1e-10, tol_abs=1e-12,
+                       tol_rb=0.0, maxit=60, trace_cap=10000)
+    (Lp, Lj, Lx), (Up, Uj, Ux) = M.factors()
+    o = O.solve(O.BICGSTAB, O.CSR(n, Ap, Aj, Ax), b, L=O.CSR(n, Lp, Lj, Lx), U=O.CSR(n, Up, Uj, Ux),
+                rtol=1e-10, atol=1e-12, rbtol=0.0, maxit=60, mode=O.TREE)
+    assert r.nits == o.nits
+    assert r.residual == o.residual
+    assert np.array_equal(r.trace, o.trace)
+    assert np.array_equal(x.download(), o.x)
+    M.close()
+    A.close()

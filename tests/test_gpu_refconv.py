@@ -118,7 +118,7 @@ def test_tree_mode_512_bicgstab_converges():
     assert true_res <= TRUE_FACTOR * scale
 
 
-SERIAL_CASES = [c for c in FULL if c["solver"] == 4 and c["N"] == 216]
+SERIAL_CASES = [c for c in FULL if c["solver"] == 4 and c["N"] in (216, 256)]
 
 
 @pytest.mark.timeout(900)

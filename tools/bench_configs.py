@@ -2,7 +2,7 @@
 
     python tools/bench_configs.py cg-thermal   [--iters 1000] [--ref-iters 1000]
     python tools/bench_configs.py gmres-ilut   [--grid 256]   [--ref-iters 30]
-    python tools/bench_configs.py bicgstab-iluk --grid 512     (config 4's matrix on one GPU)
+    python tools/bench_configs.py bicgstab-iluk [--grid 256]  (config 2; --grid 512: config 4's matrix on one GPU)
     python tools/bench_configs.py general-ilu  [--grid 216]   (the packet-sweep ILU path)
 
 Each prints ONE JSON line: GPU throughput (Krylov it/s with HIP-event SpMV
@@ -31,7 +31,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0
+from bench import HBM_PEAK_GBS, ilu_apply_bytes, spmv_bytes  # noqa: E402  (one byte accounting)
+
 T0 = time.perf_counter()
 
 
@@ -58,9 +59,12 @@ def spmv_leg(dev, A, nnz, n, reps=50):
     e1.record(s)
     e1.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    b = 12 * nnz + 20 * n + 4
+    # the bytes the kernel moves (1-byte diagonal ids on coded stencils) and the
+    # int32-CSR equivalent, as bench.py reports them
+    b = spmv_bytes(nnz, n, coded=A.ndiag > 0)
+    b32 = spmv_bytes(nnz, n)
     return {"ms": round(ms, 5), "GBps": round(b / ms / 1e6, 1), "frac_hbm_peak": round(b / ms / 1e6 / HBM_PEAK_GBS, 4),
-            "bytes": b}
+            "bytes": b, "csr_int32_equiv_GBps": round(b32 / ms / 1e6, 1)}
 
 
 def apply_leg(dev, M, n, reps=5):
@@ -75,9 +79,9 @@ def apply_leg(dev, M, n, reps=5):
     e1.synchronize()
     M.check()
     ms = e0.elapsed_time(e1) / reps
-    b = 12 * (M.nnzL + M.nnzU) + 8 * (n + 1) + 32 * n
-    return {"ms": round(ms, 4), "GBps": round(b / ms / 1e6, 1), "bytes": b, "levels_L": M.levelsL,
-            "levels_U": M.levelsU}
+    b = ilu_apply_bytes(M.nnzL, M.nnzU, n)  # SURVEY 8(d) B_ilu, the bytes bench.py's roofline uses
+    return {"ms": round(ms, 4), "GBps": round(b / ms / 1e6, 1), "frac_hbm_peak": round(b / ms / 1e6 / HBM_PEAK_GBS, 4),
+            "bytes": b, "levels_L": M.levelsL, "levels_U": M.levelsU}
 
 
 def timed_solve(dev, A, M, n, solver, iters, restart=30, reduction=None):
@@ -181,7 +185,12 @@ def gmres_ilut(args):
 
 
 def bicgstab_iluk(args):
+    """configs 2 (256^3, one GPU) and 4's matrix on one GPU (512^3): BiCGSTAB +
+    ILUK(0), tree reductions, zero tolerances (exactly --iters iterations), then
+    a solve to the reference's default tolerances; with the reference built, its
+    own CPU time on a bounded sample (--ref-iters iterations, 1 core)."""
     import lssp_amd
+    import oracle as O
     N = args.grid
     Ap, Aj, Ax = lssp_amd.poisson(3, N)
     n, nnz = Ap.size - 1, int(Ap[-1])
@@ -195,13 +204,28 @@ def bicgstab_iluk(args):
            "ilu_setup_s": round(t_pc, 2), "spmv": spmv_leg(dev, A, nnz, n), "ilu_apply": apply_leg(dev, M, n)}
     timed_solve(dev, A, M, n, lssp_amd.BICGSTAB, 3)
     r, t = timed_solve(dev, A, M, n, lssp_amd.BICGSTAB, args.iters)
-    out["gpu"] = {"iters": r.nits, "iters_per_s": round(r.nits / t, 2), "ms_per_iter": round(t / r.nits * 1e3, 4)}
+    out["gpu"] = {"iters": r.nits, "iters_per_s": round(r.nits / t, 2), "ms_per_iter": round(t / r.nits * 1e3, 4),
+                  "reduction": "tree"}
     x = dev.vec(n, np.zeros(n))
     b = dev.vec(n, np.ones(n))
+    dev.sync()
+    t0 = time.perf_counter()
     r = lssp_amd.solve(dev, A, M, x, b, solver=lssp_amd.BICGSTAB, maxit=5000)
-    out["converged"] = {"nits": r.nits, "residual": r.residual}
+    dev.sync()
+    out["converged"] = {"nits": r.nits, "residual": r.residual, "seconds": round(time.perf_counter() - t0, 3),
+                        "reference_nits": {216: 145, 256: 155}.get(N)}
+    print(json.dumps(out), flush=True)  # GPU half first
+    if args.ref_iters > 0 and O.ref_available():
+        log(f"reference: {args.ref_iters} iterations on 1 core")
+        ref = O.ref_solve(O.BICGSTAB, O.CSR(n, Ap, Aj, Ax), np.ones(n), rtol=0.0, atol=0.0, rbtol=0.0,
+                          maxit=args.ref_iters, pc=O.PC_ILUK, level=0)
+        out["cpu_baseline"] = {"value": round(ref.nits / ref.t_solve, 4), "unit": "iters/s", "cores": 1,
+                               "kind": "reference",
+                               "sample": f"reference lssp_solver_solve, {ref.nits} iterations in {ref.t_solve:.2f} s "
+                                         f"(PC setup {ref.t_setup:.2f} s)"}
+        out["vs_cpu"] = round(out["gpu"]["iters_per_s"] / out["cpu_baseline"]["value"], 1)
+        print(json.dumps(out), flush=True)
     dev.close()
-    print(json.dumps(out), flush=True)
 
 
 def general_ilu(args):
@@ -288,7 +312,8 @@ def main():
         args.grid = 216 if args.grid == 256 else args.grid
         general_ilu(args)
     else:
-        args.iters = min(args.iters, 50)
+        args.iters = min(args.iters, 100)
+        args.ref_iters = (3 if args.grid <= 256 else 0) if args.ref_iters is None else args.ref_iters
         bicgstab_iluk(args)
 
 

@@ -15,7 +15,8 @@
 #   quick=PATH       the same with a 120 s per-test limit and -x (new kernels)
 #   project512       tools/project_ranks.py --grid 512 --ranks 1,8 -> project_ranks_512.jsonl
 #   project216       tools/project_ranks.py --grid 216 --ranks 1,2,4,8 -> project_ranks_216.jsonl
-#   config3 / config5 / general   tools/bench_configs.py gmres-ilut / cg-thermal / general-ilu
+#   config2 / config3 / config5 / general   tools/bench_configs.py bicgstab-iluk --grid 256 /
+#                    gmres-ilut / cg-thermal / general-ilu
 #   linediag=N[:LIB] tools/line_diag.py N 0 (optionally with LSSP_AMD_LIB=build/LIB.so)
 #   linetrace=N      tools/line_trace.py N 150 -> line_trace_N.txt
 #   pk6trace=N       tools/pk6_trace.py N 60 ilut -> pk6_trace_N.txt
@@ -69,6 +70,10 @@ for step in "$@"; do
   config3)
     timeout -k 10 900 python -u tools/bench_configs.py gmres-ilut > $O/config3.json 2> $O/config3.err || { tail -20 $O/config3.err; fail $step $?; }
     tail -c 600 $O/config3.json
+    ;;
+  config2)
+    timeout -k 10 600 python -u tools/bench_configs.py bicgstab-iluk --grid 256 > $O/config2.json 2> $O/config2.err || { tail -20 $O/config2.err; fail $step $?; }
+    tail -c 900 $O/config2.json
     ;;
   config5)
     timeout -k 10 300 python -u tools/bench_configs.py cg-thermal > $O/config5.json 2> $O/config5.err || { tail -20 $O/config5.err; fail $step $?; }
