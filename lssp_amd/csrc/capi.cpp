@@ -374,6 +374,9 @@ int lssp_amd_ctx_create(int device, lssp_amd_ctx **out)
     LSSP_HIP(hipHostMalloc(&c->h_scal, sizeof(double) * NSCAL, hipHostMallocDefault));
     LSSP_HIP(hipMalloc(&c->d_err, sizeof(int)));
     LSSP_HIP(hipMemset(c->d_err, 0, sizeof(int)));
+    LSSP_HIP(hipHostMalloc(&c->h_snap, sizeof(double) * 2 * (S_H + S_HB), hipHostMallocDefault));
+    LSSP_HIP(hipHostMalloc(&c->h_snap_err, sizeof(int) * 2, hipHostMallocDefault));
+    for (auto &e : c->ev_snap) LSSP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     const char *m = getenv("LSSP_AMD_REDUCE");
     if (m && !strcmp(m, "serial")) c->reduce_mode = LSSP_AMD_REDUCE_SERIAL;
     *out = c;
@@ -394,6 +397,10 @@ int lssp_amd_ctx_destroy(lssp_amd_ctx *c)
     if (c->d_rcnt) (void)hipFree(c->d_rcnt);
     (void)hipHostFree(c->h_scal);
     (void)hipFree(c->d_err);
+    if (c->h_snap) (void)hipHostFree(c->h_snap);
+    if (c->h_snap_err) (void)hipHostFree(c->h_snap_err);
+    for (auto e : c->ev_snap)
+        if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return LSSP_AMD_OK;

@@ -29,7 +29,8 @@ enum Scal {
     S_RHO0 = 0, S_RHO1, S_ALPHA, S_BETA, S_OMEGA, S_RES, S_SNORM, S_BREAK, S_BNORM, S_TMP,
     S_DONE, S_TOL, S_NIT,  // batched iterations (solvers.cpp cg): stop flag, tolerance, iterations run
     S_SUM0 = 16,   // raw reduced sums of the last reduction
-    S_H = 32,      // GMRES Hessenberg column (up to NSCAL - 32 entries)
+    S_H = 32,      // GMRES Hessenberg column (up to NSCAL - 32 entries); batched residual history ring
+    S_HB = 32,     // ... of S_HB entries: iteration k's residual at S_H + k % S_HB (two batches in flight)
 };
 
 // finalize programs run by one lane after a reduction (same code for every
@@ -42,13 +43,13 @@ enum FinOp {
     FIN_BICG_S,          // snorm = sqrt(s0); break = snorm <= 1e-40
     FIN_BICG_OMEGA,      // omega = s0 / s1
     FIN_BICG_RES_RHO,    // res = sqrt(s0); then FIN_BICG_RHO on s1
-    FIN_BICG_RES_RHO_B,  // FIN_BICG_RES_RHO, then res -> history S_H + nit, nit += 1, done = 2 breakdown
+    FIN_BICG_RES_RHO_B,  // FIN_BICG_RES_RHO, then res -> history S_H + nit % S_HB, nit += 1, done = 2 breakdown
                          // (S_BREAK), 1 res <= tol, 3 the next iteration's rho1 == 0
     FIN_CG_RHO,          // rho1 = s0; beta = rho1 / rho0
     FIN_CG_ALPHA,        // alpha = rho1 / s0; rho0 = rho1
     FIN_CG_RES,          // res = sqrt(s0)
     FIN_CG_RES_RHO,      // res = sqrt(s0); rho1 = s0; beta = rho1/rho0  (PC_NON: z == r)
-    FIN_CG_RES_RHO_B,    // FIN_CG_RES_RHO, then res -> history S_H + nit, nit += 1, done = res <= tol
+    FIN_CG_RES_RHO_B,    // FIN_CG_RES_RHO, then res -> history S_H + nit % S_HB, nit += 1, done = res <= tol
     FIN_BICG_S_OMEGA,    // sums (t.s, t.t, s.s): FIN_BICG_S on s2 (traced at tpos[2]), then FIN_BICG_OMEGA
 };
 
@@ -77,6 +78,12 @@ struct lssp_amd_ctx {
     double *d_trace = nullptr; // device trace buffer
     long trace_cap = 0;
     int *d_err = nullptr;      // error word (trisolve timeouts)
+    // batched iterations: the stream copies each batch's scalars and error word
+    // into snapshot k (pinned) and records ev_snap[k], so the host reads batch
+    // j while batch j + 1 runs (solvers.cpp Pipe)
+    double *h_snap = nullptr;  // [2][S_H + S_HB]
+    int *h_snap_err = nullptr; // [2]
+    hipEvent_t ev_snap[2] = {nullptr, nullptr};
     // while set: every k_ew / k_spmv3 / reduction launch returns at once when
     // *guard != 0 (batched iterations past the one that converged)
     const double *guard = nullptr;

@@ -101,7 +101,7 @@ __device__ void finalize(const Fin &f, const double *s, double *scal, double *tr
         scal[S_RHO0] = rho1;
         if (f.op == FIN_BICG_RES_RHO_B) {  // :117 / :149 / :89 decided here; the host reads the batch afterwards
             const int k = (int)scal[S_NIT];
-            scal[S_H + k] = t0;
+            scal[S_H + k % S_HB] = t0;
             scal[S_NIT] = k + 1;
             if (scal[S_BREAK] != 0.0) scal[S_DONE] = 2.0;
             else if (t0 <= scal[S_TOL]) scal[S_DONE] = 1.0;
@@ -138,7 +138,7 @@ __device__ void finalize(const Fin &f, const double *s, double *scal, double *tr
         scal[S_BETA] = s[0] / scal[S_RHO0];
         if (f.op == FIN_CG_RES_RHO_B) {  // :109 decided here; the host reads the batch afterwards
             const int k = (int)scal[S_NIT];
-            scal[S_H + k] = t0;
+            scal[S_H + k % S_HB] = t0;
             scal[S_NIT] = k + 1;
             if (t0 <= scal[S_TOL]) scal[S_DONE] = k + 1;  // the stamp of k_cg_fused's deferred x update
         }

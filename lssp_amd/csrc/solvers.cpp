@@ -159,6 +159,43 @@ struct Run {
         }
         return LSSP_AMD_OK;
     }
+    // batched iterations, two batches in flight: the stream copies the scalar
+    // slots (0 .. S_H + S_HB: the stop flag, the iteration count and the residual
+    // history ring) and the error word of the batch just queued into snapshot k
+    // and records ev_snap[k]; the host queues the next batch and only then waits
+    // for snapshot k, so the GPU runs batch j + 1 while the host reads batch j
+    // (the launches past a stop return at once: ctx guard)
+    int snap_issue(int k)
+    {
+        LSSP_HIP(hipMemcpyAsync(c->h_snap + k * (S_H + S_HB), c->d_scal, sizeof(double) * (S_H + S_HB),
+                                hipMemcpyDeviceToHost, c->stream));
+        LSSP_HIP(hipMemcpyAsync(c->h_snap_err + k, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        LSSP_HIP(hipEventRecord(c->ev_snap[k], c->stream));
+        return LSSP_AMD_OK;
+    }
+    int snap_wait(int k)
+    {
+        LSSP_HIP(hipEventSynchronize(c->ev_snap[k]));
+        memcpy(c->h_scal, c->h_snap + k * (S_H + S_HB), sizeof(double) * (S_H + S_HB));
+        if (c->h_snap_err[k]) {
+            LSSP_HIP(hipStreamSynchronize(c->stream));  // the batch queued after it runs out first
+            LSSP_HIP(hipMemset(c->d_err, 0, sizeof(int)));
+            if (M && M->line.ntiles) LSSP_TRY(line_rearm(c, const_cast<lssp_amd_ilu *>(M)->line));
+            LSSP_HIP(hipStreamSynchronize(c->stream));
+            return LSSP_AMD_ETIMEOUT;
+        }
+        return LSSP_AMD_OK;
+    }
+    // start a batched run: stop flag 0, tolerance, iteration count 0
+    int batch_begin(double tol)
+    {
+        c->h_scal[S_DONE] = 0.0;
+        c->h_scal[S_TOL] = tol;
+        c->h_scal[S_NIT] = 0.0;
+        LSSP_HIP(hipMemcpyAsync(c->d_scal + S_DONE, c->h_scal + S_DONE, 3 * sizeof(double), hipMemcpyHostToDevice,
+                                c->stream));
+        return LSSP_AMD_OK;
+    }
     double h(int i) const { return c->h_scal[i]; }
     int spmv(int epi, double alpha, double *x, double beta, const double *y, double *z, int nred = 0,
              const double *w0 = nullptr, const double *w1 = nullptr)
@@ -350,52 +387,69 @@ int bicgstab(Run &R, const lssp_amd_solve_params &P, double *x, const double *b,
         // batches and the stop tests run on the device (FIN_BICG_RES_RHO_B:
         // breakdown :117, res <= tol :149, rho1 == 0 :89 of the next); the
         // launches past the stop return at once (ctx guard), and the host reads a
-        // batch's residuals with one round trip.  Same kernels, same arithmetic.
+        // batch's residuals from its snapshot while the next batch runs
+        // (Run::snap_issue).  Same kernels, same arithmetic.
         constexpr int BATCH = 8;
+        static_assert(2 * BATCH <= S_HB, "two batches in the residual history ring");
         lssp_amd_ctx *c = R.c;
-        it = 0;
-        bool stop = false;
-        while (it < maxit && !stop) {
-            const int nb = std::min(BATCH, maxit - it);
-            c->h_scal[S_DONE] = 0.0;
-            c->h_scal[S_TOL] = tol;
-            c->h_scal[S_NIT] = 0.0;
-            LSSP_HIP(hipMemcpyAsync(c->d_scal + S_DONE, c->h_scal + S_DONE, 3 * sizeof(double),
-                                    hipMemcpyHostToDevice, c->stream));
+        struct Batch {
+            int it0 = 0, nb = 0;
             long tl_after[BATCH], pos_s[BATCH];
+        } bq[2];
+        int queued = 0, nq = 0, nr = 0;  // iterations queued, batches queued, batches read
+        auto push = [&]() -> int {
+            Batch &B = bq[nq & 1];
+            B.it0 = queued;
+            B.nb = std::min(BATCH, maxit - queued);
             c->guard = c->d_scal + S_DONE;
             int st = LSSP_AMD_OK;
-            for (int j = 0; j < nb && st == LSSP_AMD_OK; j++) {
-                st = enqueue(it + j, FIN_BICG_RES_RHO_B, &pos_s[j]);
-                tl_after[j] = R.tl;
+            for (int j = 0; j < B.nb && st == LSSP_AMD_OK; j++) {
+                st = enqueue(queued + j, FIN_BICG_RES_RHO_B, &B.pos_s[j]);
+                B.tl_after[j] = R.tl;
             }
             c->guard = nullptr;
             LSSP_TRY(st);
-            LSSP_TRY(R.sync(0, S_H + nb));
-            const int ran = std::max(1, std::min(nb, (int)R.h(S_NIT)));
+            LSSP_TRY(R.snap_issue(nq & 1));
+            queued += B.nb;
+            nq++;
+            return LSSP_AMD_OK;
+        };
+        it = 0;
+        LSSP_TRY(R.batch_begin(tol));
+        LSSP_TRY(push());
+        for (;;) {
+            if (queued < maxit) LSSP_TRY(push());  // runs while the batch before it is read
+            const Batch &B = bq[nr & 1];
+            LSSP_TRY(R.snap_wait(nr & 1));
+            nr++;
+            auto hist = [&](int q) { return R.h(S_H + (B.it0 + q) % S_HB); };
+            const int ran = std::max(1, std::min(B.nb, (int)R.h(S_NIT) - B.it0));
             const int code = (int)R.h(S_DONE);
-            for (int q = 0; q < ran - (code == 2 ? 1 : 0); q++) itr_line(it + q, R.h(S_H + q));
-            res = R.h(S_H + ran - 1);
+            for (int q = 0; q < ran - (code == 2 ? 1 : 0); q++) itr_line(it + q, hist(q));
+            res = hist(ran - 1);
             pending_rho = true;
             if (code == 2) {  // breakdown in iteration it + ran - 1
                 it += ran - 1;
                 pending_rho = false;
-                LSSP_TRY(breakdown(pos_s[ran - 1]));
-                stop = true;
+                LSSP_TRY(breakdown(B.pos_s[ran - 1]));
+                break;
             } else if (code == 1) {  // converged
-                R.tl = tl_after[ran - 1];
+                R.tl = B.tl_after[ran - 1];
                 it += ran - 1;
-                stop = true;
+                break;
             } else if (code == 3) {  // the next iteration's rho1 == 0
-                R.tl = tl_after[ran - 1];
+                R.tl = B.tl_after[ran - 1];
                 it += ran;
                 pending_rho = false;
-                if (it < maxit && R.rank == 0) lprint("bicgstab: method failed.!\n");
-                if (it < maxit) stop = true;
-                else pending_rho = true;
+                if (it < maxit) {
+                    if (R.rank == 0) lprint("bicgstab: method failed.!\n");
+                    break;
+                }
+                pending_rho = true;
             } else {
-                it += nb;
+                it += B.nb;
             }
+            if (nr == nq) break;  // maxit
         }
     } else {
         for (it = 0; it < maxit; it++) {
@@ -470,31 +524,32 @@ int cg(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *
         // PC_NON: iterations are queued in batches and the stop
         // test :109 runs on the device (FIN_CG_RES_RHO_B); the launches of the
         // iterations after the one that converged return at once (ctx guard),
-        // and the host reads a batch's residuals with ONE round trip instead of
-        // one per iteration.  Same kernels, same arithmetic.
+        // and the host reads a batch's residuals from its snapshot while the
+        // next batch runs (Run::snap_issue).  Same kernels, same arithmetic.
         constexpr int BATCH = 16;
+        static_assert(2 * BATCH <= S_HB, "two batches in the residual history ring");
         lssp_amd_ctx *c = R.c;
         const bool fuse_l2 = R.tree && c->nranks == 1 && R.n > 0;
-        it = 0;
-        bool stop = false;
-        while (it < maxit && !stop) {
-            const int nb = std::min(BATCH, maxit - it);
-            c->h_scal[S_DONE] = 0.0;
-            c->h_scal[S_TOL] = tol;
-            c->h_scal[S_NIT] = 0.0;
-            LSSP_HIP(hipMemcpyAsync(c->d_scal + S_DONE, c->h_scal + S_DONE, 3 * sizeof(double),
-                                    hipMemcpyHostToDevice, c->stream));
+        struct Batch {
+            int it0 = 0, nb = 0;
             long tl_after[BATCH];
+        } bq[2];
+        int queued = 0, nq = 0, nr = 0;  // iterations queued, batches queued, batches read
+        auto push = [&]() -> int {
+            Batch &B = bq[nq & 1];
+            B.it0 = queued;
+            B.nb = std::min(BATCH, maxit - queued);
             c->guard = c->d_scal + S_DONE;
             int st = LSSP_AMD_OK;
             // one rank, tree reductions: each reduction's level 2 runs inside
             // the vector update that consumes it (k_cg_fused): q.p (partial
             // row 0, from the product) in the x/r update, r.r (row 1) in the
-            // next iteration's p update; the batch's last r.r on its own
+            // next iteration's p update; the batch's last r.r on its own.
+            // Stamps are global iteration counts (FIN_CG_RES_RHO_B's S_DONE)
             Fin held;
             bool have_held = false;
-            for (int j = 0; j < nb && st == LSSP_AMD_OK; j++) {
-                const int k = it + j;
+            for (int j = 0; j < B.nb && st == LSSP_AMD_OK; j++) {
+                const int k = queued + j;
                 Ew e;
                 if (k == 0) {
                     st = R.dot1(r, r, R.fin(FIN_CG_RHO, 1, R.T()));  // :80 (z == r)
@@ -505,8 +560,8 @@ int cg(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *
                 e.x = z;
                 e.out0 = p;
                 if (st == LSSP_AMD_OK) {
-                    // with the x update of the previous x/r pass (CGF_R): its stop test is stamped j
-                    if (have_held) st = launch_cg_fused(c, CGF_PX, R.n, x, p, nullptr, z, nullptr, 1, 1, held, j);
+                    // with the x update of the previous x/r pass (CGF_R): its stop test is stamped k
+                    if (have_held) st = launch_cg_fused(c, CGF_PX, R.n, x, p, nullptr, z, nullptr, 1, 1, held, k);
                     else st = R.ew(e);
                 }
                 have_held = false;
@@ -530,36 +585,48 @@ int cg(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *
                 }
                 int t0 = R.T(), t1 = R.T();
                 const Fin fr = R.fin(FIN_CG_RES_RHO_B, 1, t0, t1);  // :106-109, next :80
-                if (fuse_l2 && j + 1 < nb) {
+                if (fuse_l2 && j + 1 < B.nb) {
                     held = fr;
                     have_held = true;
                 } else if (fuse_l2) {
                     if (st == LSSP_AMD_OK) st = launch_reduce_tree(c, num_chunks(R.n), 1, fr, 1);
                     if (st == LSSP_AMD_OK)
-                        st = launch_cg_fused(c, CGF_X, R.n, x, p, nullptr, nullptr, nullptr, 1, 1, Fin(), j + 1);
+                        st = launch_cg_fused(c, CGF_X, R.n, x, p, nullptr, nullptr, nullptr, 1, 1, Fin(), k + 1);
                 } else {
                     if (st == LSSP_AMD_OK) st = R.fin1(r, r, fr);
                 }
-                tl_after[j] = R.tl;
+                B.tl_after[j] = R.tl;
             }
             c->guard = nullptr;
             LSSP_TRY(st);
-            LSSP_TRY(R.sync(0, S_H + nb));
-            const int ran = std::max(1, std::min(nb, (int)R.h(S_NIT)));
+            LSSP_TRY(R.snap_issue(nq & 1));
+            queued += B.nb;
+            nq++;
+            return LSSP_AMD_OK;
+        };
+        it = 0;
+        LSSP_TRY(R.batch_begin(tol));
+        LSSP_TRY(push());
+        for (;;) {
+            if (queued < maxit) LSSP_TRY(push());  // runs while the batch before it is read
+            const Batch &B = bq[nr & 1];
+            LSSP_TRY(R.snap_wait(nr & 1));
+            nr++;
+            const int ran = std::max(1, std::min(B.nb, (int)R.h(S_NIT) - B.it0));
             for (int q = 0; q < ran; q++) {
-                res = R.h(S_H + q);
+                res = R.h(S_H + (B.it0 + q) % S_HB);
                 if (P.verb >= 1 && R.rank == 0)
                     lprint("cg: itr: %5d, abs res: %.6e, rel res: %.6e, rbn: %.6e\n", it + q, res,
                            (err_rel == 0 ? 0 : res / err_rel), (b_norm == 0 ? 0 : res / b_norm));
             }
             pending_rho = true;
             if (R.h(S_DONE) != 0.0) {  // :109 held at iteration it + ran - 1
-                R.tl = tl_after[ran - 1];
+                R.tl = B.tl_after[ran - 1];
                 it += ran - 1;
-                stop = true;
-            } else {
-                it += nb;
+                break;
             }
+            it += B.nb;
+            if (nr == nq) break;  // maxit
         }
     } else {
         for (it = 0; it < maxit; it++) {
