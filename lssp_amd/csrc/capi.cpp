@@ -501,6 +501,9 @@ int lssp_amd_mat_upload(lssp_amd_ctx *c, int nrows, int ncols, int nnz, const in
         lssp_amd_mat_destroy(M);
         return st;
     }
+    // a measurement only: if it cannot run (no memory for its two vectors) the
+    // product keeps the default block order
+    if (tune_spmv_streams(c, M) != LSSP_AMD_OK) (void)hipGetLastError();
     *out = M;
     return LSSP_AMD_OK;
 }

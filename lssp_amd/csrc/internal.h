@@ -141,6 +141,8 @@ struct lssp_amd_mat {
     // device bytes held beside the CSR arrays (offset ids + table, window spans,
     // the sliced copy): lssp_amd_mat_bytes
     long long aux_bytes = 0;
+    // k_spmv3's block streams, timed at upload (tune_spmv_streams); 0: the default 8
+    int streams = 0;
     // distributed layout
     int n_global = 0, row0 = 0, nhalo = 0;
     // halo exchange plan: for each peer, indices (local) to send and the count to receive
@@ -285,6 +287,7 @@ namespace lssp_amd {
 enum Epi { EPI_MXY = 0, EPI_AMXY, EPI_AXPBY, EPI_AMX };  // see spmv kernel
 int build_diag_ids(lssp_amd_mat *M, const int *Ap, const int *Aj);
 int build_windows(lssp_amd_mat *M, const int *Ap, const int *Aj, const double *Ax);
+int tune_spmv_streams(lssp_amd_ctx *c, lssp_amd_mat *M);
 constexpr int WIN_ROWS = 1024, WIN_CAP = 16384;
 int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, const double *x,
                 double beta, const double *y, double *z, int nred, const double *w0,

@@ -678,14 +678,21 @@ static int spmv_ntv()
     return k;
 }
 
-static int spmv_streams()
+// LSSP_AMD_SPMV_STREAMS=K forces K streams (A/B runs); 0: the matrix's own
+// choice (tune_spmv_streams), 8 when it has none
+static int spmv_streams_env()
 {
     static const int k = [] {
         const char *e = getenv("LSSP_AMD_SPMV_STREAMS");
-        const int v = e ? atoi(e) : 8;
-        return v >= 8 && v % 8 == 0 && v <= 4096 ? v : 8;
+        const int v = e ? atoi(e) : 0;
+        return v >= 8 && v % 8 == 0 && v <= 4096 ? v : 0;
     }();
     return k;
+}
+static int spmv_streams(const lssp_amd_mat *A)
+{
+    const int e = spmv_streams_env();
+    return e ? e : A->streams > 0 ? A->streams : 8;
 }
 
 template <int EPI, bool CMP>
@@ -720,7 +727,7 @@ int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, c
     const long nb = ce - cb;
     if (nb == 0) return LSSP_AMD_OK;
     SpmvArgs a{A->nrows, A->Ap, A->Aj, A->Ax, x, y, z, alpha, beta, w0, w1, c->d_part, c->part_cap,
-               A->Ad, A->d_off, A->ndiag, c->guard, cb, spmv_streams(), 0, 0, 0, spmv_ntv()};
+               A->Ad, A->d_off, A->ndiag, c->guard, cb, spmv_streams(A), 0, 0, 0, spmv_ntv()};
     const long plane = A->max_off_int;
     if (A->ndiag > 0 && plane >= 256 * 8 && plane % 256 == 0) {
         const long bpp = plane / 256;
@@ -750,6 +757,56 @@ int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, c
     }
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;
+}
+
+// The block streams of k_spmv3, measured at upload.  Each XCD walks its
+// 1/K of the rows in K/8 contiguous ranges; which K is fastest depends on the
+// size (7-pt y = A x, ms, profiles/r06/r06f_spmv_streams.txt: 216^3 K = 8
+// 0.145 vs 64 0.155; 256^3 8 0.282 vs 16 0.255; 288^3 8 0.415 vs 64 0.402;
+// 320^3 8 0.557 vs 16 0.534) and no address rule we tried explained it
+// (skewing each range's start did not, r06e), so matrices of >= 4 Mi rows
+// time K = 8, 16, 32, 64 on three products each and keep the fastest unless
+// K = 8 is within 2 %.  The product's values do not depend on K (every block
+// writes its own rows and chunk partials).
+int tune_spmv_streams(lssp_amd_ctx *c, lssp_amd_mat *A)
+{
+    A->streams = 0;
+    if (spmv_streams_env() || A->nrows < (1 << 22) || A->d_win || A->nhalo > 0 || A->n_global != A->nrows)
+        return LSSP_AMD_OK;
+    double *x = nullptr, *z = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int st = LSSP_AMD_OK;
+    auto run = [&]() -> int {
+        LSSP_HIP(hipMalloc(&x, sizeof(double) * A->ncols));
+        LSSP_HIP(hipMalloc(&z, sizeof(double) * A->nrows));
+        LSSP_HIP(hipMemsetAsync(x, 0, sizeof(double) * A->ncols, c->stream));
+        LSSP_HIP(hipEventCreate(&e0));
+        LSSP_HIP(hipEventCreate(&e1));
+        float best = 0.f, t8 = 0.f;
+        int kbest = 8;
+        for (int k : {8, 16, 32, 64}) {
+            A->streams = k;
+            LSSP_TRY(launch_spmv(c, A, EPI_MXY, 1.0, x, 0.0, nullptr, z, 0, nullptr, nullptr));
+            LSSP_HIP(hipEventRecord(e0, c->stream));
+            for (int r = 0; r < 3; r++) LSSP_TRY(launch_spmv(c, A, EPI_MXY, 1.0, x, 0.0, nullptr, z, 0, nullptr, nullptr));
+            LSSP_HIP(hipEventRecord(e1, c->stream));
+            LSSP_HIP(hipEventSynchronize(e1));
+            float ms = 0.f;
+            LSSP_HIP(hipEventElapsedTime(&ms, e0, e1));
+            if (k == 8) best = t8 = ms;
+            else if (ms < best) best = ms, kbest = k;
+        }
+        A->streams = best < 0.98f * t8 ? kbest : 8;
+        return LSSP_AMD_OK;
+    };
+    st = run();
+    if (st != LSSP_AMD_OK) A->streams = 0;
+    (void)hipStreamSynchronize(c->stream);
+    if (x) (void)hipFree(x);
+    if (z) (void)hipFree(z);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    return st;
 }
 
 // ---------------------------------------------------------------------------
