@@ -528,7 +528,7 @@ constexpr int LINE_RW = 6;  // rhs wave: a run block's loads land LINE_RW steps 
 // wave priority and hold the loaders' DMA issue back ~6 x 64 clk after each
 // barrier, so the step's hand-off polls enter the CU's memory queue ahead of
 // the 10 KB of coefficient DMAs (whose lead is 10 steps): 216^3 apply 957 ->
-// 922 us (tools/gpu_exp.sh; the standalone natural-order sweeps got slower with
+// 922 us (tools/variant_ab.sh; the standalone natural-order sweeps got slower with
 // it, so they keep 0 / 0).  -DLINE_POLL_PRIO / -DLINE_LOAD_SLEEP override both.
 #ifndef LINE_STORE_SLEEP
 #define LINE_STORE_SLEEP 0  // tuning: storers' delay before their stores (64 clk units)

@@ -1,11 +1,10 @@
 #!/bin/bash
-# Tuning aid (GPU box): 216^3 bench it/s with environment settings A/B'd,
-# alternated -- tools/env_ab.sh OUT "VAR=val ..." "VAR=val ..." ...
+# Tuning aid (GPU box): a command under several environment settings,
+# alternated -- tools/env_ab.sh OUT REPS "CMD" "ENV1" "ENV2" ...  ("-" = none)
 set -o pipefail
-O=gpurun_out/$1; shift; mkdir -p $O
-for rep in 1 2 3; do
-  for v in "" "$@"; do
-    echo "== ${v:-default}" >> $O/ab.txt
-    env $v timeout -k 10 200 python bench.py --steps 100 --warmup 10 --no-cpu --config4-steps 0 >> $O/ab.txt || exit 1
-  done
-done
+O=gpurun_out/$1; REPS=$2; CMD=$3; shift 3; mkdir -p $O
+for rep in $(seq $REPS); do for e in "$@"; do
+  echo "== $e" >> $O/ab.txt
+  if [ "$e" = "-" ]; then timeout -k 10 300 bash -c "$CMD" >> $O/ab.txt 2>>$O/err.txt || exit 1
+  else env $e timeout -k 10 300 bash -c "$CMD" >> $O/ab.txt 2>>$O/err.txt || exit 1; fi
+done; done
