@@ -209,7 +209,7 @@ struct LineTile {  // one workgroup's unit of work, in its sweep's coordinates
 struct LineSweep {
     int nx = 0, ny = 0, nz = 0, ntiles = 0, tmax = 0, NA = 3;
     int P = 4;    // planes per tile
-    int NJ = 64;  // lines per tile (k_line: 256 / P; k_line2: 16)
+    int NJ = 64;  // lines per tile (k_line2: 16)
     int LV = 1;   // levels per workgroup step (k_line2: 2; its planes P/2.. run one level later)
     long rows_total = 0;
     LineTile *d_tiles = nullptr;

@@ -490,11 +490,7 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
 #pragma unroll
             for (int q = 0; q < NRED; q++) v[q] = 0.0;
         }
-#ifdef SPMV_DIAG_NORED  // tuning builds: no chunk reduction (WRONG dots), the cost of chunk_reduce
-        if (v[0] == 12345.678) a.part[blk] = v[0];
-#else
         chunk_reduce<NRED>(v, a.part, a.pcap, blk, lds);
-#endif
     }
 }
 
@@ -870,13 +866,7 @@ __global__ __launch_bounds__(256) void k_ew(EwArgs g)
         bool w0 = false, w1 = false;  // this element's out0 / out1 written by the kind below
         double o0 = 0.0, o1 = 0.0, p0a = 0.0, p0b = 0.0, p1a = 0.0, p1b = 0.0;
         double p2a = 0.0, p2b = 0.0, p3a = 0.0, p3b = 0.0;
-#ifdef EW_PRE_NT  // tuning builds: the reduction operands as non-temporal loads
-        auto pre = [&](const double *q) {
-            return (in && q != g.out0 && q != g.out1) ? __builtin_nontemporal_load(q + i) : 0.0;
-        };
-#else
         auto pre = [&](const double *q) { return (in && q != g.out0 && q != g.out1) ? q[i] : 0.0; };
-#endif
         if (NRED > 0) {
             p0a = pre(g.r0a);
             p0b = pre(g.r0b);
@@ -901,26 +891,12 @@ __global__ __launch_bounds__(256) void k_ew(EwArgs g)
             case EW_SCALE: w0 = true, g.out0[i] = o0 = g.out0[i] * g.a; break;
             case EW_DIVS: w0 = true, g.out0[i] = o0 = g.out0[i] / g.scal[g.sidx]; break;
             case EW_DOT: break;
-#ifdef EW_PS_NT  // tuning builds: the p / s passes' operands as non-temporal loads
-            case EW_BICG_P: {
-                const double beta = g.scal[S_BETA], omega = g.scal[S_OMEGA];
-                w0 = true, g.out0[i] = o0 = __builtin_nontemporal_load(g.x + i) +
-                                           beta * (__builtin_nontemporal_load(g.out0 + i) -
-                                                   omega * __builtin_nontemporal_load(g.y + i));
-                break;
-            }
-            case EW_BICG_S:
-                w0 = true, g.out0[i] = o0 = __builtin_nontemporal_load(g.x + i) -
-                                           g.scal[S_ALPHA] * __builtin_nontemporal_load(g.y + i);
-                break;
-#else
             case EW_BICG_P: {
                 const double beta = g.scal[S_BETA], omega = g.scal[S_OMEGA];
                 w0 = true, g.out0[i] = o0 = g.x[i] + beta * (g.out0[i] - omega * g.y[i]);
                 break;
             }
             case EW_BICG_S: w0 = true, g.out0[i] = o0 = g.x[i] - g.scal[S_ALPHA] * g.y[i]; break;
-#endif
             case EW_BICG_XR: {
                 const double alpha = g.scal[S_ALPHA];
                 if (g.scal[S_BREAK] != 0.0) {
@@ -929,31 +905,16 @@ __global__ __launch_bounds__(256) void k_ew(EwArgs g)
                     // every operand loaded before the first store (the compiler
                     // may not move u, v above a store to out0 they might alias)
                     const double omega = g.scal[S_OMEGA];
-#ifdef EW_XR_LATE  // tuning builds: round 4's order (u, v loaded after the out0 store)
-                    w0 = true, g.out0[i] = o0 = g.out0[i] + alpha * g.x[i] + omega * g.y[i];
-                    w1 = true, g.out1[i] = o1 = g.u[i] - omega * g.v[i];
-#elif !defined(EW_XR_TEMPORAL)
                     // x, ph, sh, s, t as non-temporal accesses (none is read again
                     // before the next iteration's sweeps have streamed through the
                     // caches; r, read by the next p pass, stays temporal): 216^3
-                    // 632.3 -> 640.9 it/s, profiles/r05/r05x_xr_nt_ab.txt.
-                    // -DEW_XR_TEMPORAL: plain accesses (A/B)
+                    // 632.3 -> 640.9 it/s, profiles/r05/r05x_xr_nt_ab.txt
                     const double xo = __builtin_nontemporal_load(g.out0 + i), xp = __builtin_nontemporal_load(g.x + i),
                                  xs = __builtin_nontemporal_load(g.y + i), su = __builtin_nontemporal_load(g.u + i),
                                  tv = __builtin_nontemporal_load(g.v + i);
                     w0 = true, o0 = xo + alpha * xp + omega * xs;
                     __builtin_nontemporal_store(o0, g.out0 + i);
-#ifdef EW_XR_RNT  // tuning builds: r stored non-temporal too
-                    w1 = true, o1 = su - omega * tv;
-                    __builtin_nontemporal_store(o1, g.out1 + i);
-#else
                     w1 = true, g.out1[i] = o1 = su - omega * tv;
-#endif
-#else
-                    const double xo = g.out0[i], xp = g.x[i], xs = g.y[i], su = g.u[i], tv = g.v[i];
-                    w0 = true, g.out0[i] = o0 = xo + alpha * xp + omega * xs;
-                    w1 = true, g.out1[i] = o1 = su - omega * tv;
-#endif
                 }
                 break;
             }

@@ -65,10 +65,6 @@
 
 namespace lssp_amd {
 
-#ifndef LINE2_EARLY_SHFL
-#define LINE2_EARLY_SHFL 1  // the BN shuffle issued before the level's stores (linesweep.hip k_line2)
-#endif
-
 namespace lf {
 constexpr int P = 8, NJ = 16, LV = 2, HKS = 18, ROWS = P * NJ;
 constexpr int HJ0 = 2;  // hj row of q = -2 (the compute runs from level -2)
@@ -430,11 +426,8 @@ int build_linefill(lssp_amd_ctx *c, int n, const std::vector<int> &Lp, const std
             }
         }
     };
-    static const bool keep_all = getenv("LSSP_AMD_LINEF_ALLTILES") != nullptr;  // A/B and tests only
-    if (!keep_all) {
-        skip_off_grid(Lt);
-        skip_off_grid(Ut);
-    }
+    skip_off_grid(Lt);
+    skip_off_grid(Ut);
     const long pl = (long)g.nx * g.ny;
     const int NAL = g.unitL ? 6 : 7;
     FillCoef cl, cu;
@@ -662,23 +655,14 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
                         r = r - cur.c[3][lv] * sep;
                         r = r - cur.c[4][lv] * se;
                         r = r - cur.c[5][lv] * xp;
-#ifndef LINEF_NODIV
                         if constexpr (NA == 7) r = r / cur.c[6][lv];
-#else
-                        if constexpr (NA == 7) r = r * cur.c[6][lv];  // timing experiments only
-#endif
                         const bool ok = lane_ok && (unsigned)(v - off) < (unsigned)nx;
                         const double x = sel_lanes(__builtin_amdgcn_ballot_w64(ok), r, 0.0);
-#if LINE2_EARLY_SHFL
                         // the next level's BN shuffle before this level's stores (as k_line2)
                         xu = up16(x);
                         __builtin_amdgcn_sched_barrier(0);
-#endif
                         publish(v, x, se);
                         res[(v & (RSL - 1)) * ROWS + pw * NJ + ll] = x;
-#if !LINE2_EARLY_SHFL
-                        xu = up16(x);
-#endif
                         bep = be;
                         sep = se;
                         bnp = bn;
@@ -781,8 +765,7 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
                 const bool bk = vk && kvb == TRI_SENTINEL, bj = vj && jvb == TRI_SENTINEL;
                 if (__any(bk || bj)) {
                     // resync: drain, wait for these values, re-issue the later polls
-                    // (k_line2's episode; -DLINEF_RESYNC_FAR: also wait for the
-                    // furthest step in flight)
+                    // (k_line2's episode)
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     auto spin = [&](const double *src) {
                         for (;;) {
@@ -792,18 +775,11 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
                                 atomicOr(a.err, 8);
                                 return (uint64_t)0x7FF8000000000000ull;
                             }
-#ifndef LINEF_SPIN_SLEEP
-#define LINEF_SPIN_SLEEP 1
-#endif
-                            if (LINEF_SPIN_SLEEP) __builtin_amdgcn_s_sleep(LINEF_SPIN_SLEEP);
+                            __builtin_amdgcn_s_sleep(1);
                         }
                     };
                     if (bk) *kslot = __longlong_as_double((long long)spin(kaddr(qk)));
                     if (bj) *jslot = __longlong_as_double((long long)spin(jaddr(qj)));
-#ifdef LINEF_RESYNC_FAR
-                    if (kin && kval(s + DH) && 2 * (s + DH) + 2 <= kmax) (void)spin(kaddr(s + DH));
-                    if (jin && jval(s + DH + 1) && 2 * (s + DH + 1) + 1 + HJ0 <= jmax) (void)spin(jaddr(s + DH + 1));
-#endif
                     for (int k = 2; k <= DH; k++) issue(s + k);  // the polls issued at steps s+k-DH
                 }
                 line_barrier();
@@ -937,11 +913,7 @@ __global__ __launch_bounds__(256) void k_linef_rhs(const LineTile *__restrict__ 
         const int lv = q0 + m, i = lv - 2 * l - p - sig(p), j = d.j0 + l - d.k0 - p;
         const bool ok = lv < d.T && p < d.np && l < d.nj && (unsigned)j < (unsigned)ny && (unsigned)i < (unsigned)nx;
         const long r = ((long)(d.k0 + p) * ny + j) * nx + i;
-#ifdef LFRHS_NT  // tuning builds: the apply's rhs read non-temporal
-        v[it] = ok ? __builtin_nontemporal_load(rhs + (mirror ? n - 1 - r : r)) : 0.0;
-#else
         v[it] = ok ? rhs[mirror ? n - 1 - r : r] : 0.0;
-#endif
         o[it] = ok ? d.cbase + (long)lv * P * d.nj + p * d.nj + l : -1;
     }
 #pragma unroll

@@ -265,16 +265,13 @@ static int upload_sweep(lssp_amd_ctx *c, const LineGeom &g, const std::vector<Li
         // workgroups hold tiles of the advancing wavefront instead of tiles
         // many hops ahead of it (row order: the first 256 claims of a 216^3 sweep
         // reach K = 18, whose tiles wait ~30 hops before they can start).
-        // LSSP_AMD_LINE2_ROWORDER=1: row order (A/B).
         const int W = (g.ny + ls.NJ - 1) / ls.NJ, nt = (int)tt.size();
         std::vector<int> ord(nt);
         for (int q = 0; q < nt; q++) ord[q] = q;
-        const char *ro = getenv("LSSP_AMD_LINE2_ROWORDER");
-        if (!(ro && atoi(ro)))
-            std::stable_sort(ord.begin(), ord.end(), [W](int x, int y) {
-                const int dx = x % W + x / W, dy = y % W + y / W;
-                return dx != dy ? dx < dy : x < y;
-            });
+        std::stable_sort(ord.begin(), ord.end(), [W](int x, int y) {
+            const int dx = x % W + x / W, dy = y % W + y / W;
+            return dx != dy ? dx < dy : x < y;
+        });
         LSSP_HIP(hipMalloc(&ls.d_order, sizeof(int) * nt));
         LSSP_HIP(hipMemcpy(ls.d_order, ord.data(), sizeof(int) * nt, hipMemcpyHostToDevice));
     }
@@ -282,43 +279,11 @@ static int upload_sweep(lssp_amd_ctx *c, const LineGeom &g, const std::vector<Li
     return LSSP_AMD_OK;
 }
 
-// planes per tile: the P in {4, 8, 16} with the fewest tile hops on a sweep's
-// critical path, (W - 1) + (S - 1) for W tiles across the lines and S down the
-// longest plane segment (ties: the smaller P).  216^3: 64 x 4 tiles 56 hops,
-// 32 x 8 32, 16 x 16 26; a 27-plane block-Jacobi slab of it: 9, 9, 14.
-static int line_choose_P(const LineGeom &g)
+// tiles of k_line2: 8 planes x 16 lines, two levels per workgroup step (round 3's
+// k_line -- 256 rows and one level per step, 64 x 4 / 32 x 8 / 16 x 16 tiles --
+// was removed in round 6 after two rounds as an A/B option only)
+static void line_plan(const LineGeom &, int &P, int &NJ, int &LV)
 {
-#ifdef LINE_P_FORCE
-    return LINE_P_FORCE;  // tuning builds (tools/build_variant.sh)
-#endif
-    int seg = 1;
-    for (int k = 0; k < g.nz;) {
-        int e = k + 1;
-        while (e < g.nz && g.kin[e]) e++;
-        seg = std::max(seg, e - k);
-        k = e;
-    }
-    int best = 4;
-    long bh = -1;
-    for (int P : {4, 8, 16}) {
-        const long hops = (g.ny + 256 / P - 1) / (256 / P) + (seg + P - 1) / P - 2;
-        if (bh < 0 || hops < bh) best = P, bh = hops;
-    }
-    return best;
-}
-
-// which kernel sweeps a factor: k_line2 (8 planes x 16 lines, two levels per
-// step; the default) or k_line (256 rows per step, one level per step; P from
-// line_choose_P).  LSSP_AMD_LINE_MODE=1 selects k_line (A/B runs, tests).
-static void line_plan(const LineGeom &g, int &P, int &NJ, int &LV)
-{
-    const char *e = getenv("LSSP_AMD_LINE_MODE");
-    if (e && atoi(e) == 1) {
-        P = line_choose_P(g);
-        NJ = 256 / P;
-        LV = 1;
-        return;
-    }
     // (the kernel is generic in P = 4 x compute waves; 16-plane tiles measured
     // slower: 216^3 apply 666 against 593 us, 512^3 4.72 against 4.59 ms,
     // profiles/r04/r04e_*, r04f_line2_512_p8_p16.txt)
@@ -485,557 +450,6 @@ struct LineArgs {
     LineTail tl;
 };
 
-// slot layout (bytes): the step's coefficient block, its rhs, the hand-off inputs
-template <int P, int NA, bool RHS_NAT>
-struct LineSlot {
-    static constexpr int NJ = 4 * 64 / P;                        // lines per tile (P * NJ = 256 rows per step)
-    static constexpr int NPC = (P * NJ * NA * 8 + 1023) / 1024;  // 1 KB DMA pieces of the coefficient block
-    static constexpr int NRP = (P * NJ * 8 + 1023) / 1024;       // ... of a U rhs-stream block
-    static constexpr int NRD = RHS_NAT ? 0 : NRP;                // rhs DMA instructions per step
-    static constexpr int COEF = 0;
-    static constexpr int RHS = NPC * 1024;
-    static constexpr int KFIN = RHS + (RHS_NAT ? 0 : NRP * 1024);  // double[NJ]
-    static constexpr int JFIN = KFIN + NJ * 8;                      // double[P]
-    static constexpr int BYTES = (JFIN + 8 * P + 15) & ~15;
-};
-
-// LDS after the slot ring: the compute results of the last RS steps
-// ([RS][P][NJ] doubles: the next compute group's k-input, and the storers'
-// source -- natural-order output is written in 8-step runs per line, so it
-// keeps two 8-step blocks), the claimed tile, the poller's DMA sink and, for
-// a natural-order rhs, two 8-step rhs blocks ([8][P*NJ+1] doubles each,
-// filled by the rhs wave in runs the same way)
-template <int OUT>
-constexpr int line_rs() { return OUT == 1 ? 16 : 2; }
-template <int P>
-constexpr int line_rhs_blk() { return 8 * (256 + 1); }  // doubles per rhs block (P * NJ = 256)
-template <int P, int NA, bool RHS_NAT, int OUT, int D>
-constexpr int line_lds_bytes()
-{
-    return (D + 1) * LineSlot<P, NA, RHS_NAT>::BYTES + line_rs<OUT>() * 256 * 8 + 16 + 512 +
-           (RHS_NAT ? 2 * line_rhs_blk<P>() * 8 : 0);
-}
-template <int CW, int NL, int SW, bool RHS_NAT>
-constexpr int line_waves() { return CW + NL + 1 + SW + (RHS_NAT ? 1 : 0); }
-constexpr int LINE_RW = 6;  // rhs wave: a run block's loads land LINE_RW steps after they are issued
-
-// P planes per tile, NA coefficient components (3: unit L, 4: with diagonal),
-// RHS_NAT: the rhs is read in natural order (else from the U rhs stream), CW
-// compute waves (P/CW planes each), NL loader waves, D loader lead (steps),
-// DH poller lead (steps), SW storer waves; OUT 1: natural-order output, 2: the
-// U rhs stream (the L sweep of an apply); TRACE: diagnostics.
-// The apply's two sweeps (L -> U rhs stream, U from it) raise the poller's
-// wave priority and hold the loaders' DMA issue back ~6 x 64 clk after each
-// barrier, so the step's hand-off polls enter the CU's memory queue ahead of
-// the 10 KB of coefficient DMAs (whose lead is 10 steps): 216^3 apply 957 ->
-// 922 us (tools/variant_ab.sh; the standalone natural-order sweeps got slower with
-// it, so they keep 0 / 0).  -DLINE_POLL_PRIO / -DLINE_LOAD_SLEEP override both.
-#ifndef LINE_STORE_SLEEP
-#define LINE_STORE_SLEEP 0  // tuning: storers' delay before their stores (64 clk units)
-#endif
-#ifndef LINE_RHS_SLEEP
-#define LINE_RHS_SLEEP 0  // tuning: rhs wave's delay before its loads
-#endif
-template <bool RHS_NAT, int OUT>
-constexpr int line_poll_prio()
-{
-#ifdef LINE_POLL_PRIO
-    return LINE_POLL_PRIO;
-#else
-    return (OUT == 2 || !RHS_NAT) ? 3 : 0;
-#endif
-}
-template <bool RHS_NAT, int OUT>
-constexpr int line_load_sleep()
-{
-#ifdef LINE_LOAD_SLEEP
-    return LINE_LOAD_SLEEP;
-#else
-    return (OUT == 2 || !RHS_NAT) ? 6 : 0;
-#endif
-}
-
-template <int P, int NA, bool RHS_NAT, int OUT, int CW, int NL, int D, int DH, int SW, bool TRACE>
-__global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_line(LineArgs a)
-{
-    // landing lead: the loaders and the poller complete step s+LA's slot during
-    // step s; the compute reads it at step s+LA-1 (into registers, one step ahead)
-    constexpr int LA = 2;
-    using SL = LineSlot<P, NA, RHS_NAT>;
-    // a compute wave's lanes are G groups of NJ lines; lane (g, l) holds PC
-    // planes of line l: planes p0 + g*PC .. p0 + g*PC + PC-1 of the wave's PW
-    constexpr int NJ = SL::NJ, G = 64 / NJ, PW = P / CW, PC = PW / G;
-    static_assert(DH >= 2 && DH < D && P % CW == 0 && PW % G == 0 && PC >= 1 && (OUT == 1 || OUT == 2), "lead");
-    constexpr int R = D + 1;
-    // first step of every role (a multiple of 2, 3 and 4); the rhs wave writes
-    // block 0 from step -9 on, its loads LINE_RW steps earlier
-    constexpr int S0 = -(((D > 9 + LINE_RW ? D : 9 + LINE_RW) + 11) / 12) * 12;
-    constexpr int NITEM = SL::NPC + SL::NRD;          // DMA instructions per step, shared by the loaders
-    constexpr int KPER = (NITEM + NL - 1) / NL;
-    static_assert((D - LA) * KPER <= 63 && 2 * (DH - 1) <= 63, "vmcnt range");
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    char *ring = smem;
-    constexpr int RS = line_rs<OUT>();
-    double *res = reinterpret_cast<double *>(smem + R * SL::BYTES);  // [RS][P][NJ]
-    int *s_tile = reinterpret_cast<int *>(res + RS * P * NJ);
-    double *rhsblk = reinterpret_cast<double *>(smem + R * SL::BYTES + RS * P * NJ * 8 + 16 + 512);  // [2][8][P*NJ+1]
-    const unsigned lds0 = (unsigned)(uintptr_t)smem;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int nx = a.nx;
-    if (a.guard && *a.guard != 0.0) {  // a batched iteration past the stop: consume the launch's tile claims
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(a.claim, (unsigned long long)a.ntiles + gridDim.x);
-        return;
-    }
-
-    for (;;) {
-        __syncthreads();
-        if (threadIdx.x == 0) *s_tile = (int)(atomicAdd(a.claim, 1ull) - a.base);
-        __syncthreads();
-        const int t = __builtin_amdgcn_readfirstlane(*s_tile);
-        if (t >= a.ntiles) break;
-        if (TRACE && threadIdx.x == 0) a.trace[8 * t] = __builtin_amdgcn_s_memrealtime();
-        const LineTile d = a.tiles[t];
-        const int T = d.T, nj = d.nj, np = d.np;
-        const long SB = (long)P * nj;  // rows per step block
-        const bool kin = d.flags & LT_KIN, jin = d.flags & LT_JIN, kout = d.flags & LT_KOUT,
-                   jout = d.flags & LT_JOUT;
-        // compute and storer lanes: group gl (plane offset), line ll
-        const int ll = lane & (NJ - 1), gl = lane / NJ;
-        const int lc = min(ll, nj - 1);
-        // natural row of (i, line lane, plane p) = nb(p) + i (mirror: nb(p) - i)
-        auto nb = [&](int p, int l) {
-            const long r = ((long)(d.k0 + p) * a.ny + (d.j0 + l)) * nx;
-            return a.mirror ? a.n - 1 - r : r;
-        };
-        unsigned long long *ts = TRACE ? a.trace + 8 * (long)a.ntiles : nullptr;
-        const bool trs = TRACE && t == a.ttile && lane == 0;
-
-        if (wave < CW) {
-          {
-            // ---------------- compute: planes p0 .. p0+PC-1 ----------------
-            // Coefficients, rhs and j-inputs of step s+1 are read from LDS at the
-            // start of step s (their slot was completed before the barrier that
-            // ended step s-1), so that latency overlaps step s's arithmetic.  The
-            // k-input of the first plane (the poller's, or the previous compute
-            // wave's result) is read first; planes run in descending order, so it
-            // is needed last.  The per-step overhead is kept off the critical
-            // path: ring offsets advance by adds (no modulo), the
-            // rows valid at a step come from a lane-mask shift register (plane 0's
-            // mask at step s is its mask at s-1 shifted one lane up, plus lane 0
-            // while 0 <= s < nx; plane p's is plane 0's of step s-p), every plane
-            // is computed in one straight-line block, and the hand-off stores
-            // drop the lanes that publish nothing through out-of-range offsets.
-            // Published values need no canonicalisation: every one is the result
-            // of an f64 add or division, and those never return the sentinel (a
-            // signalling NaN) in IEEE mode.
-            const int p0 = wave * PW;     // the wave's first plane
-            const int pg = p0 + gl * PC;  // the lane group's first plane
-            struct In {
-                double ck[PC], cj[PC], ci[PC], dg[PC], rh[PC], jv[PC];
-
-            };
-            auto load = [&](int s, unsigned so, In &in) {
-                const char *slot = ring + so;
-#pragma unroll
-                for (int u = 0; u < PC; u++) {
-                    const int p = pg + u;
-                    const double *b = reinterpret_cast<const double *>(slot + SL::COEF) + (p * nj + lc) * NA;
-                    in.ck[u] = b[0];
-                    in.cj[u] = b[1];
-                    in.ci[u] = b[2];
-                    if constexpr (NA == 4) in.dg[u] = b[3];
-                    if constexpr (RHS_NAT) {
-                        in.rh[u] = rhsblk[((s >> 3) & 1) * line_rhs_blk<P>() + (s & 7) * (P * NJ + 1) + p * NJ + ll];
-                    } else {
-                        in.rh[u] = reinterpret_cast<const double *>(slot + SL::RHS)[p * nj + lc];
-                    }
-                    in.jv[u] = reinterpret_cast<const double *>(slot + SL::JFIN)[p];
-                }
-            };
-            double xc[PC];
-#pragma unroll
-            for (int u = 0; u < PC; u++) xc[u] = 0.0;
-            In A, B;
-            constexpr int OOB = 0x40000000;  // + any soffset below stays < 2^31: dropped, never wraps
-            const __amdgpu_buffer_rsrc_t hko =
-                __builtin_amdgcn_make_buffer_rsrc(a.hk + (long)t * a.hk_stride, 0, (int)(a.hk_stride * 8), 0x00020000);
-            const __amdgpu_buffer_rsrc_t hjo =
-                __builtin_amdgcn_make_buffer_rsrc(a.hj + (long)t * a.hj_stride, 0, (int)(a.hj_stride * 8), 0x00020000);
-            const uint64_t njm = nj >= 64 ? ~0ull : ((1ull << nj) - 1);
-            constexpr uint64_t GM = NJ >= 64 ? ~0ull : ((1ull << NJ) - 1);  // group 0's lanes
-            constexpr uint64_t GS = G == 1 ? 1ull : G == 2 ? 0x100000001ull : 0x0001000100010001ull;  // group starts
-            // the plane this wave publishes to the next k-tile: register uk (-1: none) of group gk
-            const int ko = np - 1 - p0;
-            const bool kw = kout && ko >= 0 && ko < PW;
-            const int uk = kw ? ko % PC : -1;
-            const uint64_t kgm = kw ? GM << ((ko / PC) * NJ % 64) : 0ull;
-            const int jl_off = ll == nj - 1 ? gl * PC * 8 : OOB;  // line nj-1 feeds the next j-tile
-            // hw[u]: the lanes whose row of register u's plane exists at the current
-            // step (line l's row i = s - p - l is valid iff line l-1's was at s-1,
-            // and line 0's iff 0 <= s - p < nx), pm[u]: 0 for planes past the tile
-            uint64_t hw[PC], pm[PC];
-#pragma unroll
-            for (int u = 0; u < PC; u++) {
-                hw[u] = 0;
-                pm[u] = 0;
-#pragma unroll
-                for (int g = 0; g < G; g++)
-                    if (p0 + g * PC + u < np) pm[u] |= njm << (g * NJ % 64);
-            }
-            unsigned so = (unsigned)(((S0 % R) + R) % R) * SL::BYTES;  // slot of step s
-            constexpr unsigned RB = (unsigned)(R * SL::BYTES);
-            auto body = [&](int s, In &cur, In &nxt) {
-                if (TRACE && lane == 0 && wave == 0 && s == 0) a.trace[8 * t + 1] = __builtin_amdgcn_s_memrealtime();
-                if (trs && wave == 0 && s >= 0 && s < T) ts[8 * s] = __builtin_amdgcn_s_memtime();
-                const unsigned sn = so + SL::BYTES == RB ? 0u : so + SL::BYTES;  // slot of step s+1
-                // k-input of the group's first plane: the poller's (wave 0, group 0),
-                // else plane pg-1 of the previous step (another group or wave)
-                const double kx = (wave == 0 && gl == 0)
-                                      ? reinterpret_cast<const double *>(ring + so + SL::KFIN)[ll]
-                                      : res[((s - 1) & (RS - 1)) * P * NJ + (pg - 1) * NJ + ll];
-                asm volatile("" ::: "memory");  // kx's read is issued first (LDS returns in order)
-                load(s + 1, sn, nxt);
-#pragma unroll
-                for (int u = 0; u < PC; u++) {
-                    uint64_t nb = 0;  // line 0 of each group; bit = 0 <= y < nx, in integer ops (SALU)
-#pragma unroll
-                    for (int g = 0; g < G; g++) {
-                        const int y = s - (p0 + g * PC + u);
-                        nb |= (uint64_t)(((unsigned)((y - nx) & ~y)) >> 31) << (g * NJ % 64);
-                    }
-                    hw[u] = (((hw[u] << 1) & ~GS) | nb) & pm[u];
-                }
-                if (s >= 0 && s < T) {
-                    double xn[PC];
-#pragma unroll
-                    for (int u = PC - 1; u >= 0; u--) {
-                        const uint64_t m = hw[u];
-                        const double xk = u > 0 ? xc[u - 1] : kx;
-                        const double xj = dpp_shr1g<G>(xc[u], cur.jv[u]);
-                        double v = cur.rh[u] - cur.ck[u] * xk;
-                        v = v - cur.cj[u] * xj;
-                        v = v - cur.ci[u] * xc[u];
-                        if constexpr (NA == 4) v = v / cur.dg[u];
-                        xn[u] = sel_lanes(m, v, xc[u]);
-                    }
-                    if (uk >= 0) {  // uniform
-                        const int q = s + 1 - np;
-                        uint64_t m = hw[0];
-                        double v = xn[0];
-#pragma unroll
-                        for (int u = 1; u < PC; u++)
-                            if (uk == u) m = hw[u], v = xn[u];
-                        m &= kgm;
-                        int vo = ll * 8;
-                        asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(vo) : "v"(OOB), "v"(vo), "s"(m));
-                        if (q < 0) vo = OOB;  // (no row of plane np-1 exists before step np-1)
-                        // soffset is not range-checked: only voffset carries the drop
-                        __builtin_amdgcn_raw_buffer_store_b64(split64((uint64_t)__double_as_longlong(v)), hko, vo,
-                                                              max(q, 0) * (NJ * 8), 16);  // sc1
-                    }
-                    if (jout) {
-                        // planes past the tile (p >= np) publish nothing: the two sweeps
-                        // share the hand-off buffers, and the other sweep's tile of this
-                        // index may have more planes, whose consumer would take a value
-                        // left here for a ready one
-                        // steps q < 0 publish nothing: the drop goes in voffset (the
-                        // buffer range check covers voffset, not soffset)
-                        const int q = s + 1 - nj;
-                        const int sof = (max(q, 0) * P + p0) * 8;
-                        const int jlq = q >= 0 ? jl_off : OOB;
-                        if constexpr (PC == 2) {
-                            const uint64_t b0 = (uint64_t)__double_as_longlong(xn[0]);
-                            const uint64_t b1 = (uint64_t)__double_as_longlong(xn[1]);
-                            line_v4u d4;
-                            d4.x = (unsigned)b0;
-                            d4.y = (unsigned)(b0 >> 32);
-                            d4.z = (unsigned)b1;
-                            d4.w = (unsigned)(b1 >> 32);
-                            __builtin_amdgcn_raw_buffer_store_b128(d4, hjo, pg + 1 < np ? jlq : OOB, sof, 16);
-                            if (np & 1)  // uniform: the group whose second plane is past the tile
-                                __builtin_amdgcn_raw_buffer_store_b64(split64(b0), hjo, pg + 1 == np ? jlq : OOB,
-                                                                      sof, 16);
-                        } else {
-#pragma unroll
-                            for (int u = 0; u < PC; u++)
-                                __builtin_amdgcn_raw_buffer_store_b64(split64((uint64_t)__double_as_longlong(xn[u])), hjo,
-                                                                      pg + u < np ? jlq + 8 * u : OOB, sof, 16);
-                        }
-                    }
-                    if (trs && wave == 0 && s >= 0 && s < T) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
-#pragma unroll
-                    for (int u = 0; u < PC; u++) {
-                        xc[u] = xn[u];
-                        res[((s & (RS - 1)) * P + pg + u) * NJ + ll] = xc[u];
-                    }
-                }
-                so = sn;
-                if (trs && s >= 0 && s < T) ts[8 * s + (wave == 0 ? 1 : 7)] = __builtin_amdgcn_s_memtime();
-                line_barrier();
-            };
-            for (int s = S0; s <= T; s += 2) {
-                body(s, A, B);
-                if (s + 1 <= T) body(s + 1, B, A);
-            }
-            if (TRACE && lane == 0 && wave == 0) {
-                a.trace[8 * t + 2] = __builtin_amdgcn_s_memrealtime();
-                unsigned xcc;
-                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-                a.trace[8 * t + 4] = xcc;
-            }
-          }
-        } else if (wave < CW + NL) {
-            // ---------------- loaders: every step's DMAs spread over the NL waves ----------------
-            const int w = wave - CW;
-            long nbr[P];
-#pragma unroll
-            for (int p = 0; p < P; p++) nbr[p] = nb(min(p, np - 1), lc);
-            auto issue = [&](int q) {
-                const int qc = min(max(q, 0), T - 1);
-                const unsigned sl = lds0 + (unsigned)(((q % R + R) % R) * SL::BYTES);
-                const char *cb = reinterpret_cast<const char *>(a.coef) + (d.cbase + qc * SB) * (8L * NA);
-#pragma unroll
-                for (int k = 0; k < KPER; k++) {
-                    const int m = w + k * NL;
-                    if (m < SL::NPC) {
-                        dma16(cb + m * 1024 + lane * 16, sl + SL::COEF + m * 1024);
-                    } else if (m < NITEM) {
-                        const int r = m - SL::NPC;
-                        const char *ub = reinterpret_cast<const char *>(a.rhs) + (d.cbase + qc * SB) * 8L;
-                        dma16(ub + r * 1024 + lane * 16, sl + SL::RHS + r * 1024);
-                    } else {
-                        dma16(cb + lane * 16, sl + SL::COEF);  // keeps the per-wave count fixed
-                    }
-                }
-            };
-            for (int s = S0; s <= T; s++) {
-                const unsigned long long i0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
-                if constexpr (line_load_sleep<RHS_NAT, OUT>() > 0) __builtin_amdgcn_s_sleep(line_load_sleep<RHS_NAT, OUT>());
-                if (!(a.diag & 2)) issue(s + D);  // dummies past T keep the wait counts exact
-                const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
-                // steps s+LA+1 .. s+D were issued after step s+LA's
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - LA) * KPER) : "memory");
-                if (trs && w == 0 && s >= 0 && s < T) {
-                    ts[8 * s + 4] = w0 - i0;
-                    ts[8 * s + 3] = __builtin_amdgcn_s_memtime() - w0;
-                }
-                line_barrier();
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else if (wave == CW + NL) {
-            // ---------------- poller ----------------
-            // LDS-DMA sc1 reads of the hand-off inputs straight into their ring
-            // slots, DH steps ahead: at step s the k-input of step s+DH (NJ/2 lanes x
-            // 16 B) and the j-input of step s+DH+1 (P/2 lanes x 16 B) are issued,
-            // and those of steps s+1 (k) and s+2 (j) -- issued DH-1 steps ago -- are
-            // waited for and checked (the compute reads k at its step start, j one
-            // step earlier with the coefficients).  DMA loads have no register
-            // destination, so the ring depth is bounded only by the slot ring.
-            // A tile without a k (j) input gets +0.0 there: its coefficient is
-            // +0.0 and +0.0 * +0.0 leaves the row's sum bit for bit unchanged.
-            const double *hk = a.hk + (long)max(d.tk, 0) * a.hk_stride;
-            const double *hj = a.hj + (long)max(d.tj, 0) * a.hj_stride;
-            const int qmax = (int)(a.hk_stride / NJ) - 1;
-            auto kval = [&](int q) { return q >= 0 && q < T && lane < nj && q - lane >= 0 && q - lane < nx; };
-            auto jval = [&](int q) { return q >= 0 && q < T && lane < np && q - lane >= 0 && q - lane < nx; };
-            const unsigned sink = lds0 + (unsigned)(R * SL::BYTES + RS * P * NJ * 8 + 16);
-            auto issue = [&](int q) {
-                // k-input of step q (lanes 0..NJ/2-1), j-input of step q+1 (lanes 0..P/2-1)
-                const char *kp = reinterpret_cast<const char *>(hk + (long)min(max(q, 0), qmax) * NJ) + lane * 16;
-                const char *jp = reinterpret_cast<const char *>(hj + (long)min(max(q + 1, 0), qmax) * P) + lane * 16;
-                const unsigned ks = kin ? lds0 + (unsigned)((((q % R) + R) % R) * SL::BYTES + SL::KFIN) : sink;
-                const unsigned js = jin ? lds0 + (unsigned)(((((q + 1) % R) + R) % R) * SL::BYTES + SL::JFIN) : sink;
-                if (lane < NJ / 2) dma16_sc1(kp, ks);
-                if (lane < P / 2) dma16_sc1(jp, js);
-            };
-            if (!kin || !jin) {
-                for (int q = 0; q < R; q++) {
-                    if (!kin && lane < NJ) reinterpret_cast<double *>(ring + q * SL::BYTES + SL::KFIN)[lane] = 0.0;
-                    if (!jin && lane < P) reinterpret_cast<double *>(ring + q * SL::BYTES + SL::JFIN)[lane] = 0.0;
-                }
-            }
-            if constexpr (line_poll_prio<RHS_NAT, OUT>() > 0) __builtin_amdgcn_s_setprio(line_poll_prio<RHS_NAT, OUT>());
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            unsigned polls = 0;
-            for (int s = S0; s <= T; s++) {
-                // every step issues and waits (past T too), so the load queue has
-                // one shape on every path; only the slot work and the barrier stop at T
-                const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
-                issue(s + DH);
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (DH - 1)) : "memory");
-                if (s > T) break;
-                const int qk = s + 1, qj = s + 2;
-                double *kslot = reinterpret_cast<double *>(ring + (qk % R) * SL::BYTES + SL::KFIN) + lane;
-                double *jslot = reinterpret_cast<double *>(ring + (qj % R) * SL::BYTES + SL::JFIN) + min(lane, P - 1);
-                const bool vk = kin && kval(qk), vj = jin && jval(qj);
-                const uint64_t kv = vk ? (uint64_t)__double_as_longlong(*kslot) : 0;
-                const uint64_t jv = vj ? (uint64_t)__double_as_longlong(*jslot) : 0;
-                const bool bk = vk && kv == TRI_SENTINEL, bj = vj && jv == TRI_SENTINEL;
-                if (__any(!(a.diag & 8) && (bk || bj))) {
-                    // resync episode: the producer was not done when these polls were
-                    // issued, so probably neither for the polls still in flight.
-                    // Drain them, wait for these values and for the furthest step in
-                    // flight (so the consumer settles that much further behind and
-                    // its early polls find their values from then on), re-issue.
-                    polls++;
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    auto spin = [&](const double *src) {
-                        for (;;) {
-                            const uint64_t b = line_ld_agent(src);
-                            if (b != TRI_SENTINEL) return b;
-                            if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {  // 4 s
-                                atomicOr(a.err, 8);
-                                return (uint64_t)0x7FF8000000000000ull;
-                            }
-                            __builtin_amdgcn_s_sleep(1);
-                        }
-                    };
-                    if (bk) *kslot = __longlong_as_double((long long)spin(hk + (long)qk * NJ + lane));
-                    if (bj) *jslot = __longlong_as_double((long long)spin(hj + (long)qj * P + lane));
-                    if (kin && kval(s + DH)) (void)spin(hk + (long)(s + DH) * NJ + lane);
-                    if (jin && jval(s + DH + 1)) (void)spin(hj + (long)(s + DH + 1) * P + lane);
-                    for (int k = 2; k <= DH; k++) issue(s + k);  // the polls issued at steps s+k-DH
-                }
-                if (trs && s >= 0 && s < T) ts[8 * s + 2] = __builtin_amdgcn_s_memtime() - w0;
-                line_barrier();
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (TRACE) {
-                for (int o = 32; o >= 1; o >>= 1) polls += __shfl_xor(polls, o);
-                if (lane == 0) a.trace[8 * t + 3] = polls;
-            }
-        } else if (RHS_NAT && wave == CW + NL + 1 + SW) {
-            // ---------------- rhs wave (natural-order rhs) ----------------
-            // Block b (steps 8b .. 8b+7) of the rhs is loaded as runs -- the 8
-            // consecutive rows (i = 8b - l - p + m, m = 0..7) of line l, plane p go
-            // to 8 consecutive lanes, so a load touches 8 runs instead of 64 lines
-            // -- in 8 slices of P*NJ values; slice k is written to LDS at step
-            // 8b - 9 + k, from loads issued LINE_RW steps earlier (a register ring
-            // the compiler tracks: plain loads, no asm).  The compute reads block b
-            // from step 8b-1 on; two buffers alternate.
-            constexpr int NI = P * NJ / 64;  // loads per lane per slice
-            auto slice_of = [&](int s, int &b, int &k) {
-                b = (s + 9) >> 3;
-                k = (s + 9) & 7;
-            };
-            double ring_v[LINE_RW][NI];
-            auto issue = [&](int s, double (&dst)[NI]) {
-                int b, k;
-                slice_of(s, b, k);
-#pragma unroll
-                for (int it = 0; it < NI; it++) {
-                    const int v = k * P * NJ + it * 64 + lane;
-                    const int r = v >> 3, m = v & 7;
-                    const int p = r / NJ, l = r % NJ;
-                    const int i = 8 * b + m - l - p;
-                    const bool ok = b >= 0 && p < np && l < nj && (unsigned)i < (unsigned)nx;
-                    const long row = ok ? (a.mirror ? nb(p, l) - i : nb(p, l) + i) : 0;
-                    dst[it] = ok ? a.rhs[row] : 0.0;
-                }
-            };
-            auto write = [&](int s, const double (&src)[NI]) {
-                int b, k;
-                slice_of(s, b, k);
-                if (b < 0) return;
-                double *blk = rhsblk + (b & 1) * line_rhs_blk<P>();
-#pragma unroll
-                for (int it = 0; it < NI; it++) {
-                    const int v = k * P * NJ + it * 64 + lane;
-                    const int r = v >> 3, m = v & 7;
-                    blk[m * (P * NJ + 1) + r] = src[it];  // r = p*NJ + l
-                }
-            };
-            auto rstep = [&](int s, auto U) {
-                constexpr int u = decltype(U)::value;  // set u: issued at step s, written at s + LINE_RW
-                if (s > T) return;
-                write(s, ring_v[u]);
-                if (LINE_RHS_SLEEP) __builtin_amdgcn_s_sleep(LINE_RHS_SLEEP);
-                issue(s + LINE_RW, ring_v[u]);
-                line_barrier();
-            };
-            static_for<0, LINE_RW>([&](auto U) { issue(S0 + decltype(U)::value, ring_v[decltype(U)::value]); });
-            for (int s = S0; s <= T; s += LINE_RW) static_for<0, LINE_RW>([&](auto U) { rstep(s + decltype(U)::value, U); });
-        } else {
-            // ---------------- storers: results, re-arms ----------------
-            // OUT 2 (the U sweep's rhs stream, contiguous per plane and step):
-            // storer w writes 64-value chunks w, w+SW, ... of step s-1.  OUT 1 (natural
-            // order): the results of an 8-step block are written during the next
-            // 8 steps as runs -- 8 consecutive rows of one line (one lane, one
-            // plane) go to 8 consecutive lanes, so a store touches 8 runs instead
-            // of 64 lines.  Storer 0 re-arms the consumed j-inputs, storer SW-1
-            // the k-inputs.
-            const int w = wave - (CW + NL + 1);
-            uint64_t *hki = reinterpret_cast<uint64_t *>(a.hk + (long)max(d.tk, 0) * a.hk_stride) + lane;
-            uint64_t *hji = reinterpret_cast<uint64_t *>(a.hj + (long)max(d.tj, 0) * a.hj_stride) + min(lane, P - 1);
-            const bool rk = w == SW - 1 && kin && lane < nj, rj = w == 0 && jin && lane < np;
-            auto rearm = [&](int q) {
-                if (rk && (unsigned)(q - lane) < (unsigned)nx) hki[(long)q * NJ] = TRI_SENTINEL;
-                if (rj && (unsigned)(q - lane) < (unsigned)nx) hji[(long)q * P] = TRI_SENTINEL;
-            };
-            if constexpr (OUT == 1) {
-                // block B (steps 8B .. 8B+7) is written during steps 8B+8 .. 8B+15,
-                // slice k = s - 8B - 8 at step s: values k*NV + w*NV/SW + it*64 + lane
-                constexpr int NV = P * NJ;  // values per slice (a block holds 8 * NV)
-                static_assert(NV % (64 * SW) == 0 && RS == 16, "slices");
-                auto slice = [&](int s) {
-                    const int B = (s >> 3) - 1, k = s & 7;
-                    if (B < 0) return;
-#pragma unroll
-                    for (int it = 0; it < NV / (64 * SW); it++) {
-                        const int v = k * NV + w * (NV / SW) + it * 64 + lane;
-                        const int r = v >> 3, m = v & 7;  // run r = (plane, line), step 8B+m
-                        const int p = r / NJ, l = r % NJ, q = 8 * B + m;
-                        const int i = q - l - p;
-                        const double x = res[((q & (RS - 1)) * P + p) * NJ + l];
-                        if (!(a.diag & 1) && p < np && l < nj && (unsigned)i < (unsigned)nx)
-                            a.out[a.mirror ? nb(p, l) - i : nb(p, l) + i] = x;
-                    }
-                };
-                for (int s = S0; s <= T; s++) {
-                    const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
-                    if (LINE_STORE_SLEEP) __builtin_amdgcn_s_sleep(LINE_STORE_SLEEP);
-                    if (s >= 0) slice(s);
-                    if (s >= 1 && s <= T) rearm(s - 1);
-                    if (trs && w == 0 && s >= 0 && s < T) ts[8 * s + 5] = __builtin_amdgcn_s_memtime() - w0;
-                    line_barrier();
-                }
-                // the last blocks' remaining slices (every compute result is in LDS)
-                for (int s = T + 1; s < 8 * ((T >> 3) + 2); s++) slice(s);
-            } else {
-                // chunk c of a step's results: 64 lanes = G planes (c*G + gl) x NJ lines (ll)
-                constexpr int PS = P * NJ / 64 / SW;
-                static_assert(P * NJ % (64 * SW) == 0, "chunks");
-                double *po[PS];
-                int vlo[PS];
-#pragma unroll
-                for (int u = 0; u < PS; u++) {
-                    const int p = (w + u * SW) * G + gl, pp = min(p, np - 1);
-                    vlo[u] = p < np && ll < nj ? ll + p : 1 << 30;  // valid iff 0 <= q - vlo < nx
-                    // the mirror U tile's row of (step T-1-q, plane np-1-p, line nj-1-l) at q = 0
-                    po[u] = a.out + d.ubase + (long)(T - 1) * SB + (long)(np - 1 - pp) * nj + (nj - 1 - lc);
-                }
-                for (int s = S0; s <= T; s++) {
-                    const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
-                    if (LINE_STORE_SLEEP) __builtin_amdgcn_s_sleep(LINE_STORE_SLEEP);
-                    const int q = s - 1;
-                    if (q >= 0 && q < T) {
-                        const double *rs = res + (q & (RS - 1)) * P * NJ;
-#pragma unroll
-                        for (int u = 0; u < PS; u++) {
-                            const double v = rs[(w + u * SW) * 64 + lane];
-                            if (!(a.diag & 33) && (unsigned)(q - vlo[u]) < (unsigned)nx) po[u][-SB * q] = v;
-                        }
-                        rearm(q);
-                    }
-                    if (trs && w == 0 && s >= 0 && s < T) ts[8 * s + 5] = __builtin_amdgcn_s_memtime() - w0;
-                    line_barrier();
-                }
-            }
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------
 // k_line2: two levels per workgroup step (the default line sweep)
 // ---------------------------------------------------------------------------
@@ -1073,9 +487,6 @@ __global__ __launch_bounds__((64 * line_waves<CW, NL, SW, RHS_NAT>())) void k_li
 // plain division (profiles/r04/r04d_*, r04e_*, r04f_*): its range checks and
 // the extra operand cost as much as the shorter chain saves.
 
-#ifndef LINE2_EARLY_SHFL
-#define LINE2_EARLY_SHFL 1  // k-operand shuffle issued before the level's stores (k_line2 compute)
-#endif
 
 namespace l2 {
 constexpr int NJ = 16;  // lines per tile; LV (2 or 4) levels per step; P (8 or 16) planes per tile: 2 or 4 compute waves
@@ -1274,19 +685,14 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                         if constexpr (NA == 4) v = v / cur.dg[lv];
                         const double x = sel_lanes(h[lv], v, xq);
                         if (trs && wave == 0 && lv == LV - 1) ts[8 * s + 6] = __builtin_amdgcn_s_memtime();
-#if LINE2_EARLY_SHFL
                         // the next level's k operand (the next step's first, for the
                         // last level) is shuffled BEFORE this level's hand-off and
                         // LDS stores: its ds_bpermute round trip runs under them
-                        // instead of after them
+                        // instead of after them (~1 %, profiles/r05/r05b_*)
                         xu = up16(x);
                         __builtin_amdgcn_sched_barrier(0);
-#endif
                         publish(LV * s + lv, h[lv], x);  // its store issues under the next level's arithmetic
                         res[((LV * s + lv) & (RSL - 1)) * ROWS + pw * NJ + ll] = x;
-#if !LINE2_EARLY_SHFL
-                        xu = up16(x);
-#endif
                         xq = x;
                     }
                     xp = xq;
@@ -1333,9 +739,6 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
             };
             for (int s = S0; s <= TS; s++) {
                 const unsigned long long i0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
-#if LINE2_LOAD_SLEEP
-                __builtin_amdgcn_s_sleep(LINE2_LOAD_SLEEP);  // tuning: let the step's polls enter the memory queue first
-#endif
                 issue(s + D);  // dummies past TS keep the wait counts exact
                 const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
                 // steps s+LA+1 .. s+D were issued after step s+LA's
@@ -1406,7 +809,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     // furthest step in flight, so the re-issued polls cannot miss; that
                     // holds the tile DH steps behind its producer after every episode:
                     // 216^3 apply 528.5 -> 508.9 us without it, bitwise the same,
-                    // profiles/r05/r05p_resync_near.txt.  -DLINE2_RESYNC_FAR restores it)
+                    // profiles/r05/r05p_resync_near.txt)
                     polls++;
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     auto spin = [&](const double *src) {
@@ -1417,19 +820,10 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                                 atomicOr(a.err, 8);
                                 return (uint64_t)0x7FF8000000000000ull;
                             }
-#ifndef LINE2_SPIN_SLEEP
-#define LINE2_SPIN_SLEEP 0  // resync spin: back-to-back polls (r05q)
-#endif
-                            if (LINE2_SPIN_SLEEP) __builtin_amdgcn_s_sleep(LINE2_SPIN_SLEEP);
                         }
                     };
                     if (bk) *kslot = __longlong_as_double((long long)spin(hk + (long)lk * NJ + kl));
                     if (bj) *jslot = __longlong_as_double((long long)spin(hj + (long)lj * P + jp));
-#ifdef LINE2_RESYNC_FAR  // tuning builds: also wait for the furthest step in flight
-                    const int fk = LV * (s + DH) + kv, fj = LV * (s + DH + 1) + jv;
-                    if (kin && kval(fk)) (void)spin(hk + (long)fk * NJ + kl);
-                    if (jin && jval(fj)) (void)spin(hj + (long)fj * P + jp);
-#endif
                     for (int k = 2; k <= DH; k++) issue(s + k);  // the polls issued at steps s+k-DH
                 }
                 if (trs && s >= 0 && s < TS) ts[8 * s + 2] = __builtin_amdgcn_s_memtime() - w0;
@@ -1476,11 +870,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                         if (!(a.diag & 1) && p < np && l < nj && (unsigned)i < (unsigned)nx) {
                             double *o = a.out + (a.mirror ? nb(p, l) - i : nb(p, l) + i);
                             if (tail) st_sc1d(o, x);  // read by the tail product on other CUs
-#ifdef LINE2_OUT_NT  // tuning builds: the natural-order output as non-temporal stores
-                            else __builtin_nontemporal_store(x, o);
-#else
                             else *o = x;
-#endif
                         }
                     }
                 };
@@ -1546,102 +936,6 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
 // ---------------------------------------------------------------------------
 // launch
 // ---------------------------------------------------------------------------
-// Leads (steps): loaders D, poller DH.  The apply's sweeps (rhs from a stream)
-// measured fastest at D = 7, DH = 3 (apply 795-799 us against 818-823 at 10 /
-// 2, three sessions; D 4-6 and 8-10 at DH = 3 and DH 2 or 4 at D = 7 were
-// slower, profiles/r03/r03n_line_leads.txt); the standalone sweeps (natural-
-// order rhs through the rhs wave) keep 10 / 2, where DH = 3 costs 15-30 us.
-template <bool RHS_NAT>
-constexpr int line_d()
-{
-#ifdef LINE_D_OVERRIDE
-    return LINE_D_OVERRIDE;
-#else
-    return RHS_NAT ? 10 : 7;
-#endif
-}
-template <bool RHS_NAT>
-constexpr int line_dh()
-{
-#ifdef LINE_DH_OVERRIDE
-    return LINE_DH_OVERRIDE;
-#else
-    return RHS_NAT ? 2 : 3;
-#endif
-}
-constexpr int LINE_CW = 2;  // two compute waves: P / 4 lane groups x two planes each
-#ifndef LINE_NL_OVERRIDE
-constexpr int LINE_NL = 4;
-#else
-constexpr int LINE_NL = LINE_NL_OVERRIDE;
-#endif
-#ifndef LINE_SW_OVERRIDE
-constexpr int LINE_SW = 4;  // storer waves (2 -> 4: 216^3 apply 751 -> 693 us, r03ae)
-#else
-constexpr int LINE_SW = LINE_SW_OVERRIDE;  // tuning builds
-#endif
-
-template <int P, int NA, bool RHS_NAT, int OUT, bool TRACE>
-static int launch_line_k(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &g, int lds)
-{
-    auto kern = k_line<P, NA, RHS_NAT, OUT, LINE_CW, LINE_NL, line_d<RHS_NAT>(), line_dh<RHS_NAT>(), LINE_SW, TRACE>;
-    static int attr = 0;
-    if (lds > attr) {
-        LSSP_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        attr = lds;
-    }
-    const int grid = std::min(ls.ntiles, c->num_cus);
-    kern<<<grid, 64 * line_waves<LINE_CW, LINE_NL, LINE_SW, RHS_NAT>(), lds, c->stream>>>(g);
-    ls.base += (unsigned long long)ls.ntiles + grid;
-    LSSP_HIP(hipGetLastError());
-    return LSSP_AMD_OK;
-}
-
-template <int P, int NA, bool RHS_NAT, int OUT>
-static int launch_line_p(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a)
-{
-    const int lds = line_lds_bytes<P, NA, RHS_NAT, OUT, line_d<RHS_NAT>()>();
-    if (lds > 160 * 1024) return LSSP_AMD_EUNSUPPORTED;
-    // diagnostics only: LSSP_AMD_LINE_TRACE=path[:tile] appends one JSON line per sweep
-    static const char *trp = getenv("LSSP_AMD_LINE_TRACE");
-    if (!trp) return launch_line_k<P, NA, RHS_NAT, OUT, false>(c, ls, a, lds);
-    LineArgs g = a;
-    const size_t tn = 8 * (size_t)ls.ntiles + 8 * (size_t)ls.tmax + 64;
-    const char *colon = strrchr(trp, ':');
-    g.ttile = colon ? atoi(colon + 1) : ls.ntiles / 2;
-    LSSP_HIP(hipMalloc(&g.trace, sizeof(unsigned long long) * tn));
-    LSSP_HIP(hipMemsetAsync(g.trace, 0, sizeof(unsigned long long) * tn, c->stream));
-    const int grid = std::min(ls.ntiles, c->num_cus);
-    LSSP_TRY((launch_line_k<P, NA, RHS_NAT, OUT, true>(c, ls, g, lds)));
-    std::vector<unsigned long long> h(tn);
-    LSSP_HIP(hipMemcpyAsync(h.data(), g.trace, sizeof(unsigned long long) * tn, hipMemcpyDeviceToHost, c->stream));
-    LSSP_HIP(hipStreamSynchronize(c->stream));
-    (void)hipFree(g.trace);
-    std::string path(trp, colon ? colon - trp : strlen(trp));
-    FILE *f = fopen(path.c_str(), "a");
-    if (f) {
-        fprintf(f, "{\"mirror\": %d, \"ntiles\": %d, \"W\": %d, \"ttile\": %d, \"T\": %d, \"grid\": %d, \"data\": [",
-                a.mirror, ls.ntiles, (ls.ny + 256 / P - 1) / (256 / P), g.ttile, ls.h_tiles[g.ttile].T, grid);
-        for (size_t i = 0; i < tn; i++) fprintf(f, "%s%llu", i ? ", " : "", h[i]);
-        fprintf(f, "]}\n");
-        fclose(f);
-    }
-    return LSSP_AMD_OK;
-}
-template <int NA, bool RHS_NAT, int OUT>
-static int launch_line_t(lssp_amd_ctx *c, const LineSweep &ls, const LineArgs &a)
-{
-    switch (ls.P) {
-    case 4: return launch_line_p<4, NA, RHS_NAT, OUT>(c, ls, a);
-    case 8: return launch_line_p<8, NA, RHS_NAT, OUT>(c, ls, a);
-    case 16: return launch_line_p<16, NA, RHS_NAT, OUT>(c, ls, a);
-    default: return LSSP_AMD_EUNSUPPORTED;
-    }
-}
-
-// which: 0 = L sweep, 1 = U sweep.  The rhs is natural order unless u_in (the
-// U rhs stream); the output goes to out (natural order) or, when out_u, to the
-// U rhs stream (the L sweep of an apply)
 // The apply's rhs (natural order) into the L sweep's stream layout.  A block
 // moves 8 consecutive steps of one tile (P x NJ x 8 values): value v of the
 // block is (plane p, line l, step q0 + m) with m = v & 7, so 8 neighbouring
@@ -1717,11 +1011,7 @@ __global__ __launch_bounds__(256) void k_line_rhs2(const LineTile *__restrict__ 
         const bool ok = q0 + m < d.T && p < d.np && l < d.nj && (unsigned)i < (unsigned)nx;
         const long r = ((long)(d.k0 + p) * ny + (d.j0 + l)) * nx + i;
         if (OP == 0) {
-#ifdef LRHS2_NT  // tuning builds: the apply's rhs read non-temporal
-            v[it] = ok ? __builtin_nontemporal_load(rhs + r) : 0.0;
-#else
             v[it] = ok ? rhs[r] : 0.0;
-#endif
         } else {
             v[it] = 0.0;
             if (ok) {
@@ -1766,8 +1056,8 @@ __global__ __launch_bounds__(256) void k_line_rhs2(const LineTile *__restrict__ 
 // the L sweep, li.d_ustream for the U sweep)
 static int launch_line_gather(lssp_amd_ctx *c, const LineSweep &ls, int mirror, const double *rhs, double *stream)
 {
-    if (ls.LV >= 2 && (ls.P != 8 || ls.NJ != 16)) return LSSP_AMD_EUNSUPPORTED;
-    if (ls.LV == 2 && !mirror) {
+    if (ls.LV != 2 || ls.P != 8 || ls.NJ != 16) return LSSP_AMD_EUNSUPPORTED;
+    if (!mirror) {
         const int nq2 = (ls.tmax + LRHS2_RUN - 1) / LRHS2_RUN;
         k_line_rhs2<LRHS2_RUN, 0><<<8L * ((ls.ntiles + 7) / 8) * nq2, 256, 0, c->stream>>>(
             ls.d_tiles, ls.ntiles, nq2, ls.nx, ls.ny, rhs, stream, c->guard, nullptr, nullptr, nullptr);
@@ -1776,8 +1066,7 @@ static int launch_line_gather(lssp_amd_ctx *c, const LineSweep &ls, int mirror, 
     }
     const int nq = (ls.tmax + LRHS_RUN - 1) / LRHS_RUN;
     const long grid = 8L * ((ls.ntiles + 7) / 8) * nq;
-    auto kr = ls.LV == 4 ? k_line_rhs<8, 16, 3> : ls.LV == 2 ? k_line_rhs<8, 16, 1>
-              : ls.P == 16 ? k_line_rhs<16, 16, 0> : ls.P == 8 ? k_line_rhs<8, 32, 0> : k_line_rhs<4, 64, 0>;
+    auto kr = k_line_rhs<8, 16, 1>;  // (the U sweep's mirrored tiles; the L sweep takes k_line_rhs2 above)
     const long n = (long)ls.nx * ls.ny * ls.nz;
     kr<<<grid, 256, 0, c->stream>>>(ls.d_tiles, ls.ntiles, nq, ls.nx, ls.ny, n, mirror, rhs, stream, c->guard);
     LSSP_HIP(hipGetLastError());
@@ -1806,12 +1095,9 @@ int launch_line_gather_ew(lssp_amd_ctx *c, const LineILU &li, int op, const doub
     const LineSweep &ls = li.L;
     if (!line_gather_ew_ok(li, (long)ls.nx * ls.ny * ls.nz) || (op != GEW_BICG_P && op != GEW_BICG_S))
         return LSSP_AMD_EINVAL;
-#ifndef LRHS2_RUN_EW
-#define LRHS2_RUN_EW LRHS2_RUN
-#endif
-    const int nq = (ls.tmax + LRHS2_RUN_EW - 1) / LRHS2_RUN_EW;
+    const int nq = (ls.tmax + LRHS2_RUN - 1) / LRHS2_RUN;
     const long grid = 8L * ((ls.ntiles + 7) / 8) * nq;
-    auto kr = op == GEW_BICG_P ? k_line_rhs2<LRHS2_RUN_EW, GEW_BICG_P> : k_line_rhs2<LRHS2_RUN_EW, GEW_BICG_S>;
+    auto kr = op == GEW_BICG_P ? k_line_rhs2<LRHS2_RUN, GEW_BICG_P> : k_line_rhs2<LRHS2_RUN, GEW_BICG_S>;
     kr<<<grid, 256, 0, c->stream>>>(ls.d_tiles, ls.ntiles, nq, ls.nx, ls.ny, x, li.d_lstream, c->guard, y, out, scal);
     LSSP_HIP(hipGetLastError());
     li.lstream_of = out;
@@ -1933,56 +1219,16 @@ static int launch_line2(lssp_amd_ctx *c, const LineILU &li, int which, const dou
     return ls.NA == 3 ? launch_line2_t<8, 2, 3, 1>(c, ls, a) : launch_line2_t<8, 2, 4, 1>(c, ls, a);
 }
 
-static int launch_line(lssp_amd_ctx *c, const LineILU &li, int which, const double *rhs, bool u_in, double *out,
-                       bool out_u, bool l_in = false)
-{
-    const LineSweep &ls = which ? li.U : li.L;
-    LineArgs a{};
-    a.nx = ls.nx;
-    a.ny = ls.ny;
-    a.ntiles = ls.ntiles;
-    a.n = (long)ls.nx * ls.ny * ls.nz;
-    a.tiles = ls.d_tiles;
-    a.coef = ls.d_coef;
-    a.rhs = u_in ? li.d_ustream : l_in ? li.d_lstream : rhs;
-    a.out = out_u ? li.d_ustream : out;
-    a.hk = li.d_hk;
-    a.hj = li.d_hj;
-    a.hk_stride = li.hk_stride;
-    a.hj_stride = li.hj_stride;
-    a.claim = ls.d_claim;
-    a.base = ls.base;
-    a.mirror = which;
-    a.err = c->d_err;
-    a.guard = c->guard;
-    {
-        const char *dg = getenv("LSSP_AMD_LINE_DIAG");
-        a.diag = dg ? atoi(dg) : 0;
-    }
-    if (u_in) return launch_line_t<4, false, 1>(c, ls, a);
-    if (l_in) return ls.NA == 3 ? launch_line_t<3, false, 2>(c, ls, a) : launch_line_t<4, false, 2>(c, ls, a);
-    if (out_u) return ls.NA == 3 ? launch_line_t<3, true, 2>(c, ls, a) : launch_line_t<4, true, 2>(c, ls, a);
-    return ls.NA == 3 ? launch_line_t<3, true, 1>(c, ls, a) : launch_line_t<4, true, 1>(c, ls, a);
-}
-
 int launch_line_apply(lssp_amd_ctx *c, const LineILU &li, double *x, const double *rhs)
 {
     const bool ready = rhs == li.lstream_of;  // the stream holds rhs already (launch_line_gather_ew)
     li.lstream_of = nullptr;
     if (li.g2) return launch_lineg(c, li, 0, x, rhs);
     if (li.kind == 1) return launch_linefill_apply(c, li, x, rhs);
-    if (li.LV >= 2) {  // k_line2: gather, L sweep -> the U rhs stream, U sweep -> x
-        if (!ready) LSSP_TRY(launch_line_gather(c, li.L, 0, rhs, li.d_lstream));
-        LSSP_TRY(launch_line2(c, li, 0, li.d_lstream, li.d_ustream, 2));
-        return launch_line2(c, li, 1, li.d_ustream, x, 1);
-    }
-#ifdef LINE_APPLY_NAT  // tuning builds: the L sweep reads the natural-order rhs itself (rhs wave)
-    LSSP_TRY(launch_line(c, li, 0, rhs, false, nullptr, true));
-    return launch_line(c, li, 1, nullptr, true, x, false);
-#endif
-    LSSP_TRY(launch_line_gather(c, li.L, 0, rhs, li.d_lstream));
-    LSSP_TRY(launch_line(c, li, 0, nullptr, false, nullptr, true, true));
-    return launch_line(c, li, 1, nullptr, true, x, false);
+    // k_line2: gather, L sweep -> the U rhs stream, U sweep -> x
+    if (!ready) LSSP_TRY(launch_line_gather(c, li.L, 0, rhs, li.d_lstream));
+    LSSP_TRY(launch_line2(c, li, 0, li.d_lstream, li.d_ustream, 2));
+    return launch_line2(c, li, 1, li.d_ustream, x, 1);
 }
 
 unsigned *tail_dbg_host = nullptr;  // LSSP_AMD_TAIL_DIAG (lssp_amd_debug_words)
@@ -2097,12 +1343,10 @@ int launch_line_sweep(lssp_amd_ctx *c, const LineILU &li, int which, double *x, 
     li.lstream_of = nullptr;
     if (li.g2) return launch_lineg(c, li, which ? 2 : 1, x, rhs);
     if (li.kind == 1) return launch_linefill_sweep(c, li, which, x, rhs);
-    if (li.LV >= 2) {  // one sweep: its rhs gathered into its own stream, natural-order output
-        double *st = which ? li.d_ustream : li.d_lstream;
-        LSSP_TRY(launch_line_gather(c, which ? li.U : li.L, which, rhs, st));
-        return launch_line2(c, li, which, st, x, 1);
-    }
-    return launch_line(c, li, which, rhs, false, x, false);
+    // one sweep: its rhs gathered into its own stream, natural-order output
+    double *st = which ? li.d_ustream : li.d_lstream;
+    LSSP_TRY(launch_line_gather(c, which ? li.U : li.L, which, rhs, st));
+    return launch_line2(c, li, which, st, x, 1);
 }
 
 }  // namespace lssp_amd

@@ -1,5 +1,5 @@
 // linesweep_dev.h -- device helpers shared by the line sweeps (linesweep.hip:
-// k_line, k_line2 for ILU(0); linefill.hip: k_linef for the 7-point ILU(1)
+// k_line2 for ILU(0); linefill.hip: k_linef for the 7-point ILU(1)
 // pattern): LDS-DMA issue, the workgroup barrier, agent-scope hand-off loads,
 // lane selects, DPP row shifts and the lane - 16 shuffle.
 #pragma once

@@ -213,21 +213,15 @@ def _box7(nx, ny, nz, seed):
     return np.array(Ap, np.int32), np.array(Aj, np.int32), np.array(Ax)
 
 
-# boxes whose k_line tiles (LSSP_AMD_LINE_MODE=1, 256 rows per level) are 64 x 4
-# (planes per tile chosen by hop count: (20, 100, 6)), 32 x 8 ((20, 60, 24))
-# and 16 x 16 ((20, 40, 40), (13, 37, 35)); k_line2 (the default) always takes
-# 16 x 8 -- partial tiles in j and k, an odd last plane count, slabs with 1..3
-# planes in the second compute wave ((13, 37, 35): 35 = 4 x 8 + 3; (9, 21, 13):
-# 13 = 8 + 5, (20, 17, 6): one tile of 6 planes, (11, 16, 4): planes in wave 0 only)
-@pytest.mark.parametrize("nx,ny,nz,tile,mode", [(20, 100, 6, (64, 4), 1), (20, 60, 24, (32, 8), 1),
-                                                (20, 40, 40, (16, 16), 1), (13, 37, 35, (16, 16), 1),
-                                                (20, 100, 6, (16, 8), 2), (13, 37, 35, (16, 8), 2),
-                                                (9, 21, 13, (16, 8), 2), (20, 17, 6, (16, 8), 2),
-                                                (11, 16, 4, (16, 8), 2), (40, 33, 19, (16, 8), 2)])
-def test_line_sweep_tile_shapes_bitwise_vs_oracle(dev, monkeypatch, nx, ny, nz, tile, mode):
-    """mode 1: k_line; 2: k_line2 (the default)"""
+# k_line2's 16-line x 8-plane tiles on boxes with partial tiles in j and k, an
+# odd last plane count, slabs with 1..3 planes in the second compute wave
+# ((13, 37, 35): 35 = 4 x 8 + 3; (9, 21, 13): 13 = 8 + 5, (20, 17, 6): one tile
+# of 6 planes, (11, 16, 4): planes in wave 0 only), 40 x 40 planes, a long thin box
+@pytest.mark.parametrize("nx,ny,nz", [(20, 100, 6), (13, 37, 35), (9, 21, 13), (20, 17, 6), (11, 16, 4),
+                                      (40, 33, 19), (20, 40, 40), (20, 60, 24)])
+def test_line_sweep_tile_shapes_bitwise_vs_oracle(dev, nx, ny, nz):
     import lssp_amd
-    monkeypatch.setenv("LSSP_AMD_LINE_MODE", str(mode))
+    tile = (16, 8)
     Ap, Aj, Ax = _box7(nx, ny, nz, nx + ny + nz)
     n = Ap.size - 1
     M = lssp_amd.DILU.create(dev, Ap, Aj, Ax, kind=1, level=0)

@@ -1,5 +1,5 @@
-"""The packet sweep's loader (trisolve.hip k_tri_pk6) and the line sweep's
-poller (linesweep.hip k_line) issue loads from inline asm with explicit
+"""The packet sweep's loader (trisolve.hip k_tri_pk6) and the line sweeps'
+loaders and pollers (linesweep.hip k_line2, linefill.hip k_linef) issue loads from inline asm with explicit
 vmcnt waits.  Compile the device code for gfx950 and
 check, on the generated assembly, that no instruction touches a VGPR that is
 still the destination of an outstanding load, and that no instantiation spills
@@ -62,29 +62,6 @@ def test_pk6_no_scratch(device_asm):
         assert m, name
         priv = int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", m.group(1)).group(1))
         assert priv == 0, (name, priv)
-
-
-def _line_kernels(path):
-    return sorted(set(re.findall(r"^(_ZN8lssp_amd6k_line\w+):", open(path).read(), re.M)))
-
-
-def test_line_instantiations_hazard_free_and_no_scratch(line_asm):
-    import check_vmcnt
-    names = _line_kernels(line_asm)
-    assert len(names) >= 3, names
-    text = open(line_asm).read()
-    for name in names:
-        assert check_vmcnt.check_loader(line_asm, name) == 0, name
-        # no scratch in the two instantiations an ILU apply runs (L: unit, rhs
-        # in natural order, into the U rhs stream; U: from the stream, natural
-        # output).  The others (TRACE diagnostics, single sweeps, non-unit L) may
-        # spill: the line sweep's only asm loads are LDS-DMAs, which have no
-        # register destination a spill could catch in flight.
-        if not (name.startswith("_ZN8lssp_amd6k_lineILi4ELi3ELb1ELi2E") or
-                name.startswith("_ZN8lssp_amd6k_lineILi4ELi4ELb0ELi1E")) or name.endswith("Lb1EEEvNS_8LineArgsE"):
-            continue
-        m = re.search(r"\.amdhsa_kernel " + name + r"\n(.*?)\.end_amdhsa_kernel", text, re.S)
-        assert int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", m.group(1)).group(1)) == 0, name
 
 
 def test_line2_instantiations_hazard_free_and_no_scratch(line_asm):
