@@ -564,14 +564,10 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
             const bool lane_ok = pw < np && ll < nj && (unsigned)jg < (unsigned)a.ny;
             struct In {
                 double c[NA][LV];
-                double rh[LV], se0[LV], be0[LV];
+                double rh[LV];
             };
-            // the next step's inputs from LDS (its slot, and this step's slot for
-            // the line -1 entries of plane pw-1 one row back)
-            auto load = [&](unsigned sn, unsigned sc, In &in) {
-                const double *jn = reinterpret_cast<const double *>(ring + sn + SL::JFIN);
-                const double *jc = reinterpret_cast<const double *>(ring + sc + SL::JFIN);
-                const int pm = max(pw - 1, 0);
+            // the next step's coefficients and rhs from LDS (its slot)
+            auto load = [&](unsigned sn, In &in) {
 #pragma unroll
                 for (int v = 0; v < LV; v++) {
                     const long r = v * SB + pw * nj + lc;
@@ -579,12 +575,9 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
 #pragma unroll
                     for (int q = 0; q < NA; q++) in.c[q][v] = b[q];
                     in.rh[v] = reinterpret_cast<const double *>(ring + sn + SL::RHS)[r];
-                    in.se0[v] = jn[v * P + min(pw, P - 1)];
-                    // line -1 of plane pw-1, row i+1: hj q = v - [pw == 4]
-                    //   (slot rows: q = 2s+1, 2s+2 at [0], [1]; the previous slot's 2s-1, 2s)
-                    in.be0[v] = pw == 4 ? jc[v * P + 3] : (v == 0 ? jc[P + pm] : jn[pm]);
                 }
             };
+            const int pm = max(pw - 1, 0);
             In A, B;
             double xp = 0.0;   // x(v-1)
             double bnp = 0.0;  // BN(v-1)
@@ -625,6 +618,7 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
             constexpr unsigned RB = (unsigned)(R * SL::BYTES);
             auto body = [&](int s, In &cur, In &nxt) {
                 const unsigned sn = so + SL::BYTES == RB ? 0u : so + SL::BYTES;  // slot of step s+1
+                const unsigned sp = so == 0 ? RB - SL::BYTES : so - SL::BYTES;    // slot of step s-1
                 // group 0's k-sources: wave 0 the poller's k-input (BN: entry 1+l,
                 // line 0's BE: entry 0), wave 1 plane 3's results of the previous step
                 double kx0, kx1, kb0 = 0.0, kb1 = 0.0;
@@ -638,17 +632,31 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
                     kx0 = res[((2 * s - 2) & (RSL - 1)) * ROWS + 3 * NJ + ll];
                     kx1 = res[((2 * s - 1) & (RSL - 1)) * ROWS + 3 * NJ + ll];
                 }
+                // the j-inputs, read at the step that uses them (as k_line2's): this
+                // step's slot, and the previous step's for the line -1 entries of
+                // plane pw-1 one row back (slot rows: q = 2s+1, 2s+2 at [0], [1]; the
+                // previous slot's 2s-1, 2s); line -1 of plane pw-1, row i+1: hj q = v - [pw == 4]
+                double se0[LV], be0[LV];
+                {
+                    const double *jc = reinterpret_cast<const double *>(ring + so + SL::JFIN);
+                    const double *jp = reinterpret_cast<const double *>(ring + sp + SL::JFIN);
+#pragma unroll
+                    for (int v = 0; v < LV; v++) {
+                        se0[v] = jc[v * P + min(pw, P - 1)];
+                        be0[v] = pw == 4 ? jp[v * P + 3] : (v == 0 ? jp[P + pm] : jc[pm]);
+                    }
+                }
                 asm volatile("" ::: "memory");
-                load(sn, so, nxt);
+                load(sn, nxt);
                 if (s >= SC && s < TS) {
                     double xu = xs;  // lane - 16's x of the previous level
 #pragma unroll
                     for (int lv = 0; lv < LV; lv++) {
                         const int v = 2 * s + lv;
                         const double bn = sel_lanes(G0M, lv == 0 ? kx0 : kx1, xu);
-                        const double be0 = wave == 0 ? sel_lanes(G0M, lv == 0 ? kb0 : kb1, cur.be0[lv]) : cur.be0[lv];
-                        const double be = dpp_shr1g<4>(bnp, be0);
-                        const double se = dpp_shr1g<4>(xp, cur.se0[lv]);
+                        const double bel = wave == 0 ? sel_lanes(G0M, lv == 0 ? kb0 : kb1, be0[lv]) : be0[lv];
+                        const double be = dpp_shr1g<4>(bnp, bel);
+                        const double se = dpp_shr1g<4>(xp, se0[lv]);
                         double r = cur.rh[lv] - cur.c[0][lv] * bep;
                         r = r - cur.c[1][lv] * be;
                         r = r - cur.c[2][lv] * bn;
@@ -733,11 +741,11 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
             const unsigned sink = lds0 + (unsigned)(R * SL::BYTES + RSL * ROWS * 8 + 16);
             auto issue = [&](int q) {
                 const int Q0 = min(max(2 * q + 2, 0), kmax);
-                const int J0 = min(max(2 * (q + 1) + 1 + HJ0, 0), jmax);
+                const int J0 = min(max(2 * q + 1 + HJ0, 0), jmax);
                 const char *kp = reinterpret_cast<const char *>(hk + (long)Q0 * HKS) + lane * 16;
                 const char *jp2 = reinterpret_cast<const char *>(hj + (long)J0 * P) + lane * 16;
                 const unsigned ks = kin ? lds0 + (unsigned)((((q % R) + R) % R) * SL::BYTES + SL::KFIN) : sink;
-                const unsigned js = jin ? lds0 + (unsigned)(((((q + 1) % R) + R) % R) * SL::BYTES + SL::JFIN) : sink;
+                const unsigned js = jin ? lds0 + (unsigned)((((q % R) + R) % R) * SL::BYTES + SL::JFIN) : sink;
                 if (lane < LV * HKS / 2) dma16_sc1(kp, ks);
                 if (lane < LV * P / 2) dma16_sc1(jp2, js);
             };
@@ -753,7 +761,7 @@ __global__ __launch_bounds__(64 * lf::waves(NL, SW)) void k_linef(FillArgs a)
                 issue(s + DH);
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (DH - 1)) : "memory");
                 if (s > TS) break;
-                const int qk = s + 1, qj = s + 2;  // steps
+                const int qk = s + 1, qj = s + 1;  // steps (the j-inputs are read at their own step)
                 // (steps from -1 are checked: the ring index of a negative step wraps)
                 double *kslot = reinterpret_cast<double *>(ring + ((qk % R + R) % R) * SL::BYTES + SL::KFIN) +
                                 min(lane, LV * HKS - 1);

@@ -592,7 +592,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
             const int pw = wave * 4 + gl;
             const int sg = (LV - 1) * wave;  // sigma of the wave's planes
             struct In {
-                double ck[LV], cj[LV], ci[LV], dg[LV], rh[LV], jv[LV];
+                double ck[LV], cj[LV], ci[LV], dg[LV], rh[LV];
             };
             // the step's inputs, read from LDS one step ahead (their slot was
             // completed before the barrier that ended the previous step)
@@ -607,7 +607,6 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     in.ci[v] = b[2];
                     if constexpr (NA == 4) in.dg[v] = b[3];
                     in.rh[v] = reinterpret_cast<const double *>(slot + SL::RHS)[r];
-                    in.jv[v] = reinterpret_cast<const double *>(slot + SL::JFIN)[v * P + pw];
                 }
             };
             In A, B;
@@ -662,6 +661,14 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                 for (int lv = 0; lv < LV; lv++)
                     kx[lv] = wave == 0 ? reinterpret_cast<const double *>(ring + so + SL::KFIN)[lv * NJ + ll]
                                        : res[((LV * s - LV + lv) & (RSL - 1)) * ROWS + (4 * wave - 1) * NJ + ll];
+                // j-inputs of line 0, read with the k-inputs at the step that uses
+                // them: polled one step later than when they were read a step ahead
+                // with the coefficients, so a j-hop's consumer starts a step
+                // earlier (216^3 apply 0.489 -> 0.474 ms, bench 650 -> 664 it/s, the
+                // 8-rank 512^3 slab 2.405 -> 2.346 ms; profiles/r06/r06i_*)
+                double jx[LV];
+#pragma unroll
+                for (int lv = 0; lv < LV; lv++) jx[lv] = reinterpret_cast<const double *>(ring + so + SL::JFIN)[lv * P + pw];
                 asm volatile("" ::: "memory");
                 load(sn, nxt);
                 // lanes whose row exists at each level: one per-lane compare each
@@ -678,7 +685,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                     for (int lv = 0; lv < LV; lv++) {
                         // level LV s + lv
                         const double xk = sel_lanes(G0M, kx[lv], xu);
-                        const double xj = dpp_shr1g<4>(xq, cur.jv[lv]);
+                        const double xj = dpp_shr1g<4>(xq, jx[lv]);
                         double v = cur.rh[lv] - cur.ck[lv] * xk;
                         v = v - cur.cj[lv] * xj;
                         v = v - cur.ci[lv] * xq;
@@ -753,10 +760,9 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
         } else if (wave == CW + NL) {
             // ---------------- poller ----------------
             // At step s: LDS-DMA sc1 reads of step s+DH's k-inputs (two levels x NJ
-            // lines: 16 lanes x 16 B) and step s+DH+1's j-inputs (two levels x P
-            // planes: 8 lanes x 16 B); then the k-inputs of step s+1 and the
-            // j-inputs of step s+2 (issued DH-1 steps ago) are waited for and
-            // checked.  A tile without a k (j) input gets +0.0 there (its
+            // lines: 16 lanes x 16 B) and j-inputs (two levels x P planes: 8 lanes x
+            // 16 B); then the k- and j-inputs of step s+1 (issued DH-1 steps ago)
+            // are waited for and checked.  A tile without a k (j) input gets +0.0 there (its
             // coefficient is +0.0 too).
             const double *hk = a.hk + (long)max(d.tk, 0) * a.hk_stride;
             const double *hj = a.hj + (long)max(d.tj, 0) * a.hj_stride;
@@ -772,9 +778,9 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
             const unsigned sink = lds0 + (unsigned)(R * SL::BYTES + RSL * ROWS * 8 + 16);
             auto issue = [&](int q) {
                 const char *kp = reinterpret_cast<const char *>(hk + (long)min(max(q, 0), qmax) * LV * NJ) + lane * 16;
-                const char *jp2 = reinterpret_cast<const char *>(hj + (long)min(max(q + 1, 0), qmax) * LV * P) + lane * 16;
+                const char *jp2 = reinterpret_cast<const char *>(hj + (long)min(max(q, 0), qmax) * LV * P) + lane * 16;
                 const unsigned ks = kin ? lds0 + (unsigned)((((q % R) + R) % R) * SL::BYTES + SL::KFIN) : sink;
-                const unsigned js = jin ? lds0 + (unsigned)(((((q + 1) % R) + R) % R) * SL::BYTES + SL::JFIN) : sink;
+                const unsigned js = jin ? lds0 + (unsigned)((((q % R) + R) % R) * SL::BYTES + SL::JFIN) : sink;
                 if (lane < LV * NJ / 2) dma16_sc1(kp, ks);
                 if (lane < LV * P / 2) dma16_sc1(jp2, js);
             };
@@ -795,7 +801,7 @@ __global__ __launch_bounds__(64 * l2::waves(P, NL, SW)) void k_line2(LineArgs a)
                 issue(s + DH);
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (DH - 1)) : "memory");
                 if (s > TS) break;
-                const int qk = s + 1, qj = s + 2;  // steps
+                const int qk = s + 1, qj = s + 1;  // steps
                 double *kslot = reinterpret_cast<double *>(ring + (qk % R) * SL::BYTES + SL::KFIN) + min(lane, LV * NJ - 1);
                 double *jslot = reinterpret_cast<double *>(ring + (qj % R) * SL::BYTES + SL::JFIN) + min(lane, LV * P - 1);
                 const int lk = LV * qk + kv, lj = LV * qj + jv;  // levels checked by this lane
