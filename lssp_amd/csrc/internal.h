@@ -174,6 +174,7 @@ struct TriSched {
     int *bp_pos = nullptr;   // row -> schedule position (the inverse of bp_perm)
     // packets v6 (k_tri_pk6: schedule-ordered shadow vectors between sweeps)
     int pk6_n = 0, pk6_ep = 4, pk6_rows = 256;
+    int pk6_ext = 2;  // HBM operand loads per loader lane per packet (2 or 3: the largest packet's nx / 256)
     int *pk6_blk = nullptr, *pk6_desc = nullptr, *pk6_idx = nullptr;
     uint32_t *pk6_rec = nullptr;
     mutable unsigned long long pk6_base = 0;
@@ -181,7 +182,8 @@ struct TriSched {
     std::vector<int> h_pos;  // L factor: row -> schedule position (for the U factor's build)
 };
 constexpr int PK3_ROWS = 256;    // v6: rows per packet = compute lanes = loader lanes
-constexpr int PK3_EXT = 2;       // v6: HBM x operands per packet row (on average)
+constexpr int PK3_EXT = 3;       // v6: HBM x operands per packet row, at most (on average; the kernel
+                                 // runs 2 or 3 loads per lane, TriSched::pk6_ext; 2 before round 6)
 constexpr int PK3_CAP = 4096;    // v6: packets per block (descriptors staged in LDS)
 
 // ---- line sweeps of structured ILU(0) factors (linesweep.hip) ----------------

@@ -214,7 +214,7 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
         std::vector<int> idx;
     };
     std::vector<BlkPk> bp(nb);
-    std::atomic<int> status{LSSP_AMD_OK};
+    std::atomic<int> status{LSSP_AMD_OK}, maxnx{0};
     parallel_for(nb, [&](long b0, long b1) {
         std::vector<int> stamp(n, -1), slot(n, 0), xl;
         int pid = 0;
@@ -255,6 +255,11 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
                         nr++;
                     }
                     const int nx = (int)xl.size();
+                    if (nx > maxnx.load(std::memory_order_relaxed)) {
+                        int m = maxnx.load();
+                        while (nx > m && !maxnx.compare_exchange_weak(m, nx)) {
+                        }
+                    }
                     const int par = (int)(desc.size() / 4) & 1;  // the packet's index in its block, mod 2
                     const long ro = (long)rec.size() / 4, io = (long)idx.size();  // block-relative
                     desc.push_back((int)ro);
@@ -307,6 +312,12 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
     SetupTimer tm;
     t.pk6_n = blk[nb];
     t.pk6_ep = EP;
+    // the loader lanes fetch ceil(max nx / 256) operands each: a third load per
+    // lane only where a packet needs more than 512 HBM operands (7-pt 256^3
+    // ILUT: the cap of 512 split the levels into 2,550 packets per block against
+    // 1,580 levels, 13.6 -> 10.8 ms per apply; at 128^3 no packet needs it and
+    // the third load would cost ~3 %, profiles/r06/r06o_*)
+    t.pk6_ext = maxnx.load() > ROWS * 2 ? 3 : 2;
     t.pk6_rows = ROWS;
     const size_t ndesc = std::max<size_t>(4L * blk[nb], 1), nrec = rec_off[nb] + 4, nidx = idx_off[nb] + 1;
     std::unique_ptr<int[]> desc(new int[ndesc]);

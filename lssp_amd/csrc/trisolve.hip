@@ -251,7 +251,7 @@ __device__ __forceinline__ T &sel4(T &a, T &b, T &c, T &d)
 // registers; the loader lanes fetch it KE steps ahead with the gathers and land
 // it in an LDS slot at the end of the step before, and the compute lanes read
 // it from there (D unused).
-template <int EP, int KE, int IA, int D, int NR, bool LREC = false, bool TRACE = false>
+template <int EP, int KE, int IA, int D, int NR, bool LREC = false, bool TRACE = false, int EXT = 2>
 __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
 {
     constexpr int Q = 4;
@@ -423,18 +423,22 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
             // vmcnt waits: its register sets rotate across the loop back-edge,
             // where the compiler's own wait counting turns conservative and
             // waited for the previous step's gathers before issuing new ones.
-            // Per step, in issue order: 3 index loads (packet j+IA), then 3
-            // gathers (packet j+KE) -- so before the gathers, the indices they
-            // use (issued at step j-2) have exactly 12 younger loads, and the
-            // gathers landed at the end of step j (packet j+1, issued at step
-            // j+1-KE) have 6 (KE 2) or 0 (KE 1) younger loads.
+            // Per step, in issue order: E = 1 + EXT index loads (packet
+            // j+IA: the rhs index and EXT operand indices), then E gathers
+            // (packet j+KE) -- so before the gathers, the indices they use
+            // (issued at step j-(IA-KE)) have E + (IA-KE-1)(RL+2E) + RL + E
+            // younger loads, and the gathers landed at the end of step j
+            // (packet j+1, issued at step j+1-KE) have (KE-1)(RL+2E).
             // LREC: RL record loads (packet j+KE) open every step, so per step
-            // the queue grows by RL + 3 + 3 in the order records, indices, gathers
-            static_assert(PK3_EXT == 2, "wait counts below assume 3 + 3 loads per step");
+            // the queue grows by RL + E + E in the order records, indices, gathers
+            static_assert(EXT == 2 || EXT == 3, "operand loads per lane");
+            static_assert(EXT <= PK3_EXT, "the landed-operand buffers hold PK3_EXT per row");
+            constexpr int E = 1 + EXT;
             constexpr int RL = LREC ? 4 : 0;
             static_assert(!LREC || PK6_REC16 == RL * NR, "record loads cover one LDS slot");
-            constexpr int WAIT_IDX = 3 + (IA - KE - 1) * (RL + 6) + RL + 3;  // younger than the indices the gathers use
-            constexpr int WAIT_G = (KE - 1) * (RL + 6);  // younger than packet j+1's gathers (and records)
+            constexpr int WAIT_IDX = E + (IA - KE - 1) * (RL + 2 * E) + RL + E;  // younger than the indices the gathers use
+            constexpr int WAIT_G = (KE - 1) * (RL + 2 * E);  // younger than packet j+1's gathers (and records)
+            static_assert(WAIT_IDX <= 63 && WAIT_G + RL + 2 * E <= 63, "vmcnt range");
             auto issue_rec = [&](const int4 d, PkLd &L) {
                 if constexpr (LREC) {
                     const int nr = d.z & 0x3ff, n1 = nr > 0 ? nr : 1;
@@ -452,22 +456,28 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
                 const int nr = d.z & 0x3ff, nx = (d.z >> 10) & 0x7ff;
                 const int *base = a.idx + d.y;
                 const int *p0 = base + max(min(t, nr - 1), 0);
-                const int *p1 = base + nr + max(min(t, nx - 1), 0);
-                const int *p2 = base + nr + max(min(t + NR, nx - 1), 0);
                 asm volatile("global_load_dword %0, %1, off" : "=v"(L.row) : "v"(p0) : "memory");
-                asm volatile("global_load_dword %0, %1, off" : "=v"(L.xi[0]) : "v"(p1) : "memory");
-                asm volatile("global_load_dword %0, %1, off" : "=v"(L.xi[1]) : "v"(p2) : "memory");
+#pragma unroll
+                for (int e = 0; e < EXT; e++) {
+                    const int *pe = base + nr + max(min(t + NR * e, nx - 1), 0);
+                    asm volatile("global_load_dword %0, %1, off" : "=v"(L.xi[e]) : "v"(pe) : "memory");
+                }
                 L.nr = nr;
                 L.nx = nx;
             };
             auto gather = [&](PkLd &L) {
-                asm volatile("s_waitcnt vmcnt(%3)" : "+v"(L.row), "+v"(L.xi[0]), "+v"(L.xi[1]) : "n"(WAIT_IDX) : "memory");
+                if constexpr (EXT == 3)
+                    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(L.row), "+v"(L.xi[0]), "+v"(L.xi[1]), "+v"(L.xi[EXT - 1])
+                                 : "n"(WAIT_IDX) : "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(%3)" : "+v"(L.row), "+v"(L.xi[0]), "+v"(L.xi[1]) : "n"(WAIT_IDX) : "memory");
                 const double *pr = a.rhs + L.row;
-                const double *px0 = a.sh + L.xi[0];
-                const double *px1 = a.sh + L.xi[1];
                 asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(L.rh) : "v"(pr) : "memory");
-                asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(L.ev[0]) : "v"(px0) : "memory");
-                asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(L.ev[1]) : "v"(px1) : "memory");
+#pragma unroll
+                for (int e = 0; e < EXT; e++) {
+                    const double *pxe = a.sh + L.xi[e];
+                    asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(L.ev[e]) : "v"(pxe) : "memory");
+                }
             };
             int4 dl = descc(J0 + IA);  // descriptor of packet j+IA, read one step ahead
             int4 dlr = dread(J0 + IA + 1);
@@ -483,12 +493,21 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
                 dlr = dread(j + IA + 2);
                 const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
                 // gathers of packet j+1 were issued at step j+1-KE
-                if constexpr (LREC)
+                if constexpr (LREC && EXT == 3)
+                    asm volatile("s_waitcnt vmcnt(%8)"
+                                 : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]), "+v"(Ll.ev[EXT - 1]), "+v"(Ll.rw[0]),
+                                   "+v"(Ll.rw[1]), "+v"(Ll.rw[2]), "+v"(Ll.rw[3])
+                                 : "n"(WAIT_G)
+                                 : "memory");
+                else if constexpr (LREC)
                     asm volatile("s_waitcnt vmcnt(%7)"
                                  : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]), "+v"(Ll.rw[0]), "+v"(Ll.rw[1]),
                                    "+v"(Ll.rw[2]), "+v"(Ll.rw[3])
                                  : "n"(WAIT_G)
                                  : "memory");
+                else if constexpr (EXT == 3)
+                    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]), "+v"(Ll.ev[EXT - 1])
+                                 : "n"(WAIT_G) : "memory");
                 else
                     asm volatile("s_waitcnt vmcnt(%3)" : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]) : "n"(WAIT_G) : "memory");
                 // land packet j+1 (nr = nx = 0 outside the block's packets)
@@ -499,7 +518,7 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
                         if (t + NR * u < Ll.rlen) recbuf[(j + 1) & 1][t + NR * u] = Ll.rw[u];
                 }
 #pragma unroll
-                for (int e = 0; e < PK3_EXT; e++) {
+                for (int e = 0; e < EXT; e++) {
                     const int k = t + NR * e;
                     if (k < Ll.nx) {
                         uint64_t bits = Ll.ev[e];
@@ -569,6 +588,13 @@ static void launch_pk6_k(lssp_amd_ctx *c, const TriSched &t, const Pk6Args &g, i
     // EP 4 / 8 with register records, EP 16 / 24 with LDS records -- the
     // variants whose inline-asm loader tools/check_vmcnt.py
     // (tests/test_isa_vmcnt.py) verifies hazard-free
+    if (t.pk6_ext == 3) {
+        if (t.pk6_ep == 4) k_tri_pk6<4, 2, 4, 3, 256, false, TRACE, 3><<<grid, 512, 0, c->stream>>>(g);
+        else if (t.pk6_ep == 8) k_tri_pk6<8, 2, 4, 3, 256, false, TRACE, 3><<<grid, 512, 0, c->stream>>>(g);
+        else if (t.pk6_ep == 16) k_tri_pk6<16, 3, 4, 1, 256, true, TRACE, 3><<<grid, 512, 0, c->stream>>>(g);
+        else k_tri_pk6<24, 3, 4, 1, 256, true, TRACE, 3><<<grid, 512, 0, c->stream>>>(g);
+        return;
+    }
     if (t.pk6_ep == 4) k_tri_pk6<4, 2, 4, 3, 256, false, TRACE><<<grid, 512, 0, c->stream>>>(g);
     else if (t.pk6_ep == 8) k_tri_pk6<8, 2, 4, 3, 256, false, TRACE><<<grid, 512, 0, c->stream>>>(g);
     else if (t.pk6_ep == 16) k_tri_pk6<16, 3, 4, 1, 256, true, TRACE><<<grid, 512, 0, c->stream>>>(g);
