@@ -174,7 +174,7 @@ struct TriSched {
     int *bp_pos = nullptr;   // row -> schedule position (the inverse of bp_perm)
     // packets v6 (k_tri_pk6: schedule-ordered shadow vectors between sweeps)
     int pk6_n = 0, pk6_ep = 4, pk6_rows = 256;
-    int pk6_ext = 2;  // HBM operand loads per loader lane per packet (2 or 3: the largest packet's nx / 256)
+    int pk6_ext = 2;  // HBM operand loads per loader lane per packet (2, 3 or 4; build_packets6)
     int *pk6_blk = nullptr, *pk6_desc = nullptr, *pk6_idx = nullptr;
     uint32_t *pk6_rec = nullptr;
     mutable unsigned long long pk6_base = 0;
@@ -182,8 +182,8 @@ struct TriSched {
     std::vector<int> h_pos;  // L factor: row -> schedule position (for the U factor's build)
 };
 constexpr int PK3_ROWS = 256;    // v6: rows per packet = compute lanes = loader lanes
-constexpr int PK3_EXT = 3;       // v6: HBM x operands per packet row, at most (on average; the kernel
-                                 // runs 2 or 3 loads per lane, TriSched::pk6_ext; 2 before round 6)
+constexpr int PK3_EXT = 4;       // v6: HBM x operands per packet row, at most (on average; the kernel
+                                 // runs 2, 3 or 4 loads per lane, TriSched::pk6_ext; 2 before round 6)
 constexpr int PK3_CAP = 4096;    // v6: packets per block (descriptors staged in LDS)
 
 // ---- line sweeps of structured ILU(0) factors (linesweep.hip) ----------------
@@ -467,5 +467,58 @@ int halo_exchange(const lssp_amd_mat *A, double *x);
 int spmv_halo(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, double *x, double beta,
               const double *y, double *z, int nred, const double *w0, const double *w1);
 int comm_destroy(lssp_amd_ctx *c);
+
+// The canonical level-1 halving tree of one wave: lane 0 gets
+// (((v0 + v32) + (v16 + v48)) + ...), the pairs of an xor butterfly over 32,
+// 16, 8, 4, 2, 1 -- evaluated for lane 0 only: the 32- and 16-lane steps by
+// v_permlane32_swap / v_permlane16_swap, the 8, 4, 2, 1 steps by DPP row
+// shifts (row_shl:k), instead of six dependent ds_bpermute round trips per
+// half.  Lane 0 adds the same operands in the same pairs, so its value is
+// bitwise the butterfly's; the other lanes hold partial sums (every caller
+// reads lane 0).  -DWAVE_SUM_BPERM restores the butterfly (A/B).
+__device__ __forceinline__ double wave_sum_l0(double v)
+{
+#ifdef WAVE_SUM_BPERM
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
+    return v;
+#else
+    auto split = [](double x, unsigned &lo, unsigned &hi) {
+        const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+        lo = (unsigned)b;
+        hi = (unsigned)(b >> 32);
+    };
+    auto join = [](unsigned lo, unsigned hi) {
+        return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+    };
+    unsigned lo, hi;
+    split(v, lo, hi);
+    {  // lanes 0..31 <- lanes 32..63
+        const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        v = v + join(a[1], b[1]);
+    }
+    split(v, lo, hi);
+    {  // lanes 0..15 <- lanes 16..31
+        const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        v = v + join(a[1], b[1]);
+    }
+    // lanes l <- l + k inside each 16-lane row (row_shl:k = 0x100 + k)
+    split(v, lo, hi);
+    v = v + join((unsigned)__builtin_amdgcn_update_dpp((int)lo, (int)lo, 0x108, 0xf, 0xf, false),
+                 (unsigned)__builtin_amdgcn_update_dpp((int)hi, (int)hi, 0x108, 0xf, 0xf, false));
+    split(v, lo, hi);
+    v = v + join((unsigned)__builtin_amdgcn_update_dpp((int)lo, (int)lo, 0x104, 0xf, 0xf, false),
+                 (unsigned)__builtin_amdgcn_update_dpp((int)hi, (int)hi, 0x104, 0xf, 0xf, false));
+    split(v, lo, hi);
+    v = v + join((unsigned)__builtin_amdgcn_update_dpp((int)lo, (int)lo, 0x102, 0xf, 0xf, false),
+                 (unsigned)__builtin_amdgcn_update_dpp((int)hi, (int)hi, 0x102, 0xf, 0xf, false));
+    split(v, lo, hi);
+    v = v + join((unsigned)__builtin_amdgcn_update_dpp((int)lo, (int)lo, 0x101, 0xf, 0xf, false),
+                 (unsigned)__builtin_amdgcn_update_dpp((int)hi, (int)hi, 0x101, 0xf, 0xf, false));
+    return v;
+#endif
+}
 
 }  // namespace lssp_amd

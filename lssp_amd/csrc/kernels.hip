@@ -33,9 +33,7 @@ namespace lssp_amd {
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double wave_sum(double v)
 {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
-    return v;  // lane 0 holds the halving-tree result
+    return wave_sum_l0(v);  // lane 0 holds the halving-tree result (internal.h)
 }
 
 // level-1 combine of one 256-element chunk held one element per thread of a

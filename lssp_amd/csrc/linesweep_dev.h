@@ -95,12 +95,7 @@ __device__ __forceinline__ double dpp_shr1g(double v, double old)
 
 // the canonical level-1 halving tree of one wave (kernels.hip wave_sum): lane 0
 // holds the result
-__device__ __forceinline__ double wave_sum_d(double v)
-{
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
-    return v;
-}
+__device__ __forceinline__ double wave_sum_d(double v) { return wave_sum_l0(v); }
 
 template <int I, int N, class F>
 __device__ __forceinline__ void static_for(F &&f)

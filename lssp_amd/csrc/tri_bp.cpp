@@ -213,8 +213,57 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
         std::vector<uint32_t> rec;
         std::vector<int> idx;
     };
+    // The HBM operands a packet may gather (xcap = EXT x 256: the loader lanes
+    // fetch EXT each).  A packet is closed early when its rows' new operands
+    // would pass the cap, so a small cap splits levels into several packets,
+    // and every packet is a step of its block (7-pt 256^3 ILUT: 512 split 1,580
+    // levels into 2,546 packets per block, profiles/r06/r06k_*; the U factor
+    // needs 1,024).  Each extra load per lane costs the step ~3 %, so the
+    // packets are first counted for EXT = 2, 3, 4 and the smallest EXT whose
+    // count is within 1 % of EXT = 4's is kept.
+    auto packets_at = [&](int cap) {
+        std::atomic<long> total{0};
+        parallel_for(nb, [&](long b0, long b1) {
+            std::vector<int> stamp(n, -1);
+            int pid = 0;
+            long cnt = 0;
+            for (long b = b0; b < b1; b++)
+                for (int s = blk_step[b]; s < blk_step[b + 1]; s++) {
+                    int p = step_pos[s];
+                    while (p < step_pos[s + 1]) {
+                        int nr = 0, nx = 0;
+                        while (p + nr < step_pos[s + 1] && nr < ROWS) {
+                            const int r = p + nr;
+                            if (EP >= 16 && rec_words(nr + 1) > 4 * PK6_REC_WORDS16) break;
+                            int newx = 0;
+                            for (int k = rp[r]; k < rp[r + 1]; k++)
+                                if (cols[k] >= 0 && stamp[cols[k]] != pid) newx++;
+                            if (nx + newx > cap) break;
+                            for (int k = rp[r]; k < rp[r + 1]; k++)
+                                if (cols[k] >= 0 && stamp[cols[k]] != pid) stamp[cols[k]] = pid, nx++;
+                            nr++;
+                        }
+                        p += nr;
+                        pid++;
+                        cnt++;
+                    }
+                }
+            total += cnt;
+        }, 1);
+        return total.load();
+    };
+    int ext = PK3_EXT;
+    {
+        const long c4 = packets_at(ROWS * PK3_EXT);
+        for (int e = 2; e < PK3_EXT; e++)
+            if (packets_at(ROWS * e) <= c4 + c4 / 100) {
+                ext = e;
+                break;
+            }
+    }
+    const int xcap = ROWS * ext;
     std::vector<BlkPk> bp(nb);
-    std::atomic<int> status{LSSP_AMD_OK}, maxnx{0};
+    std::atomic<int> status{LSSP_AMD_OK};
     parallel_for(nb, [&](long b0, long b1) {
         std::vector<int> stamp(n, -1), slot(n, 0), xl;
         int pid = 0;
@@ -242,7 +291,7 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
                         int newx = 0;
                         for (int k = rp[r]; k < rp[r + 1]; k++)
                             if (cols[k] >= 0 && stamp[cols[k]] != pid) newx++;
-                        if ((long)xl.size() + newx > (long)ROWS * PK3_EXT) break;
+                        if ((long)xl.size() + newx > (long)xcap) break;
                         for (int k = rp[r]; k < rp[r + 1]; k++) {
                             const int g = cols[k];
                             if (g >= 0 && stamp[g] != pid) {
@@ -255,11 +304,6 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
                         nr++;
                     }
                     const int nx = (int)xl.size();
-                    if (nx > maxnx.load(std::memory_order_relaxed)) {
-                        int m = maxnx.load();
-                        while (nx > m && !maxnx.compare_exchange_weak(m, nx)) {
-                        }
-                    }
                     const int par = (int)(desc.size() / 4) & 1;  // the packet's index in its block, mod 2
                     const long ro = (long)rec.size() / 4, io = (long)idx.size();  // block-relative
                     desc.push_back((int)ro);
@@ -312,12 +356,7 @@ int build_packets6(int n, const std::vector<int> &perm, const std::vector<int> &
     SetupTimer tm;
     t.pk6_n = blk[nb];
     t.pk6_ep = EP;
-    // the loader lanes fetch ceil(max nx / 256) operands each: a third load per
-    // lane only where a packet needs more than 512 HBM operands (7-pt 256^3
-    // ILUT: the cap of 512 split the levels into 2,550 packets per block against
-    // 1,580 levels, 13.6 -> 10.8 ms per apply; at 128^3 no packet needs it and
-    // the third load would cost ~3 %, profiles/r06/r06o_*)
-    t.pk6_ext = maxnx.load() > ROWS * 2 ? 3 : 2;
+    t.pk6_ext = ext;
     t.pk6_rows = ROWS;
     const size_t ndesc = std::max<size_t>(4L * blk[nb], 1), nrec = rec_off[nb] + 4, nidx = idx_off[nb] + 1;
     std::unique_ptr<int[]> desc(new int[ndesc]);

@@ -431,7 +431,7 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
             // (packet j+1, issued at step j+1-KE) have (KE-1)(RL+2E).
             // LREC: RL record loads (packet j+KE) open every step, so per step
             // the queue grows by RL + E + E in the order records, indices, gathers
-            static_assert(EXT == 2 || EXT == 3, "operand loads per lane");
+            static_assert(EXT >= 2 && EXT <= 4, "operand loads per lane");
             static_assert(EXT <= PK3_EXT, "the landed-operand buffers hold PK3_EXT per row");
             constexpr int E = 1 + EXT;
             constexpr int RL = LREC ? 4 : 0;
@@ -466,7 +466,11 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
                 L.nx = nx;
             };
             auto gather = [&](PkLd &L) {
-                if constexpr (EXT == 3)
+                if constexpr (EXT == 4)
+                    asm volatile("s_waitcnt vmcnt(%5)"
+                                 : "+v"(L.row), "+v"(L.xi[0]), "+v"(L.xi[1]), "+v"(L.xi[EXT - 2]), "+v"(L.xi[EXT - 1])
+                                 : "n"(WAIT_IDX) : "memory");
+                else if constexpr (EXT == 3)
                     asm volatile("s_waitcnt vmcnt(%4)" : "+v"(L.row), "+v"(L.xi[0]), "+v"(L.xi[1]), "+v"(L.xi[EXT - 1])
                                  : "n"(WAIT_IDX) : "memory");
                 else
@@ -493,7 +497,13 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
                 dlr = dread(j + IA + 2);
                 const unsigned long long w0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
                 // gathers of packet j+1 were issued at step j+1-KE
-                if constexpr (LREC && EXT == 3)
+                if constexpr (LREC && EXT == 4)
+                    asm volatile("s_waitcnt vmcnt(%9)"
+                                 : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]), "+v"(Ll.ev[EXT - 2]), "+v"(Ll.ev[EXT - 1]),
+                                   "+v"(Ll.rw[0]), "+v"(Ll.rw[1]), "+v"(Ll.rw[2]), "+v"(Ll.rw[3])
+                                 : "n"(WAIT_G)
+                                 : "memory");
+                else if constexpr (LREC && EXT == 3)
                     asm volatile("s_waitcnt vmcnt(%8)"
                                  : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]), "+v"(Ll.ev[EXT - 1]), "+v"(Ll.rw[0]),
                                    "+v"(Ll.rw[1]), "+v"(Ll.rw[2]), "+v"(Ll.rw[3])
@@ -505,6 +515,10 @@ __global__ __launch_bounds__(2 * NR) void k_tri_pk6(Pk6Args a)
                                    "+v"(Ll.rw[2]), "+v"(Ll.rw[3])
                                  : "n"(WAIT_G)
                                  : "memory");
+                else if constexpr (EXT == 4)
+                    asm volatile("s_waitcnt vmcnt(%5)"
+                                 : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]), "+v"(Ll.ev[EXT - 2]), "+v"(Ll.ev[EXT - 1])
+                                 : "n"(WAIT_G) : "memory");
                 else if constexpr (EXT == 3)
                     asm volatile("s_waitcnt vmcnt(%4)" : "+v"(Ll.rh), "+v"(Ll.ev[0]), "+v"(Ll.ev[1]), "+v"(Ll.ev[EXT - 1])
                                  : "n"(WAIT_G) : "memory");
@@ -588,6 +602,13 @@ static void launch_pk6_k(lssp_amd_ctx *c, const TriSched &t, const Pk6Args &g, i
     // EP 4 / 8 with register records, EP 16 / 24 with LDS records -- the
     // variants whose inline-asm loader tools/check_vmcnt.py
     // (tests/test_isa_vmcnt.py) verifies hazard-free
+    if (t.pk6_ext == 4) {
+        if (t.pk6_ep == 4) k_tri_pk6<4, 2, 4, 3, 256, false, TRACE, 4><<<grid, 512, 0, c->stream>>>(g);
+        else if (t.pk6_ep == 8) k_tri_pk6<8, 2, 4, 3, 256, false, TRACE, 4><<<grid, 512, 0, c->stream>>>(g);
+        else if (t.pk6_ep == 16) k_tri_pk6<16, 3, 4, 1, 256, true, TRACE, 4><<<grid, 512, 0, c->stream>>>(g);
+        else k_tri_pk6<24, 3, 4, 1, 256, true, TRACE, 4><<<grid, 512, 0, c->stream>>>(g);
+        return;
+    }
     if (t.pk6_ext == 3) {
         if (t.pk6_ep == 4) k_tri_pk6<4, 2, 4, 3, 256, false, TRACE, 3><<<grid, 512, 0, c->stream>>>(g);
         else if (t.pk6_ep == 8) k_tri_pk6<8, 2, 4, 3, 256, false, TRACE, 3><<<grid, 512, 0, c->stream>>>(g);
