@@ -30,7 +30,7 @@ enum Scal {
     S_DONE, S_TOL, S_NIT,  // batched iterations (solvers.cpp cg): stop flag, tolerance, iterations run
     S_SUM0 = 16,   // raw reduced sums of the last reduction
     S_H = 32,      // GMRES Hessenberg column (up to NSCAL - 32 entries); batched residual history ring
-    S_HB = 32,     // ... of S_HB entries: iteration k's residual at S_H + k % S_HB (two batches in flight)
+    S_HB = 64,     // ... of S_HB entries: iteration k's residual at S_H + k % S_HB (two batches in flight)
 };
 
 // finalize programs run by one lane after a reduction (same code for every

@@ -526,7 +526,10 @@ int cg(Run &R, const lssp_amd_solve_params &P, double *x, const double *b, int *
         // iterations after the one that converged return at once (ctx guard),
         // and the host reads a batch's residuals from its snapshot while the
         // next batch runs (Run::snap_issue).  Same kernels, same arithmetic.
-        constexpr int BATCH = 16;
+#ifndef CG_BATCH
+#define CG_BATCH 32  // config 5: 32 against 16 / 8 per batch 21.54-21.84 K / 21.34-21.44 K / 20.98-21.09 K it/s (r06u)
+#endif
+        constexpr int BATCH = CG_BATCH;  // iterations per batch (A/B: -DCG_BATCH)
         static_assert(2 * BATCH <= S_HB, "two batches in the residual history ring");
         lssp_amd_ctx *c = R.c;
         const bool fuse_l2 = R.tree && c->nranks == 1 && R.n > 0;
