@@ -386,7 +386,9 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
     __shared__ __attribute__((aligned(16))) int sj[CMP ? SPMV_CAP / 4 + 8 : SPMV_CAP + 4];
     __shared__ int soff[CMP ? 256 : 1];
     __shared__ double lds[MAX_SLOTS][4];
-    if (a.guard && *a.guard != 0.0) return;
+    // the guard is read with the row bounds and tested before the entries are
+    // loaded: its round trip overlaps theirs instead of preceding it
+    const double gv = a.guard ? *a.guard : 0.0;
     const long per = gridDim.x / a.streams;
     long lb = (blockIdx.x % a.streams) * per + blockIdx.x / a.streams;
     if (lb >= nblk) return;
@@ -416,6 +418,7 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
             if (NRED > 1 && a.w1 && a.w1 != a.z) w1p = a.w1[rr];
         }
     }
+    if (gv != 0.0) return;  // a batched iteration past the stop (lssp_amd_ctx::guard)
     double sum = 0;
     if (cnt <= SPMV_CAP) {
         typedef double dbl2_t __attribute__((ext_vector_type(2)));
@@ -517,13 +520,20 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_sell(SpmvArgs a, const int *w
     __shared__ __attribute__((aligned(16))) double sxw[WIN_CAP];
     __shared__ double zb[WIN_ROWS];
     __shared__ double lds[4][MAX_SLOTS][4];
-    if (a.guard && *a.guard != 0.0) return;
+    // the guard is read with the block's metadata (window, slice base, row
+    // map) and tested before the x span and the entries are loaded
+    const double gv = a.guard ? *a.guard : 0.0;
     const long per = gridDim.x / 8;
     const long blk = (blockIdx.x % 8) * per + blockIdx.x / 8;
     if (blk >= nblk) return;
     const int tid = threadIdx.x;
     const int r = (int)(blk * WIN_ROWS) + tid;
     const int lo = win[2 * blk], span = win[2 * blk + 1] - lo;
+    const int lane = tid & 63;
+    const long sl = blk * (WIN_ROWS / 64) + (tid >> 6);
+    const int sbase = __builtin_amdgcn_readfirstlane(smeta[2 * sl]);
+    const uint32_t ri = srow[blk * WIN_ROWS + tid];
+    if (gv != 0.0) return;  // a batched iteration past the stop (lssp_amd_ctx::guard)
     // x span: staged from lo2 = lo rounded down to even, as 16-byte vectors when
     // x is 16-byte aligned (uniform); the last odd entry alone (nothing past hi is read)
     constexpr int NS = WIN_CAP / WIN_ROWS;
@@ -542,10 +552,6 @@ __global__ __launch_bounds__(WIN_ROWS) void k_spmv_sell(SpmvArgs a, const int *w
     }
     // this wave's slice; its first NK entries per lane, unconditionally (the
     // arrays are padded past the last slice)
-    const int lane = tid & 63;
-    const long sl = blk * (WIN_ROWS / 64) + (tid >> 6);
-    const int sbase = __builtin_amdgcn_readfirstlane(smeta[2 * sl]);
-    const uint32_t ri = srow[blk * WIN_ROWS + tid];
     const int len = (int)(ri >> 10), lr = (int)(ri & 1023);
     constexpr int NK = 10;
     double ax[NK];
@@ -1111,26 +1117,54 @@ struct CgFusedArgs {
     const double *guard;
 };
 
+// lane l's double, uniform (two v_readlane)
+__device__ __forceinline__ double lane_bcast(double v, int l)
+{
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Every global read a workgroup makes before its first store is issued up
+// front, ahead of the guard test: the guard, the scalars, the level-2
+// partials and the first element's operands (the element loop then loads one
+// element ahead).  A pass starts streaming after one memory round trip instead
+// of three dependent ones (guard -> partials -> scalars -> operands).
+template <int KIND>
 __global__ __launch_bounds__(1024) void k_cg_fused(CgFusedArgs a)
 {
     __shared__ double wl[16];
     __shared__ double red[2][4][4];
     __shared__ double sc[2];
-    if (a.guard) {  // a batched iteration past the stop; the stop's own pass keeps its x update
-        const double g = *a.guard;
-        if (g != 0.0 && g != (double)a.stamp) return;
-    }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (a.kind == CGF_X) {  // the batch's deferred x update alone
-        const double al = a.scal[S_ALPHA];
-        for (long i = blockIdx.x * 1024L + tid; i < a.n; i += gridDim.x * 1024L) a.x[i] = a.x[i] + al * a.p[i];
-        return;
-    }
-    {
+    constexpr int kind = KIND;
+    const long stride = gridDim.x * 1024L, n = a.n;
+    // operands of element i: PX p x z, P p z, R q r, XR q r x p, X x p
+    auto load = [&](long i, double (&v)[4]) {
+        if (i >= n) return;
+        if constexpr (kind == CGF_R || kind == CGF_XR) {
+            v[0] = a.q[i];
+            v[1] = a.r[i];
+            if (kind == CGF_XR) v[2] = a.x[i], v[3] = a.p[i];
+        } else {
+            v[0] = a.p[i];
+            if (kind != CGF_P) v[1] = a.x[i];
+            if (kind != CGF_X) v[2] = a.z[i];
+        }
+    };
+    // the scalars and the guard by ONE vector load (lane l reads its own
+    // address): scalar loads would share the kernel arguments' lgkmcnt waits
+    // and delay the operand loads behind their round trip
+    const double *sp = a.scal + (lane == 0 ? S_ALPHA : lane == 1 ? S_RHO1 : lane == 2 ? S_RHO0 : S_TOL);
+    if (lane == 4 && a.guard) sp = a.guard;
+    const double sv = *sp;
+    double cur[4] = {0.0, 0.0, 0.0, 0.0};
+    long i = blockIdx.x * 1024L + tid;
+    load(i, cur);
+    double acc = 0.0;
+    if (kind != CGF_X) {
         // lane t adds partials t, t+1024, ... in order; the loads of 8 of them
-        // are issued before the adds (k_reduce2m's form), so the prologue waits
-        // for one L2 round trip instead of one per partial
-        double acc = 0.0;
+        // are issued before the adds (k_reduce2m's form)
         for (long k0 = tid; k0 < a.C; k0 += 8L * L2_LANES) {
             double v[8];
 #pragma unroll
@@ -1142,6 +1176,22 @@ __global__ __launch_bounds__(1024) void k_cg_fused(CgFusedArgs a)
             for (int u = 0; u < 8; u++)
                 if (k0 + (long)u * L2_LANES < a.C) acc += v[u];
         }
+    }
+    const double al = lane_bcast(sv, 0), rho1 = lane_bcast(sv, 1), rho0 = lane_bcast(sv, 2),
+                 tolv = lane_bcast(sv, 3), gv = a.guard ? lane_bcast(sv, 4) : 0.0;
+    // a batched iteration past the stop; the stop's own pass keeps its x update
+    if (gv != 0.0 && gv != (double)a.stamp) return;
+    if (kind == CGF_X) {  // the batch's deferred x update alone
+        for (; i < n; i += stride) {
+            double nx[4];
+            load(i + stride, nx);
+            a.x[i] = cur[1] + al * cur[0];
+#pragma unroll
+            for (int u = 0; u < 4; u++) cur[u] = nx[u];
+        }
+        return;
+    }
+    {
         acc = wave_sum(acc);
         if (lane == 0) wl[wave] = acc;
         __syncthreads();
@@ -1156,11 +1206,11 @@ __global__ __launch_bounds__(1024) void k_cg_fused(CgFusedArgs a)
             const double s = u[0];
             double v;
             bool stop = false;
-            if (a.kind == CGF_XR || a.kind == CGF_R) {
-                v = a.scal[S_RHO1] / s;  // finalize FIN_CG_ALPHA's alpha (S_RHO1 is not written below)
+            if (kind == CGF_XR || kind == CGF_R) {
+                v = rho1 / s;  // finalize FIN_CG_ALPHA's alpha (S_RHO1 is not written below)
             } else {
-                v = s / a.scal[S_RHO0];  // FIN_CG_RES_RHO's beta (S_RHO0 is not written below)
-                stop = a.f.op == FIN_CG_RES_RHO_B && sqrt(s) <= a.scal[S_TOL];
+                v = s / rho0;  // FIN_CG_RES_RHO's beta (S_RHO0 is not written below)
+                stop = a.f.op == FIN_CG_RES_RHO_B && sqrt(s) <= tolv;
             }
             if (blockIdx.x == 0) {
                 a.sums[0] = s;
@@ -1172,28 +1222,32 @@ __global__ __launch_bounds__(1024) void k_cg_fused(CgFusedArgs a)
         __syncthreads();
     }
     const bool stop = sc[1] != 0.0;
-    if (a.kind == CGF_PX) {  // x += alpha p of the previous x/r pass (CGF_R), then p = r + beta p
-        const double al = a.scal[S_ALPHA], v = sc[0];  // workgroup 0's finalize does not write S_ALPHA
-        for (long i = blockIdx.x * 1024L + tid; i < a.n; i += gridDim.x * 1024L) {
-            const double pv = a.p[i];
-            a.x[i] = a.x[i] + al * pv;
-            if (!stop) a.p[i] = a.z[i] + v * pv;
+    const double v = sc[0];
+    if (kind == CGF_PX) {  // x += alpha p of the previous x/r pass (CGF_R), then p = r + beta p
+        // (workgroup 0's finalize does not write S_ALPHA)
+        for (; i < n; i += stride) {
+            double nx[4];
+            load(i + stride, nx);
+            const double pv = cur[0];
+            a.x[i] = cur[1] + al * pv;
+            if (!stop) a.p[i] = cur[2] + v * pv;
+#pragma unroll
+            for (int u = 0; u < 4; u++) cur[u] = nx[u];
         }
         return;
     }
     if (stop) return;
-    const double v = sc[0];
     int par = 0;
-    for (long g = blockIdx.x; g * 1024 < a.n; g += gridDim.x, par ^= 1) {
-        const long i = g * 1024 + tid;
-        if (a.kind == CGF_P) {
-            if (i < a.n) a.p[i] = a.z[i] + v * a.p[i];
+    for (long g = blockIdx.x; g * 1024 < n; g += gridDim.x, par ^= 1, i += stride) {
+        double nx[4];
+        load(i + stride, nx);
+        if (kind == CGF_P) {
+            if (i < n) a.p[i] = cur[2] + v * cur[0];
         } else {
             double rr = 0.0;
-            if (i < a.n) {
-                const double qv = a.q[i];
-                if (a.kind == CGF_XR) a.x[i] = a.x[i] + v * a.p[i];
-                const double rn = a.r[i] - v * qv;
+            if (i < n) {
+                if (kind == CGF_XR) a.x[i] = cur[2] + v * cur[3];
+                const double rn = cur[1] - v * cur[0];
                 a.r[i] = rn;
                 rr = rn * rn;
             }
@@ -1202,11 +1256,13 @@ __global__ __launch_bounds__(1024) void k_cg_fused(CgFusedArgs a)
             if (lane == 0) red[par][wave >> 2][wave & 3] = w;
             __syncthreads();
             const long chunk = g * 4 + (tid >> 8);
-            if ((tid & 255) == 0 && chunk * 256 < a.n) {
+            if ((tid & 255) == 0 && chunk * 256 < n) {
                 const int cq = tid >> 8;
                 a.pout[chunk] = (red[par][cq][0] + red[par][cq][1]) + (red[par][cq][2] + red[par][cq][3]);
             }
         }
+#pragma unroll
+        for (int u = 0; u < 4; u++) cur[u] = nx[u];
     }
 }
 
@@ -1222,7 +1278,13 @@ int launch_cg_fused(lssp_amd_ctx *c, int kind, long n, double *x, double *p, dou
 #define CGF_PER_CU 2  // tuning builds override it
 #endif
     const long grid = std::min<long>((n + 1023) / 1024, (long)CGF_PER_CU * c->num_cus);  // 2 per CU
-    k_cg_fused<<<grid, 1024, 0, c->stream>>>(g);
+    switch (kind) {
+    case CGF_P: k_cg_fused<CGF_P><<<grid, 1024, 0, c->stream>>>(g); break;
+    case CGF_XR: k_cg_fused<CGF_XR><<<grid, 1024, 0, c->stream>>>(g); break;
+    case CGF_R: k_cg_fused<CGF_R><<<grid, 1024, 0, c->stream>>>(g); break;
+    case CGF_PX: k_cg_fused<CGF_PX><<<grid, 1024, 0, c->stream>>>(g); break;
+    default: k_cg_fused<CGF_X><<<grid, 1024, 0, c->stream>>>(g); break;
+    }
     LSSP_HIP(hipGetLastError());
     return LSSP_AMD_OK;
 }

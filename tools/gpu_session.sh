@@ -15,6 +15,7 @@
 #   quick=PATH       the same with a 120 s per-test limit and -x (new kernels)
 #   project512       tools/project_ranks.py --grid 512 --ranks 1,8 -> project_ranks_512.jsonl
 #   project216       tools/project_ranks.py --grid 216 --ranks 1,2,4,8 -> project_ranks_216.jsonl
+#   prof5            rocprofv3 --kernel-trace of config 5 (CG) + tools/kgaps.py
 #   config2 / config3 / config5 / general   tools/bench_configs.py bicgstab-iluk --grid 256 /
 #                    gmres-ilut / cg-thermal / general-ilu
 #   linediag=N[:LIB] tools/line_diag.py N 0 (optionally with LSSP_AMD_LIB=build/LIB.so)
@@ -74,6 +75,10 @@ for step in "$@"; do
   config2)
     timeout -k 10 600 python -u tools/bench_configs.py bicgstab-iluk --grid 256 > $O/config2.json 2> $O/config2.err || { tail -20 $O/config2.err; fail $step $?; }
     tail -c 900 $O/config2.json
+    ;;
+  prof5)
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_config5 -o cg -- python3 tools/bench_configs.py cg-thermal --ref-iters 0 > $O/prof_config5.log 2>&1 || { tail -20 $O/prof_config5.log; fail $step $?; }
+    python3 tools/kgaps.py $(find $O/prof_config5 -name "*kernel_trace.csv") --last 3000 | head -20
     ;;
   config5)
     timeout -k 10 300 python -u tools/bench_configs.py cg-thermal > $O/config5.json 2> $O/config5.err || { tail -20 $O/config5.err; fail $step $?; }
