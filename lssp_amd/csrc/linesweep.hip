@@ -1082,16 +1082,12 @@ static int launch_line_gather(lssp_amd_ctx *c, const LineSweep &ls, int mirror, 
 // Fusing BiCGSTAB's p / s passes with the gather saves the gather's read of
 // the vector just written and its launch: 216^3, 2 x 33.7 us of k_line_rhs per
 // iteration become two passes ~10 us longer than k_ew's (the values leave in
-// 64-byte runs of a line, the stream in 128-byte steps).  LSSP_AMD_GATHER_EW=0
-// keeps the separate passes (A/B runs).
+// 64-byte runs of a line, the stream in 128-byte steps).  The separate passes
+// remain for the factors this does not cover.
 bool line_gather_ew_ok(const LineILU &li, long n)
 {
-    static const int on = [] {
-        const char *e = getenv("LSSP_AMD_GATHER_EW");
-        return e ? atoi(e) : 1;
-    }();
     const char *te = getenv("LSSP_AMD_TAIL");  // the tail product gathers itself (and its EINVAL mode)
-    return on && !(te && atoi(te)) && li.ntiles > 0 && li.kind == 0 && !li.g2 && li.LV == 2 && li.L.P == 8 &&
+    return !(te && atoi(te)) && li.ntiles > 0 && li.kind == 0 && !li.g2 && li.LV == 2 && li.L.P == 8 &&
            li.L.NJ == 16 && li.d_lstream && (long)li.L.nx * li.L.ny * li.L.nz == n;
 }
 
