@@ -510,122 +510,173 @@ __global__ __launch_bounds__(256) void k_spmv3(SpmvArgs a, long nblk, long nnz_p
 // order onto 0.0 -- the arithmetic of k_spmv3 -- and writes the sum to LDS at
 // the row's place in the block; after a barrier thread t takes row t, so the
 // output store and the fused dots' 256-row chunk partials are those of the
-// natural order.  Every global load is issued before the first barrier.
+// natural order.
+// The product runs persistently (round 6; one workgroup per block before,
+// 1.7 % slower on config 5's product, profiles/r06/r06z8_*): one 1024-thread
+// workgroup per CU (the LDS ring allows one) walks a contiguous range of
+// blocks.  x is staged in an LDS ring of WIN_CAP entries indexed by column
+// mod WIN_CAP, and a block loads only the part of its span [lo2, hi) that is
+// not already resident from the previous block (consecutive spans of a locally
+// shuffled numbering mostly coincide: config 5 loads ~1 K of a block's ~12 K
+// span entries).  Two spans of at most WIN_CAP entries that overlap never map
+// a needed column onto another needed column, so after the load [lo2, hi) is
+// resident whatever was there before.  The next block's entries, row map, dot
+// operands and the first XPF x entries of its missing span are loaded into
+// registers while the current block is computed; its window and slice bases
+// one block earlier still.
 template <int EPI, int NRED>
-__global__ __launch_bounds__(WIN_ROWS) void k_spmv_sell(SpmvArgs a, const int *win, const double *__restrict__ sax,
-                                                        const uint32_t *__restrict__ scol,
-                                                        const uint32_t *__restrict__ srow,
-                                                        const int *__restrict__ smeta, long nblk)
+__global__ __launch_bounds__(WIN_ROWS) void k_spmv_sell(SpmvArgs a, const int *__restrict__ win,
+                                                         const double *__restrict__ sax,
+                                                         const uint32_t *__restrict__ scol,
+                                                         const uint32_t *__restrict__ srow,
+                                                         const int *__restrict__ smeta, long nblk)
 {
-    __shared__ __attribute__((aligned(16))) double sxw[WIN_CAP];
+    __shared__ double sxw[WIN_CAP];
     __shared__ double zb[WIN_ROWS];
     __shared__ double lds[4][MAX_SLOTS][4];
-    // the guard is read with the block's metadata (window, slice base, row
-    // map) and tested before the x span and the entries are loaded
-    const double gv = a.guard ? *a.guard : 0.0;
-    const long per = gridDim.x / 8;
-    const long blk = (blockIdx.x % 8) * per + blockIdx.x / 8;
-    if (blk >= nblk) return;
-    const int tid = threadIdx.x;
-    const int r = (int)(blk * WIN_ROWS) + tid;
-    const int lo = win[2 * blk], span = win[2 * blk + 1] - lo;
-    const int lane = tid & 63;
-    const long sl = blk * (WIN_ROWS / 64) + (tid >> 6);
-    const int sbase = __builtin_amdgcn_readfirstlane(smeta[2 * sl]);
-    const uint32_t ri = srow[blk * WIN_ROWS + tid];
-    if (gv != 0.0) return;  // a batched iteration past the stop (lssp_amd_ctx::guard)
-    // x span: staged from lo2 = lo rounded down to even, as 16-byte vectors when
-    // x is 16-byte aligned (uniform); the last odd entry alone (nothing past hi is read)
-    constexpr int NS = WIN_CAP / WIN_ROWS;
-    typedef double dbl2w_t __attribute__((ext_vector_type(2)));
-    const int hi = lo + span, lo2 = lo & ~1;
-    const bool xv16 = (reinterpret_cast<uintptr_t>(a.x) & 15) == 0;
-    dbl2w_t xs[NS / 2];
+    constexpr int NK = 10, XPF = 2, MASK = WIN_CAP - 1;
+    static_assert((WIN_CAP & MASK) == 0, "ring of a power of two");
+    if (a.guard && *a.guard != 0.0) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long b0 = blockIdx.x * nblk / gridDim.x, b1 = (blockIdx.x + 1) * nblk / gridDim.x;
+    if (b0 >= b1) return;
+    const double *x = a.x;
+    struct Next {
+        int lo2, hi;       // the block's span
+        uint32_t ri;       // row map word
+        uint32_t cw[NK / 2];
+        double ax[NK];
+        double w0p, w1p;
+        double xv[XPF];    // missing-span entries tid, tid + 1024 (flat order: A then B)
+        int na, a0, b0c, nmiss;
+    };
+    // missing part of [lo2, hi) against the resident [vlo, vhi): A = [lo2, min(hi, vlo)),
+    // B = [max(lo2, vhi), hi); flat index f < na is A's, else B's
+    auto miss_col = [](const Next &q, int f) { return f < q.na ? q.a0 + f : q.b0c + (f - q.na); };
+    auto fetch = [&](long b, int mlo, int mhi, int vlo, int vhi, int sb, Next &q) {
+        q.lo2 = mlo;
+        q.hi = mhi;
+        const int ae = min(mhi, vlo);
+        q.a0 = mlo;
+        q.na = ae > mlo ? ae - mlo : 0;
+        q.b0c = max(mlo, vhi);
+        const int nbm = mhi > q.b0c ? mhi - q.b0c : 0;
+        q.nmiss = q.na + nbm;
 #pragma unroll
-    for (int u = 0; u < NS / 2; u++) {
-        const int e = lo2 + 2 * (tid + WIN_ROWS * u);
-        xs[u] = dbl2w_t{0.0, 0.0};
-        if (e < hi) {
-            if (xv16 && e + 1 < hi) xs[u] = *reinterpret_cast<const dbl2w_t *>(a.x + e);
-            else xs[u] = dbl2w_t{e >= lo ? a.x[e] : 0.0, e + 1 < hi ? a.x[e + 1] : 0.0};
+        for (int u = 0; u < XPF; u++) {
+            const int f = tid + WIN_ROWS * u;
+            q.xv[u] = f < q.nmiss ? x[miss_col(q, f)] : 0.0;
         }
-    }
-    // this wave's slice; its first NK entries per lane, unconditionally (the
-    // arrays are padded past the last slice)
-    const int len = (int)(ri >> 10), lr = (int)(ri & 1023);
-    constexpr int NK = 10;
-    double ax[NK];
-    uint32_t cw[NK / 2];
+        q.ri = srow[b * WIN_ROWS + tid];
 #pragma unroll
-    for (int k = 0; k < NK / 2; k++) cw[k] = scol[sbase / 2 + 64 * k + lane];
+        for (int k = 0; k < NK / 2; k++) q.cw[k] = scol[sb / 2 + 64 * k + lane];
 #pragma unroll
-    for (int k = 0; k < NK; k++) ax[k] = sax[sbase + 64 * k + lane];
-    const int rr = min(r, a.nrows - 1);
-    // a fused dot with x itself (CG's q.p): when the block's rows lie inside
-    // its x span, x[r] is read from the staged span (uniform), not again from HBM
-    const int r0 = (int)(blk * WIN_ROWS), r1 = min(r0 + WIN_ROWS, a.nrows);
-    const bool w0x = NRED > 0 && a.w0 == a.x && a.w0 != a.z && r0 >= lo && r1 <= hi;
-    double w0p = 0.0, w1p = 0.0;
-    if (NRED > 0) {
-        if (a.w0 != a.z && !w0x) w0p = a.w0[rr];
-        if (NRED > 1 && a.w1 && a.w1 != a.z) w1p = a.w1[rr];
-    }
-#pragma unroll
-    for (int u = 0; u < NS / 2; u++)
-        if (lo2 + 2 * (tid + WIN_ROWS * u) < hi) reinterpret_cast<dbl2w_t *>(sxw)[tid + WIN_ROWS * u] = xs[u];
-    __syncthreads();
-    double sum = 0;
-#pragma unroll
-    for (int k = 0; k < NK; k++)
-        if (k < len) sum += sxw[(cw[k >> 1] >> (16 * (k & 1))) & 0xffffu] * ax[k];
-    for (int k = NK; k < len; k++) {  // rows longer than NK entries
-        const uint32_t c = scol[sbase / 2 + 64 * (k >> 1) + lane];
-        sum += sxw[(c >> (16 * (k & 1))) & 0xffffu] * sax[sbase + 64L * k + lane];
-    }
-    zb[lr] = sum;
-    __syncthreads();
-    sum = zb[tid];
-    if (w0x && r < a.nrows) w0p = sxw[r - lo2];
-    double zv = 0;
-    if (r < a.nrows) {
-        if (EPI == EPI_MXY) zv = sum;
-        else if (EPI == EPI_AMXY) zv = sum * a.alpha;
-        else if (EPI == EPI_AXPBY) zv = a.y[r] * a.beta + a.alpha * sum;
-        else zv = a.alpha * sum;
-        a.z[r] = zv;
-    }
-    if (NRED > 0) {
-        double v[NRED > 0 ? NRED : 1];
-        if (r < a.nrows) {
-            v[0] = zv * (a.w0 == a.z ? zv : w0p);
-            if (NRED > 1) v[NRED > 1 ? 1 : 0] = zv * (a.w1 && a.w1 != a.z ? w1p : zv);
-        } else {
-#pragma unroll
-            for (int q = 0; q < NRED; q++) v[q] = 0.0;
+        for (int k = 0; k < NK; k++) q.ax[k] = sax[sb + 64 * k + lane];
+        const int r = (int)(b * WIN_ROWS) + tid, rr = min(r, a.nrows - 1);
+        const int r0 = (int)(b * WIN_ROWS), r1 = min(r0 + WIN_ROWS, a.nrows);
+        const bool w0x = NRED > 0 && a.w0 == a.x && a.w0 != a.z && r0 >= mlo && r1 <= mhi;
+        q.w0p = 0.0;
+        q.w1p = 0.0;
+        if (NRED > 0) {
+            if (a.w0 != a.z && !w0x) q.w0p = a.w0[rr];
+            if (NRED > 1 && a.w1 && a.w1 != a.z) q.w1p = a.w1[rr];
         }
-        // chunk_reduce's order for each of the 4 chunks (waves 4q .. 4q+3)
-        const int wave = tid >> 6, q = wave >> 2;
+    };
+    auto meta = [&](long b, int &mlo, int &mhi, int &sb) {
+        mlo = win[2 * b] & ~1;
+        mhi = win[2 * b + 1];
+        sb = __builtin_amdgcn_readfirstlane(smeta[2 * (b * (WIN_ROWS / 64) + wave)]);
+    };
+    int vlo = 0, vhi = 0;  // resident span (none)
+    int mlo, mhi, msb;
+    meta(b0, mlo, mhi, msb);
+    Next cur, nxt;
+    fetch(b0, mlo, mhi, vlo, vhi, msb, nxt);
+    if (b0 + 1 < b1) meta(b0 + 1, mlo, mhi, msb);
+    int par = 0;
+    for (long b = b0; b < b1; b++, par ^= 1) {
+        cur = nxt;
+        __syncthreads();  // the previous block's ring and zb reads are done
 #pragma unroll
-        for (int t = 0; t < NRED; t++) {
-            const double sv = wave_sum(v[t]);
-            if (lane == 0) lds[q][t][wave & 3] = sv;
+        for (int u = 0; u < XPF; u++) {
+            const int f = tid + WIN_ROWS * u;
+            if (f < cur.nmiss) sxw[miss_col(cur, f) & MASK] = cur.xv[u];
         }
+        for (int f = tid + WIN_ROWS * XPF; f < cur.nmiss; f += WIN_ROWS) {  // a span mostly new
+            const int col = miss_col(cur, f);
+            sxw[col & MASK] = x[col];
+        }
+        vlo = cur.lo2;
+        vhi = cur.hi;
         __syncthreads();
-        const long chunk = blk * 4 + (tid >> 8);
-        if ((tid & 255) == 0 && chunk * 256 < a.nrows) {
-            const int cq = tid >> 8;
+        if (b + 1 < b1) {
+            fetch(b + 1, mlo, mhi, vlo, vhi, msb, nxt);
+            if (b + 2 < b1) meta(b + 2, mlo, mhi, msb);
+        }
+        const int r = (int)(b * WIN_ROWS) + tid;
+        const int len = (int)(cur.ri >> 10), lr = (int)(cur.ri & 1023);
+        const int lo2 = cur.lo2;
+        double sum = 0;
 #pragma unroll
-            for (int t = 0; t < NRED; t++)
-                a.part[t * a.pcap + chunk] = (lds[cq][t][0] + lds[cq][t][1]) + (lds[cq][t][2] + lds[cq][t][3]);
+        for (int k = 0; k < NK; k++)
+            if (k < len) sum += sxw[(lo2 + (int)((cur.cw[k >> 1] >> (16 * (k & 1))) & 0xffffu)) & MASK] * cur.ax[k];
+        if (len > NK) {  // rows longer than NK entries
+            const long sl = b * (WIN_ROWS / 64) + wave;
+            const int sb = __builtin_amdgcn_readfirstlane(smeta[2 * sl]);
+            for (int k = NK; k < len; k++) {
+                const uint32_t c = scol[sb / 2 + 64 * (k >> 1) + lane];
+                sum += sxw[(lo2 + (int)((c >> (16 * (k & 1))) & 0xffffu)) & MASK] * sax[sb + 64L * k + lane];
+            }
+        }
+        zb[lr] = sum;
+        __syncthreads();
+        sum = zb[tid];
+        const int r0 = (int)(b * WIN_ROWS), r1 = min(r0 + WIN_ROWS, a.nrows);
+        const bool w0x = NRED > 0 && a.w0 == a.x && a.w0 != a.z && r0 >= cur.lo2 && r1 <= cur.hi;
+        double w0p = cur.w0p;
+        if (w0x && r < a.nrows) w0p = sxw[r & MASK];
+        double zv = 0;
+        if (r < a.nrows) {
+            if (EPI == EPI_MXY) zv = sum;
+            else if (EPI == EPI_AMXY) zv = sum * a.alpha;
+            else if (EPI == EPI_AXPBY) zv = a.y[r] * a.beta + a.alpha * sum;
+            else zv = a.alpha * sum;
+            a.z[r] = zv;
+        }
+        if (NRED > 0) {
+            double v[NRED > 0 ? NRED : 1];
+            if (r < a.nrows) {
+                v[0] = zv * (a.w0 == a.z ? zv : w0p);
+                if (NRED > 1) v[NRED > 1 ? 1 : 0] = zv * (a.w1 && a.w1 != a.z ? cur.w1p : zv);
+            } else {
+#pragma unroll
+                for (int q = 0; q < NRED; q++) v[q] = 0.0;
+            }
+            // chunk_reduce's order for each of the 4 chunks (waves 4q .. 4q+3);
+            // the next block writes lds only after three more barriers
+            const int q = wave >> 2;
+#pragma unroll
+            for (int t = 0; t < NRED; t++) {
+                const double sv = wave_sum(v[t]);
+                if (lane == 0) lds[q][t][wave & 3] = sv;
+            }
+            __syncthreads();
+            const long chunk = b * 4 + (tid >> 8);
+            if ((tid & 255) == 0 && chunk * 256 < a.nrows) {
+                const int cq = tid >> 8;
+#pragma unroll
+                for (int t = 0; t < NRED; t++)
+                    a.part[t * a.pcap + chunk] = (lds[cq][t][0] + lds[cq][t][1]) + (lds[cq][t][2] + lds[cq][t][3]);
+            }
         }
     }
 }
 
 template <int EPI>
-static void spmv_sell_dispatch(const SpmvArgs &a, const lssp_amd_mat *A, int nred, hipStream_t s)
+static void spmv_sell_dispatch(const SpmvArgs &a, const lssp_amd_mat *A, int nred, hipStream_t s, int num_cus)
 {
     const long nb = (a.nrows + WIN_ROWS - 1) / WIN_ROWS;
-    const long g = (nb + 7) / 8 * 8;
+    const long g = std::min<long>(nb, num_cus);  // one workgroup per CU (the LDS ring)
     if (nred == 0) k_spmv_sell<EPI, 0><<<g, WIN_ROWS, 0, s>>>(a, A->d_win, A->s_ax, A->s_col, A->s_row, A->s_meta, nb);
     else if (nred == 1) k_spmv_sell<EPI, 1><<<g, WIN_ROWS, 0, s>>>(a, A->d_win, A->s_ax, A->s_col, A->s_row, A->s_meta, nb);
     else k_spmv_sell<EPI, 2><<<g, WIN_ROWS, 0, s>>>(a, A->d_win, A->s_ax, A->s_col, A->s_row, A->s_meta, nb);
@@ -741,10 +792,10 @@ int launch_spmv(lssp_amd_ctx *c, const lssp_amd_mat *A, int epi, double alpha, c
     }
     if (A->d_win && nb == nall && nred <= 2) {
         switch (epi) {
-        case EPI_MXY: spmv_sell_dispatch<EPI_MXY>(a, A, nred, c->stream); break;
-        case EPI_AMXY: spmv_sell_dispatch<EPI_AMXY>(a, A, nred, c->stream); break;
-        case EPI_AXPBY: spmv_sell_dispatch<EPI_AXPBY>(a, A, nred, c->stream); break;
-        default: spmv_sell_dispatch<EPI_AMX>(a, A, nred, c->stream); break;
+        case EPI_MXY: spmv_sell_dispatch<EPI_MXY>(a, A, nred, c->stream, c->num_cus); break;
+        case EPI_AMXY: spmv_sell_dispatch<EPI_AMXY>(a, A, nred, c->stream, c->num_cus); break;
+        case EPI_AXPBY: spmv_sell_dispatch<EPI_AXPBY>(a, A, nred, c->stream, c->num_cus); break;
+        default: spmv_sell_dispatch<EPI_AMX>(a, A, nred, c->stream, c->num_cus); break;
         }
         LSSP_HIP(hipGetLastError());
         return LSSP_AMD_OK;
